@@ -1,0 +1,159 @@
+/*
+ * kaboodle_sim.h — C ABI of the MI355X bulk-synchronous Kaboodle SWIM-round simulator.
+ *
+ * One handle = one simulated mesh of up to `capacity` virtual Kaboodle peers (ids 0..capacity-1),
+ * all advancing in lock-step rounds on the GPU.  Each entry point below replaces a piece of the
+ * per-instance Rust surface of serval/kaboodle v0.1.5 (paths relative to the reference root):
+ *
+ *   kb_sim_create / kb_sim_destroy   Kaboodle::new            src/lib.rs:93-133   (per mesh, not per peer)
+ *   kb_sim_step                      KaboodleInner::run/tick  src/kaboodle.rs:746-786 (all peers, R rounds)
+ *   kb_sim_start_node                Kaboodle::start          src/lib.rs:136-156, src/kaboodle.rs:114-185
+ *   kb_sim_stop_node                 Kaboodle::stop           src/lib.rs:159-183
+ *   kb_sim_ping_addrs                Kaboodle::ping_addrs     src/lib.rs:268-297
+ *   kb_sim_fingerprint               Kaboodle::fingerprint    src/lib.rs:301-304 -> generate_fingerprint
+ *                                                             src/kaboodle.rs:71-83
+ *   kb_sim_peers                     Kaboodle::peers          src/lib.rs:339-345
+ *   kb_sim_peer_states               Kaboodle::peer_states    src/lib.rs:348-354 (PeerState src/structs.rs:27-41)
+ *   kb_sim_set_identity              Kaboodle::set_identity   src/lib.rs:323-336
+ *   kb_sim_is_running                Kaboodle::is_running     src/lib.rs:307-309
+ *   kb_format_addr                   Kaboodle::self_addr      src/lib.rs:312-314 (canonical simulated address)
+ *   kb_fingerprint_of_set            generate_fingerprint     src/kaboodle.rs:71-83 (pure function)
+ *   status codes                     KaboodleError            src/errors.rs:8-24
+ *
+ * Semantics ("round semantics v1") are specified in DESIGN.md §2; the CPU restatement used as the
+ * parity oracle lives under oracle/ and exports the same functions with the prefix `kbo_`.
+ *
+ * Ownership: the library owns the handle and all device memory; every output buffer is caller-owned
+ * (pass cap = 0 to query the required element count).  A handle is NOT thread-safe.  kb_sim_step is
+ * synchronous: it returns after the simulated rounds have completed on the device.
+ */
+#ifndef KABOODLE_SIM_H
+#define KABOODLE_SIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KB_ABI_VERSION 1u
+
+/* ---- status codes (mirror KaboodleError, src/errors.rs:8-24) ------------------------------------ */
+enum {
+  KB_OK = 0,
+  KB_INVALID_OPERATION = 1,  /* KaboodleError::InvalidOperation (e.g. ping_addrs while stopped)      */
+  KB_IO_ERROR = 2,           /* KaboodleError::IoError -> HIP runtime / RCCL failure                 */
+  KB_NO_DEVICE = 3,          /* KaboodleError::NoAvailableInterfaces -> no usable GPU                */
+  KB_STOPPING_FAILED = 4,    /* KaboodleError::StoppingFailed                                        */
+  KB_INVALID_ARGUMENT = 5,   /* bad config / id out of range / null pointer                          */
+  KB_CAPACITY = 6            /* a declared fixed capacity was exceeded             */
+};
+
+/* ---- configuration ------------------------------------------------------------------------------ */
+enum { KB_INIT_JOIN = 0,        /* initial nodes start at round 0 knowing only themselves (config 2)   */
+       KB_INIT_CONVERGED = 1 }; /* initial nodes know every initial node, all stamps "ancient"          */
+
+enum { KB_FAILED_SIM_SENDER = 0,      /* Failed(p) honoured iff the broadcasting node is known (Q1)    */
+       KB_FAILED_SOCKET_FAITHFUL = 1 };/* Failed is never honoured (real-socket sender never matches)  */
+
+typedef struct kb_config {
+  uint32_t abi_version;      /* must be KB_ABI_VERSION                                               */
+  uint32_t capacity;         /* C: number of peer ids (initial nodes + churn reserve), <= 7,800,000  */
+  uint32_t initial_nodes;    /* ids 0..initial_nodes-1 are running at round 0                        */
+  uint32_t init_mode;        /* KB_INIT_*                                                            */
+  uint64_t seed;             /* Philox4x32-10 key                                                    */
+  uint32_t loss_threshold;   /* a delivery is lost iff philox word < loss_threshold (p*2^32)         */
+  uint32_t churn_threshold;  /* a running node leaves at round start iff philox word < threshold     */
+  int32_t  fault_end_round;  /* loss and churn act only in rounds r < fault_end_round (-1: forever)   */
+  uint32_t max_waves;        /* unicast delivery waves per round (>= 1; default 8)                   */
+  uint32_t failed_mode;      /* KB_FAILED_*                                                          */
+  uint32_t id_len;           /* default identity length in bytes (0..32) for every id               */
+  uint32_t partition_groups; /* 0/1: none; G: ids split into G contiguous groups                      */
+  int32_t  partition_start;  /* cross-group deliveries dropped for partition_start <= r < partition_end */
+  int32_t  partition_end;
+  int32_t  device;           /* HIP device ordinal, -1 = current device (ignored by the oracle)      */
+  uint32_t reserved[6];
+} kb_config;
+
+/* Per-peer state as reported by peer_states() (PeerState, src/structs.rs:27-41). */
+enum { KB_STATE_KNOWN = 0, KB_STATE_WAITING_FOR_PING = 1, KB_STATE_WAITING_FOR_INDIRECT_PING = 2 };
+typedef struct kb_peer_state {
+  uint32_t peer;             /* peer id                                                             */
+  uint32_t state;            /* KB_STATE_*                                                          */
+  int32_t  since;            /* round of the state's Instant; INT32_MIN = older than the stamp window */
+  uint32_t reserved;
+} kb_peer_state;
+
+/* Cumulative counters since creation (all ranks summed when sharded). */
+typedef struct kb_stats {
+  int32_t  round;                 /* next round to simulate                                          */
+  uint32_t alive;                 /* running nodes now                                               */
+  uint32_t agree;                 /* running nodes whose fingerprint at the last round's ping step
+                                     equalled the fingerprint of the true running set               */
+  int32_t  first_converged_round; /* first round with agree == alive (-1: never)                     */
+  int32_t  last_converged_round;  /* most recent such round (-1: never)                              */
+  uint32_t next_free_id;          /* next fresh id for churn joins                                   */
+  uint64_t sent_ping, sent_ping_req, sent_ack, sent_known_peers, sent_kpr;
+  uint64_t bcast_join, bcast_failed;
+  uint64_t drop_dead, drop_loss, drop_window, drop_oversize, drop_partition, drop_bcast;
+  uint64_t removed_timeout, removed_failed, join_responses, curious_overflow, churn_leaves, churn_joins;
+  uint64_t reserved[8];
+} kb_stats;
+
+typedef struct kb_sim kb_sim;
+
+/* Fill *cfg with defaults: capacity 1024, all running, KB_INIT_JOIN, seed 1, no faults, 8 waves. */
+void kb_config_default(kb_config* cfg);
+
+int  kb_sim_create(const kb_config* cfg, kb_sim** out);
+int  kb_sim_destroy(kb_sim* sim);
+/* Advance every running peer by `rounds` protocol periods. */
+int  kb_sim_step(kb_sim* sim, uint32_t rounds);
+
+int  kb_sim_start_node(kb_sim* sim, uint32_t node);                 /* takes effect next round start */
+int  kb_sim_stop_node(kb_sim* sim, uint32_t node);                  /* takes effect next round start */
+int  kb_sim_is_running(kb_sim* sim, uint32_t node, int* running);
+int  kb_sim_ping_addrs(kb_sim* sim, uint32_t node, const uint32_t* peers, size_t n);
+int  kb_sim_set_identity(kb_sim* sim, uint32_t node, const uint8_t* identity, size_t len);
+
+int  kb_sim_fingerprint(kb_sim* sim, uint32_t node, uint32_t* fp);
+int  kb_sim_fingerprints(kb_sim* sim, uint32_t* fps, size_t cap);   /* all ids; 0 for non-running  */
+int  kb_sim_peers(kb_sim* sim, uint32_t node, uint32_t* peers, size_t cap, size_t* n);
+int  kb_sim_peer_states(kb_sim* sim, uint32_t node, kb_peer_state* out, size_t cap, size_t* n);
+int  kb_sim_stats(kb_sim* sim, kb_stats* out);
+/* fingerprint of the true running set (what every converged node should report) */
+int  kb_sim_true_fingerprint(kb_sim* sim, uint32_t* fp);
+
+/* ---- parity / test surface ---------------------------------------------------------------------- */
+/* Raw stamp row of `node` (capacity bytes, DESIGN.md §2.2 encoding). */
+int  kb_sim_dump_row(kb_sim* sim, uint32_t node, uint8_t* row, size_t cap);
+/* Per-node scalars, canonical layout: for each id: alive, n, last_bcast, start_round (4 x int32).  */
+int  kb_sim_dump_scalars(kb_sim* sim, int32_t* out, size_t cap);
+/* Canonical suspect table: sorted (peer, kind, since) triples for `node`; n = triples written.      */
+int  kb_sim_dump_suspects(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, size_t* n);
+/* Canonical curious table: for each entry sorted by peer: peer, nobs, obs[0..3] (6 x int32).       */
+int  kb_sim_dump_curious(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, size_t* n);
+
+/* ---- pure helpers ------------------------------------------------------------------------------- */
+/* Canonical simulated address of an id: "10.100.100.<100 + id/50000>:<10000 + id%50000>".          */
+int  kb_format_addr(uint32_t id, char* buf, size_t cap);
+/* generate_fingerprint over explicit (address, identity) pairs given as ids with a uniform identity
+   table (identities[id*id_stride .. + id_lens[id]]); ids need not be sorted. */
+uint32_t kb_fingerprint_of_set(const uint32_t* ids, size_t n, const uint8_t* identities,
+                               size_t id_stride, const uint8_t* id_lens);
+
+const char* kb_last_error(void);
+
+/* ---- timing surface for bench.py ---------------------------------------------------------------- */
+/* HIP-event durations (ms, summed since last reset) of the round's kernels, recorded on the stream
+   they run on.  kind: 0 = ping-step row sweep (the dominant kernel), 1 = whole round.              */
+int  kb_sim_kernel_time(kb_sim* sim, int kind, double* ms, uint64_t* launches);
+int  kb_sim_reset_kernel_time(kb_sim* sim);
+/* Algorithmic HBM bytes moved by the row-sweep kernel since the last reset.         */
+int  kb_sim_sweep_bytes(kb_sim* sim, uint64_t* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KABOODLE_SIM_H */

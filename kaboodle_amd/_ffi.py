@@ -1,0 +1,281 @@
+"""ctypes binding of the C ABI declared in include/kaboodle_sim.h.
+
+`SimLib(path, prefix)` binds one shared library that implements the ABI.  The product binds the
+in-tree HIP library (`kaboodle_amd/libkaboodle_sim.so`, prefix ``kb_``); the test suite uses the same
+class to bind the CPU oracle (prefix ``kbo_``) so both are driven through identical calls.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+KB_ABI_VERSION = 1
+KB_OK, KB_INVALID_OPERATION, KB_IO_ERROR, KB_NO_DEVICE, KB_STOPPING_FAILED, KB_INVALID_ARGUMENT, KB_CAPACITY = range(7)
+KB_INIT_JOIN, KB_INIT_CONVERGED = 0, 1
+KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL = 0, 1
+STATE_NAMES = {0: "Known", 1: "WaitingForPing", 2: "WaitingForIndirectPing"}
+
+
+class KbConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_uint32), ("capacity", C.c_uint32), ("initial_nodes", C.c_uint32),
+        ("init_mode", C.c_uint32), ("seed", C.c_uint64), ("loss_threshold", C.c_uint32),
+        ("churn_threshold", C.c_uint32), ("fault_end_round", C.c_int32), ("max_waves", C.c_uint32),
+        ("failed_mode", C.c_uint32), ("id_len", C.c_uint32), ("partition_groups", C.c_uint32),
+        ("partition_start", C.c_int32), ("partition_end", C.c_int32), ("device", C.c_int32),
+        ("reserved", C.c_uint32 * 6),
+    ]
+
+
+class KbPeerState(C.Structure):
+    _fields_ = [("peer", C.c_uint32), ("state", C.c_uint32), ("since", C.c_int32), ("reserved", C.c_uint32)]
+
+
+class KbStats(C.Structure):
+    _fields_ = [
+        ("round", C.c_int32), ("alive", C.c_uint32), ("agree", C.c_uint32),
+        ("first_converged_round", C.c_int32), ("last_converged_round", C.c_int32), ("next_free_id", C.c_uint32),
+        ("sent_ping", C.c_uint64), ("sent_ping_req", C.c_uint64), ("sent_ack", C.c_uint64),
+        ("sent_known_peers", C.c_uint64), ("sent_kpr", C.c_uint64),
+        ("bcast_join", C.c_uint64), ("bcast_failed", C.c_uint64),
+        ("drop_dead", C.c_uint64), ("drop_loss", C.c_uint64), ("drop_window", C.c_uint64),
+        ("drop_oversize", C.c_uint64), ("drop_partition", C.c_uint64), ("drop_bcast", C.c_uint64),
+        ("removed_timeout", C.c_uint64), ("removed_failed", C.c_uint64), ("join_responses", C.c_uint64),
+        ("curious_overflow", C.c_uint64), ("churn_leaves", C.c_uint64), ("churn_joins", C.c_uint64),
+        ("reserved", C.c_uint64 * 8),
+    ]
+
+    def as_dict(self) -> dict:
+        return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
+
+
+class KbError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what} failed with status {code}")
+        self.code = code
+
+
+@dataclass
+class SimConfig:
+    """Python-side mirror of kb_config (defaults as kb_config_default)."""
+    capacity: int = 1024
+    initial_nodes: int = 1024
+    init_mode: int = KB_INIT_JOIN
+    seed: int = 1
+    loss: float = 0.0            # per-delivery loss probability
+    churn: float = 0.0           # per-node per-round leave probability
+    fault_end_round: int = -1
+    max_waves: int = 8
+    failed_mode: int = KB_FAILED_SIM_SENDER
+    id_len: int = 0
+    partition_groups: int = 0
+    partition_start: int = 0
+    partition_end: int = 0
+    device: int = -1
+
+    def to_c(self) -> KbConfig:
+        c = KbConfig()
+        c.abi_version = KB_ABI_VERSION
+        c.capacity, c.initial_nodes, c.init_mode = self.capacity, self.initial_nodes, self.init_mode
+        c.seed = self.seed
+        c.loss_threshold = min(int(round(self.loss * 2**32)), 2**32 - 1)
+        c.churn_threshold = min(int(round(self.churn * 2**32)), 2**32 - 1)
+        c.fault_end_round, c.max_waves, c.failed_mode = self.fault_end_round, self.max_waves, self.failed_mode
+        c.id_len = self.id_len
+        c.partition_groups, c.partition_start, c.partition_end = (
+            self.partition_groups, self.partition_start, self.partition_end)
+        c.device = self.device
+        return c
+
+
+_SIGS = {
+    "sim_create": (C.c_int, [C.POINTER(KbConfig), C.POINTER(C.c_void_p)]),
+    "sim_destroy": (C.c_int, [C.c_void_p]),
+    "sim_step": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sim_start_node": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sim_stop_node": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sim_is_running": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_int)]),
+    "sim_ping_addrs": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t]),
+    "sim_set_identity": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]),
+    "sim_fingerprint": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "sim_fingerprints": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t]),
+    "sim_true_fingerprint": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "sim_peers": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t)]),
+    "sim_peer_states": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(KbPeerState), C.c_size_t,
+                                  C.POINTER(C.c_size_t)]),
+    "sim_stats": (C.c_int, [C.c_void_p, C.POINTER(KbStats)]),
+    "sim_dump_row": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint8), C.c_size_t]),
+    "sim_dump_scalars": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.c_size_t]),
+    "sim_dump_suspects": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_int32), C.c_size_t,
+                                    C.POINTER(C.c_size_t)]),
+    "sim_dump_curious": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_int32), C.c_size_t,
+                                   C.POINTER(C.c_size_t)]),
+    "format_addr": (C.c_int, [C.c_uint32, C.c_char_p, C.c_size_t]),
+    "last_error": (C.c_char_p, []),
+}
+_OPTIONAL = {
+    "sim_kernel_time": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "sim_reset_kernel_time": (C.c_int, [C.c_void_p]),
+    "sim_sweep_bytes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+}
+
+
+class SimLib:
+    """One loaded implementation of the ABI (functions named `<prefix><name>`)."""
+
+    def __init__(self, path: str, prefix: str = "kb_"):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.path, self.prefix = path, prefix
+        self.lib = C.CDLL(path)
+        self.fn = {}
+        for name, (res, args) in _SIGS.items():
+            f = getattr(self.lib, prefix + name)
+            f.restype, f.argtypes = res, args
+            self.fn[name] = f
+        for name, (res, args) in _OPTIONAL.items():
+            f = getattr(self.lib, prefix + name, None)
+            if f is not None:
+                f.restype, f.argtypes = res, args
+                self.fn[name] = f
+
+    def call(self, name: str, *args) -> None:
+        rc = self.fn[name](*args)
+        if rc != KB_OK:
+            err = self.fn["last_error"]()
+            raise KbError(rc, f"{self.prefix}{name} ({err.decode(errors='replace') if err else ''})")
+
+
+class Sim:
+    """A simulated mesh (one handle) bound to a SimLib."""
+
+    def __init__(self, lib: SimLib, cfg: SimConfig):
+        self.lib, self.cfg = lib, cfg
+        self._c = cfg.to_c()
+        h = C.c_void_p()
+        lib.call("sim_create", C.byref(self._c), C.byref(h))
+        self.h = h
+        self.capacity = cfg.capacity
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.call("sim_destroy", self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- lifecycle --
+    def step(self, rounds: int = 1) -> None:
+        self.lib.call("sim_step", self.h, rounds)
+
+    def start_node(self, node: int) -> None:
+        self.lib.call("sim_start_node", self.h, node)
+
+    def stop_node(self, node: int) -> None:
+        self.lib.call("sim_stop_node", self.h, node)
+
+    def is_running(self, node: int) -> bool:
+        v = C.c_int()
+        self.lib.call("sim_is_running", self.h, node, C.byref(v))
+        return bool(v.value)
+
+    def ping_addrs(self, node: int, peers) -> None:
+        arr = (C.c_uint32 * len(peers))(*peers)
+        self.lib.call("sim_ping_addrs", self.h, node, arr, len(peers))
+
+    def set_identity(self, node: int, identity: bytes) -> None:
+        self.lib.call("sim_set_identity", self.h, node, identity, len(identity))
+
+    # -- inspection --
+    def fingerprint(self, node: int) -> int:
+        v = C.c_uint32()
+        self.lib.call("sim_fingerprint", self.h, node, C.byref(v))
+        return v.value
+
+    def fingerprints(self):
+        import numpy as np
+        out = np.zeros(self.capacity, dtype=np.uint32)
+        self.lib.call("sim_fingerprints", self.h, out.ctypes.data_as(C.POINTER(C.c_uint32)), self.capacity)
+        return out
+
+    def true_fingerprint(self) -> int:
+        v = C.c_uint32()
+        self.lib.call("sim_true_fingerprint", self.h, C.byref(v))
+        return v.value
+
+    def peers(self, node: int):
+        n = C.c_size_t()
+        self.lib.call("sim_peers", self.h, node, None, 0, C.byref(n))
+        arr = (C.c_uint32 * max(n.value, 1))()
+        self.lib.call("sim_peers", self.h, node, arr, n.value, C.byref(n))
+        return list(arr[: n.value])
+
+    def peer_states(self, node: int):
+        n = C.c_size_t()
+        self.lib.call("sim_peer_states", self.h, node, None, 0, C.byref(n))
+        arr = (KbPeerState * max(n.value, 1))()
+        self.lib.call("sim_peer_states", self.h, node, arr, n.value, C.byref(n))
+        return [(a.peer, a.state, a.since) for a in arr[: n.value]]
+
+    def stats(self) -> dict:
+        st = KbStats()
+        self.lib.call("sim_stats", self.h, C.byref(st))
+        return st.as_dict()
+
+    def row(self, node: int):
+        import numpy as np
+        out = np.zeros(self.capacity, dtype=np.uint8)
+        self.lib.call("sim_dump_row", self.h, node, out.ctypes.data_as(C.POINTER(C.c_uint8)), self.capacity)
+        return out
+
+    def rows(self):
+        import numpy as np
+        return np.stack([self.row(i) for i in range(self.capacity)])
+
+    def scalars(self):
+        import numpy as np
+        out = np.zeros((self.capacity, 4), dtype=np.int32)
+        self.lib.call("sim_dump_scalars", self.h, out.ctypes.data_as(C.POINTER(C.c_int32)), out.size)
+        return out
+
+    def suspects(self, node: int):
+        n = C.c_size_t()
+        buf = (C.c_int32 * (3 * 8))()
+        self.lib.call("sim_dump_suspects", self.h, node, buf, len(buf), C.byref(n))
+        return [tuple(buf[3 * k: 3 * k + 3]) for k in range(n.value)]
+
+    def curious(self, node: int):
+        n = C.c_size_t()
+        buf = (C.c_int32 * (6 * 8))()
+        self.lib.call("sim_dump_curious", self.h, node, buf, len(buf), C.byref(n))
+        return [tuple(buf[6 * k: 6 * k + 6]) for k in range(n.value)]
+
+    def format_addr(self, node: int) -> str:
+        buf = C.create_string_buffer(32)
+        self.lib.call("format_addr", node, buf, 32)
+        return buf.value.decode()
+
+    # -- bench surface (HIP library only) --
+    def kernel_time(self, kind: int = 0):
+        ms, n = C.c_double(), C.c_uint64()
+        self.lib.call("sim_kernel_time", self.h, kind, C.byref(ms), C.byref(n))
+        return ms.value, n.value
+
+    def reset_kernel_time(self) -> None:
+        self.lib.call("sim_reset_kernel_time", self.h)
+
+    def sweep_bytes(self) -> int:
+        v = C.c_uint64()
+        self.lib.call("sim_sweep_bytes", self.h, C.byref(v))
+        return v.value

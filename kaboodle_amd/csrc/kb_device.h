@@ -1,0 +1,122 @@
+// kb_device.h — device-side primitives of the MI355X Kaboodle round simulator (gfx950, wave64).
+//
+// Everything here is written for CDNA4 directly: 64-lane wavefronts, __ballot returns 64 bits,
+// cross-lane traffic through __shfl* (ds_bpermute) and LDS.  Semantics constants follow
+// src/kaboodle.rs:38-65 of the reference and DESIGN.md §2.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kb {
+
+// ---- protocol constants (src/kaboodle.rs:38-65), in rounds -------------------------------------
+constexpr int PING_TIMEOUT = 2;     // :62
+constexpr int SHARE_AGE = 10;       // :49
+constexpr int REBROADCAST = 10;     // :65
+constexpr int NUM_INDIRECT = 3;     // :52
+constexpr int NUM_CANDIDATES = 5;   // :57
+constexpr int BUFSZ = 10240;        // :43
+// declared capacities
+constexpr int SLOTS = 8;            // suspect slots per node
+constexpr int CSLOTS = 8;           // curious_peers entries per node
+constexpr int NOBS = 4;             // observers per curious entry
+constexpr int PAQ = 8;              // queued ping_addrs per node
+constexpr int MAXID = 32;           // identity bytes
+constexpr int ADDR_LEN = 20;        // "10.100.100.ddd:ppppp"
+constexpr int TICK_MAX = 3 * SLOTS + 1 + PAQ;   // unicast emissions of one tick
+constexpr int FLOYD_MAX_N = 262144; // LDS bitmap bound for truncated Join responses
+// stamp byte encoding
+constexpr uint8_t ST_UNKNOWN = 0, ST_SUSPECT = 1, ST_ANCIENT = 2;
+constexpr int EPOCH = 64, EOFF = 192;
+// message kinds (SwimMessage, src/structs.rs:94-116)
+enum : uint32_t { K_PING = 0, K_PINGREQ = 1, K_ACK = 2, K_KP = 3, K_KPR = 4 };
+// Philox purposes
+enum : uint32_t { P_PING = 1, P_INDIRECT = 2, P_RESPOND = 3, P_TRUNC = 4, P_LOSS = 5, P_BLOSS = 6, P_CHURN = 7 };
+enum : int32_t { SK_WFP = 1, SK_WFIP = 2 };
+constexpr int32_t NONE_ROUND = INT32_MIN;
+constexpr uint32_t CRC_POLY = 0xEDB88320u;
+
+// error codes raised on the device (checked by the host after each step)
+enum : uint32_t { DERR_NONE = 0, DERR_SLOTS = 1, DERR_OUTBOX = 2, DERR_PAYLOAD = 3, DERR_FLOYD = 4, DERR_INBOX = 5,
+                  DERR_RESP = 6 };
+
+// ---- records ------------------------------------------------------------------------------------
+struct Msg {            // 32 B unicast record
+  uint32_t dest, sender, seq, kind;
+  uint32_t a;           // PingRequest: peer; Ack: peer; KnownPeers: payload length
+  uint32_t fp, n;       // Ack / KnownPeersRequest
+  uint32_t off;         // KnownPeers: payload offset
+};
+struct Susp { uint32_t peer; int32_t since; int32_t kind; int32_t pad; };         // kind 0 = free
+struct Cur { uint32_t peer; uint32_t nobs; uint32_t obs[NOBS]; uint32_t used; uint32_t pad; };  // 32 B
+struct BCast { uint32_t sender, peer, bseq, pad; };
+struct Tmpl { uint32_t raw; uint32_t mask_cnt; };   // 16-id block template: raw crc0, mask | cnt<<16
+
+// ---- Philox4x32-10 (Salmon et al. SC'11), counter = (c0,c1,c2,c3), key = seed -------------------
+struct U4 { uint32_t x, y, z, w; };
+__host__ __device__ inline U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1; c3 = (uint32_t)p0; c0 = n0; c2 = n2;
+  }
+  return U4{c0, c1, c2, c3};
+}
+__host__ __device__ inline uint32_t mulhi(uint32_t u, uint32_t k) { return (uint32_t)(((uint64_t)u * k) >> 32); }
+
+// ---- GF(2) arithmetic mod the CRC-32 polynomial, reflected (x^0 = 0x80000000) ---------------------
+__host__ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll 4
+  for (int k = 31; k >= 0; --k) {
+    if (a & (1u << k)) p ^= b;
+    b = (b & 1u) ? (b >> 1) ^ CRC_POLY : b >> 1;
+  }
+  return p;
+}
+
+// ---- stamp window --------------------------------------------------------------------------------
+__host__ __device__ inline int32_t epoch_base(int32_t r) { return (r / EPOCH) * EPOCH; }
+__host__ __device__ inline uint8_t enc(int32_t t, int32_t r) {
+  int32_t v = t - epoch_base(r) + EOFF;
+  v = v < ST_ANCIENT ? ST_ANCIENT : (v > 255 ? 255 : v);
+  return (uint8_t)v;
+}
+
+// ---- wave helpers (wave64) ---------------------------------------------------------------------
+__device__ inline uint32_t lane() { return __lane_id(); }
+__device__ inline uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline uint32_t wave_min(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { uint32_t t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
+  return v;
+}
+__device__ inline uint32_t wave_or(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+  return v;
+}
+// exclusive prefix sum across the 64 lanes
+__device__ inline uint32_t wave_excl(uint32_t v) {
+  const uint32_t l = lane();
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) { uint32_t t = __shfl_up(x, o, 64); if (l >= (uint32_t)o) x += t; }
+  return x - v;
+}
+__device__ inline uint32_t bcast(uint32_t v, int src) { return __shfl(v, src, 64); }
+// Make this wave's earlier global stores visible to its own later loads (same CU; workgroup scope).
+__device__ inline void wave_mem_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+}  // namespace kb

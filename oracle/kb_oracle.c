@@ -1,0 +1,951 @@
+/*
+ * kb_oracle.c — CPU restatement of Kaboodle's SWIM round ("round semantics v1").
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity oracle: tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load it; the product (kaboodle_amd/, include/) never does.
+ *
+ * It follows the reference handler by handler, in its order (paths relative to the reference root):
+ *   tick order               src/kaboodle.rs:746-779   (join -> suspects -> ping -> ping_addrs -> window)
+ *   maybe_broadcast_join     src/kaboodle.rs:228-251
+ *   handle_suspected_peers   src/kaboodle.rs:558-653
+ *   ping_random_peer         src/kaboodle.rs:655-703
+ *   handle_incoming_ping_requests src/kaboodle.rs:550-556
+ *   handle_incoming_broadcasts    src/kaboodle.rs:256-311 (Failed :268-283, Join :284-304)
+ *   should_respond_to_broadcast   src/kaboodle.rs:333-354
+ *   maybe_send_known_peers_to_peer src/kaboodle.rs:356-392
+ *   handle_incoming_messages      src/kaboodle.rs:394-548 (prologue :406-415, Ack :418-447,
+ *                                  KnownPeers :448-472, KnownPeersRequest :473-512, Ping :513-532,
+ *                                  PingRequest :533-545)
+ *   maybe_sync_known_peers   src/kaboodle.rs:707-740
+ *   generate_fingerprint     src/kaboodle.rs:71-83
+ *   ObservableHashMap insert/remove/update  src/observable_hashmap.rs:84-142
+ *   Kaboodle::start/stop/ping_addrs/set_identity  src/lib.rs:136-183, 268-297, 323-336
+ *
+ * Data layout is deliberately the same dense representation the GPU uses (stamp byte per (node, peer),
+ * DESIGN.md §2.2), because the declared stamp window (rebase every 64 rounds, "ancient" saturation)
+ * is part of the semantics.  Everything else is plain sequential code: every node processes its
+ * inbox one message at a time, exactly like the reference's receive loop.
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+#include <limits.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+#include "../include/kaboodle_sim.h"
+#include "kb_oracle_prims.h"
+
+/* ---- constants (src/kaboodle.rs:38-65), in rounds ----------------------------------------------- */
+#define PING_TIMEOUT 2          /* PING_TIMEOUT 2000 ms            :62 */
+#define SHARE_AGE 10            /* MAX_PEER_SHARE_AGE 10000 ms     :49 */
+#define REBROADCAST 10          /* REBROADCAST_INTERVAL 10000 ms   :65 */
+#define NUM_INDIRECT 3          /* NUM_INDIRECT_PING_PEERS         :52 */
+#define NUM_CANDIDATES 5        /* NUM_CANDIDATE_TARGET_PEERS      :57 */
+#define BUFSZ 10240             /* INCOMING_BUFFER_SIZE            :43 */
+/* declared capacities */
+#define SLOTS 8
+#define CSLOTS 8
+#define NOBS 4
+#define PAQ 8
+#define MAXID 32
+#define ADDR_LEN 20
+/* stamp encoding */
+#define ST_UNKNOWN 0
+#define ST_SUSPECT 1
+#define ST_ANCIENT 2
+#define EPOCH 64
+#define EOFF 192
+/* message kinds (SwimMessage, src/structs.rs:94-116) */
+enum { K_PING = 0, K_PINGREQ = 1, K_ACK = 2, K_KP = 3, K_KPR = 4 };
+/* Philox purposes */
+enum { P_PING = 1, P_INDIRECT = 2, P_RESPOND = 3, P_TRUNC = 4, P_LOSS = 5, P_BLOSS = 6, P_CHURN = 7 };
+enum { SK_WFP = 1, SK_WFIP = 2 };
+
+typedef struct { uint32_t peer; int32_t since; int32_t kind; } osusp;       /* kind 0 = free */
+typedef struct { uint32_t peer; uint32_t nobs; uint32_t obs[NOBS]; int32_t used; } ocur;
+typedef struct {
+  uint32_t dest, sender, seq, kind;
+  uint32_t a, fp, n;
+  uint32_t* pay; uint32_t pay_len;
+} omsg;
+typedef struct { omsg* v; size_t n, cap; } ovec;
+typedef struct { uint32_t sender, peer, bseq; } obcast;
+typedef struct { int stop; uint32_t node; } oevent;
+
+struct kbo_sim {
+  kb_config cfg;
+  uint32_t C;
+  uint32_t k0, k1;
+  uint8_t* stamp;             /* C x C */
+  uint8_t* alive;
+  uint8_t* ever;
+  int32_t* start_round;
+  uint32_t* n;
+  uint32_t* fp;
+  uint8_t* dirty;
+  int32_t* last_bcast;
+  osusp* susp;                /* C x SLOTS */
+  ocur* cur;                  /* C x CSLOTS */
+  uint32_t* paq; uint32_t* paq_n;
+  uint8_t* ident; uint8_t* id_len;
+  uint32_t* cseg; uint32_t* segmul;   /* crc0(addr||identity), x^(8*seglen) */
+  uint32_t* seglen;
+  uint32_t mulz_tab[4][256]; int uniform; uint32_t ulen;
+  int32_t round;
+  uint32_t next_free;
+  obcast* bfail; size_t nbfail, capbfail;
+  obcast* bjoin; size_t nbjoin, capbjoin;
+  oevent* ev; size_t nev, capev;
+  ovec* out;                  /* per-node outbox of the wave being produced */
+  uint32_t* oseq;             /* per-node emission counter for the wave being produced */
+  int32_t* a3fp;              /* unused */
+  kb_stats st;
+};
+typedef struct kbo_sim kbo_sim;
+
+static char g_err[256];
+static void seterr(const char* m) { snprintf(g_err, sizeof g_err, "%s", m); }
+const char* kbo_last_error(void) { return g_err; }
+
+/* ---- helpers ------------------------------------------------------------------------------------ */
+static inline int32_t epoch_base(int32_t r) { return (r / EPOCH) * EPOCH; }
+/* encode Known(t) at round r (t <= r) */
+static inline uint8_t enc(int32_t t, int32_t r) {
+  int32_t v = t - epoch_base(r) + EOFF;
+  if (v < ST_ANCIENT) v = ST_ANCIENT;
+  if (v > 255) v = 255;
+  return (uint8_t)v;
+}
+static inline uint8_t* row(kbo_sim* s, uint32_t i) { return s->stamp + (size_t)i * s->C; }
+static inline int active_faults(kbo_sim* s, int32_t r) { return s->cfg.fault_end_round < 0 || r < s->cfg.fault_end_round; }
+static inline o_u32x4 ph(kbo_sim* s, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+  return o_philox(c0, c1, c2, c3, s->k0, s->k1);
+}
+static inline int partition_blocks(kbo_sim* s, int32_t r, uint32_t a, uint32_t b) {
+  uint32_t G = s->cfg.partition_groups;
+  if (G <= 1 || r < s->cfg.partition_start || r >= s->cfg.partition_end) return 0;
+  uint64_t ga = (uint64_t)a * G / s->C, gb = (uint64_t)b * G / s->C;
+  return ga != gb;
+}
+
+int kbo_format_addr(uint32_t id, char* buf, size_t cap) {
+  char tmp[32];
+  int len = snprintf(tmp, sizeof tmp, "10.100.100.%u:%u", 100u + id / 50000u, 10000u + id % 50000u);
+  if (!buf || cap < (size_t)len + 1) return KB_INVALID_ARGUMENT;
+  memcpy(buf, tmp, (size_t)len + 1);
+  return KB_OK;
+}
+
+static void default_identity(uint32_t id, uint32_t len, uint8_t* out) {
+  for (uint32_t k = 0; k < len; ++k) out[k] = (uint8_t)('a' + ((id * 31u + k * 7u) % 26u));
+}
+
+static void compute_seg(kbo_sim* s, uint32_t id) {
+  char a[32];
+  kbo_format_addr(id, a, sizeof a);
+  uint32_t reg = o_crc_update(0, (const uint8_t*)a, ADDR_LEN);
+  reg = o_crc_update(reg, s->ident + (size_t)id * MAXID, s->id_len[id]);
+  s->cseg[id] = reg;
+  s->seglen[id] = ADDR_LEN + s->id_len[id];
+  s->segmul[id] = o_xpow8(s->seglen[id]);
+}
+
+static void build_mulz(kbo_sim* s) {
+  uint32_t z = o_xpow8(s->ulen);
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t v = 0; v < 256; ++v) s->mulz_tab[k][v] = o_multmodp(z, v << (8 * k));
+}
+static inline uint32_t mulz(const kbo_sim* s, uint32_t a) {
+  return s->mulz_tab[0][a & 0xFF] ^ s->mulz_tab[1][(a >> 8) & 0xFF] ^ s->mulz_tab[2][(a >> 16) & 0xFF] ^
+         s->mulz_tab[3][a >> 24];
+}
+
+/* generate_fingerprint (src/kaboodle.rs:71-83): CRC-32 over addr.to_string() || identity of every
+ * entry in ascending address order (= ascending id).  Computed by folding the per-peer segment CRCs:
+ * crc0(A||B) = crc0(A)*x^(8|B|) ^ crc0(B); final = crc0 ^ 0xFFFFFFFF*x^(8 len) ^ 0xFFFFFFFF. */
+static uint32_t fold_row(kbo_sim* s, uint32_t i) {
+  const uint8_t* rw = row(s, i);
+  uint32_t raw = 0; uint64_t len = 0;
+  if (s->uniform) {
+    uint64_t cnt = 0;
+    for (uint32_t j = 0; j < s->C; ++j)
+      if (rw[j]) { raw = mulz(s, raw) ^ s->cseg[j]; ++cnt; }
+    len = cnt * s->ulen;
+  } else {
+    for (uint32_t j = 0; j < s->C; ++j)
+      if (rw[j]) { raw = o_multmodp(s->segmul[j], raw) ^ s->cseg[j]; len += s->seglen[j]; }
+  }
+  return raw ^ o_multmodp(o_xpow8(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+}
+
+/* The literal reference definition, byte by byte (kept for the equivalence test). */
+uint32_t kbo_fingerprint_direct(kbo_sim* s, uint32_t i) {
+  const uint8_t* rw = row(s, i);
+  uint32_t reg = 0xFFFFFFFFu;
+  char a[32];
+  for (uint32_t j = 0; j < s->C; ++j) {
+    if (!rw[j]) continue;
+    kbo_format_addr(j, a, sizeof a);
+    reg = o_crc_update(reg, (const uint8_t*)a, strlen(a));
+    reg = o_crc_update(reg, s->ident + (size_t)j * MAXID, s->id_len[j]);
+  }
+  return reg ^ 0xFFFFFFFFu;
+}
+
+static inline uint32_t cur_fp(kbo_sim* s, uint32_t i) {
+  if (s->dirty[i]) { s->fp[i] = fold_row(s, i); s->dirty[i] = 0; }
+  return s->fp[i];
+}
+
+/* ---- ObservableHashMap operations on row i (src/observable_hashmap.rs:84-142) ------------------- */
+static osusp* susp_find(kbo_sim* s, uint32_t i, uint32_t p) {
+  osusp* sl = s->susp + (size_t)i * SLOTS;
+  for (int k = 0; k < SLOTS; ++k) if (sl[k].kind && sl[k].peer == p) return &sl[k];
+  return NULL;
+}
+static int susp_count(kbo_sim* s, uint32_t i) {
+  osusp* sl = s->susp + (size_t)i * SLOTS; int c = 0;
+  for (int k = 0; k < SLOTS; ++k) c += sl[k].kind != 0;
+  return c;
+}
+/* insert(p, Known(t)): overwrite; clears WaitingFor* state. returns 1 if p was new */
+static int map_insert_known(kbo_sim* s, uint32_t i, uint32_t p, int32_t t, int32_t r) {
+  uint8_t* b = row(s, i) + p;
+  int was = *b;
+  if (was == ST_SUSPECT) { osusp* q = susp_find(s, i, p); if (q) q->kind = 0; }
+  *b = enc(t, r);
+  if (was == ST_UNKNOWN) { s->n[i]++; s->dirty[i] = 1; return 1; }
+  return 0;
+}
+static int map_remove(kbo_sim* s, uint32_t i, uint32_t p) {
+  uint8_t* b = row(s, i) + p;
+  if (*b == ST_UNKNOWN) return 0;
+  if (*b == ST_SUSPECT) { osusp* q = susp_find(s, i, p); if (q) q->kind = 0; }
+  *b = ST_UNKNOWN;
+  s->n[i]--; s->dirty[i] = 1;
+  return 1;
+}
+static int set_suspect(kbo_sim* s, uint32_t i, uint32_t p, int kind, int32_t r) {
+  osusp* q = susp_find(s, i, p);
+  if (!q) {
+    osusp* sl = s->susp + (size_t)i * SLOTS;
+    for (int k = 0; k < SLOTS; ++k) if (!sl[k].kind) { q = &sl[k]; break; }
+    if (!q) return KB_CAPACITY;
+    q->peer = p;
+  }
+  q->kind = kind; q->since = r;
+  row(s, i)[p] = ST_SUSPECT;
+  return KB_OK;
+}
+
+/* curious_peers (src/kaboodle.rs:101, :536-540, :423, :644) */
+static ocur* cur_find(kbo_sim* s, uint32_t i, uint32_t p) {
+  ocur* c = s->cur + (size_t)i * CSLOTS;
+  for (int k = 0; k < CSLOTS; ++k) if (c[k].used && c[k].peer == p) return &c[k];
+  return NULL;
+}
+static void cur_add(kbo_sim* s, uint32_t i, uint32_t p, uint32_t observer) {
+  ocur* e = cur_find(s, i, p);
+  if (!e) {
+    ocur* c = s->cur + (size_t)i * CSLOTS;
+    for (int k = 0; k < CSLOTS; ++k) if (!c[k].used) { e = &c[k]; break; }
+    if (!e) {
+#pragma omp atomic
+      s->st.curious_overflow++;
+      return;
+    }
+    e->used = 1; e->peer = p; e->nobs = 0;
+  }
+  for (uint32_t k = 0; k < e->nobs; ++k) if (e->obs[k] == observer) return;
+  if (e->nobs == NOBS) {
+#pragma omp atomic
+    s->st.curious_overflow++;
+    return;
+  }
+  e->obs[e->nobs++] = observer;
+}
+static void cur_remove(kbo_sim* s, uint32_t i, uint32_t p) {
+  ocur* e = cur_find(s, i, p);
+  if (e) e->used = 0;
+}
+
+/* ---- emission ----------------------------------------------------------------------------------- */
+static void vpush(ovec* v, const omsg* m) {
+  if (v->n == v->cap) { v->cap = v->cap ? v->cap * 2 : 8; v->v = (omsg*)realloc(v->v, v->cap * sizeof(omsg)); }
+  v->v[v->n++] = *m;
+}
+static void emit(kbo_sim* s, uint32_t from, uint32_t to, uint32_t kind, uint32_t a, uint32_t fp, uint32_t n,
+                 uint32_t* pay, uint32_t pay_len) {
+  omsg m;
+  m.dest = to; m.sender = from; m.seq = s->oseq[from]++; m.kind = kind;
+  m.a = a; m.fp = fp; m.n = n; m.pay = pay; m.pay_len = pay_len;
+  vpush(&s->out[from], &m);
+}
+
+/* bincode 1.3.3 size of SwimEnvelope{identity, KnownPeers(map)} (src/structs.rs:78-116):
+ * identity u64 len + bytes, u32 variant tag, u64 map len, per entry SocketAddr::V4 (u32 tag + 4 + 2)
+ * + Bytes (u64 len + bytes). */
+static uint64_t kp_size(kbo_sim* s, uint32_t self, const uint32_t* ids, uint32_t n) {
+  uint64_t sz = 8 + s->id_len[self] + 4 + 8;
+  for (uint32_t k = 0; k < n; ++k) sz += 10 + 8 + s->id_len[ids[k]];
+  return sz;
+}
+static uint32_t kp_cap_uniform(kbo_sim* s) {   /* largest k with 20 + L + k(18+L) < 10240 */
+  uint32_t L = s->cfg.id_len;
+  return (BUFSZ - 20 - L - 1) / (18 + L);
+}
+
+/* ---- lifecycle (src/lib.rs:136-183, src/kaboodle.rs:114-185) ------------------------------------ */
+static void node_start(kbo_sim* s, uint32_t i, int32_t r) {
+  s->alive[i] = 1; s->ever[i] = 1; s->start_round[i] = r;
+  map_insert_known(s, i, i, r, r);          /* known_peers.insert(self_addr, Known(now)) :145-152 */
+  s->dirty[i] = 1;
+  s->last_bcast[i] = INT32_MIN;             /* last_broadcast_time: None                    :170 */
+  memset(s->cur + (size_t)i * CSLOTS, 0, sizeof(ocur) * CSLOTS);   /* fresh KaboodleInner     */
+  s->paq_n[i] = 0;
+}
+static void node_stop(kbo_sim* s, uint32_t i) {
+  map_remove(s, i, i);                      /* known_peers.remove(&self_addr)   src/lib.rs:167-170 */
+  s->alive[i] = 0;
+  s->paq_n[i] = 0;
+}
+
+/* ---- creation ----------------------------------------------------------------------------------- */
+void kbo_config_default(kb_config* c) {
+  memset(c, 0, sizeof *c);
+  c->abi_version = KB_ABI_VERSION; c->capacity = 1024; c->initial_nodes = 1024; c->init_mode = KB_INIT_JOIN;
+  c->seed = 1; c->fault_end_round = -1; c->max_waves = 8; c->failed_mode = KB_FAILED_SIM_SENDER;
+  c->device = -1;
+}
+
+int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
+  o_crc_init();
+  if (!cfg || !out || cfg->abi_version != KB_ABI_VERSION) { seterr("bad config"); return KB_INVALID_ARGUMENT; }
+  if (cfg->capacity == 0 || cfg->capacity > 7800000u || cfg->initial_nodes > cfg->capacity || cfg->id_len > MAXID ||
+      cfg->max_waves == 0 || cfg->max_waves > 64) {
+    seterr("config out of range"); return KB_INVALID_ARGUMENT;
+  }
+  kbo_sim* s = (kbo_sim*)calloc(1, sizeof *s);
+  s->cfg = *cfg; s->C = cfg->capacity;
+  s->k0 = (uint32_t)cfg->seed; s->k1 = (uint32_t)(cfg->seed >> 32);
+  size_t C = s->C;
+  s->stamp = (uint8_t*)calloc(C * C, 1);
+  s->alive = (uint8_t*)calloc(C, 1); s->ever = (uint8_t*)calloc(C, 1);
+  s->start_round = (int32_t*)calloc(C, 4); s->n = (uint32_t*)calloc(C, 4); s->fp = (uint32_t*)calloc(C, 4);
+  s->dirty = (uint8_t*)calloc(C, 1); s->last_bcast = (int32_t*)calloc(C, 4);
+  s->susp = (osusp*)calloc(C * SLOTS, sizeof(osusp)); s->cur = (ocur*)calloc(C * CSLOTS, sizeof(ocur));
+  s->paq = (uint32_t*)calloc(C * PAQ, 4); s->paq_n = (uint32_t*)calloc(C, 4);
+  s->ident = (uint8_t*)calloc(C * MAXID, 1); s->id_len = (uint8_t*)calloc(C, 1);
+  s->cseg = (uint32_t*)calloc(C, 4); s->segmul = (uint32_t*)calloc(C, 4); s->seglen = (uint32_t*)calloc(C, 4);
+  s->out = (ovec*)calloc(C, sizeof(ovec)); s->oseq = (uint32_t*)calloc(C, 4);
+  if (!s->stamp || !s->susp || !s->cur) { seterr("out of host memory"); free(s); return KB_CAPACITY; }
+  for (uint32_t i = 0; i < s->C; ++i) {
+    s->id_len[i] = (uint8_t)cfg->id_len;
+    default_identity(i, cfg->id_len, s->ident + (size_t)i * MAXID);
+    compute_seg(s, i);
+    s->last_bcast[i] = INT32_MIN;
+    s->start_round[i] = INT32_MIN;
+  }
+  s->uniform = 1; s->ulen = ADDR_LEN + cfg->id_len; build_mulz(s);
+  s->round = 0; s->next_free = cfg->initial_nodes;
+  for (uint32_t i = 0; i < cfg->initial_nodes; ++i) {
+    node_start(s, i, 0);
+    if (cfg->init_mode == KB_INIT_CONVERGED) {
+      uint8_t* rw = row(s, i);
+      for (uint32_t j = 0; j < cfg->initial_nodes; ++j) if (j != i) rw[j] = ST_ANCIENT;
+      s->n[i] = cfg->initial_nodes;
+      s->last_bcast[i] = -1000;             /* running for a while: no Join at round 0 */
+    }
+  }
+  s->st.first_converged_round = -1; s->st.last_converged_round = -1;
+  *out = s;
+  return KB_OK;
+}
+
+int kbo_sim_destroy(kbo_sim* s) {
+  if (!s) return KB_INVALID_ARGUMENT;
+  for (uint32_t i = 0; i < s->C; ++i) free(s->out[i].v);
+  free(s->stamp); free(s->alive); free(s->ever); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
+  free(s->last_bcast); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len);
+  free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
+  free(s->ev); free(s);
+  return KB_OK;
+}
+
+/* ---- broadcast phase: deliveries of round r-1's broadcasts ---------------------- */
+static void bpush(obcast** v, size_t* n, size_t* cap, uint32_t sender, uint32_t peer, uint32_t bseq) {
+  if (*n == *cap) { *cap = *cap ? *cap * 2 : 16; *v = (obcast*)realloc(*v, *cap * sizeof(obcast)); }
+  (*v)[*n].sender = sender; (*v)[*n].peer = peer; (*v)[*n].bseq = bseq; (*n)++;
+}
+
+static int bcast_lost(kbo_sim* s, uint32_t recv, const obcast* b, int32_t r) {
+  if (partition_blocks(s, r, b->sender, recv)) return 2;
+  if (!active_faults(s, r) || s->cfg.loss_threshold == 0) return 0;
+  return ph(s, recv, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | b->bseq, b->sender).v[0] < s->cfg.loss_threshold;
+}
+
+/* should_respond_to_broadcast (src/kaboodle.rs:333-354), integer restatement of gen_bool */
+static int should_respond(kbo_sim* s, uint32_t i, uint32_t joiner, int32_t r) {
+  int64_t o = (int64_t)s->n[i] - 2;
+  if (o <= 0) return 1;
+  int64_t pct = 100 - o * o;
+  if (pct < 1) pct = 1;
+  uint32_t u = ph(s, i, (uint32_t)r, (uint32_t)P_RESPOND << 24, joiner).v[0];
+  return (int64_t)o_mulhi(u, 100) < pct;
+}
+
+/* maybe_send_known_peers_to_peer (src/kaboodle.rs:356-392): every entry of the map (self, the joiner
+ * and suspects included); while the encoding is >= 10240 B drop a uniformly random entry — restated
+ * as a uniform random subset of the largest size that fits, drawn with Floyd's algorithm. */
+static void join_response(kbo_sim* s, uint32_t i, uint32_t joiner, int32_t r) {
+  const uint8_t* rw = row(s, i);
+  uint32_t n = s->n[i];
+  uint32_t* members = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  uint32_t m = 0;
+  for (uint32_t j = 0; j < s->C; ++j) if (rw[j]) members[m++] = j;
+  uint32_t cap = kp_cap_uniform(s);
+  uint32_t* pay;
+  uint32_t plen;
+  if (m <= cap || !s->uniform) {
+    pay = members; plen = m;
+  } else {
+    /* Floyd: for t in [0,cap): j = m-cap+t; v = uniform[0, j]; add v unless present, else add j */
+    uint8_t* chosen = (uint8_t*)calloc(m, 1);
+    for (uint32_t t = 0; t < cap; ++t) {
+      uint32_t j = m - cap + t;
+      o_u32x4 w = ph(s, i, (uint32_t)r, ((uint32_t)P_TRUNC << 24) | (t >> 2), joiner);
+      uint32_t v = o_mulhi(w.v[t & 3], j + 1);
+      if (chosen[v]) chosen[j] = 1; else chosen[v] = 1;
+    }
+    pay = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+    plen = 0;
+    for (uint32_t k = 0; k < m; ++k) if (chosen[k]) pay[plen++] = members[k];
+    free(chosen); free(members);
+  }
+  emit(s, i, joiner, K_KP, plen, 0, 0, pay, plen);
+#pragma omp atomic
+  s->st.join_responses++;
+}
+
+static void phase_broadcasts(kbo_sim* s, uint32_t i, int32_t r) {
+  uint64_t lost = 0, removed = 0;
+  /* Failed(p) (src/kaboodle.rs:268-283) */
+  for (size_t k = 0; k < s->nbfail; ++k) {
+    const obcast* b = &s->bfail[k];
+    if (b->sender == i) continue;                     /* own broadcasts are not delivered to self */
+    if (bcast_lost(s, i, b, r)) { lost++; continue; }
+    if (b->peer == i) continue;                       /* Failed(self) ignored            :269-273 */
+    if (s->cfg.failed_mode == KB_FAILED_SIM_SENDER && row(s, i)[b->sender] != ST_UNKNOWN)
+      removed += (uint64_t)map_remove(s, i, b->peer); /* sender is a mesh member         :275-279 */
+  }
+  /* Join{addr} (src/kaboodle.rs:284-304) */
+  for (size_t k = 0; k < s->nbjoin; ++k) {
+    const obcast* b = &s->bjoin[k];
+    if (b->sender == i) continue;                     /* addr == self_addr               :285-287 */
+    if (bcast_lost(s, i, b, r)) { lost++; continue; }
+    int is_new = map_insert_known(s, i, b->sender, r, r);
+    if (is_new && should_respond(s, i, b->sender, r)) join_response(s, i, b->sender, r);
+  }
+#pragma omp atomic
+  s->st.drop_bcast += lost;
+#pragma omp atomic
+  s->st.removed_failed += removed;
+}
+
+/* ---- tick (src/kaboodle.rs:746-779) -------------------------------------------------------------- */
+typedef struct { uint32_t fail_peers[SLOTS]; int nfail; int join; } otick_bc;
+
+static inline uint32_t rot_key(uint32_t j, uint32_t i, uint32_t C) {  /* rotated address order from self+1 */
+  return (j + C - i - 1) % C;
+}
+
+static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
+  uint8_t* rw = row(s, i);
+  bc->nfail = 0; bc->join = 0;
+  /* A1 maybe_broadcast_join (:228-251) */
+  if (s->last_bcast[i] == INT32_MIN || (r - s->last_bcast[i] >= REBROADCAST && s->n[i] <= 1)) {
+    bc->join = 1; s->last_bcast[i] = r;
+  }
+  /* A2 handle_suspected_peers (:558-653) */
+  {
+    uint32_t m = s->n[i] - 1 - (uint32_t)susp_count(s, i);   /* Known && != self (:571-577) */
+    osusp* sl = s->susp + (size_t)i * SLOTS;
+    int order[SLOTS], no = 0;
+    for (int k = 0; k < SLOTS; ++k) if (sl[k].kind) order[no++] = k;
+    for (int a = 1; a < no; ++a) {            /* ascending peer id */
+      int t = order[a], b = a - 1;
+      while (b >= 0 && sl[order[b]].peer > sl[t].peer) { order[b + 1] = order[b]; --b; }
+      order[b + 1] = t;
+    }
+    uint32_t indirect[SLOTS], removed[SLOTS]; int nind = 0, nrem = 0;
+    uint32_t* cand = NULL;
+    for (int q = 0; q < no; ++q) {
+      osusp* e = &sl[order[q]];
+      if (r - e->since < PING_TIMEOUT) continue;
+      if (e->kind == SK_WFP) {
+        uint32_t k = m < NUM_INDIRECT ? m : NUM_INDIRECT;
+        if (k == 0) { removed[nrem++] = e->peer; continue; }
+        if (!cand) {
+          cand = (uint32_t*)malloc(sizeof(uint32_t) * m);
+          uint32_t c = 0;
+          for (uint32_t j = 0; j < s->C; ++j) if (rw[j] >= ST_ANCIENT && j != i) cand[c++] = j;
+        }
+        o_u32x4 w = ph(s, i, (uint32_t)r, (uint32_t)P_INDIRECT << 24, e->peer);
+        uint32_t pick[3];
+        pick[0] = o_mulhi(w.v[0], m);
+        if (k > 1) { uint32_t b = o_mulhi(w.v[1], m - 1); pick[1] = b + (b >= pick[0]); }
+        if (k > 2) {
+          uint32_t lo = pick[0] < pick[1] ? pick[0] : pick[1], hi = pick[0] < pick[1] ? pick[1] : pick[0];
+          uint32_t c = o_mulhi(w.v[2], m - 2);
+          if (c >= lo) c++;
+          if (c >= hi) c++;
+          pick[2] = c;
+        }
+        for (uint32_t t = 0; t < k; ++t) emit(s, i, cand[pick[t]], K_PINGREQ, e->peer, 0, 0, NULL, 0);
+        indirect[nind++] = e->peer;
+      } else {
+        removed[nrem++] = e->peer;
+      }
+    }
+    free(cand);
+    for (int q = 0; q < nind; ++q) set_suspect(s, i, indirect[q], SK_WFIP, r);     /* :631-639 */
+    for (int q = 0; q < nrem; ++q) {                                              /* :641-652 */
+      map_remove(s, i, removed[q]);
+      cur_remove(s, i, removed[q]);
+      bc->fail_peers[bc->nfail++] = removed[q];
+    }
+    if (nrem) {
+#pragma omp atomic
+      s->st.removed_timeout += (uint64_t)nrem;
+    }
+  }
+  /* A3 ping_random_peer (:655-703): oldest 5 by (stamp, rotated id), one uniformly */
+  {
+    uint32_t best[NUM_CANDIDATES]; uint32_t bkey_hi[NUM_CANDIDATES], bkey_lo[NUM_CANDIDATES]; int nb = 0;
+    for (uint32_t j = 0; j < s->C; ++j) {
+      uint8_t b = rw[j];
+      if (b < ST_ANCIENT || j == i) continue;
+      uint32_t kh = b, kl = rot_key(j, i, s->C);
+      if (nb == NUM_CANDIDATES && (kh > bkey_hi[nb - 1] || (kh == bkey_hi[nb - 1] && kl > bkey_lo[nb - 1]))) continue;
+      int pos = nb < NUM_CANDIDATES ? nb : NUM_CANDIDATES - 1;
+      while (pos > 0 && (bkey_hi[pos - 1] > kh || (bkey_hi[pos - 1] == kh && bkey_lo[pos - 1] > kl))) {
+        bkey_hi[pos] = bkey_hi[pos - 1]; bkey_lo[pos] = bkey_lo[pos - 1]; best[pos] = best[pos - 1]; --pos;
+      }
+      bkey_hi[pos] = kh; bkey_lo[pos] = kl; best[pos] = j;
+      if (nb < NUM_CANDIDATES) nb++;
+    }
+    if (nb > 0) {
+      uint32_t u = ph(s, i, (uint32_t)r, (uint32_t)P_PING << 24, 0).v[0];
+      uint32_t t = best[o_mulhi(u, (uint32_t)nb)];
+      if (set_suspect(s, i, t, SK_WFP, r) != KB_OK) return KB_CAPACITY;
+      emit(s, i, t, K_PING, 0, 0, 0, NULL, 0);
+    }
+  }
+  /* A4 handle_incoming_ping_requests (:550-556) */
+  for (uint32_t q = 0; q < s->paq_n[i]; ++q) emit(s, i, s->paq[(size_t)i * PAQ + q], K_PING, 0, 0, 0, NULL, 0);
+  s->paq_n[i] = 0;
+  return KB_OK;
+}
+
+/* ---- unicast handling (src/kaboodle.rs:394-548) -------------------------------------------------- */
+static void maybe_sync(kbo_sim* s, uint32_t i, uint32_t peer, uint32_t their_fp, uint32_t their_n) {  /* :707-740 */
+  uint32_t f = cur_fp(s, i);
+  if (f == their_fp) return;
+  if (s->n[i] > their_n) return;
+  emit(s, i, peer, K_KPR, 0, f, s->n[i], NULL, 0);
+}
+
+static void handle_message(kbo_sim* s, uint32_t i, const omsg* m, int32_t r) {
+  uint32_t from = m->sender;
+  map_insert_known(s, i, from, r, r);            /* prologue :406-415 */
+  switch (m->kind) {
+    case K_ACK: {                                  /* :418-447 */
+      ocur* e = cur_find(s, i, m->a);
+      if (e) {
+        uint32_t nobs = e->nobs, obs[NOBS];
+        memcpy(obs, e->obs, sizeof obs);
+        e->used = 0;
+        for (uint32_t k = 0; k < nobs; ++k) emit(s, i, obs[k], K_ACK, m->a, m->fp, m->n, NULL, 0);
+      }
+      maybe_sync(s, i, m->a, m->fp, m->n);
+      break;
+    }
+    case K_KP: {                                   /* :448-472 */
+      uint8_t* rw = row(s, i);
+      for (uint32_t k = 0; k < m->pay_len; ++k) {
+        uint32_t p = m->pay[k];
+        if (rw[p] == ST_UNKNOWN) map_insert_known(s, i, p, r - SHARE_AGE, r);
+      }
+      break;
+    }
+    case K_KPR: {                                  /* :473-512 */
+      const uint8_t* rw = row(s, i);
+      uint8_t fresh = enc(r - (SHARE_AGE - 1), r);
+      uint32_t cnt = 0, cap = 64;
+      uint32_t* pay = (uint32_t*)malloc(sizeof(uint32_t) * cap);
+      for (uint32_t j = 0; j < s->C; ++j) {
+        if (rw[j] >= fresh && j != i && j != from) {
+          if (cnt == cap) { cap *= 2; pay = (uint32_t*)realloc(pay, sizeof(uint32_t) * cap); }
+          pay[cnt++] = j;
+        }
+      }
+      if (kp_size(s, i, pay, cnt) > BUFSZ) {        /* truncated at the receiver -> undeliverable (Q3) */
+        free(pay);
+#pragma omp atomic
+        s->st.drop_oversize++;
+      } else {
+        emit(s, i, from, K_KP, cnt, 0, 0, pay, cnt);
+      }
+      maybe_sync(s, i, from, m->fp, m->n);
+      break;
+    }
+    case K_PING:                                   /* :513-532 */
+      emit(s, i, from, K_ACK, i, cur_fp(s, i), s->n[i], NULL, 0);
+      break;
+    case K_PINGREQ:                                /* :533-545 */
+      cur_add(s, i, m->a, from);
+      emit(s, i, m->a, K_PING, 0, 0, 0, NULL, 0);
+      break;
+  }
+}
+
+/* ---- routing of one wave ------------------------------------------------------------------------- */
+typedef struct { uint32_t* idx; size_t n, cap; } oidx;
+static void ipush(oidx* v, uint32_t x) {
+  if (v->n == v->cap) { v->cap = v->cap ? v->cap * 2 : 4; v->idx = (uint32_t*)realloc(v->idx, v->cap * 4); }
+  v->idx[v->n++] = x;
+}
+
+/* Collect per-node outboxes (sender order, then seq) into one array, and reset them. */
+static omsg* gather_out(kbo_sim* s, size_t* total) {
+  size_t t = 0;
+  for (uint32_t i = 0; i < s->C; ++i) t += s->out[i].n;
+  omsg* all = (omsg*)malloc(sizeof(omsg) * (t ? t : 1));
+  size_t k = 0;
+  for (uint32_t i = 0; i < s->C; ++i) {
+    for (size_t q = 0; q < s->out[i].n; ++q) {
+      all[k++] = s->out[i].v[q];
+      switch (s->out[i].v[q].kind) {
+        case K_PING: s->st.sent_ping++; break;
+        case K_PINGREQ: s->st.sent_ping_req++; break;
+        case K_ACK: s->st.sent_ack++; break;
+        case K_KP: s->st.sent_known_peers++; break;
+        case K_KPR: s->st.sent_kpr++; break;
+      }
+    }
+    s->out[i].n = 0;
+    s->oseq[i] = 0;
+  }
+  *total = t;
+  return all;
+}
+
+static int run_waves(kbo_sim* s, int32_t r) {
+  uint32_t C = s->C;
+  oidx* inb0 = (oidx*)calloc(C, sizeof(oidx));
+  oidx* inb1 = (oidx*)calloc(C, sizeof(oidx));
+  for (uint32_t w = 0; w < s->cfg.max_waves; ++w) {
+    size_t M;
+    omsg* all = gather_out(s, &M);
+    if (M == 0) { free(all); break; }
+    for (uint32_t i = 0; i < C; ++i) { inb0[i].n = 0; inb1[i].n = 0; }
+    for (size_t k = 0; k < M; ++k) {
+      omsg* m = &all[k];
+      if (!s->alive[m->dest]) { s->st.drop_dead++; continue; }
+      if (partition_blocks(s, r, m->sender, m->dest)) { s->st.drop_partition++; continue; }
+      if (active_faults(s, r) && s->cfg.loss_threshold &&
+          ph(s, m->sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m->seq).v[0] < s->cfg.loss_threshold) {
+        s->st.drop_loss++; continue;
+      }
+      ipush(m->kind == K_KP ? &inb0[m->dest] : &inb1[m->dest], (uint32_t)k);
+    }
+#pragma omp parallel for schedule(dynamic, 64)
+    for (uint32_t i = 0; i < C; ++i) {
+      /* KnownPeers first (arrival order is free; this group commutes), then the rest,
+         each in (sender, seq) order */
+      for (size_t q = 0; q < inb0[i].n; ++q) handle_message(s, i, &all[inb0[i].idx[q]], r);
+      for (size_t q = 0; q < inb1[i].n; ++q) handle_message(s, i, &all[inb1[i].idx[q]], r);
+    }
+    for (size_t k = 0; k < M; ++k) free(all[k].pay);
+    free(all);
+  }
+  /* whatever was emitted in the last wave misses the receive window */
+  for (uint32_t i = 0; i < C; ++i) {
+    s->st.drop_window += s->out[i].n;
+    for (size_t q = 0; q < s->out[i].n; ++q) {
+      switch (s->out[i].v[q].kind) {
+        case K_PING: s->st.sent_ping++; break;
+        case K_PINGREQ: s->st.sent_ping_req++; break;
+        case K_ACK: s->st.sent_ack++; break;
+        case K_KP: s->st.sent_known_peers++; break;
+        case K_KPR: s->st.sent_kpr++; break;
+      }
+      free(s->out[i].v[q].pay);
+    }
+    s->out[i].n = 0; s->oseq[i] = 0;
+  }
+  for (uint32_t i = 0; i < C; ++i) { free(inb0[i].idx); free(inb1[i].idx); }
+  free(inb0); free(inb1);
+  return KB_OK;
+}
+
+/* fingerprint of the true running set */
+static uint32_t true_fp(kbo_sim* s) {
+  uint32_t raw = 0; uint64_t len = 0;
+  for (uint32_t j = 0; j < s->C; ++j)
+    if (s->alive[j]) { raw = o_multmodp(s->segmul[j], raw) ^ s->cseg[j]; len += s->seglen[j]; }
+  return raw ^ o_multmodp(o_xpow8(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+}
+
+/* ---- one round ----------------------------------------------------------------------------------- */
+static int step_round(kbo_sim* s) {
+  int32_t r = s->round;
+  uint32_t C = s->C;
+  /* 0. stamp window: every EPOCH rounds the base advances; known stamps shift down, saturating */
+  if (r > 0 && r % EPOCH == 0) {
+    size_t tot = (size_t)C * C;
+#pragma omp parallel for
+    for (size_t k = 0; k < tot; ++k) {
+      uint8_t b = s->stamp[k];
+      if (b > ST_ANCIENT) s->stamp[k] = (uint8_t)(b - EPOCH > ST_ANCIENT ? b - EPOCH : ST_ANCIENT);
+    }
+  }
+  /* 1. lifecycle: API events in call order, then churn (leaves in id order, joins with fresh ids) */
+  for (size_t k = 0; k < s->nev; ++k) {
+    uint32_t i = s->ev[k].node;
+    if (s->ev[k].stop) { if (s->alive[i]) node_stop(s, i); }
+    else if (!s->alive[i]) node_start(s, i, r);
+  }
+  s->nev = 0;
+  if (active_faults(s, r) && s->cfg.churn_threshold) {
+    uint32_t leaves = 0;
+    for (uint32_t i = 0; i < C; ++i) {
+      if (!s->alive[i] || s->start_round[i] == r) continue;
+      if (ph(s, i, (uint32_t)r, (uint32_t)P_CHURN << 24, 0).v[0] < s->cfg.churn_threshold) { node_stop(s, i); leaves++; }
+    }
+    s->st.churn_leaves += leaves;
+    for (uint32_t k = 0; k < leaves && s->next_free < C; ++k) { node_start(s, s->next_free++, r); s->st.churn_joins++; }
+  }
+  /* 2. broadcasts emitted during round r-1 */
+#pragma omp parallel for schedule(dynamic, 64)
+  for (uint32_t i = 0; i < C; ++i)
+    if (s->alive[i] && s->start_round[i] < r) phase_broadcasts(s, i, r);
+  /* 3. tick */
+  otick_bc* bc = (otick_bc*)calloc(C, sizeof(otick_bc));
+  int err = KB_OK;
+  uint32_t tfp = true_fp(s);
+  uint32_t agree = 0, alive = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+:agree, alive)
+  for (uint32_t i = 0; i < C; ++i) {
+    if (!s->alive[i]) continue;
+    if (tick(s, i, r, &bc[i]) != KB_OK) err = KB_CAPACITY;
+    alive++;
+    agree += cur_fp(s, i) == tfp;        /* fingerprint at the ping step */
+  }
+  if (err) { free(bc); seterr("suspect slots exhausted"); return err; }
+  s->nbfail = 0; s->nbjoin = 0;
+  for (uint32_t i = 0; i < C; ++i) {
+    uint32_t bseq = 0;
+    if (bc[i].join) { bpush(&s->bjoin, &s->nbjoin, &s->capbjoin, i, i, bseq++); s->st.bcast_join++; }
+    for (int q = 0; q < bc[i].nfail; ++q) { bpush(&s->bfail, &s->nbfail, &s->capbfail, i, bc[i].fail_peers[q], bseq++); s->st.bcast_failed++; }
+  }
+  free(bc);
+  /* 4. receive window: unicast waves */
+  err = run_waves(s, r);
+  if (err) return err;
+  s->st.agree = agree; s->st.alive = alive;
+  if (alive && agree == alive) {
+    if (s->st.first_converged_round < 0) s->st.first_converged_round = r;
+    s->st.last_converged_round = r;
+  }
+  s->round = r + 1;
+  return KB_OK;
+}
+
+int kbo_sim_step(kbo_sim* s, uint32_t rounds) {
+  if (!s) return KB_INVALID_ARGUMENT;
+  for (uint32_t k = 0; k < rounds; ++k) { int e = step_round(s); if (e) return e; }
+  return KB_OK;
+}
+
+/* ---- API ---------------------------------------------------------------------------------------- */
+static int check(kbo_sim* s, uint32_t node) { return (!s || node >= s->C) ? KB_INVALID_ARGUMENT : KB_OK; }
+
+int kbo_sim_start_node(kbo_sim* s, uint32_t node) {
+  if (check(s, node)) return KB_INVALID_ARGUMENT;
+  if (s->nev == s->capev) { s->capev = s->capev ? s->capev * 2 : 16; s->ev = (oevent*)realloc(s->ev, s->capev * sizeof(oevent)); }
+  s->ev[s->nev].stop = 0; s->ev[s->nev].node = node; s->nev++;
+  return KB_OK;
+}
+int kbo_sim_stop_node(kbo_sim* s, uint32_t node) {
+  if (check(s, node)) return KB_INVALID_ARGUMENT;
+  if (s->nev == s->capev) { s->capev = s->capev ? s->capev * 2 : 16; s->ev = (oevent*)realloc(s->ev, s->capev * sizeof(oevent)); }
+  s->ev[s->nev].stop = 1; s->ev[s->nev].node = node; s->nev++;
+  return KB_OK;
+}
+int kbo_sim_is_running(kbo_sim* s, uint32_t node, int* running) {
+  if (check(s, node) || !running) return KB_INVALID_ARGUMENT;
+  *running = s->alive[node];
+  return KB_OK;
+}
+/* Kaboodle::ping_addrs (src/lib.rs:268-297): error while stopped; addresses already known are skipped */
+int kbo_sim_ping_addrs(kbo_sim* s, uint32_t node, const uint32_t* peers, size_t n) {
+  if (check(s, node) || (n && !peers)) return KB_INVALID_ARGUMENT;
+  if (!s->alive[node]) { seterr("Cannot ping while we are not started"); return KB_INVALID_OPERATION; }
+  for (size_t k = 0; k < n; ++k) {
+    if (peers[k] >= s->C) return KB_INVALID_ARGUMENT;
+    if (row(s, node)[peers[k]] != ST_UNKNOWN) continue;
+    if (s->paq_n[node] == PAQ) { seterr("ping_addrs queue full"); return KB_CAPACITY; }
+    s->paq[(size_t)node * PAQ + s->paq_n[node]++] = peers[k];
+  }
+  return KB_OK;
+}
+/* Kaboodle::set_identity (src/lib.rs:323-336); the simulator additionally requires that the id has
+ * never run (identity is per id) and a uniform length when truncation is possible. */
+int kbo_sim_set_identity(kbo_sim* s, uint32_t node, const uint8_t* identity, size_t len) {
+  if (check(s, node) || len > MAXID || (len && !identity)) return KB_INVALID_ARGUMENT;
+  if (s->alive[node] || s->ever[node]) {
+    seterr("Cannot change identity while the mesh is running; call .stop first");
+    return KB_INVALID_OPERATION;
+  }
+  if (len != s->cfg.id_len && s->C > 200) { seterr("non-uniform identity length needs capacity <= 200"); return KB_INVALID_ARGUMENT; }
+  memcpy(s->ident + (size_t)node * MAXID, identity, len);
+  s->id_len[node] = (uint8_t)len;
+  compute_seg(s, node);
+  s->uniform = 1;
+  for (uint32_t j = 0; j < s->C; ++j) if (s->id_len[j] != s->cfg.id_len) { s->uniform = 0; break; }
+  for (uint32_t j = 0; j < s->C; ++j) s->dirty[j] = 1;
+  return KB_OK;
+}
+
+int kbo_sim_fingerprint(kbo_sim* s, uint32_t node, uint32_t* fp) {
+  if (check(s, node) || !fp) return KB_INVALID_ARGUMENT;
+  *fp = cur_fp(s, node);
+  return KB_OK;
+}
+int kbo_sim_fingerprints(kbo_sim* s, uint32_t* fps, size_t cap) {
+  if (!s || !fps || cap < s->C) return KB_INVALID_ARGUMENT;
+#pragma omp parallel for schedule(dynamic, 64)
+  for (uint32_t i = 0; i < s->C; ++i) fps[i] = s->alive[i] ? cur_fp(s, i) : 0;
+  return KB_OK;
+}
+int kbo_sim_true_fingerprint(kbo_sim* s, uint32_t* fp) {
+  if (!s || !fp) return KB_INVALID_ARGUMENT;
+  *fp = true_fp(s);
+  return KB_OK;
+}
+int kbo_sim_peers(kbo_sim* s, uint32_t node, uint32_t* peers, size_t cap, size_t* n) {
+  if (check(s, node) || !n) return KB_INVALID_ARGUMENT;
+  const uint8_t* rw = row(s, node);
+  size_t c = 0;
+  for (uint32_t j = 0; j < s->C; ++j) if (rw[j]) { if (peers && c < cap) peers[c] = j; c++; }
+  *n = c;
+  return (peers && cap < c) ? KB_CAPACITY : KB_OK;
+}
+int kbo_sim_peer_states(kbo_sim* s, uint32_t node, kb_peer_state* out, size_t cap, size_t* n) {
+  if (check(s, node) || !n) return KB_INVALID_ARGUMENT;
+  const uint8_t* rw = row(s, node);
+  size_t c = 0;
+  int32_t E = epoch_base(s->round);
+  for (uint32_t j = 0; j < s->C; ++j) {
+    if (!rw[j]) continue;
+    if (out && c < cap) {
+      kb_peer_state* o = &out[c];
+      o->peer = j; o->reserved = 0;
+      if (rw[j] == ST_SUSPECT) {
+        osusp* q = susp_find(s, node, j);
+        o->state = q && q->kind == SK_WFIP ? KB_STATE_WAITING_FOR_INDIRECT_PING : KB_STATE_WAITING_FOR_PING;
+        o->since = q ? q->since : 0;
+      } else {
+        o->state = KB_STATE_KNOWN;
+        o->since = rw[j] == ST_ANCIENT ? INT32_MIN : (int32_t)rw[j] + E - EOFF;
+      }
+    }
+    c++;
+  }
+  *n = c;
+  return (out && cap < c) ? KB_CAPACITY : KB_OK;
+}
+int kbo_sim_stats(kbo_sim* s, kb_stats* out) {
+  if (!s || !out) return KB_INVALID_ARGUMENT;
+  *out = s->st;
+  out->round = s->round;
+  out->next_free_id = s->next_free;
+  uint32_t a = 0;
+  for (uint32_t i = 0; i < s->C; ++i) a += s->alive[i];
+  out->alive = a;
+  return KB_OK;
+}
+int kbo_sim_dump_row(kbo_sim* s, uint32_t node, uint8_t* rw, size_t cap) {
+  if (check(s, node) || !rw || cap < s->C) return KB_INVALID_ARGUMENT;
+  memcpy(rw, row(s, node), s->C);
+  return KB_OK;
+}
+int kbo_sim_dump_scalars(kbo_sim* s, int32_t* out, size_t cap) {
+  if (!s || !out || cap < (size_t)s->C * 4) return KB_INVALID_ARGUMENT;
+  for (uint32_t i = 0; i < s->C; ++i) {
+    out[4 * i] = s->alive[i]; out[4 * i + 1] = (int32_t)s->n[i];
+    out[4 * i + 2] = s->last_bcast[i]; out[4 * i + 3] = s->start_round[i];
+  }
+  return KB_OK;
+}
+int kbo_sim_dump_suspects(kbo_sim* s, uint32_t node, int32_t* out, size_t cap, size_t* n) {
+  if (check(s, node) || !n) return KB_INVALID_ARGUMENT;
+  osusp* sl = s->susp + (size_t)node * SLOTS;
+  int32_t tmp[SLOTS][3]; size_t c = 0;
+  for (int k = 0; k < SLOTS; ++k) if (sl[k].kind) { tmp[c][0] = (int32_t)sl[k].peer; tmp[c][1] = sl[k].kind; tmp[c][2] = sl[k].since; c++; }
+  for (size_t a = 1; a < c; ++a) for (size_t b = a; b > 0 && tmp[b - 1][0] > tmp[b][0]; --b) {
+    int32_t t[3]; memcpy(t, tmp[b], sizeof t); memcpy(tmp[b], tmp[b - 1], sizeof t); memcpy(tmp[b - 1], t, sizeof t);
+  }
+  *n = c;
+  if (out) { if (cap < 3 * c) return KB_CAPACITY; memcpy(out, tmp, sizeof(int32_t) * 3 * c); }
+  return KB_OK;
+}
+int kbo_sim_dump_curious(kbo_sim* s, uint32_t node, int32_t* out, size_t cap, size_t* n) {
+  if (check(s, node) || !n) return KB_INVALID_ARGUMENT;
+  ocur* cu = s->cur + (size_t)node * CSLOTS;
+  int32_t tmp[CSLOTS][6]; size_t c = 0;
+  for (int k = 0; k < CSLOTS; ++k) if (cu[k].used) {
+    tmp[c][0] = (int32_t)cu[k].peer; tmp[c][1] = (int32_t)cu[k].nobs;
+    for (int q = 0; q < NOBS; ++q) tmp[c][2 + q] = q < (int)cu[k].nobs ? (int32_t)cu[k].obs[q] : -1;
+    c++;
+  }
+  for (size_t a = 1; a < c; ++a) for (size_t b = a; b > 0 && tmp[b - 1][0] > tmp[b][0]; --b) {
+    int32_t t[6]; memcpy(t, tmp[b], sizeof t); memcpy(tmp[b], tmp[b - 1], sizeof t); memcpy(tmp[b - 1], t, sizeof t);
+  }
+  *n = c;
+  if (out) { if (cap < 6 * c) return KB_CAPACITY; memcpy(out, tmp, sizeof(int32_t) * 6 * c); }
+  return KB_OK;
+}
+
+/* pure helpers */
+uint32_t kbo_fingerprint_of_ids(const uint32_t* ids, size_t n, const uint8_t* identities, size_t stride,
+                                const uint8_t* lens) {
+  o_crc_init();
+  uint32_t* v = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
+  memcpy(v, ids, sizeof(uint32_t) * n);
+  for (size_t a = 1; a < n; ++a) { uint32_t t = v[a]; size_t b = a; while (b > 0 && v[b - 1] > t) { v[b] = v[b - 1]; --b; } v[b] = t; }
+  uint32_t reg = 0xFFFFFFFFu;
+  char a[32];
+  for (size_t k = 0; k < n; ++k) {
+    kbo_format_addr(v[k], a, sizeof a);
+    reg = o_crc_update(reg, (const uint8_t*)a, strlen(a));
+    if (identities && lens) reg = o_crc_update(reg, identities + v[k] * stride, lens[v[k]]);
+  }
+  free(v);
+  return n ? reg ^ 0xFFFFFFFFu : 0;
+}
+uint32_t kbo_crc32(const uint8_t* p, size_t n) { o_crc_init(); return o_crc32(p, n); }
+void kbo_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t* out4) {
+  o_u32x4 o = o_philox(c0, c1, c2, c3, k0, k1);
+  memcpy(out4, o.v, 16);
+}
+int kbo_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}

@@ -1,0 +1,151 @@
+"""Parity harness: drive the HIP library and the CPU oracle through identical ABI calls and compare the
+complete simulator state (stamp rows, per-node scalars, suspect and curious tables, fingerprints,
+counters) after every round.  Used by tests/test_gpu_parity.py and runnable as a script on the GPU box:
+
+    python tests/parity.py            # the standard matrix, prints one line per case
+"""
+from __future__ import annotations
+
+import os
+import sys
+from dataclasses import replace
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from kaboodle_amd._ffi import (KB_INIT_CONVERGED, KB_INIT_JOIN, KB_FAILED_SOCKET_FAITHFUL,  # noqa: E402
+                               Sim, SimConfig, SimLib)
+
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libkb_oracle.so")
+ORACLE_OMP_SO = os.path.join(ROOT, "oracle", "_build", "libkb_oracle_omp.so")
+GPU_SO = os.path.join(ROOT, "kaboodle_amd", "libkaboodle_sim.so")
+
+CONFIG1_IDS = [b"top-left", b"top-right", b"bottom-left", b"bottom-right"]   # 2x2-layout.kdl:6-20
+
+
+def oracle_lib(omp: bool = False) -> SimLib:
+    return SimLib(ORACLE_OMP_SO if omp else ORACLE_SO, "kbo_")
+
+
+def gpu_lib() -> SimLib:
+    return SimLib(GPU_SO, "kb_")
+
+
+def state_of(sim: Sim, full_rows: bool = True) -> dict:
+    st = {"stats": sim.stats(), "scalars": sim.scalars(), "fps": sim.fingerprints(),
+          "truefp": sim.true_fingerprint()}
+    C = sim.capacity
+    if full_rows:
+        st["rows"] = sim.rows()
+    st["susp"] = [sim.suspects(i) for i in range(C)]
+    st["cur"] = [sim.curious(i) for i in range(C)]
+    return st
+
+
+def diff_states(a: dict, b: dict) -> list[str]:
+    out = []
+    for k in ("stats",):
+        for f, v in a[k].items():
+            if b[k][f] != v:
+                out.append(f"stats.{f}: {v} != {b[k][f]}")
+    if a["truefp"] != b["truefp"]:
+        out.append(f"truefp {a['truefp']:#x} != {b['truefp']:#x}")
+    for k in ("scalars", "fps"):
+        if not np.array_equal(a[k], b[k]):
+            bad = np.argwhere(a[k] != b[k])
+            out.append(f"{k}: {len(bad)} mismatches, first {bad[:4].tolist()}")
+    if "rows" in a and "rows" in b and not np.array_equal(a["rows"], b["rows"]):
+        bad = np.argwhere(a["rows"] != b["rows"])
+        i, j = bad[0]
+        out.append(f"rows: {len(bad)} mismatches, first node {i} peer {j}: {a['rows'][i, j]} != {b['rows'][i, j]}")
+    for k in ("susp", "cur"):
+        for i, (x, y) in enumerate(zip(a[k], b[k])):
+            if x != y:
+                out.append(f"{k}[{i}]: {x} != {y}")
+                break
+    return out
+
+
+def setup(sim: Sim, case: dict) -> None:
+    for i, ident in case.get("identities", {}).items():
+        sim.set_identity(i, ident)
+    for i in case.get("start", []):
+        sim.start_node(i)
+
+
+def run_case(case: dict, rounds: int, check_every: int = 1, full_rows: bool = True, verbose: bool = False):
+    """Run `case` on both implementations; returns (ok, message, final gpu stats)."""
+    cfg = case["cfg"]
+    o = Sim(oracle_lib(), cfg)
+    g = Sim(gpu_lib(), cfg)
+    setup(o, case)
+    setup(g, case)
+    events = case.get("events", {})
+    for r in range(rounds):
+        for kind, node, arg in events.get(r, []):
+            for s in (o, g):
+                if kind == "stop":
+                    s.stop_node(node)
+                elif kind == "start":
+                    s.start_node(node)
+                elif kind == "ping":
+                    s.ping_addrs(node, arg)
+        o.step(1)
+        g.step(1)
+        if (r + 1) % check_every == 0 or r == rounds - 1:
+            d = diff_states(state_of(o, full_rows), state_of(g, full_rows))
+            if d:
+                return False, f"round {r}: " + "; ".join(d[:6]), g.stats()
+            if verbose:
+                st = g.stats()
+                print(f"  round {r}: agree {st['agree']}/{st['alive']} ok", flush=True)
+    return True, "ok", g.stats()
+
+
+def standard_cases() -> list[tuple[str, dict, int]]:
+    cases = []
+    cases.append(("config1_2x2", {"cfg": SimConfig(capacity=4, initial_nodes=0),
+                                  "identities": {i: n for i, n in enumerate(CONFIG1_IDS)},
+                                  "start": [0, 1, 2, 3]}, 6))
+    cases.append(("join_64", {"cfg": SimConfig(capacity=64, initial_nodes=64)}, 8))
+    cases.append(("config2_join_1k", {"cfg": SimConfig(capacity=1024, initial_nodes=1024)}, 6))
+    cases.append(("converged_loss_256", {"cfg": SimConfig(capacity=256, initial_nodes=256, init_mode=KB_INIT_CONVERGED,
+                                                          loss=0.05, seed=7)}, 30))
+    cases.append(("churn_loss_512", {"cfg": SimConfig(capacity=640, initial_nodes=512, init_mode=KB_INIT_CONVERGED,
+                                                      loss=0.01, churn=0.01, fault_end_round=25, seed=3)}, 40))
+    cases.append(("join_loss_300_ids", {"cfg": SimConfig(capacity=300, initial_nodes=300, loss=0.02, id_len=5,
+                                                         seed=11)}, 20))
+    cases.append(("socket_faithful", {"cfg": SimConfig(capacity=200, initial_nodes=200, init_mode=KB_INIT_CONVERGED,
+                                                       loss=0.05, failed_mode=KB_FAILED_SOCKET_FAITHFUL, seed=5)}, 20))
+    cases.append(("partition_heal", {"cfg": SimConfig(capacity=256, initial_nodes=256, init_mode=KB_INIT_CONVERGED,
+                                                      loss=0.02, partition_groups=2, partition_start=3,
+                                                      partition_end=12, seed=9),
+                                     "events": {12: [("ping", i, [(i + 128) % 256]) for i in range(0, 256, 16)]}}, 30))
+    cases.append(("stop_start", {"cfg": SimConfig(capacity=128, initial_nodes=100, init_mode=KB_INIT_CONVERGED,
+                                                  seed=2),
+                                 "events": {2: [("stop", 5, None), ("stop", 17, None)], 4: [("start", 120, None)],
+                                            9: [("start", 5, None)]}}, 20))
+    cases.append(("rebase_window", {"cfg": SimConfig(capacity=192, initial_nodes=192, init_mode=KB_INIT_CONVERGED,
+                                                     loss=0.01, churn=0.002, seed=4)}, 140))
+    cases.append(("waves_2", {"cfg": SimConfig(capacity=256, initial_nodes=256, loss=0.03, max_waves=2, seed=13)}, 15))
+    return cases
+
+
+def main() -> int:
+    fails = 0
+    only = sys.argv[1:]
+    for name, case, rounds in standard_cases():
+        if only and name not in only:
+            continue
+        ok, msg, st = run_case(case, rounds)
+        print(f"{'PASS' if ok else 'FAIL'} {name:24s} rounds={rounds:4d} {msg} "
+              f"(agree {st['agree']}/{st['alive']}, sent ping {st['sent_ping']} kpr {st['sent_kpr']} "
+              f"kp {st['sent_known_peers']} removed {st['removed_timeout']}+{st['removed_failed']})", flush=True)
+        fails += not ok
+    return 1 if fails else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

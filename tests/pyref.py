@@ -1,0 +1,409 @@
+"""pyref.py — a second, independent restatement of "round semantics v1" (TEST INFRASTRUCTURE ONLY).
+
+Written the way the reference is written, not the way the oracle or the GPU are: every peer owns a
+`known_peers` dict {addr-id: (state, instant)} like `ObservableHashMap<Peer, PeerInfo>`
+(src/structs.rs:12-41), the fingerprint is the literal CRC-32 of the sorted address strings and
+identities computed by zlib (src/kaboodle.rs:71-83), and instants are exact round numbers.  The dense
+stamp-byte window of DESIGN.md §2.2 appears only where the semantics define it (the ordering key of
+ping_random_peer).  Pure-Python loops: for small meshes only.
+
+It pins the C oracle (tests/test_pyref_pin.py) and generates the committed round-trace fixtures
+(tests/golden/make_golden.py).
+"""
+from __future__ import annotations
+
+import zlib
+
+MASK = 0xFFFFFFFF
+PING_TIMEOUT, SHARE_AGE, REBROADCAST, NUM_INDIRECT, NUM_CANDIDATES, BUFSZ = 2, 10, 10, 3, 5, 10240
+CSLOTS, NOBS, PAQ = 8, 4, 8
+P_PING, P_INDIRECT, P_RESPOND, P_TRUNC, P_LOSS, P_BLOSS, P_CHURN = 1, 2, 3, 4, 5, 6, 7
+KNOWN, WFP, WFIP = "Known", "WaitingForPing", "WaitingForIndirectPing"
+
+
+def philox(c0, c1, c2, c3, k0, k1):
+    for r in range(10):
+        if r:
+            k0 = (k0 + 0x9E3779B9) & MASK
+            k1 = (k1 + 0xBB67AE85) & MASK
+        p0 = 0xD2511F53 * c0
+        p1 = 0xCD9E8D57 * c2
+        c0, c1, c2, c3 = ((p1 >> 32) ^ c1 ^ k0) & MASK, p1 & MASK, ((p0 >> 32) ^ c3 ^ k1) & MASK, p0 & MASK
+    return c0, c1, c2, c3
+
+
+def mulhi(u, k):
+    return (u * k) >> 32
+
+
+def addr(i: int) -> str:
+    return f"10.100.100.{100 + i // 50000}:{10000 + i % 50000}"
+
+
+def default_identity(i: int, n: int) -> bytes:
+    return bytes(ord("a") + ((i * 31 + k * 7) % 26) for k in range(n))
+
+
+def fingerprint(ids, identity) -> int:
+    """generate_fingerprint (src/kaboodle.rs:71-83), literally."""
+    h = 0
+    for p in sorted(ids):
+        h = zlib.crc32(addr(p).encode(), h)
+        h = zlib.crc32(identity[p], h)
+    return h
+
+
+def epoch_base(r):
+    return (r // 64) * 64
+
+
+def stamp_key(t, r):
+    """the declared stamp window: instants older than the window compare equal ("ancient")"""
+    return max(2, min(255, t - epoch_base(r) + 192))
+
+
+class Peer:
+    def __init__(self, i):
+        self.id = i
+        self.running = False
+        self.ever = False
+        self.start_round = None
+        self.known = {}          # peer -> [state, instant]
+        self.curious = {}        # peer -> [observers]
+        self.last_bcast = None
+        self.paq = []
+
+
+class PyMesh:
+    def __init__(self, capacity, initial_nodes, converged=False, seed=1, loss=0.0, churn=0.0, fault_end=-1,
+                 max_waves=8, failed_honoured=True, id_len=0, partition=None):
+        self.C = capacity
+        self.k0, self.k1 = seed & MASK, (seed >> 32) & MASK
+        self.loss_thr = min(int(round(loss * 2 ** 32)), MASK)
+        self.churn_thr = min(int(round(churn * 2 ** 32)), MASK)
+        self.fault_end, self.max_waves, self.failed_honoured = fault_end, max_waves, failed_honoured
+        self.partition = partition      # (groups, start, end) or None
+        self.id_len = id_len
+        self.identity = [default_identity(i, id_len) for i in range(capacity)]
+        self.peers = [Peer(i) for i in range(capacity)]
+        self.round = 0
+        self.next_free = initial_nodes
+        self.events = []
+        self.bfail, self.bjoin = [], []
+        self.stats = dict(sent_ping=0, sent_ping_req=0, sent_ack=0, sent_known_peers=0, sent_kpr=0, bcast_join=0,
+                          bcast_failed=0, drop_dead=0, drop_loss=0, drop_window=0, drop_oversize=0, drop_partition=0,
+                          drop_bcast=0, removed_timeout=0, removed_failed=0, join_responses=0, curious_overflow=0,
+                          churn_leaves=0, churn_joins=0)
+        self.agree = 0
+        self.first_converged = -1
+        for i in range(initial_nodes):
+            self._start(i, 0)
+            if converged:
+                p = self.peers[i]
+                for j in range(initial_nodes):
+                    if j != i:
+                        p.known[j] = [KNOWN, -(10 ** 6)]    # an instant long before the stamp window
+                p.last_bcast = -1000
+
+    # ---------------------------------------------------------------- helpers
+    def ph(self, *c):
+        return philox(*c, self.k0, self.k1)
+
+    def faults(self, r):
+        return self.fault_end < 0 or r < self.fault_end
+
+    def blocked(self, r, a, b):
+        if not self.partition:
+            return False
+        g, s, e = self.partition
+        if g <= 1 or not (s <= r < e):
+            return False
+        return a * g // self.C != b * g // self.C
+
+    def _start(self, i, r):
+        p = self.peers[i]
+        p.running, p.ever, p.start_round = True, True, r
+        p.known[i] = [KNOWN, r]
+        p.last_bcast = None
+        p.curious = {}
+        p.paq = []
+
+    def _stop(self, i):
+        p = self.peers[i]
+        p.known.pop(i, None)
+        p.running = False
+        p.paq = []
+
+    def set_identity(self, i, ident: bytes):
+        self.identity[i] = ident
+
+    def start_node(self, i):
+        self.events.append(("start", i))
+
+    def stop_node(self, i):
+        self.events.append(("stop", i))
+
+    def ping_addrs(self, i, addrs):
+        p = self.peers[i]
+        for a in addrs:
+            if a not in p.known:
+                p.paq.append(a)
+
+    def kp_size(self, sender, ids):
+        return 8 + len(self.identity[sender]) + 4 + 8 + sum(10 + 8 + len(self.identity[j]) for j in ids)
+
+    # ---------------------------------------------------------------- round
+    def step(self):
+        r = self.round
+        self.out = {}
+        for kind, i in self.events:
+            if kind == "stop" and self.peers[i].running:
+                self._stop(i)
+            elif kind == "start" and not self.peers[i].running:
+                self._start(i, r)
+        self.events = []
+        if self.faults(r) and self.churn_thr:
+            leaves = [i for i in range(self.C) if self.peers[i].running and self.peers[i].start_round != r
+                      and self.ph(i, r, P_CHURN << 24, 0)[0] < self.churn_thr]
+            for i in leaves:
+                self._stop(i)
+            self.stats["churn_leaves"] += len(leaves)
+            for _ in leaves:
+                if self.next_free < self.C:
+                    self._start(self.next_free, r)
+                    self.next_free += 1
+                    self.stats["churn_joins"] += 1
+        for i in range(self.C):
+            p = self.peers[i]
+            if p.running and p.start_round < r:
+                self.broadcasts(p, r)
+        live = [i for i in range(self.C) if self.peers[i].running]
+        true_fp = fingerprint(live, self.identity)
+        bjoin, bfail = [], []
+        agree = 0
+        for i in live:
+            j, f = self.tick(self.peers[i], r)
+            bseq = 0
+            if j:
+                bjoin.append((i, i, bseq))
+                bseq += 1
+            for q in f:
+                bfail.append((i, q, bseq))
+                bseq += 1
+            agree += fingerprint(self.peers[i].known, self.identity) == true_fp
+        self.bjoin, self.bfail = bjoin, bfail
+        self.stats["bcast_join"] += len(bjoin)
+        self.stats["bcast_failed"] += len(bfail)
+        self.waves(r)
+        self.agree = agree
+        if live and agree == len(live) and self.first_converged < 0:
+            self.first_converged = r
+        self.round += 1
+
+    def emit(self, sender, dest, kind, **kw):
+        box = self.out.setdefault(sender, [])
+        box.append(dict(dest=dest, sender=sender, seq=len(box), kind=kind, **kw))
+
+    # handle_incoming_broadcasts (src/kaboodle.rs:256-311)
+    def broadcasts(self, p, r):
+        for (s, peer, bseq) in self.bfail:
+            if s == p.id:
+                continue
+            if self.lost_b(p.id, s, bseq, r):
+                continue
+            if peer == p.id:
+                continue
+            if self.failed_honoured and s in p.known and peer in p.known:
+                del p.known[peer]
+                self.stats["removed_failed"] += 1
+        for (a, _, bseq) in self.bjoin:
+            if a == p.id or self.lost_b(p.id, a, bseq, r):
+                continue
+            is_new = a not in p.known
+            p.known[a] = [KNOWN, r]
+            if is_new and self.should_respond(p, a, r):
+                self.send_known_peers_to(p, a, r)
+
+    def lost_b(self, recv, sender, bseq, r):
+        if self.blocked(r, sender, recv):
+            self.stats["drop_bcast"] += 1
+            return True
+        if self.faults(r) and self.loss_thr and self.ph(recv, r, (P_BLOSS << 24) | bseq, sender)[0] < self.loss_thr:
+            self.stats["drop_bcast"] += 1
+            return True
+        return False
+
+    def should_respond(self, p, joiner, r):              # src/kaboodle.rs:333-354
+        o = len(p.known) - 2
+        if o <= 0:
+            return True
+        pct = max(1, 100 - o * o)
+        return mulhi(self.ph(p.id, r, P_RESPOND << 24, joiner)[0], 100) < pct
+
+    def send_known_peers_to(self, p, joiner, r):         # src/kaboodle.rs:356-392
+        members = sorted(p.known)
+        L = self.id_len
+        cap = (BUFSZ - 20 - L - 1) // (18 + L)
+        if len(members) > cap:
+            n = len(members)
+            chosen = set()
+            for t in range(cap):
+                j = n - cap + t
+                v = mulhi(self.ph(p.id, r, (P_TRUNC << 24) | (t >> 2), joiner)[t & 3], j + 1)
+                chosen.add(j if v in chosen else v)
+            members = [members[k] for k in sorted(chosen)]
+        self.emit(p.id, joiner, "KnownPeers", peers=members)
+        self.stats["join_responses"] += 1
+
+    # tick (src/kaboodle.rs:746-779)
+    def tick(self, p, r):
+        join = False
+        if p.last_bcast is None or (r - p.last_bcast >= REBROADCAST and len(p.known) <= 1):   # :228-251
+            join = True
+            p.last_bcast = r
+        # handle_suspected_peers :558-653
+        cands = sorted(q for q, (st, _) in p.known.items() if st == KNOWN and q != p.id)
+        removed, indirect = [], []
+        for q in sorted(p.known):
+            st, t = p.known[q]
+            if st == KNOWN or r - t < PING_TIMEOUT:
+                continue
+            if st == WFP:
+                m = len(cands)
+                k = min(NUM_INDIRECT, m)
+                if k == 0:
+                    removed.append(q)
+                    continue
+                x, y, z, _ = self.ph(p.id, r, P_INDIRECT << 24, q)
+                picks = [mulhi(x, m)]
+                if k > 1:
+                    b = mulhi(y, m - 1)
+                    picks.append(b + (b >= picks[0]))
+                if k > 2:
+                    lo, hi = sorted(picks)
+                    c = mulhi(z, m - 2)
+                    c += c >= lo
+                    c += c >= hi
+                    picks.append(c)
+                for pk in picks:
+                    self.emit(p.id, cands[pk], "PingRequest", peer=q)
+                indirect.append(q)
+            else:
+                removed.append(q)
+        for q in indirect:
+            p.known[q] = [WFIP, r]
+        fails = []
+        for q in removed:
+            del p.known[q]
+            p.curious.pop(q, None)
+            fails.append(q)
+            self.stats["removed_timeout"] += 1
+        # ping_random_peer :655-703
+        c = [q for q, (st, _) in p.known.items() if st == KNOWN and q != p.id]
+        c.sort(key=lambda q: (stamp_key(p.known[q][1], r), (q - p.id - 1) % self.C))
+        c = c[:NUM_CANDIDATES]
+        if c:
+            t = c[mulhi(self.ph(p.id, r, P_PING << 24, 0)[0], len(c))]
+            p.known[t] = [WFP, r]
+            self.emit(p.id, t, "Ping")
+        for a in p.paq:                                   # :550-556
+            self.emit(p.id, a, "Ping")
+        p.paq = []
+        return join, fails
+
+    def count_sent(self, msgs):
+        key = {"Ping": "sent_ping", "PingRequest": "sent_ping_req", "Ack": "sent_ack", "KnownPeers": "sent_known_peers",
+               "KnownPeersRequest": "sent_kpr"}
+        for m in msgs:
+            self.stats[key[m["kind"]]] += 1
+
+    def waves(self, r):
+        for w in range(self.max_waves):
+            msgs = [m for s in sorted(self.out) for m in self.out[s]]
+            self.out = {}
+            if not msgs:
+                return
+            self.count_sent(msgs)
+            inbox = {}
+            for m in msgs:
+                d = m["dest"]
+                if not self.peers[d].running:
+                    self.stats["drop_dead"] += 1
+                    continue
+                if self.blocked(r, m["sender"], d):
+                    self.stats["drop_partition"] += 1
+                    continue
+                if self.faults(r) and self.loss_thr and \
+                        self.ph(m["sender"], r, (P_LOSS << 24) | w, m["seq"])[0] < self.loss_thr:
+                    self.stats["drop_loss"] += 1
+                    continue
+                inbox.setdefault(d, []).append(m)
+            for d in sorted(inbox):
+                box = inbox[d]
+                for m in [m for m in box if m["kind"] == "KnownPeers"] + [m for m in box if m["kind"] != "KnownPeers"]:
+                    self.handle(self.peers[d], m, r)
+        left = [m for s in sorted(self.out) for m in self.out[s]]
+        self.count_sent(left)
+        self.stats["drop_window"] += len(left)
+        self.out = {}
+
+    # handle_incoming_messages (src/kaboodle.rs:394-548)
+    def handle(self, p, m, r):
+        s = m["sender"]
+        p.known[s] = [KNOWN, r]                                   # :406-415
+        kind = m["kind"]
+        if kind == "Ack":                                         # :418-447
+            peer = m["peer"]
+            obs = p.curious.pop(peer, None)
+            if obs:
+                for o in obs:
+                    self.emit(p.id, o, "Ack", peer=peer, fp=m["fp"], n=m["n"])
+            self.maybe_sync(p, peer, m["fp"], m["n"])
+        elif kind == "KnownPeers":                                # :448-472
+            for q in m["peers"]:
+                if q not in p.known:
+                    p.known[q] = [KNOWN, r - SHARE_AGE]
+        elif kind == "KnownPeersRequest":                         # :473-512
+            lst = sorted(q for q, (st, t) in p.known.items()
+                         if st == KNOWN and q != p.id and q != s and r - t < SHARE_AGE)
+            if self.kp_size(p.id, lst) > BUFSZ:
+                self.stats["drop_oversize"] += 1
+            else:
+                self.emit(p.id, s, "KnownPeers", peers=lst)
+            self.maybe_sync(p, s, m["fp"], m["n"])
+        elif kind == "Ping":                                      # :513-532
+            self.emit(p.id, s, "Ack", peer=p.id, fp=fingerprint(p.known, self.identity), n=len(p.known))
+        elif kind == "PingRequest":                               # :533-545
+            peer = m["peer"]
+            if peer in p.curious:
+                obs = p.curious[peer]
+                if s not in obs:
+                    if len(obs) == NOBS:
+                        self.stats["curious_overflow"] += 1
+                    else:
+                        obs.append(s)
+            elif len(p.curious) == CSLOTS:
+                self.stats["curious_overflow"] += 1
+            else:
+                p.curious[peer] = [s]
+            self.emit(p.id, peer, "Ping")
+
+    def maybe_sync(self, p, peer, their_fp, their_n):           # :707-740
+        f = fingerprint(p.known, self.identity)
+        if f == their_fp or len(p.known) > their_n:
+            return
+        self.emit(p.id, peer, "KnownPeersRequest", fp=f, n=len(p.known))
+
+    # ---------------------------------------------------------------- views
+    def row(self, i):
+        """the dense stamp-byte view of peer i's map, for comparison with the oracle"""
+        out = [0] * self.C
+        for q, (st, t) in self.peers[i].known.items():
+            out[q] = 1 if st != KNOWN else stamp_key(t, max(self.round - 1, 0))
+        return out
+
+    def suspects(self, i):
+        return sorted((q, 1 if st == WFP else 2, t) for q, (st, t) in self.peers[i].known.items() if st != KNOWN)
+
+    def curious_view(self, i):
+        return sorted((q, len(o), *(list(o) + [-1] * (NOBS - len(o)))) for q, o in self.peers[i].curious.items())

@@ -1,0 +1,17 @@
+"""Quick timing of the HIP simulator on a config (dev tool)."""
+import os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from kaboodle_amd._ffi import SimConfig, KB_INIT_CONVERGED
+import kaboodle_amd
+N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
+R = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+cfg = SimConfig(capacity=N + N // 4, initial_nodes=N, init_mode=KB_INIT_CONVERGED, loss=0.01, churn=0.001, seed=1)
+t = time.time(); m = kaboodle_amd.Mesh(cfg); print("create", round(time.time() - t, 2), flush=True)
+m.step(2)
+m.reset_kernel_time()
+t = time.time(); m.step(R); dt = time.time() - t
+sw, n = m.kernel_time(0); rd, _ = m.kernel_time(1)
+st = m.stats()
+print(f"N={N} R={R} wall {dt/R*1e3:.2f} ms/round  sweep {sw/n:.3f} ms  round(ev) {rd/n:.3f} ms  "
+      f"node-rounds/s {st['alive']*R/dt:.3e}  sweep GB/s {m.sweep_bytes()/ (sw*1e-3)/1e9:.1f}", flush=True)
+print(st)
