@@ -66,7 +66,8 @@ struct Dev {
   uint32_t* seglen;
   uint32_t* zpow;               // Z^k, Z = x^(8L), k in [0, C+1]
   uint32_t* ztab;               // [17][8][16] nibble tables of multiplication by Z^c
-  Tmpl* tmpl;                   // [W/16]
+  Tmpl* tmpl;                   // [W/16] running-set block raws (true fingerprint)
+  uint32_t* htab;               // [(W/8) * 256] crc0 fold of every member pattern of every 8-id half block
   unsigned long long* stats;
   uint32_t* ctr;
   uint32_t* truefp;
@@ -87,9 +88,27 @@ __device__ inline uint32_t mulzc(const uint32_t* tab, uint32_t x, uint32_t c) {
   return t[x & 15] ^ t[16 + ((x >> 4) & 15)] ^ t[32 + ((x >> 8) & 15)] ^ t[48 + ((x >> 12) & 15)] ^
          t[64 + ((x >> 16) & 15)] ^ t[80 + ((x >> 20) & 15)] ^ t[96 + ((x >> 24) & 15)] ^ t[112 + (x >> 28)];
 }
+constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
 __device__ inline void load_ztab(const Dev& d, uint32_t* lds) {
-  for (uint32_t k = threadIdx.x; k < 17 * 128; k += blockDim.x) lds[k] = d.ztab[k];
+  for (uint32_t k = threadIdx.x; k < ZT * 128; k += blockDim.x) lds[k] = d.ztab[k];
   __syncthreads();
+}
+// 4-bit "byte != 0" mask of a little-endian dword (SWAR)
+__device__ inline uint32_t nzmask4(uint32_t x) {
+  const uint32_t y = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+  return ((y >> 7) | (y >> 14) | (y >> 21) | (y >> 28)) & 0xFu;
+}
+__device__ inline uint32_t nzmask16(const uint32_t (&w)[4]) {
+  return nzmask4(w[0]) | (nzmask4(w[1]) << 4) | (nzmask4(w[2]) << 8) | (nzmask4(w[3]) << 12);
+}
+// Fold the members (mask nz, bit t = id blk+t) of one 16-id block into (raw, cnt): per 8-id half one
+// table lookup of that member pattern's crc0 and one multiplication by Z^popcount.  Exact for any mask.
+__device__ inline void fold16(const Dev& d, const uint32_t* ztab, uint32_t blk, uint32_t nz, uint32_t& raw,
+                              uint32_t& cnt) {
+  const uint32_t m0 = nz & 0xFFu, m1 = nz >> 8;
+  const uint32_t* h = d.htab + (size_t)(blk >> 3) * 256;
+  if (m0) { const uint32_t c = __popc(m0); raw = mulzc(ztab, raw, c) ^ h[m0]; cnt += c; }
+  if (m1) { const uint32_t c = __popc(m1); raw = mulzc(ztab, raw, c) ^ h[256 + m1]; cnt += c; }
 }
 // x^(8*len) for arbitrary len (non-uniform identities only; small capacities)
 __device__ inline uint32_t xpow8_dev(uint64_t nbytes) {
@@ -205,10 +224,12 @@ __global__ void k_template(Dev d) {
     uint32_t raw = 0, mask = 0, cnt = 0;
     for (uint32_t t = 0; t < 16; ++t) {
       uint32_t j = b * 16 + t;
-      if (j < d.C && d.alive[j]) {
-        mask |= 1u << t; cnt++;
-        if (d.uniform) raw = multmodp(d.zpow[1], raw) ^ d.cseg[j];
-      }
+      if (j < d.C && d.alive[j]) { mask |= 1u << t; cnt++; }
+    }
+    if (d.uniform) {
+      const uint32_t m0 = mask & 0xFFu, m1 = mask >> 8;
+      if (m0) raw = d.htab[(size_t)(2 * b) * 256 + m0];
+      if (m1) raw = multmodp(d.zpow[__popc(m1)], raw) ^ d.htab[(size_t)(2 * b + 1) * 256 + m1];
     }
     d.tmpl[b].raw = raw;
     d.tmpl[b].mask_cnt = mask | (cnt << 16);
@@ -253,6 +274,8 @@ __global__ void k_truefp(Dev d) {
 // ================================================================================================
 struct PhaseB {
   const BCast* bfail; uint32_t nf;
+  const uint32_t* gid;   // per Failed entry: index of the first entry naming the same peer
+  const uint8_t* dep;    // per Failed entry: its sender is named as failed by an earlier entry
   const BCast* bjoin; uint32_t nj; uint32_t JW;
   unsigned long long* newmask; unsigned long long* respmask;   // [C * JW]
   uint32_t* nresp; uint32_t* paysum; uint32_t* nbase;           // per node
@@ -265,7 +288,24 @@ __device__ inline bool bcast_lost(const Dev& d, uint32_t recv, const BCast& b, i
   return philox(recv, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | b.bseq, b.sender, d.k0, d.k1).x < d.loss_thr;
 }
 
+// Per-list facts about the Failed broadcasts (identical for every receiver).
+__global__ void k_bfail_prep(const BCast* bf, uint32_t nf, uint32_t* gid, uint8_t* dep) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nf) return;
+  const uint32_t p = bf[q].peer, sn = bf[q].sender;
+  uint32_t g = q; uint8_t dp = 0;
+  for (uint32_t k = 0; k < q; ++k) {
+    const uint32_t pk = bf[k].peer;
+    if (pk == p && g == q) g = k;
+    if (pk == sn) dp = 1;
+  }
+  gid[q] = g; dep[q] = dp;
+}
+
+constexpr uint32_t FAIL_BITS = 16384;   // Failed entries deduplicated through an LDS bitmap per wave
+
 __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r) {
+  __shared__ uint32_t s_gbits[4][FAIL_BITS / 32];
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t l = lane();
   if (i >= d.C) return;
@@ -278,31 +318,68 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r) {
   const uint32_t n0 = n;
   uint32_t lost_cnt = 0, removed_cnt = 0;
   // ---- Failed(p) group (src/kaboodle.rs:268-283) ----
-  for (uint32_t c = 0; c < pb.nf; c += 64) {
-    const uint32_t e = c + l;
-    const bool valid = e < pb.nf;
-    BCast b = valid ? pb.bfail[e] : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
-    bool part = false;
-    const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r, part);
-    const uint32_t bs = valid ? rw[b.sender] : 0, bp = valid ? rw[b.peer] : 0;
-    unsigned long long rem = 0;
-    const uint32_t m = pb.nf - c < 64 ? pb.nf - c : 64;
-    for (uint32_t q = 0; q < m; ++q) {
-      const uint32_t s_q = bcast(b.sender, q), p_q = bcast(b.peer, q);
-      if (s_q == i || bcast((uint32_t)lost, q) || p_q == i || d.failed_mode != KB_FAILED_SIM_SENDER) continue;
-      const bool s_gone = (__ballot(b.peer == s_q) & rem) != 0;     // removed earlier in this chunk
-      if (bcast(bs, q) == ST_UNKNOWN || s_gone) continue;           // sender must be a mesh member
-      const bool p_gone = (__ballot(b.peer == p_q) & rem) != 0;
-      if (bcast(bp, q) != ST_UNKNOWN && !p_gone) rem |= 1ull << q;
+  // Entries are independent unless a sender was itself named as failed by an earlier entry (dep):
+  // process chunks in parallel (dedup of repeated peers through gid) until such an entry would act,
+  // then continue with the exact in-order loop.
+  const uint32_t wv = threadIdx.x >> 6;
+  const bool honour = d.failed_mode == KB_FAILED_SIM_SENDER;
+  bool exact = pb.nf > FAIL_BITS;
+  uint32_t c0 = 0;
+  if (!exact && pb.nf) {
+    for (uint32_t w = l; w < (pb.nf + 31) / 32; w += 64) s_gbits[wv][w] = 0;
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t rem_lane = 0;
+    for (uint32_t c = 0; c < pb.nf; c += 64) {
+      const uint32_t e = c + l;
+      const bool valid = e < pb.nf;
+      BCast b = valid ? pb.bfail[e] : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+      bool part = false;
+      const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r, part);
+      const uint32_t bs = valid ? rw[b.sender] : 0, bp = valid ? rw[b.peer] : 0;
+      const bool cond = valid && b.sender != i && !lost && b.peer != i && honour && bs != ST_UNKNOWN &&
+                        bp != ST_UNKNOWN;
+      if (__ballot(cond && pb.dep[e])) { exact = true; c0 = c; break; }
+      lost_cnt += __popcll(__ballot(lost));
+      if (cond) {
+        const uint32_t g = pb.gid[e];
+        const uint32_t old = atomicOr(&s_gbits[wv][g >> 5], 1u << (g & 31));
+        if (!(old & (1u << (g & 31)))) rem_lane++;
+        if (bp == ST_SUSPECT) susp_clear(d, i, b.peer);
+        rw[b.peer] = ST_UNKNOWN;
+      }
     }
-    lost_cnt += __popcll(__ballot(lost));
-    if ((rem >> l) & 1ull) {
-      if (bp == ST_SUSPECT) susp_clear(d, i, b.peer);
-      rw[b.peer] = ST_UNKNOWN;
-    }
-    removed_cnt += __popcll(rem);
-    n -= __popcll(rem);
+    const uint32_t rm = wave_sum(rem_lane);
+    removed_cnt += rm; n -= rm;
     wave_mem_sync();
+  }
+  if (exact) {
+    for (uint32_t c = c0; c < pb.nf; c += 64) {
+      const uint32_t e = c + l;
+      const bool valid = e < pb.nf;
+      BCast b = valid ? pb.bfail[e] : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+      bool part = false;
+      const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r, part);
+      const uint32_t bs = valid ? rw[b.sender] : 0, bp = valid ? rw[b.peer] : 0;
+      unsigned long long rem = 0;
+      const uint32_t m = pb.nf - c < 64 ? pb.nf - c : 64;
+      for (uint32_t q = 0; q < m; ++q) {
+        const uint32_t s_q = bcast(b.sender, q), p_q = bcast(b.peer, q);
+        if (s_q == i || bcast((uint32_t)lost, q) || p_q == i || !honour) continue;
+        const bool s_gone = (__ballot(b.peer == s_q) & rem) != 0;     // removed earlier in this chunk
+        if (bcast(bs, q) == ST_UNKNOWN || s_gone) continue;           // sender must be a mesh member
+        const bool p_gone = (__ballot(b.peer == p_q) & rem) != 0;
+        if (bcast(bp, q) != ST_UNKNOWN && !p_gone) rem |= 1ull << q;
+      }
+      lost_cnt += __popcll(__ballot(lost));
+      if ((rem >> l) & 1ull) {
+        if (bp == ST_SUSPECT) susp_clear(d, i, b.peer);
+        rw[b.peer] = ST_UNKNOWN;
+      }
+      removed_cnt += __popcll(rem);
+      n -= __popcll(rem);
+      wave_mem_sync();
+    }
   }
   const uint32_t nbase = n;
   // ---- Join{addr} group (src/kaboodle.rs:284-304) ----
@@ -355,44 +432,69 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r) {
 }
 
 // ================================================================================================
-// Generic exclusive scan over up to 4 arrays of length n (one workgroup of 1024 threads).
-// If `list` is given, indices j with in[0][j] != 0 are compacted into it (count -> ctr[list_ctr]).
+// Exclusive scan over up to 4 arrays of length n (+ optional compaction of indices j with in[0][j] != 0),
+// two fully parallel passes over 1024-element tiles: per-tile sums, then per-tile offsets + local scan.
 // ================================================================================================
 struct ScanArgs {
   const uint32_t* in[4]; uint32_t* out[4]; int narr; uint32_t n;
-  uint32_t* totals;   // device, narr values
+  uint32_t* totals;   // device, narr values (+ list count at totals[4] when list != null)
   uint32_t* list; uint32_t* list_count;
-  const uint32_t* add_const; // optional per-array constant added to each element before scanning (n x c)
-  uint32_t addc[4];
+  uint32_t addc[4];   // constant added to every element of array q before scanning
+  uint32_t* tiles;    // workspace [5 * ntiles]
+  uint32_t ntiles;
 };
-__global__ __launch_bounds__(1024) void k_scan(ScanArgs a) {
-  __shared__ uint32_t part[5][1024];
-  const uint32_t T = blockDim.x, t = threadIdx.x;
-  const uint32_t per = (a.n + T - 1) / T;
-  const uint32_t lo = t * per, hi = lo + per < a.n ? lo + per : a.n;
-  uint32_t sum[5] = {0, 0, 0, 0, 0};
-  for (uint32_t j = lo; j < hi; ++j) {
-    for (int q = 0; q < a.narr; ++q) sum[q] += (a.in[q] ? a.in[q][j] : 0) + a.addc[q];
-    if (a.list) sum[4] += a.in[0][j] != 0;
+__device__ inline uint32_t scan_val(const ScanArgs& a, int q, uint32_t j) {
+  if (q == 4) return a.in[0][j] != 0;
+  return (a.in[q] ? a.in[q][j] : 0) + a.addc[q];
+}
+__global__ __launch_bounds__(1024) void k_scan_tiles(ScanArgs a) {
+  __shared__ uint32_t red[5][16];
+  const uint32_t j = blockIdx.x * 1024 + threadIdx.x;
+  const int nq = a.list ? 5 : a.narr;
+  for (int q = 0; q < 5; ++q) {
+    if (q >= a.narr && !(q == 4 && a.list)) continue;
+    uint32_t v = j < a.n ? scan_val(a, q, j) : 0;
+    v = wave_sum(v);
+    if (lane() == 0) red[q][threadIdx.x >> 6] = v;
   }
-  for (int q = 0; q < 5; ++q) part[q][t] = sum[q];
   __syncthreads();
-  for (uint32_t s = 1; s < T; s <<= 1) {
-    uint32_t v[5];
-    for (int q = 0; q < 5; ++q) v[q] = t >= s ? part[q][t - s] : 0;
-    __syncthreads();
-    for (int q = 0; q < 5; ++q) part[q][t] += v[q];
-    __syncthreads();
+  if (threadIdx.x < 5 && (threadIdx.x < (uint32_t)a.narr || (threadIdx.x == 4 && a.list))) {
+    uint32_t t = 0;
+    for (int w = 0; w < 16; ++w) t += red[threadIdx.x][w];
+    a.tiles[threadIdx.x * a.ntiles + blockIdx.x] = t;
   }
-  uint32_t run[5];
-  for (int q = 0; q < 5; ++q) run[q] = part[q][t] - sum[q];
-  for (uint32_t j = lo; j < hi; ++j) {
-    for (int q = 0; q < a.narr; ++q) { a.out[q][j] = run[q]; run[q] += (a.in[q] ? a.in[q][j] : 0) + a.addc[q]; }
-    if (a.list && a.in[0][j]) a.list[run[4]++] = j;
+  (void)nq;
+}
+__global__ __launch_bounds__(1024) void k_scan_apply(ScanArgs a) {
+  __shared__ uint32_t base[5], red[5][16], wpre[5][16];
+  const uint32_t tile = blockIdx.x, t = threadIdx.x;
+  const uint32_t j = tile * 1024 + t;
+  for (int q = 0; q < 5; ++q) {
+    const bool on = q < a.narr || (q == 4 && a.list);
+    uint32_t s = 0;
+    if (on) for (uint32_t k = t; k < tile; k += 1024) s += a.tiles[q * a.ntiles + k];
+    s = wave_sum(s);
+    if (lane() == 0) red[q][t >> 6] = s;
   }
-  if (t == T - 1) {
-    for (int q = 0; q < a.narr; ++q) a.totals[q] = part[q][t];
-    if (a.list_count) *a.list_count = part[4][t];
+  __syncthreads();
+  if (t < 5) { uint32_t s = 0; for (int w = 0; w < 16; ++w) s += red[t][w]; base[t] = s; }
+  __syncthreads();
+  uint32_t v[5], ex[5];
+  for (int q = 0; q < 5; ++q) {
+    const bool on = q < a.narr || (q == 4 && a.list);
+    v[q] = (on && j < a.n) ? scan_val(a, q, j) : 0;
+    ex[q] = wave_excl(v[q]);
+    const uint32_t tot = wave_sum(v[q]);
+    if (lane() == 0) wpre[q][t >> 6] = tot;
+  }
+  __syncthreads();
+  if (t < 5) { uint32_t run = 0; for (int w = 0; w < 16; ++w) { uint32_t x = wpre[t][w]; wpre[t][w] = run; run += x; } }
+  __syncthreads();
+  for (int q = 0; q < a.narr; ++q) if (j < a.n) a.out[q][j] = base[q] + wpre[q][t >> 6] + ex[q];
+  if (a.list && j < a.n && v[4]) a.list[base[4] + wpre[4][t >> 6] + ex[4]] = j;
+  if (tile == gridDim.x - 1 && t == 1023) {
+    for (int q = 0; q < a.narr; ++q) a.totals[q] = base[q] + wpre[q][15] + ex[q] + v[q];
+    if (a.list) { const uint32_t c = base[4] + wpre[4][15] + ex[4] + v[4]; a.totals[4] = c; if (a.list_count) *a.list_count = c; }
   }
 }
 
@@ -516,6 +618,146 @@ __global__ __launch_bounds__(64) void k_resp_build(Dev d, PhaseB pb, const RespI
       ob.msgs[ob.off[i] + item.q] = m;
     }
     __syncthreads();
+  }
+}
+
+// Join responses, LDS path (rows up to RESP_LDS_W ids): one workgroup per responding node builds the
+// row's membership bitmap once, then for each of its responses (in list order) derives the member set
+// at that moment (joiners inserted later removed), samples with Floyd when it does not fit 10240 B,
+// and writes the sorted ids by rank/select on the bitmap.
+constexpr uint32_t RESP_LDS_W = 131072;
+__device__ inline uint32_t bm_rank(const uint32_t* S, const uint32_t* SP, uint32_t id) {   // members < id
+  const uint32_t blk = id >> 8, w = id >> 5;
+  uint32_t r = SP[blk];
+  for (uint32_t k = blk * 8; k < w; ++k) r += __popc(S[k]);
+  return r + __popc(S[w] & ((1u << (id & 31)) - 1u));
+}
+__device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint32_t nblk, uint32_t b) {  // b-th member
+  uint32_t lo = 0, hi = nblk;           // last block with SP[blk] <= b
+  while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (SP[mid] <= b) lo = mid; else hi = mid; }
+  uint32_t rem = b - SP[lo];
+  uint32_t w = lo * 8;
+  for (;; ++w) { const uint32_t c = __popc(S[w]); if (rem < c) break; rem -= c; }
+  uint32_t x = S[w];
+  for (uint32_t t = 0; t < rem; ++t) x &= x - 1;
+  return w * 32 + (__ffs(x) - 1);
+}
+__global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint32_t* nodes, const uint32_t* nnodes_p,
+                                                   OutBuf ob, int32_t r) {
+  extern __shared__ uint32_t lds[];
+  const uint32_t NW = d.W / 32, NB = d.W / 256;
+  uint32_t* B = lds;                 // row membership        [NW]
+  uint32_t* S = B + NW;              // members at response   [NW]
+  uint32_t* SP = S + NW;             // block prefix of S     [NB + 1]
+  uint32_t* F = SP + NB + 1;         // Floyd rank bitmap     [NW]
+  uint32_t* FP = F + NW;             // prefix of F per thread[256]
+  uint32_t* dr = FP + 256;           // Floyd draws           [1024]
+  __shared__ uint32_t s_red[16];
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  const uint32_t nnodes = *nnodes_p;
+  for (uint32_t it = blockIdx.x; it < nnodes; it += gridDim.x) {
+    const uint32_t i = nodes[it];
+    const uint8_t* rw = row_of(d, i);
+    // 1. membership bitmap of the row (two threads per 32-bit word)
+    for (uint32_t k = t; k < d.W / 16; k += T) {
+      const uint4 v = *reinterpret_cast<const uint4*>(rw + 16 * k);
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      const uint32_t m = nzmask16(w4);
+      const uint32_t o = __shfl_xor(m, 1, 64);
+      if ((k & 1) == 0) B[k >> 1] = m | (o << 16);
+    }
+    __syncthreads();
+    const unsigned long long* nm = pb.newmask + (size_t)i * pb.JW;
+    const unsigned long long* rm = pb.respmask + (size_t)i * pb.JW;
+    uint32_t poff = ob.poff[i], q = 0, ins_before = 0;
+    for (uint32_t wj = 0; wj < pb.JW; ++wj) {
+      unsigned long long rmw = rm[wj];
+      const unsigned long long nmw = nm[wj];
+      while (rmw) {
+        const uint32_t bit = (uint32_t)(__ffsll((long long)rmw) - 1);
+        const uint32_t K = wj * 64 + bit;
+        rmw &= rmw - 1;
+        const uint32_t expect = pb.nbase[i] + ins_before + __popcll(nmw & ((2ull << bit) - 1ull));
+        const uint32_t a = pb.bjoin[K].sender;
+        // 2. S = B minus the joiners inserted after K
+        for (uint32_t k = t; k < NW; k += T) S[k] = B[k];
+        __syncthreads();
+        for (uint32_t e = K + 1 + t; e < pb.nj; e += T)
+          if (newbit(nm, e)) { const uint32_t x = pb.bjoin[e].sender; atomicAnd(&S[x >> 5], ~(1u << (x & 31))); }
+        __syncthreads();
+        // 3. block prefix of S
+        uint32_t bc = 0;
+        const uint32_t per = (NB + T - 1) / T;
+        for (uint32_t k = t * per; k < (t + 1) * per && k < NB; ++k) {
+          uint32_t c = 0;
+          for (uint32_t w = 0; w < 8; ++w) c += __popc(S[k * 8 + w]);
+          SP[k] = c; bc += c;
+        }
+        uint32_t ex = wave_excl(bc);
+        const uint32_t wt = wave_sum(bc);
+        if (lane() == 0) s_red[t >> 6] = wt;
+        __syncthreads();
+        for (uint32_t w = 0; w < (t >> 6); ++w) ex += s_red[w];
+        uint32_t nk = 0;
+        for (uint32_t w = 0; w < T / 64; ++w) nk += s_red[w];
+        for (uint32_t k = t * per; k < (t + 1) * per && k < NB; ++k) { const uint32_t c = SP[k]; SP[k] = ex; ex += c; }
+        if (t == 0) SP[NB] = nk;
+        __syncthreads();
+        const bool sample = d.uniform && nk > d.capj;
+        const uint32_t cap = sample ? d.capj : nk;
+        uint32_t* pay = ob.pay + poff;
+        if (!sample) {
+          // 4a. every member, in id order: position = rank
+          for (uint32_t w = t; w < NW; w += T) {
+            uint32_t x = S[w];
+            if (!x) continue;
+            uint32_t pos = bm_rank(S, SP, w * 32);
+            while (x) { const uint32_t b = __ffs(x) - 1; x &= x - 1; pay[pos++] = w * 32 + b; }
+          }
+        } else {
+          // 4b. Floyd: uniform cap-subset of ranks [0, nk)
+          const uint32_t FW = (nk + 31) / 32;
+          for (uint32_t w = t; w < FW; w += T) F[w] = 0;
+          for (uint32_t t4 = t; t4 < (cap + 3) / 4; t4 += T) {
+            const U4 u = philox(i, (uint32_t)r, ((uint32_t)P_TRUNC << 24) | t4, a, d.k0, d.k1);
+            dr[4 * t4] = u.x; dr[4 * t4 + 1] = u.y; dr[4 * t4 + 2] = u.z; dr[4 * t4 + 3] = u.w;
+          }
+          __syncthreads();
+          if (t == 0) {
+            for (uint32_t k = 0; k < cap; ++k) {
+              const uint32_t j = nk - cap + k;
+              const uint32_t v = mulhi(dr[k], j + 1);
+              const uint32_t x = (F[v >> 5] >> (v & 31)) & 1u ? j : v;
+              F[x >> 5] |= 1u << (x & 31);
+            }
+          }
+          __syncthreads();
+          // selected ranks in increasing order -> output slots
+          const uint32_t fper = (FW + T - 1) / T;
+          uint32_t fc = 0;
+          for (uint32_t w = t * fper; w < (t + 1) * fper && w < FW; ++w) fc += __popc(F[w]);
+          uint32_t fex = wave_excl(fc);
+          const uint32_t fwt = wave_sum(fc);
+          __syncthreads();
+          if (lane() == 0) s_red[t >> 6] = fwt;
+          __syncthreads();
+          for (uint32_t w = 0; w < (t >> 6); ++w) fex += s_red[w];
+          uint32_t o = fex;
+          for (uint32_t w = t * fper; w < (t + 1) * fper && w < FW; ++w) {
+            uint32_t x = F[w];
+            while (x) { const uint32_t b = __ffs(x) - 1; x &= x - 1; pay[o++] = bm_select(S, SP, NB, w * 32 + b); }
+          }
+        }
+        if (t == 0) {
+          Msg m; m.dest = a; m.sender = i; m.seq = q; m.kind = K_KP; m.a = cap; m.fp = 0; m.n = 0; m.off = poff;
+          ob.msgs[ob.off[i] + q] = m;
+          if (nk != expect) set_err(d, DERR_RESP);
+        }
+        poff += cap; q++;
+        __syncthreads();
+      }
+      ins_before += __popcll(nmw);
+    }
   }
 }
 
@@ -676,25 +918,7 @@ __device__ inline void sweep_piece(const Dev& d, const uint8_t* rw, const uint32
     uint32_t valid = 0xFFFFu;
     if (blk < x) valid &= 0xFFFFu << (x - blk);
     if (blk + 16 > y) valid &= 0xFFFFu >> (blk + 16 - y);
-    if (FOLD) {
-      uint32_t nz = 0;
-#pragma unroll
-      for (int t = 0; t < 16; ++t) nz |= (((w4[t >> 2] >> (8 * (t & 3))) & 0xFFu) != 0) << t;
-      nz &= valid;
-      const Tmpl tp = d.tmpl[blk >> 4];
-      if (valid == 0xFFFFu && nz == (tp.mask_cnt & 0xFFFFu)) {
-        const uint32_t c = tp.mask_cnt >> 16;
-        raw = mulzc(ztab, raw, c) ^ tp.raw;
-        cnt += c;
-      } else {
-        while (nz) {
-          const int t = __ffs(nz) - 1;
-          nz &= nz - 1;
-          raw = mulzc(ztab, raw, 1) ^ d.cseg[blk + t];
-          cnt++;
-        }
-      }
-    }
+    if (FOLD) fold16(d, ztab, blk, nzmask16(w4) & valid, raw, cnt);
     if (T5 > ST_ANCIENT) {
 #pragma unroll
       for (int t = 0; t < 16; ++t) {
@@ -710,7 +934,7 @@ __device__ inline void sweep_piece(const Dev& d, const uint8_t* rw, const uint32
 }
 
 __global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
-  __shared__ uint32_t ztab[17 * 128];
+  __shared__ uint32_t ztab[ZT * 128];
   load_ztab(d, ztab);
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const uint32_t l = lane();
@@ -977,18 +1201,8 @@ __device__ uint32_t wave_fold(const Dev& d, const uint8_t* rw, const uint32_t* z
   for (uint32_t blk = lo; blk < hi; blk += 16) {
     const uint4 v = *reinterpret_cast<const uint4*>(rw + blk);
     const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-    uint32_t valid = blk + 16 > hi ? (0xFFFFu >> (blk + 16 - hi)) : 0xFFFFu;
-    uint32_t nz = 0;
-#pragma unroll
-    for (int t = 0; t < 16; ++t) nz |= (((w4[t >> 2] >> (8 * (t & 3))) & 0xFFu) != 0) << t;
-    nz &= valid;
-    const Tmpl tp = d.tmpl[blk >> 4];
-    if (valid == 0xFFFFu && nz == (tp.mask_cnt & 0xFFFFu)) {
-      const uint32_t c = tp.mask_cnt >> 16;
-      raw = mulzc(ztab, raw, c) ^ tp.raw; cnt += c;
-    } else {
-      while (nz) { const int t = __ffs(nz) - 1; nz &= nz - 1; raw = mulzc(ztab, raw, 1) ^ d.cseg[blk + t]; cnt++; }
-    }
+    const uint32_t valid = blk + 16 > hi ? (0xFFFFu >> (blk + 16 - hi)) : 0xFFFFu;
+    fold16(d, ztab, blk, nzmask16(w4) & valid, raw, cnt);
   }
 #pragma unroll
   for (int s = 1; s < 64; s <<= 1) {
@@ -1005,7 +1219,7 @@ struct NodeCtx {
 };
 
 __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r) {
-  __shared__ uint32_t ztab[17 * 128];
+  __shared__ uint32_t ztab[ZT * 128];
   __shared__ Susp s_susp[4][SLOTS];
   __shared__ Cur s_cur[4][CSLOTS];
   load_ztab(d, ztab);
@@ -1177,9 +1391,23 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
 // ================================================================================================
 // Host side
 // ================================================================================================
-__global__ void k_set_cap(uint32_t C, const uint32_t* nresp, uint32_t* cap) {
+// crc0 fold of every member pattern of every 8-id half block (uniform identity length)
+__global__ void k_build_htab(Dev d) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)(d.W / 8) * 256;
+  if (k >= total) return;
+  const uint32_t h = (uint32_t)(k >> 8), m = (uint32_t)(k & 255);
+  uint32_t raw = 0;
+  for (uint32_t t = 0; t < 8; ++t) {
+    const uint32_t j = h * 8 + t;
+    if (((m >> t) & 1u) && j < d.C) raw = multmodp(d.zpow[1], raw) ^ d.cseg[j];
+  }
+  d.htab[k] = raw;
+}
+
+__global__ void k_set_cap(uint32_t C, const uint32_t* nresp, uint32_t* cap, uint32_t* cnt) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < C) cap[i] = nresp[i] + TICK_MAX;
+  if (i < C) { cap[i] = nresp[i] + TICK_MAX; cnt[i] = nresp[i]; }
 }
 
 static thread_local std::string g_err;
@@ -1228,10 +1456,12 @@ struct kb_sim {
   BcastSlots bs;
   uint32_t* join_off; uint32_t* fail_off;
   uint32_t* scan_tot;
+  uint32_t* scan_tiles;
   // phase B
   unsigned long long* newmask; unsigned long long* respmask; size_t mask_words;
   uint32_t* nresp; uint32_t* paysum; uint32_t* nbase; uint32_t* resp_off;
   RespItem* items; uint32_t items_cap;
+  uint32_t* resp_nodes; uint32_t* bf_gid; uint8_t* bf_dep;
   // sweep
   SweepOut so;
   Event* d_events; uint32_t events_cap;
@@ -1289,6 +1519,9 @@ static int upload_segments(kb_sim* s) {
   HIPCHK(hipMemcpy(s->d.seglen, seglen.data(), 4ull * C, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(s->d.zpow, zpow.data(), 4ull * (C + 2), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(s->d.ztab, ztab.data(), 4ull * ztab.size(), hipMemcpyHostToDevice));
+  const size_t hn = (size_t)(s->W / 8) * 256;
+  k_build_htab<<<(unsigned)((hn + 255) / 256), 256>>>(s->d);
+  HIPCHK(hipDeviceSynchronize());
   return KB_OK;
 }
 
@@ -1372,7 +1605,7 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
   A(d.stamp, (size_t)C * W); A(d.alive, C); A(d.start_round, C); A(d.n, C); A(d.fp, C); A(d.dirty, C);
   A(d.last_bcast, C); A(d.susp, (size_t)C * SLOTS); A(d.cur, (size_t)C * CSLOTS); A(d.paq, (size_t)C * PAQ);
   A(d.paq_n, C); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.ztab, 17 * 128);
-  A(d.tmpl, W / 16); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1);
+  A(d.tmpl, W / 16); A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1);
   s->msg_cap = std::max<uint32_t>(8u * C + (uint32_t)TICK_MAX * C, 1u << 16);
   s->pay_cap = std::max<uint32_t>((d.capk + 1) * C, 1u << 24);
   for (int b = 0; b < 2; ++b) {
@@ -1384,8 +1617,9 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
   A(s->wc.touched, C); A(s->wc.touched_list, C);
   A(s->bfail, (size_t)C * SLOTS); A(s->bjoin, C);
   A(s->bs.join, C); A(s->bs.nfail, C); A(s->bs.fail, (size_t)C * SLOTS); A(s->join_off, C); A(s->fail_off, C);
-  A(s->scan_tot, 8);
+  A(s->scan_tot, 16); A(s->scan_tiles, 5 * ((C + 1023) / 1024) + 5);
   A(s->nresp, C); A(s->paysum, C); A(s->nbase, C); A(s->resp_off, C);
+  A(s->resp_nodes, C); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS);
   A(s->so.cand, (size_t)C * 5); A(s->so.ncand, C);
 #undef A
   if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); free_all(s); delete s; return KB_CAPACITY; }
@@ -1418,13 +1652,13 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
 static void free_all(kb_sim* s) {
   Dev& d = s->d;
   void* ptrs[] = {d.stamp, d.alive, d.start_round, d.n, d.fp, d.dirty, d.last_bcast, d.susp, d.cur, d.paq, d.paq_n,
-                  d.cseg, d.segmul, d.seglen, d.zpow, d.ztab, d.tmpl, d.stats, d.ctr, d.truefp,
+                  d.cseg, d.segmul, d.seglen, d.zpow, d.ztab, d.tmpl, d.htab, d.stats, d.ctr, d.truefp,
                   s->ob[0].msgs, s->ob[0].pay, s->ob[0].off, s->ob[0].cap, s->ob[0].cnt, s->ob[0].poff,
                   s->ob[1].msgs, s->ob[1].pay, s->ob[1].off, s->ob[1].cap, s->ob[1].cnt, s->ob[1].poff,
                   s->wc.status, s->wc.cnt1, s->wc.bnd, s->wc.bpay, s->wc.cursor, s->wc.in_off, s->wc.inbox,
                   s->wc.active, s->wc.kp_list, s->wc.touched, s->wc.touched_list, s->bfail, s->bjoin, s->bs.join,
-                  s->bs.nfail, s->bs.fail, s->join_off, s->fail_off, s->scan_tot, s->newmask, s->respmask, s->nresp,
-                  s->paysum, s->nbase, s->resp_off, s->items, s->so.cand, s->so.ncand, s->d_events};
+                  s->bs.nfail, s->bs.fail, s->join_off, s->fail_off, s->scan_tot, s->scan_tiles, s->newmask, s->respmask, s->nresp,
+                  s->paysum, s->nbase, s->resp_off, s->items, s->resp_nodes, s->bf_gid, s->bf_dep, s->so.cand, s->so.ncand, s->d_events};
   for (void* p : ptrs) if (p) hipFree(p);
 }
 
@@ -1439,8 +1673,13 @@ extern "C" int kb_sim_destroy(kb_sim* s) {
   return KB_OK;
 }
 
-static ScanArgs scan_args(uint32_t n, uint32_t* totals) {
-  ScanArgs a; memset(&a, 0, sizeof a); a.n = n; a.totals = totals; return a;
+static ScanArgs scan_args(kb_sim* s, uint32_t n, uint32_t* totals) {
+  ScanArgs a; memset(&a, 0, sizeof a); a.n = n; a.totals = totals;
+  a.tiles = s->scan_tiles; a.ntiles = (n + 1023) / 1024; return a;
+}
+static void launch_scan(const ScanArgs& a, hipStream_t st) {
+  k_scan_tiles<<<a.ntiles, 1024, 0, st>>>(a);
+  k_scan_apply<<<a.ntiles, 1024, 0, st>>>(a);
 }
 
 static int check_err(kb_sim* s) {
@@ -1501,35 +1740,41 @@ static int step_round(kb_sim* s) {
     }
   }
   pb.newmask = s->newmask; pb.respmask = s->respmask;
+  pb.gid = s->bf_gid; pb.dep = s->bf_dep;
   const bool have_b = s->nf + s->nj > 0;
+  if (s->nf) k_bfail_prep<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep);
   if (have_b) k_phaseB<<<gwave, 256, 0, st>>>(d, pb, r);
   else { HIPCHK(hipMemsetAsync(s->nresp, 0, 4ull * C, st)); HIPCHK(hipMemsetAsync(s->paysum, 0, 4ull * C, st)); }
   // wave-0 outbox regions: responses then tick messages
   {
-    ScanArgs a = scan_args(C, s->scan_tot);
+    ScanArgs a = scan_args(s, C, s->scan_tot);
     a.narr = 3;
     a.in[0] = s->nresp; a.out[0] = s->resp_off;
     a.in[1] = s->paysum; a.out[1] = o0.poff;
     a.in[2] = s->nresp; a.out[2] = o0.off; a.addc[2] = TICK_MAX;
-    k_scan<<<1, 1024, 0, st>>>(a);
+    a.list = s->resp_nodes;
+    launch_scan(a, st);
     // cap = nresp + TICK_MAX: computed from consecutive offsets inside k_resp_list's caller below
   }
-  k_set_cap<<<gnode, tb, 0, st>>>(C, s->nresp, o0.cap);
+  k_set_cap<<<gnode, tb, 0, st>>>(C, s->nresp, o0.cap, o0.cnt);
   if (have_b) {
-    uint32_t tot[4];
-    HIPCHK(hipMemcpyAsync(tot, s->scan_tot, 16, hipMemcpyDeviceToHost, st));
+    uint32_t tot[5];
+    HIPCHK(hipMemcpyAsync(tot, s->scan_tot, 20, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    const uint32_t nresp_tot = tot[0], pay_tot = tot[1], msg_tot = tot[2];
+    const uint32_t nresp_tot = tot[0], pay_tot = tot[1], msg_tot = tot[2], resp_nodes = tot[4];
     if (msg_tot > s->msg_cap || pay_tot > s->pay_cap) { seterr("wave-0 outbox exceeds preallocated capacity"); return KB_CAPACITY; }
     if (nresp_tot > s->items_cap) {
       if (s->items) hipFree(s->items);
       s->items_cap = nresp_tot * 2 + 1024;
       HIPCHK(hipMalloc(&s->items, sizeof(RespItem) * s->items_cap));
     }
-    k_resp_list<<<gnode, tb, 0, st>>>(d, pb, s->resp_off, o0.poff, s->items, o0);
-    if (nresp_tot) k_resp_build<<<std::min<uint32_t>(nresp_tot, 8192), 64, 0, st>>>(d, pb, s->items, s->scan_tot, o0, r);
-  } else {
-    HIPCHK(hipMemsetAsync(o0.cnt, 0, 4ull * C, st));
+    if (s->W <= RESP_LDS_W) {
+      const size_t lds = 4ull * (3 * (s->W / 32) + s->W / 256 + 1 + 256 + 1024);
+      if (resp_nodes) k_resp_node<<<std::min<uint32_t>(resp_nodes, 4096), 256, lds, st>>>(d, pb, s->resp_nodes, s->scan_tot + 4, o0, r);
+    } else {
+      k_resp_list<<<gnode, tb, 0, st>>>(d, pb, s->resp_off, o0.poff, s->items, o0);
+      if (nresp_tot) k_resp_build<<<std::min<uint32_t>(nresp_tot, 8192), 64, 0, st>>>(d, pb, s->items, s->scan_tot, o0, r);
+    }
   }
   // 3. tick
   k_tick_pre<<<gwave, 256, 0, st>>>(d, o0, s->bs, r);
@@ -1538,11 +1783,11 @@ static int step_round(kb_sim* s) {
   hipEventRecord(s->ev1, st);
   k_tick_post<<<gnode, tb, 0, st>>>(d, s->so, o0, r);
   {
-    ScanArgs a = scan_args(C, s->scan_tot);
+    ScanArgs a = scan_args(s, C, s->scan_tot);
     a.narr = 2;
     a.in[0] = s->bs.join; a.out[0] = s->join_off;
     a.in[1] = s->bs.nfail; a.out[1] = s->fail_off;
-    k_scan<<<1, 1024, 0, st>>>(a);
+    launch_scan(a, st);
   }
   k_bcast_write<<<gnode, tb, 0, st>>>(d, s->bs, s->join_off, s->fail_off, s->bjoin, s->bfail);
   // 4. waves
@@ -1559,13 +1804,13 @@ static int step_round(kb_sim* s) {
     k_route<<<gnode, tb, 0, st>>>(d, ib, s->wc, r, w, last);
     if (last) break;
     {
-      ScanArgs a = scan_args(C, s->scan_tot + 4);
+      ScanArgs a = scan_args(s, C, s->scan_tot + 8);
       a.narr = 3;
       a.in[0] = s->wc.cnt1; a.out[0] = s->wc.in_off;
       a.in[1] = s->wc.bnd; a.out[1] = nb.off;
       a.in[2] = s->wc.bpay; a.out[2] = nb.poff;
       a.list = s->wc.active; a.list_count = d.ctr + C_ACTIVE;
-      k_scan<<<1, 1024, 0, st>>>(a);
+      launch_scan(a, st);
     }
     HIPCHK(hipMemcpyAsync(nb.cap, s->wc.bnd, 4ull * C, hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemsetAsync(nb.cnt, 0, 4ull * C, st));
@@ -1669,14 +1914,14 @@ extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* iden
 }
 
 __global__ __launch_bounds__(64) void k_fp_one(Dev d, uint32_t i) {
-  __shared__ uint32_t ztab[17 * 128];
+  __shared__ uint32_t ztab[ZT * 128];
   load_ztab(d, ztab);
   if (!d.dirty[i]) return;
   const uint32_t f = wave_fold(d, row_of(d, i), ztab);
   if (lane() == 0) { d.fp[i] = f; d.dirty[i] = 0; }
 }
 __global__ __launch_bounds__(256) void k_fp_all(Dev d) {
-  __shared__ uint32_t ztab[17 * 128];
+  __shared__ uint32_t ztab[ZT * 128];
   load_ztab(d, ztab);
   const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= d.C || !d.dirty[i]) return;
