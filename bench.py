@@ -1,0 +1,202 @@
+"""bench.py — simulated peer-rounds/s of the MI355X SWIM-round simulator (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--nodes 65536] [--loss 0.01] [--churn 0.001]
+
+Workload (BASELINE.json configs[2]): 65,536 simulated Kaboodle peers on one MI355X, started converged,
+1% per-delivery loss and 0.1%/round churn (leaves + joins with fresh ids).  A "step" is one complete
+simulated round (lifecycle, broadcasts, tick A1-A4 for every live peer, and all receive waves) through
+the C ABI `kb_sim_step`; the timed region holds K steps with all state resident in HBM.
+
+value = peer-rounds/s summed over ranks (live peers x rounds / max-over-ranks wall time).
+N > 1: every rank simulates its own independent 64K mesh ("replicas", weak scaling, no collective on
+the data path), each with a distinct seed.
+
+Also reported, on the same JSON line:
+  roofline      the dominant kernel (k_sweep, the per-round row sweep of ping_random_peer + fingerprint):
+                algorithmic bytes per launch / its HIP-event duration on the simulator's stream, against
+                8 TB/s; `traffic` = measured HBM bytes per launch from the rocprofv3 PMC summary
+                committed under profiles/ (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), else null;
+  cpu_baseline  the CPU oracle (oracle/, OpenMP build, same semantics and seeds) on a bounded sample of
+                the same workload, on rank 0 only;
+  convergence   after the timed rounds faults stop (fault_end_round); untimed rounds continue until every
+                live peer's fingerprint equals the fingerprint of the true live set (or a cap).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM [CDNA4]")
+KT_SWEEP, KT_ROUND = 0, 1      # kb_sim_kernel_time kinds
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nodes", type=int, default=65536)
+    ap.add_argument("--loss", type=float, default=0.01)
+    ap.add_argument("--churn", type=float, default=0.001)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--conv-cap", type=int, default=150, help="max untimed quiescent rounds for convergence")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-conv", action="store_true")
+    return ap.parse_args()
+
+
+def pmc_traffic(cfg_key: str):
+    """Latest committed PMC summary for this workload (profiles/*pmc*.json), bytes per k_sweep launch."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == cfg_key and d.get("kernel") == "k_sweep":
+            best = d
+    return None if best is None else int(best["hbm_bytes_per_launch"])
+
+
+def cpu_baseline(cfg, budget_s: float, nodes: int) -> dict:
+    """The OpenMP oracle on a bounded sample of the same workload (rank 0, N=1 only)."""
+    import ctypes as C
+    from kaboodle_amd._ffi import Sim
+    so = os.path.join(ROOT, "oracle", "_build", "libkb_oracle_omp.so")
+    if not os.path.exists(so):
+        import subprocess
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    from kaboodle_amd._ffi import SimLib
+    lib = SimLib(so, "kbo_")
+    lib.lib.kbo_num_threads.restype = C.c_int
+    cores = int(lib.lib.kbo_num_threads())
+    with Sim(lib, cfg) as o:
+        o.step(1)                                # one warmup round (first touch of the dense table)
+        t0 = time.perf_counter()
+        rounds, alive_sum = 0, 0
+        while True:
+            o.step(1)
+            rounds += 1
+            alive_sum += o.stats()["alive"]
+            if time.perf_counter() - t0 >= budget_s or rounds >= 200:
+                break
+        dt = time.perf_counter() - t0
+    return {"value": alive_sum / dt, "unit": "peer-rounds/s", "cores": cores, "kind": "port",
+            "sample": f"{rounds} rounds of the same {nodes}-peer workload after 1 warmup round "
+                      f"(oracle/kb_oracle.c, OpenMP over peers, {dt:.1f} s)"}
+
+
+def main() -> int:
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    import kaboodle_amd
+    from kaboodle_amd._ffi import KB_INIT_CONVERGED, SimConfig
+    kaboodle_amd.require_gpu()
+
+    total = a.warmup + a.steps
+    reserve = max(4096, int(a.nodes * a.churn * (total + 8) * 1.5))
+    capacity = a.nodes + reserve
+    cfg = SimConfig(capacity=capacity, initial_nodes=a.nodes, init_mode=KB_INIT_CONVERGED, loss=a.loss,
+                    churn=a.churn, fault_end_round=total, seed=a.seed + 1000 * rank,
+                    device=local if world > 1 else -1)
+    workload = f"configs[2]: {a.nodes} peers, converged start, {a.loss:.0%} loss, {a.churn:.1%}/round churn"
+    mesh = kaboodle_amd.Mesh(cfg)
+
+    mesh.step(a.warmup)
+    torch.cuda.synchronize()
+    mesh.reset_kernel_time()
+    bytes0 = mesh.sweep_bytes()
+    alive_sum = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        mesh.step(1)                                 # synchronous: returns after the round's kernels
+        alive_sum += mesh.stats()["alive"]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    sweep_ms, sweep_n = mesh.kernel_time(KT_SWEEP)
+    round_ms, _ = mesh.kernel_time(KT_ROUND)
+    sweep_bytes = mesh.sweep_bytes() - bytes0
+    st = mesh.stats()
+
+    if world > 1:
+        t = torch.tensor([dt, float(alive_sum)], dtype=torch.float64, device="cuda")
+        tm = t.clone()
+        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dt, alive_total = float(tm[0]), float(t[1])
+    else:
+        alive_total = float(alive_sum)
+
+    conv = None
+    if not a.no_conv:
+        # quiescent tail: faults ended at round `total`; step untimed until all live peers agree
+        r_conv = st["first_converged_round"] if st["first_converged_round"] >= total else -1
+        extra = 0
+        while r_conv < 0 and extra < a.conv_cap:
+            mesh.step(1)
+            extra += 1
+            s2 = mesh.stats()
+            if s2["agree"] == s2["alive"]:
+                r_conv = s2["round"] - 1
+        s2 = mesh.stats()
+        conv = {"fault_end_round": total, "converged_round": r_conv if r_conv >= 0 else None,
+                "rounds_to_converge": (r_conv - total + 1) if r_conv >= 0 else None,
+                "agree_frac_at_fault_end": round(st["agree"] / max(st["alive"], 1), 4),
+                "agree_frac_final": round(s2["agree"] / max(s2["alive"], 1), 4)}
+
+    out = None
+    if rank == 0:
+        per_launch_bytes = sweep_bytes / max(sweep_n, 1)
+        sweep_avg_ms = sweep_ms / max(sweep_n, 1)
+        achieved = per_launch_bytes / (sweep_avg_ms * 1e-3) / 1e9 if sweep_n else 0.0
+        traffic = pmc_traffic(workload)
+        out = {
+            "metric": "simulated peer-rounds/sec (whole node) + rounds to fingerprint convergence",
+            "value": alive_total / dt, "unit": "peer-rounds/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic (Philox-keyed loss/churn/targets, seed-determined)",
+            "config": {"workload": workload, "peers": a.nodes, "capacity": capacity, "loss": a.loss,
+                       "churn": a.churn, "parallelism": f"replicas{world}" if world > 1 else "single",
+                       "max_waves": cfg.max_waves},
+            "roofline": {"bound": "hbm", "kernel": "k_sweep", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "algorithmic_bytes_per_launch": int(per_launch_bytes),
+                         "avg_launch_ms": round(sweep_avg_ms, 4), "launches": sweep_n},
+            "round_gpu_ms": round(round_ms / max(sweep_n, 1), 4),
+            "convergence": conv,
+        }
+        if world == 1 and not a.no_cpu:
+            ccfg = SimConfig(**{**cfg.__dict__, "device": -1})
+            out["cpu_baseline"] = cpu_baseline(ccfg, a.cpu_seconds, a.nodes)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    mesh.close()
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

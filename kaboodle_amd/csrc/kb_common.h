@@ -1,0 +1,238 @@
+// kb_common.h — device state and shared device helpers of the simulator (included by kb_sim.hip).
+//
+// HBM layout, C = capacity, W = C rounded up to 2048:
+//   stamp  [C][W]  u8   Known(t) stamp byte of (node, peer); meaningful only where the member bit is set
+//   bits   [C][W/32] u32 membership bitset (the authority for "peer in known_peers")
+//   segp   [C][64] {raw, cnt} crc0 of the members of each W/64-id segment (fingerprint checkpoints)
+//   sdirty [C] u64  segments whose checkpoint is stale; dirty[C] u8: cached fingerprint stale
+//   susp   [C][8]   WaitingForPing / WaitingForIndirectPing slots; cur [C][8] curious_peers entries
+#pragma once
+#include "kb_device.h"
+#include "../../include/kaboodle_sim.h"
+
+namespace kb {
+
+enum StatIdx {
+  S_PING, S_PINGREQ, S_ACK, S_KP, S_KPR, S_BJOIN, S_BFAIL, S_DEAD, S_LOSS, S_WINDOW, S_OVERSIZE, S_PART, S_BDROP,
+  S_RMTIMEOUT, S_RMFAILED, S_JRESP, S_CUROVF, S_CLEAVE, S_CJOIN, NSTAT
+};
+enum CtrIdx {
+  C_KP, C_TOUCH, C_ACTIVE, C_AGREE, C_ALIVE, C_LEAVES, C_NEXTFREE, C_ERR, C_FIRSTCONV, C_LASTCONV, C_LASTAGREE,
+  C_LASTALIVE, NCTR
+};
+constexpr int NSEG = 64;          // fingerprint checkpoints per row
+constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
+
+struct Dev {
+  uint32_t C, W, SEGW, NWR;       // capacity, row stride, ids per segment (W/64), bitset words per row (W/32)
+  uint32_t k0, k1;
+  uint32_t loss_thr, churn_thr;
+  int32_t fault_end;
+  uint32_t failed_mode;
+  uint32_t pgroups;
+  int32_t pstart, pend;
+  uint32_t uniform, L;            // uniform segment length (20 + id_len) when uniform != 0
+  uint32_t capk, capj;            // KnownPeers caps: KPR reply (size <= 10240), Join response (size < 10240)
+  uint32_t paybound;              // payload entries reserved per KPR reply
+  uint32_t ablate;                // timing experiments only (env KB_ABLATE): 1 = no fold in sweep, 2 = no A3
+  uint8_t* stamp;
+  uint32_t* bits;
+  uint2* segp;
+  unsigned long long* sdirty;
+  uint8_t* dirty;
+  uint8_t* alive;
+  uint32_t* abits;                // running set bitset [W/32]
+  int32_t* start_round;
+  uint32_t* n;
+  uint32_t* fp;
+  int32_t* last_bcast;
+  Susp* susp;
+  Cur* cur;
+  uint32_t* paq;
+  uint32_t* paq_n;
+  uint32_t* cseg;
+  uint32_t* segmul;
+  uint32_t* seglen;
+  uint32_t* zpow;                 // Z^k, Z = x^(8L), k in [0, C+1]
+  uint32_t* ztab;                 // [17][8][16] nibble tables of multiplication by Z^c
+  uint32_t* htab;                 // [(W/8)][256] crc0 of every member pattern of every 8-id half block
+  unsigned long long* stats;
+  uint32_t* ctr;
+  uint32_t* truefp;
+};
+
+__device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }
+__device__ inline bool faults(const Dev& d, int32_t r) { return d.fault_end < 0 || r < d.fault_end; }
+__device__ inline bool part_blocks(const Dev& d, int32_t r, uint32_t a, uint32_t b) {
+  if (d.pgroups <= 1 || r < d.pstart || r >= d.pend) return false;
+  return ((uint64_t)a * d.pgroups / d.C) != ((uint64_t)b * d.pgroups / d.C);
+}
+__device__ inline uint8_t* row_of(const Dev& d, uint32_t i) { return d.stamp + (size_t)i * d.W; }
+__device__ inline uint32_t* bits_of(const Dev& d, uint32_t i) { return d.bits + (size_t)i * d.NWR; }
+__device__ inline bool is_mem(const Dev& d, uint32_t i, uint32_t j) { return (bits_of(d, i)[j >> 5] >> (j & 31)) & 1u; }
+__device__ inline unsigned long long seg_bit(const Dev& d, uint32_t j) { return 1ull << (j / d.SEGW); }
+// membership changes: bit + stale-checkpoint mark (callers that batch marks pass mark=false)
+__device__ inline bool mem_set(const Dev& d, uint32_t i, uint32_t j) {   // returns true if newly set
+  const uint32_t m = 1u << (j & 31);
+  return !(atomicOr(&bits_of(d, i)[j >> 5], m) & m);
+}
+__device__ inline bool mem_clr(const Dev& d, uint32_t i, uint32_t j) {   // returns true if it was set
+  const uint32_t m = 1u << (j & 31);
+  return (atomicAnd(&bits_of(d, i)[j >> 5], ~m) & m) != 0;
+}
+__device__ inline void mark(const Dev& d, uint32_t i, unsigned long long segs) {
+  if (segs) { atomicOr(&d.sdirty[i], segs); d.dirty[i] = 1; }
+}
+
+// multiplication by Z^c (c in 0..8) through LDS nibble tables (conflict-free: 16 words per table)
+__device__ inline uint32_t mulzc(const uint32_t* tab, uint32_t x, uint32_t c) {
+  if (c == 0) return x;
+  const uint32_t* t = tab + c * 128;
+  return t[x & 15] ^ t[16 + ((x >> 4) & 15)] ^ t[32 + ((x >> 8) & 15)] ^ t[48 + ((x >> 12) & 15)] ^
+         t[64 + ((x >> 16) & 15)] ^ t[80 + ((x >> 20) & 15)] ^ t[96 + ((x >> 24) & 15)] ^ t[112 + (x >> 28)];
+}
+__device__ inline void load_ztab(const Dev& d, uint32_t* lds) {
+  for (uint32_t k = threadIdx.x; k < ZT * 128; k += blockDim.x) lds[k] = d.ztab[k];
+  __syncthreads();
+}
+// x^(8*len) for arbitrary len (non-uniform identities only; small capacities)
+__device__ inline uint32_t xpow8_dev(uint64_t nbytes) {
+  uint32_t res = 0x80000000u, sq = 0x00800000u;
+  while (nbytes) { if (nbytes & 1) res = multmodp(sq, res); sq = multmodp(sq, sq); nbytes >>= 1; }
+  return res;
+}
+// ordered combine of fingerprint partials: (rawA over lower ids) then (rawB, cntB)
+__device__ inline uint32_t comb(const Dev& d, uint32_t rawA, uint32_t rawB, uint32_t cntB) {
+  return multmodp(d.uniform ? d.zpow[cntB] : xpow8_dev(cntB), rawA) ^ rawB;
+}
+__device__ inline uint32_t finish_fp(const Dev& d, uint32_t raw, uint32_t cnt) {
+  return raw ^ multmodp(d.uniform ? d.zpow[cnt] : xpow8_dev(cnt), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+}
+// fold one 8-id half block (member pattern m8, first id h*8) — table lookup + multiply by Z^popc
+__device__ inline void fold_half(const Dev& d, const uint32_t* ztab, uint32_t h, uint32_t m8, uint32_t& raw,
+                                 uint32_t& cnt) {
+  if (!m8) return;
+  const uint32_t c = __popc(m8);
+  raw = mulzc(ztab, raw, c) ^ d.htab[(size_t)h * 256 + m8];
+  cnt += c;
+}
+// checkpoint of segment k of row i from its bitset (any lane, independent).  For non-uniform
+// identities (capacity <= 200) `cnt` carries the byte length instead of the member count.
+__device__ inline uint2 fold_segment(const Dev& d, const uint32_t* ztab, uint32_t i, uint32_t k) {
+  const uint32_t* b = bits_of(d, i);
+  const uint32_t w0 = k * d.SEGW / 32, w1 = w0 + d.SEGW / 32;
+  uint32_t raw = 0, cnt = 0;
+  if (d.uniform) {
+    for (uint32_t w = w0; w < w1; ++w) {
+      const uint32_t x = b[w];
+      if (!x) continue;
+      fold_half(d, ztab, 4 * w, x & 0xFFu, raw, cnt);
+      fold_half(d, ztab, 4 * w + 1, (x >> 8) & 0xFFu, raw, cnt);
+      fold_half(d, ztab, 4 * w + 2, (x >> 16) & 0xFFu, raw, cnt);
+      fold_half(d, ztab, 4 * w + 3, x >> 24, raw, cnt);
+    }
+  } else {
+    for (uint32_t w = w0; w < w1; ++w) {
+      uint32_t x = b[w];
+      while (x) {
+        const uint32_t j = w * 32 + (__ffs(x) - 1);
+        x &= x - 1;
+        raw = multmodp(d.segmul[j], raw) ^ d.cseg[j];
+        cnt += d.seglen[j];
+      }
+    }
+  }
+  return make_uint2(raw, cnt);
+}
+// Global atomics are performed in L2 and do not refresh this CU's L1: after modifying bitset words
+// with atomics, a kernel that reads them back invalidates its L1 first (agent-scope acquire).
+__device__ inline void l1_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); }
+
+// fingerprint of row i by one wave: refold the stale checkpoints (lane k <-> segment k), then an
+// ordered tree combine of the 64 checkpoints.  `extra` = segments changed by the caller and not yet
+// recorded in sdirty.  Returns the same value in every lane.
+__device__ uint32_t wave_fp(const Dev& d, const uint32_t* ztab, uint32_t i, unsigned long long extra) {
+  const uint32_t l = lane();
+  const unsigned long long sd = d.sdirty[i] | extra;
+  uint2 sp;
+  if ((sd >> l) & 1ull) { sp = fold_segment(d, ztab, i, l); d.segp[(size_t)i * NSEG + l] = sp; }
+  else sp = d.segp[(size_t)i * NSEG + l];
+  uint32_t raw = sp.x, cnt = sp.y;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const uint32_t oraw = __shfl_down(raw, s, 64), ocnt = __shfl_down(cnt, s, 64);
+    if ((l & (2 * s - 1)) == 0 && l + s < 64) { raw = comb(d, raw, oraw, ocnt); cnt += ocnt; }
+  }
+  raw = bcast(raw, 0); cnt = bcast(cnt, 0);
+  if (l == 0 && sd) atomicAnd(&d.sdirty[i], ~sd);
+  return finish_fp(d, raw, cnt);
+}
+// fingerprint of row i from its checkpoints by one thread (checkpoints must be fresh)
+__device__ inline uint32_t thread_fp(const Dev& d, uint32_t i) {
+  uint32_t raw = 0, cnt = 0;
+  for (int k = 0; k < NSEG; ++k) {
+    const uint2 sp = d.segp[(size_t)i * NSEG + k];
+    if (sp.y) { raw = comb(d, raw, sp.x, sp.y); cnt += sp.y; }
+  }
+  return finish_fp(d, raw, cnt);
+}
+
+// 4-bit "byte != 0" mask of a little-endian dword (SWAR)
+__device__ inline uint32_t nzmask4(uint32_t x) {
+  const uint32_t y = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+  return ((y >> 7) | (y >> 14) | (y >> 21) | (y >> 28)) & 0xFu;
+}
+
+// ---- node-local state, single thread ----------------------------------------------------------
+__device__ inline void susp_clear(const Dev& d, uint32_t i, uint32_t p) {
+  Susp* s = d.susp + (size_t)i * SLOTS;
+  for (int k = 0; k < SLOTS; ++k) if (s[k].kind && s[k].peer == p) s[k].kind = 0;
+}
+__device__ void node_start(const Dev& d, uint32_t i, int32_t r) {      // src/lib.rs:136-156
+  if (mem_set(d, i, i)) d.n[i] += 1;
+  else susp_clear(d, i, i);
+  row_of(d, i)[i] = enc(r, r);
+  mark(d, i, seg_bit(d, i));
+  d.alive[i] = 1; d.start_round[i] = r; d.last_bcast[i] = NONE_ROUND; d.paq_n[i] = 0;
+  for (int k = 0; k < CSLOTS; ++k) d.cur[(size_t)i * CSLOTS + k].used = 0;
+}
+__device__ void node_stop(const Dev& d, uint32_t i) {                  // src/lib.rs:159-183
+  if (mem_clr(d, i, i)) { susp_clear(d, i, i); d.n[i] -= 1; mark(d, i, seg_bit(d, i)); }
+  d.alive[i] = 0; d.paq_n[i] = 0;
+}
+
+// block-wide sum (blockDim <= 1024), valid in thread 0
+__device__ inline unsigned long long block_sum(unsigned long long v) {
+  __shared__ unsigned long long red[16];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  unsigned long long t = 0;
+  if (threadIdx.x == 0) for (int k = 0; k < (int)((blockDim.x + 63) >> 6); ++k) t += red[k];
+  return t;
+}
+__device__ inline void stat_add(const Dev& d, int idx, unsigned long long v) {
+  const unsigned long long t = block_sum(v);
+  if (threadIdx.x == 0 && t) atomicAdd(&d.stats[idx], t);
+}
+
+// ---- message outboxes --------------------------------------------------------------------------
+struct OutBuf {
+  Msg* msgs; uint32_t* pay; uint32_t* off; uint32_t* cap; uint32_t* cnt; uint32_t* poff;
+  uint32_t msg_cap, pay_cap;
+};
+__device__ inline void emit_msg(const OutBuf& ob, const Dev& d, uint32_t i, uint32_t& oseq, uint32_t dest,
+                                uint32_t kind, uint32_t a, uint32_t fp, uint32_t n, uint32_t off) {
+  if (lane() == 0) {
+    if (oseq >= ob.cap[i] || ob.off[i] + oseq >= ob.msg_cap) set_err(d, DERR_OUTBOX);
+    else {
+      Msg m; m.dest = dest; m.sender = i; m.seq = oseq; m.kind = kind; m.a = a; m.fp = fp; m.n = n; m.off = off;
+      ob.msgs[ob.off[i] + oseq] = m;
+    }
+  }
+  oseq++;
+}
+
+}  // namespace kb

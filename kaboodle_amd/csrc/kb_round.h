@@ -1,0 +1,420 @@
+// kb_round.h — round-start kernels: stamp window, lifecycle, running set, broadcast phase and Join
+// responses (included by kb_sim.hip).
+#pragma once
+#include "kb_common.h"
+
+namespace kb {
+
+// ---- stamp window: every 64 rounds known stamps shift down, saturating at "ancient"
+__global__ void k_rebase(Dev d) {
+  const size_t total = (size_t)d.C * d.W / 16;
+  uint4* p = reinterpret_cast<uint4*>(d.stamp);
+  for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (size_t)gridDim.x * blockDim.x) {
+    const uint4 v = p[k];
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      uint32_t x = w[q], y = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        uint32_t b = (x >> (8 * t)) & 0xFF;
+        if (b > ST_ANCIENT) { b = b - EPOCH > ST_ANCIENT ? b - EPOCH : ST_ANCIENT; any = true; }
+        y |= b << (8 * t);
+      }
+      w[q] = y;
+    }
+    if (any) p[k] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+// ---- lifecycle: API start/stop in call order, then churn (src/lib.rs:136-183) ------------------
+struct Event { uint32_t node, stop; };
+__global__ void k_events(Dev d, const Event* ev, uint32_t nev, int32_t r) {
+  if (threadIdx.x || blockIdx.x) return;
+  for (uint32_t k = 0; k < nev; ++k) {
+    const uint32_t i = ev[k].node;
+    if (ev[k].stop) { if (d.alive[i]) node_stop(d, i); }
+    else if (!d.alive[i]) node_start(d, i, r);
+  }
+}
+__global__ void k_churn_leave(Dev d, int32_t r) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long left = 0;
+  if (i < d.C && d.alive[i] && d.start_round[i] != r &&
+      philox(i, (uint32_t)r, (uint32_t)P_CHURN << 24, 0, d.k0, d.k1).x < d.churn_thr) { node_stop(d, i); left = 1; }
+  const unsigned long long t = block_sum(left);
+  if (threadIdx.x == 0 && t) atomicAdd(&d.ctr[C_LEAVES], (uint32_t)t);
+}
+__global__ void k_churn_join(Dev d, int32_t r) {
+  const uint32_t leaves = d.ctr[C_LEAVES];
+  const uint32_t nf = d.ctr[C_NEXTFREE];
+  const uint32_t joins = leaves < d.C - nf ? leaves : d.C - nf;
+  for (uint32_t k = threadIdx.x; k < joins; k += blockDim.x) node_start(d, nf + k, r);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    d.ctr[C_NEXTFREE] = nf + joins; d.ctr[C_LEAVES] = 0;
+    d.stats[S_CLEAVE] += leaves; d.stats[S_CJOIN] += joins;
+  }
+}
+
+// ---- running set bitset + count, and its fingerprint (what a converged node reports) -----------
+__global__ void k_alive_bits(Dev d) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long cnt = 0;
+  if (w < d.NWR) {
+    uint32_t x = 0;
+    for (uint32_t t = 0; t < 32; ++t) { const uint32_t j = w * 32 + t; if (j < d.C && d.alive[j]) x |= 1u << t; }
+    d.abits[w] = x;
+    cnt = __popc(x);
+  }
+  const unsigned long long t = block_sum(cnt);
+  if (threadIdx.x == 0 && t) atomicAdd(&d.ctr[C_ALIVE], (uint32_t)t);
+}
+__global__ __launch_bounds__(1024) void k_truefp(Dev d) {
+  __shared__ uint32_t ztab[ZT * 128];
+  __shared__ uint32_t sraw[1024], scnt[1024];
+  load_ztab(d, ztab);
+  const uint32_t T = blockDim.x, t = threadIdx.x;
+  uint32_t raw = 0, cnt = 0;
+  const uint32_t per = (d.NWR + T - 1) / T;
+  for (uint32_t w = t * per; w < (t + 1) * per && w < d.NWR; ++w) {
+    uint32_t x = d.abits[w];
+    if (!x) continue;
+    if (d.uniform) {
+      for (int h = 0; h < 4; ++h) fold_half(d, ztab, 4 * w + h, (x >> (8 * h)) & 0xFFu, raw, cnt);
+    } else {
+      while (x) { const uint32_t j = w * 32 + (__ffs(x) - 1); x &= x - 1; raw = multmodp(d.segmul[j], raw) ^ d.cseg[j]; cnt += d.seglen[j]; }
+    }
+  }
+  sraw[t] = raw; scnt[t] = cnt;
+  __syncthreads();
+  for (uint32_t s = 1; s < T; s <<= 1) {
+    uint32_t nr = 0, nc = 0;
+    const bool w = (t % (2 * s) == 0) && t + s < T;
+    if (w) { nr = comb(d, sraw[t], sraw[t + s], scnt[t + s]); nc = scnt[t] + scnt[t + s]; }
+    __syncthreads();
+    if (w) { sraw[t] = nr; scnt[t] = nc; }
+    __syncthreads();
+  }
+  if (t == 0) d.truefp[0] = finish_fp(d, sraw[0], scnt[0]);
+}
+
+// ================================================================================================
+// Broadcast phase: Failed then Join deliveries of round r-1's broadcasts (src/kaboodle.rs:256-311)
+// ================================================================================================
+struct PhaseB {
+  const BCast* bfail; uint32_t nf;
+  const uint32_t* gid;   // per Failed entry: index of the first entry naming the same peer
+  const uint8_t* dep;    // per Failed entry: its sender is named as failed by an earlier entry
+  const BCast* bjoin; uint32_t nj; uint32_t JW;
+  unsigned long long* newmask; unsigned long long* respmask;   // [C * JW]
+  uint32_t* nresp; uint32_t* paysum; uint32_t* nbase;           // per node
+};
+
+__device__ inline bool bcast_lost(const Dev& d, uint32_t recv, const BCast& b, int32_t r) {
+  if (part_blocks(d, r, b.sender, recv)) return true;
+  if (!faults(d, r) || d.loss_thr == 0) return false;
+  return philox(recv, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | b.bseq, b.sender, d.k0, d.k1).x < d.loss_thr;
+}
+
+// Per-list facts about the Failed broadcasts (identical for every receiver).
+__global__ void k_bfail_prep(const BCast* bf, uint32_t nf, uint32_t* gid, uint8_t* dep) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nf) return;
+  const uint32_t p = bf[q].peer, sn = bf[q].sender;
+  uint32_t g = q; uint8_t dp = 0;
+  for (uint32_t k = 0; k < q; ++k) {
+    const uint32_t pk = bf[k].peer;
+    if (pk == p && g == q) g = k;
+    if (pk == sn) dp = 1;
+  }
+  gid[q] = g; dep[q] = dp;
+}
+
+// One wave per node.  The node's member bitset is staged in LDS (coalesced read, LDS atomics, one
+// coalesced write-back) when it fits (W <= PB_LDS_W); wider rows work on the global bitset.
+constexpr uint32_t PB_LDS_W = 524288;
+
+template <bool LDSB>
+__global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r) {
+  extern __shared__ uint32_t pb_dyn[];
+  __shared__ uint32_t s_sp[4][SLOTS];
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t i = blockIdx.x * wpb + wv;
+  const uint32_t l = lane();
+  if (i >= d.C) return;
+  if (!d.alive[i] || d.start_round[i] >= r) {
+    if (l == 0) { pb.nresp[i] = 0; pb.paysum[i] = 0; }
+    return;
+  }
+  uint8_t* rw = row_of(d, i);
+  uint32_t* gB = bits_of(d, i);
+  uint32_t* B = LDSB ? pb_dyn + (size_t)wv * d.NWR : gB;
+  if (LDSB) for (uint32_t w = l; w < d.NWR; w += 64) B[w] = gB[w];
+  if (l < SLOTS) { const Susp sl = d.susp[(size_t)i * SLOTS + l]; s_sp[wv][l] = sl.kind ? sl.peer : 0xFFFFFFFFu; }
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  auto mem = [&](uint32_t x) -> bool {
+    const uint32_t w = LDSB ? B[x >> 5] : __hip_atomic_load(&B[x >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (w >> (x & 31)) & 1u;
+  };
+  auto is_susp = [&](uint32_t x) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
+  uint32_t n = d.n[i];
+  const uint32_t n0 = n;
+  uint32_t lost_cnt = 0, removed_cnt = 0;
+  unsigned long long segs = 0;
+  const bool honour = d.failed_mode == KB_FAILED_SIM_SENDER;
+  // ---- Failed(p) group (src/kaboodle.rs:268-283) ----
+  // Entries are independent unless a sender was itself named as failed by an earlier entry (dep):
+  // chunks run in parallel (a repeated peer is removed once: the atomic returns whether it was set)
+  // until such an entry would act, then the exact in-order loop takes over.
+  uint32_t c0 = pb.nf;
+  for (uint32_t c = 0; c < pb.nf; c += 64) {
+    const uint32_t e = c + l;
+    const bool valid = e < pb.nf;
+    const BCast b = valid ? pb.bfail[e] : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+    const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
+    const bool cond = valid && b.sender != i && !lost && b.peer != i && honour && mem(b.sender) && mem(b.peer);
+    if (__ballot(cond && pb.dep[e])) { c0 = c; break; }
+    lost_cnt += __popcll(__ballot(lost));
+    if (cond) {
+      const uint32_t m = 1u << (b.peer & 31);
+      if (atomicAnd(&B[b.peer >> 5], ~m) & m) {
+        removed_cnt++;
+        if (is_susp(b.peer)) susp_clear(d, i, b.peer);
+        segs |= seg_bit(d, b.peer);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  }
+  removed_cnt = wave_sum(removed_cnt);
+  for (uint32_t c = c0; c < pb.nf; c += 64) {          // exact in-order tail
+    const uint32_t e = c + l;
+    const bool valid = e < pb.nf;
+    const BCast b = valid ? pb.bfail[e] : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+    const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
+    lost_cnt += __popcll(__ballot(lost));
+    const uint32_t m = pb.nf - c < 64 ? pb.nf - c : 64;
+    for (uint32_t q = 0; q < m; ++q) {
+      const uint32_t s_q = bcast(b.sender, q), p_q = bcast(b.peer, q);
+      if (s_q == i || bcast((uint32_t)lost, q) || p_q == i || !honour) continue;
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      if (!mem(s_q) || !mem(p_q)) continue;
+      if (l == 0) atomicAnd(&B[p_q >> 5], ~(1u << (p_q & 31)));
+      removed_cnt++;
+      if (is_susp(p_q) && l == 0) susp_clear(d, i, p_q);
+      segs |= seg_bit(d, p_q);
+    }
+  }
+  n -= removed_cnt;
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t nbase = n;
+  // ---- Join{addr} group (src/kaboodle.rs:284-304) ----
+  uint32_t nresp = 0, paysum = 0;
+  for (uint32_t c = 0; c < pb.nj; c += 64) {
+    const uint32_t e = c + l;
+    const bool valid = e < pb.nj;
+    const BCast b = valid ? pb.bjoin[e] : BCast{0xFFFFFFFFu, 0, 0, 0};
+    const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
+    const bool deliver = valid && b.sender != i && !lost;
+    const bool known = deliver && mem(b.sender);
+    const unsigned long long newm = __ballot(deliver && !known);
+    const bool isnew = (newm >> l) & 1ull;
+    // n right after inserting this joiner = n before the chunk + new joiners up to and including it
+    const uint32_t nq = n + __popcll(newm & ((2ull << l) - 1ull));
+    bool resp = false;
+    if (isnew) {                                   // should_respond_to_broadcast :333-354
+      const int64_t o = (int64_t)nq - 2;
+      if (o <= 0) resp = true;
+      else {
+        int64_t pct = 100 - o * o; if (pct < 1) pct = 1;
+        const uint32_t u = philox(i, (uint32_t)r, (uint32_t)P_RESPOND << 24, b.sender, d.k0, d.k1).x;
+        resp = (int64_t)mulhi(u, 100) < pct;
+      }
+    }
+    const unsigned long long respm = __ballot(resp);
+    if (deliver) {
+      if (known && is_susp(b.sender)) susp_clear(d, i, b.sender);
+      rw[b.sender] = enc(r, r);
+      if (isnew) { atomicOr(&B[b.sender >> 5], 1u << (b.sender & 31)); segs |= seg_bit(d, b.sender); }
+    }
+    const uint32_t sz = resp ? (d.uniform ? (nq < d.capj ? nq : d.capj) : nq) : 0;
+    paysum += wave_sum(sz);
+    nresp += __popcll(respm);
+    n += __popcll(newm);
+    lost_cnt += __popcll(__ballot(lost));
+    if (l == 0) {
+      pb.newmask[(size_t)i * pb.JW + c / 64] = newm;
+      pb.respmask[(size_t)i * pb.JW + c / 64] = respm;
+    }
+  }
+  segs = (unsigned long long)wave_or((uint32_t)segs) | ((unsigned long long)wave_or((uint32_t)(segs >> 32)) << 32);
+  __builtin_amdgcn_s_waitcnt(0);
+  __builtin_amdgcn_wave_barrier();
+  if (LDSB && segs) {                                 // write back the changed segments of the bitset
+    const uint32_t wps = d.SEGW / 32;
+    for (uint32_t w = l; w < d.NWR; w += 64) if ((segs >> (w / wps)) & 1ull) gB[w] = B[w];
+  }
+  if (l == 0) {
+    d.n[i] = n;
+    mark(d, i, segs);
+    if (n != n0) d.dirty[i] = 1;
+    pb.nresp[i] = nresp; pb.paysum[i] = paysum; pb.nbase[i] = nbase;
+    if (lost_cnt) atomicAdd(&d.stats[S_BDROP], lost_cnt);
+    if (removed_cnt) atomicAdd(&d.stats[S_RMFAILED], removed_cnt);
+    if (nresp) atomicAdd(&d.stats[S_JRESP], nresp);
+  }
+}
+
+// ================================================================================================
+// Join responses: KnownPeers of every map entry (src/kaboodle.rs:356-392).  One workgroup per
+// responding node: the row's member bitset goes to LDS once; for each response (list order) the
+// member set at that moment is the bitset minus the joiners inserted later; when it does not fit in
+// 10240 B the kept ranks are the first cap images of a keyed permutation of [0, n),
+// each computed independently; ids come out sorted by rank/select on the bitset.
+// ================================================================================================
+__device__ inline bool newbit(const unsigned long long* nm, uint32_t e) { return (nm[e >> 6] >> (e & 63)) & 1ull; }
+__device__ inline uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+__device__ inline uint32_t prp_walk(uint32_t x, uint32_t n, const U4& key) {
+  uint32_t b = 2;
+  while ((1ull << b) < n) b += 2;
+  const uint32_t h = b / 2, mask = (1u << h) - 1u;
+  const uint32_t kk[4] = {key.x, key.y, key.z, key.w};
+  do {
+    uint32_t L = x >> h, R = x & mask;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { const uint32_t t = R; R = L ^ (mix32(R ^ kk[k]) & mask); L = t; }
+    x = (L << h) | R;
+  } while (x >= n);
+  return x;
+}
+__device__ inline uint32_t bm_rank(const uint32_t* S, const uint32_t* SP, uint32_t id) {   // members < id
+  const uint32_t blk = id >> 8, w = id >> 5;
+  uint32_t r = SP[blk];
+  for (uint32_t k = blk * 8; k < w; ++k) r += __popc(S[k]);
+  return r + __popc(S[w] & ((1u << (id & 31)) - 1u));
+}
+__device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint32_t nblk, uint32_t b) {  // b-th member
+  uint32_t lo = 0, hi = nblk;
+  while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (SP[mid] <= b) lo = mid; else hi = mid; }
+  uint32_t rem = b - SP[lo];
+  uint32_t w = lo * 8;
+  for (;; ++w) { const uint32_t c = __popc(S[w]); if (rem < c) break; rem -= c; }
+  uint32_t x = S[w];
+  for (uint32_t t = 0; t < rem; ++t) x &= x - 1;
+  return w * 32 + (__ffs(x) - 1);
+}
+constexpr uint32_t RESP_LDS_W = 131072;   // rows up to this many ids keep their bitsets in LDS
+
+__global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint32_t* nodes, const uint32_t* nnodes_p,
+                                                   OutBuf ob, int32_t r, uint32_t* gscratch) {
+  extern __shared__ uint32_t lds_dyn[];
+  // rows wider than RESP_LDS_W keep the three bitsets in a per-workgroup slice of global scratch
+  uint32_t* lds = gscratch ? gscratch + (size_t)blockIdx.x * (3 * d.NWR + d.W / 256 + 1) : lds_dyn;
+  const uint32_t NW = d.NWR, NB = d.W / 256;
+  uint32_t* B = lds;                 // row membership         [NW]
+  uint32_t* S = B + NW;              // members at response    [NW]
+  uint32_t* SP = S + NW;             // block prefix of S      [NB + 1]
+  uint32_t* F = SP + NB + 1;         // kept-rank bitmap       [NW]
+  __shared__ uint32_t s_red[16];
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  const uint32_t nnodes = *nnodes_p;
+  for (uint32_t it = blockIdx.x; it < nnodes; it += gridDim.x) {
+    const uint32_t i = nodes[it];
+    const uint32_t* bi = bits_of(d, i);
+    for (uint32_t k = t; k < NW; k += T) B[k] = bi[k];
+    __syncthreads();
+    const unsigned long long* nm = pb.newmask + (size_t)i * pb.JW;
+    const unsigned long long* rm = pb.respmask + (size_t)i * pb.JW;
+    uint32_t poff = ob.poff[i], q = 0, ins_before = 0;
+    for (uint32_t wj = 0; wj < pb.JW; ++wj) {
+      unsigned long long rmw = rm[wj];
+      const unsigned long long nmw = nm[wj];
+      while (rmw) {
+        const uint32_t bit = (uint32_t)(__ffsll((long long)rmw) - 1);
+        const uint32_t K = wj * 64 + bit;
+        rmw &= rmw - 1;
+        const uint32_t expect = pb.nbase[i] + ins_before + __popcll(nmw & ((2ull << bit) - 1ull));
+        const uint32_t a = pb.bjoin[K].sender;
+        // S = B minus the joiners inserted after K
+        for (uint32_t k = t; k < NW; k += T) S[k] = B[k];
+        __syncthreads();
+        for (uint32_t e = K + 1 + t; e < pb.nj; e += T)
+          if (newbit(nm, e)) { const uint32_t x = pb.bjoin[e].sender; atomicAnd(&S[x >> 5], ~(1u << (x & 31))); }
+        __syncthreads();
+        // exclusive block prefix of S (8 words per block)
+        uint32_t bc = 0;
+        const uint32_t per = (NB + T - 1) / T;
+        for (uint32_t k = t * per; k < (t + 1) * per && k < NB; ++k) {
+          uint32_t c = 0;
+          for (uint32_t w = 0; w < 8; ++w) c += __popc(S[k * 8 + w]);
+          SP[k] = c; bc += c;
+        }
+        uint32_t ex = wave_excl(bc);
+        const uint32_t wt = wave_sum(bc);
+        if (lane() == 0) s_red[t >> 6] = wt;
+        __syncthreads();
+        for (uint32_t w = 0; w < (t >> 6); ++w) ex += s_red[w];
+        uint32_t nk = 0;
+        for (uint32_t w = 0; w < T / 64; ++w) nk += s_red[w];
+        for (uint32_t k = t * per; k < (t + 1) * per && k < NB; ++k) { const uint32_t c = SP[k]; SP[k] = ex; ex += c; }
+        if (t == 0) SP[NB] = nk;
+        __syncthreads();
+        const bool sample = d.uniform && nk > d.capj;
+        const uint32_t cap = sample ? d.capj : nk;
+        uint32_t* pay = ob.pay + poff;
+        if (!sample) {
+          for (uint32_t w = t; w < NW; w += T) {        // every member, position = rank
+            uint32_t x = S[w];
+            if (!x) continue;
+            uint32_t pos = bm_rank(S, SP, w * 32);
+            while (x) { const uint32_t b = __ffs(x) - 1; x &= x - 1; pay[pos++] = w * 32 + b; }
+          }
+        } else {
+          const uint32_t FW = (nk + 31) / 32;
+          for (uint32_t w = t; w < FW; w += T) F[w] = 0;
+          __syncthreads();
+          const U4 key = philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1);
+          for (uint32_t k = t; k < cap; k += T) {
+            const uint32_t y = prp_walk(k, nk, key);
+            atomicOr(&F[y >> 5], 1u << (y & 31));
+          }
+          __syncthreads();
+          // kept ranks in increasing order -> output slots
+          const uint32_t fper = (FW + T - 1) / T;
+          uint32_t fc = 0;
+          for (uint32_t w = t * fper; w < (t + 1) * fper && w < FW; ++w) fc += __popc(F[w]);
+          uint32_t fex = wave_excl(fc);
+          const uint32_t fwt = wave_sum(fc);
+          __syncthreads();
+          if (lane() == 0) s_red[t >> 6] = fwt;
+          __syncthreads();
+          for (uint32_t w = 0; w < (t >> 6); ++w) fex += s_red[w];
+          uint32_t o = fex;
+          for (uint32_t w = t * fper; w < (t + 1) * fper && w < FW; ++w) {
+            uint32_t x = F[w];
+            while (x) { const uint32_t b = __ffs(x) - 1; x &= x - 1; pay[o++] = bm_select(S, SP, NB, w * 32 + b); }
+          }
+        }
+        if (t == 0) {
+          Msg m; m.dest = a; m.sender = i; m.seq = q; m.kind = K_KP; m.a = cap; m.fp = 0; m.n = 0; m.off = poff;
+          ob.msgs[ob.off[i] + q] = m;
+          if (nk != expect) set_err(d, DERR_RESP);
+        }
+        poff += cap; q++;
+        __syncthreads();
+      }
+      ins_before += __popcll(nmw);
+    }
+  }
+}
+
+}  // namespace kb

@@ -1,0 +1,299 @@
+// kb_tick.h — the tick (src/kaboodle.rs:746-779): maybe_broadcast_join + handle_suspected_peers, the
+// row sweep of ping_random_peer fused with the fingerprint fold, target choice + ping_addrs
+// (included by kb_sim.hip).
+#pragma once
+#include "kb_common.h"
+
+namespace kb {
+
+struct BcastSlots { uint32_t* join; uint32_t* nfail; uint32_t* fail; };
+
+// Candidates of handle_suspected_peers (Known && != self, :571-577) in 16-id blocks: member bit set,
+// stamp byte >= 2 (not WaitingFor*), not self.
+__device__ inline uint32_t cand16(const Dev& d, const uint8_t* rw, const uint32_t* bw, uint32_t i, uint32_t j0) {
+  const uint4 v = *reinterpret_cast<const uint4*>(rw + j0);
+  const uint32_t m = nzmask4(v.x & 0xFEFEFEFEu) | (nzmask4(v.y & 0xFEFEFEFEu) << 4) |
+                     (nzmask4(v.z & 0xFEFEFEFEu) << 8) | (nzmask4(v.w & 0xFEFEFEFEu) << 12);
+  uint32_t c = m & ((bw[j0 >> 5] >> (j0 & 16)) & 0xFFFFu);
+  if (i >= j0 && i < j0 + 16) c &= ~(1u << (i - j0));
+  return c;
+}
+// rank -> id over the candidates of row i; lane l owns ids [lo, hi) holding candidate ranks
+// [lane_off, lane_off + lane_cnt).
+__device__ uint32_t select_known(const Dev& d, const uint8_t* rw, const uint32_t* bw, uint32_t i, uint32_t rank,
+                                 uint32_t lane_off, uint32_t lane_cnt, uint32_t lo, uint32_t hi) {
+  uint32_t found = 0xFFFFFFFFu;
+  if (rank >= lane_off && rank < lane_off + lane_cnt) {
+    uint32_t c = lane_off;
+    for (uint32_t j0 = lo; j0 < hi; j0 += 16) {
+      uint32_t m = cand16(d, rw, bw, i, j0);
+      const uint32_t pc = __popc(m);
+      if (rank < c + pc) {
+        for (uint32_t t = c; t < rank; ++t) m &= m - 1;
+        found = j0 + (__ffs(m) - 1);
+        break;
+      }
+      c += pc;
+    }
+  }
+  return wave_min(found);
+}
+
+// ---- A1 maybe_broadcast_join (:228-251) + A2 handle_suspected_peers (:558-653), one wave per node
+__global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots bs, int32_t r) {
+  __shared__ uint32_t s_pick_rank[4][SLOTS * 3], s_pick_peer[4][SLOTS * 3];
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t i = blockIdx.x * 4 + wv;
+  const uint32_t l = lane();
+  if (i >= d.C) return;
+  if (!d.alive[i]) { if (l == 0) { bs.join[i] = 0; bs.nfail[i] = 0; } return; }
+  uint32_t n = d.n[i];
+  if (l == 0) {
+    const int32_t lb = d.last_bcast[i];
+    uint32_t j = 0;
+    if (lb == NONE_ROUND || (r - lb >= REBROADCAST && n <= 1)) { j = 1; d.last_bcast[i] = r; }
+    bs.join[i] = j;
+  }
+  Susp* sl = d.susp + (size_t)i * SLOTS;
+  const Susp me = l < SLOTS ? sl[l] : Susp{0, 0, 0, 0};
+  const bool occ = l < SLOTS && me.kind != 0;
+  const unsigned long long occm = __ballot(occ);
+  const unsigned long long tim = __ballot(occ && r - me.since >= PING_TIMEOUT);
+  if (!tim) { if (l == 0) bs.nfail[i] = 0; return; }
+  const uint32_t nsusp = __popcll(occm);
+  const uint32_t m = n - 1 - nsusp;                       // Known && != self (:571-577)
+  uint32_t myrank = 0;                                    // ascending-peer order of occupied slots
+  for (int k = 0; k < SLOTS; ++k) if (((occm >> k) & 1ull) && bcast(me.peer, k) < me.peer) myrank++;
+  uint32_t npick = 0, nind = 0, nrem = 0;
+  uint32_t indirect[SLOTS], removed[SLOTS];
+  for (uint32_t t = 0; t < nsusp; ++t) {
+    const unsigned long long who = __ballot(occ && myrank == t);
+    const int k = __ffsll((long long)who) - 1;
+    const uint32_t peer = bcast(me.peer, k);
+    const int32_t kind = (int32_t)bcast((uint32_t)me.kind, k), since = (int32_t)bcast((uint32_t)me.since, k);
+    if (r - since < PING_TIMEOUT) continue;
+    if (kind == SK_WFP) {
+      const uint32_t kk = m < (uint32_t)NUM_INDIRECT ? m : (uint32_t)NUM_INDIRECT;
+      if (kk == 0) { removed[nrem++] = peer; continue; }
+      const U4 w = philox(i, (uint32_t)r, (uint32_t)P_INDIRECT << 24, peer, d.k0, d.k1);
+      uint32_t pk[3];
+      pk[0] = mulhi(w.x, m);
+      if (kk > 1) { const uint32_t b = mulhi(w.y, m - 1); pk[1] = b + (b >= pk[0]); }
+      if (kk > 2) {
+        const uint32_t lo = pk[0] < pk[1] ? pk[0] : pk[1], hi = pk[0] < pk[1] ? pk[1] : pk[0];
+        uint32_t c = mulhi(w.z, m - 2);
+        if (c >= lo) c++;
+        if (c >= hi) c++;
+        pk[2] = c;
+      }
+      if (l == 0) for (uint32_t q = 0; q < kk; ++q) { s_pick_rank[wv][npick + q] = pk[q]; s_pick_peer[wv][npick + q] = peer; }
+      npick += kk;
+      indirect[nind++] = peer;
+    } else {
+      removed[nrem++] = peer;
+    }
+  }
+  const uint8_t* rw = row_of(d, i);
+  uint32_t oseq = ob.cnt[i];
+  if (npick) {                                            // choose_multiple over the candidate list
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t* bw = bits_of(d, i);
+    const uint32_t lo = l * d.SEGW, hi = lo + d.SEGW;     // padding ids are never members
+    uint32_t cnt = 0;
+    for (uint32_t j0 = lo; j0 < hi; j0 += 16) cnt += __popc(cand16(d, rw, bw, i, j0));
+    const uint32_t off = wave_excl(cnt);
+    for (uint32_t q = 0; q < npick; ++q) {
+      const uint32_t id = select_known(d, rw, bw, i, s_pick_rank[wv][q], off, cnt, lo, hi);
+      emit_msg(ob, d, i, oseq, id, K_PINGREQ, s_pick_peer[wv][q], 0, 0, 0);
+    }
+  }
+  if (l == 0) {                                           // :631-652
+    for (uint32_t q = 0; q < nind; ++q)
+      for (int k = 0; k < SLOTS; ++k) if (sl[k].kind && sl[k].peer == indirect[q]) { sl[k].kind = SK_WFIP; sl[k].since = r; }
+    Cur* cu = d.cur + (size_t)i * CSLOTS;
+    unsigned long long segs = 0;
+    for (uint32_t q = 0; q < nrem; ++q) {
+      const uint32_t p = removed[q];
+      susp_clear(d, i, p);
+      mem_clr(d, i, p);
+      segs |= seg_bit(d, p);
+      n--;
+      for (int c = 0; c < CSLOTS; ++c) if (cu[c].used && cu[c].peer == p) cu[c].used = 0;
+      bs.fail[(size_t)i * SLOTS + q] = p;
+    }
+    bs.nfail[i] = nrem;
+    if (nrem) { d.n[i] = n; mark(d, i, segs); atomicAdd(&d.stats[S_RMTIMEOUT], nrem); }
+    ob.cnt[i] = oseq;
+  }
+}
+
+// ================================================================================================
+// THE ROW SWEEP (dominant kernel).  ping_random_peer (:655-703) keeps the 5 oldest Known peers by
+// (stamp, address rotated to start right after self); generate_fingerprint (:71-83) is refreshed for
+// the segments whose membership changed.  Lane = node: a wave sweeps 64 rows over one column split,
+// every lane streaming whole 128-byte lines of its own row, all lanes sharing the same half-block
+// CRC tables.  Per (node, split) it leaves two partial top-5 lists: ids below the rotation point
+// (part A, rot = j - p + C) and from it on (part B, rot = j - p); in id order each part is monotone
+// in rot, so an equal stamp seen later never displaces an earlier one (strict < test).
+// ================================================================================================
+struct SweepOut { uint32_t* part; uint32_t S; };   // part: [C][S][10] keys (b << 24 | rot)
+
+__device__ inline void top5_insert(uint32_t (&k)[5], uint32_t nk) {
+#pragma unroll
+  for (int s = 0; s < 5; ++s) { if (nk < k[s]) { const uint32_t t = k[s]; k[s] = nk; nk = t; } }
+}
+__device__ inline uint32_t thr5(const uint32_t (&k)[5]) { return k[4] == 0xFFFFFFFFu ? 256u : (k[4] >> 24); }
+
+template <bool FOLD>
+__device__ inline void sweep_step(const Dev& d, const uint32_t* ztab, const uint8_t* rw, const uint32_t* bw,
+                                  uint32_t i, uint32_t p, uint32_t col, uint32_t (&A)[5], uint32_t (&B)[5],
+                                  uint32_t& TA, uint32_t& TB, uint32_t& raw, uint32_t& cnt) {
+  uint4 v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const uint4*>(rw + col + 16 * q);
+  const uint4 mb = *reinterpret_cast<const uint4*>(bw + (col >> 5));
+  const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
+  if (FOLD) {
+#pragma unroll
+    for (int h = 0; h < 16; ++h) fold_half(d, ztab, (col >> 3) + h, (mw[h >> 2] >> (8 * (h & 3))) & 0xFFu, raw, cnt);
+  }
+  // parts of this step: ids [col, col+128) below p belong to A, the rest to B
+  if (d.ablate & 2) return;
+  const bool needA = TA > ST_ANCIENT && col < p;
+  const bool needB = TB > ST_ANCIENT && col + 128 > p;
+  if (!(needA || needB)) return;
+  const uint32_t C = d.C;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+    const uint32_t mbits = (mw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const uint32_t b = (w4[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+      const uint32_t j = col + 16 * q + t;
+      if (!((mbits >> t) & 1u) || b < ST_ANCIENT || j == i) continue;
+      if (j >= p) { if (b < TB) { top5_insert(B, (b << 24) | (j - p)); TB = thr5(B); } }
+      else if (b < TA) { top5_insert(A, (b << 24) | (j + C - p)); TA = thr5(A); }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
+  __shared__ uint32_t ztab[ZT * 128];
+  load_ztab(d, ztab);
+  const uint32_t S = so.S;
+  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t g = wave / S, s = wave % S;
+  const uint32_t i0 = g * 64 + lane();
+  const bool act = i0 < d.C && d.alive[i0];
+  // the ballot is taken once with the full wave active: inside the select below it would run
+  // under the idle lanes' exec mask only and see no live lane
+  const unsigned long long actm = __ballot(act);
+  if (!actm) return;
+  const uint32_t shadow = g * 64 + (uint32_t)(__ffsll((long long)actm) - 1);
+  const uint32_t i = act ? i0 : shadow;                 // idle lanes shadow a live one
+  const uint8_t* rw = row_of(d, i);
+  const uint32_t* bw = bits_of(d, i);
+  const uint32_t C = d.C;
+  const uint32_t p = (i + 1 == C) ? 0 : i + 1;
+  const unsigned long long sd = (d.uniform && act) ? d.sdirty[i] : 0ull;
+  uint32_t A[5], B[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) { A[k] = 0xFFFFFFFFu; B[k] = 0xFFFFFFFFu; }
+  uint32_t TA = 256, TB = 256;
+  const uint32_t spp = NSEG / S;
+  unsigned long long folded = 0;
+  for (uint32_t k = s * spp; k < (s + 1) * spp; ++k) {
+    const uint32_t c0 = k * d.SEGW, c1 = c0 + d.SEGW < C ? c0 + d.SEGW : ((C + 127) & ~127u);
+    uint32_t raw = 0, cnt = 0;
+    const bool mine = ((sd >> k) & 1ull) && !(d.ablate & 1);
+    if (__ballot(mine)) {                 // wave-uniform: one pass for the whole wave
+      for (uint32_t col = c0; col < c1; col += 128) sweep_step<true>(d, ztab, rw, bw, i, p, col, A, B, TA, TB, raw, cnt);
+      if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; }
+    } else {
+      for (uint32_t col = c0; col < c1; col += 128) sweep_step<false>(d, ztab, rw, bw, i, p, col, A, B, TA, TB, raw, cnt);
+    }
+  }
+  if (!act) return;
+  if (folded) atomicAnd(&d.sdirty[i], ~folded);
+  uint32_t* out = so.part + ((size_t)i * S + s) * 10;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) { out[k] = A[k]; out[5 + k] = B[k]; }
+}
+
+// ---- pick the ping target (one of the oldest 5), WaitingForPing(now), Ping; ping_addrs (:550-556);
+// ---- refresh the fingerprint from the checkpoints; agreement with the running set.  Thread per node.
+__global__ void k_tick_post(Dev d, SweepOut so, OutBuf ob, int32_t r) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long agree = 0;
+  if (i < d.C && d.alive[i]) {
+    const uint32_t C = d.C, S = so.S;
+    const uint32_t p = (i + 1 == C) ? 0 : i + 1;
+    uint32_t k5[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    const uint32_t* part = so.part + (size_t)i * S * 10;
+    for (uint32_t q = 0; q < S * 10; ++q) { const uint32_t x = part[q]; if (x < k5[4]) top5_insert(k5, x); }
+    uint32_t nc = 0;
+    while (nc < 5 && k5[nc] != 0xFFFFFFFFu) nc++;
+    uint32_t oseq = ob.cnt[i];
+    if (nc) {
+      const uint32_t u = philox(i, (uint32_t)r, (uint32_t)P_PING << 24, 0, d.k0, d.k1).x;
+      const uint32_t rot = k5[mulhi(u, nc)] & 0xFFFFFFu;
+      const uint32_t t = rot + p >= C ? rot + p - C : rot + p;
+      Susp* sl = d.susp + (size_t)i * SLOTS;
+      int k = 0;
+      while (k < SLOTS && sl[k].kind) ++k;
+      if (k == SLOTS) set_err(d, DERR_SLOTS);
+      else { sl[k].peer = t; sl[k].kind = SK_WFP; sl[k].since = r; }
+      row_of(d, i)[t] = ST_SUSPECT;
+      if (oseq >= ob.cap[i]) set_err(d, DERR_OUTBOX);
+      else ob.msgs[ob.off[i] + oseq] = Msg{t, i, oseq, K_PING, 0, 0, 0, 0};
+      oseq++;
+    }
+    const uint32_t pn = d.paq_n[i];
+    for (uint32_t q = 0; q < pn; ++q) {
+      const uint32_t t = d.paq[(size_t)i * PAQ + q];
+      if (oseq >= ob.cap[i]) set_err(d, DERR_OUTBOX);
+      else ob.msgs[ob.off[i] + oseq] = Msg{t, i, oseq, K_PING, 0, 0, 0, 0};
+      oseq++;
+    }
+    d.paq_n[i] = 0;
+    ob.cnt[i] = oseq;
+    if (d.dirty[i]) {
+      if (!d.uniform && d.sdirty[i]) {            // non-uniform identities: refold stale checkpoints here
+        unsigned long long sd = d.sdirty[i];
+        while (sd) { const int k = __ffsll((long long)sd) - 1; sd &= sd - 1;
+                     d.segp[(size_t)i * NSEG + k] = fold_segment(d, nullptr, i, k); }
+        d.sdirty[i] = 0;
+      }
+      d.fp[i] = thread_fp(d, i);
+      d.dirty[i] = 0;
+    }
+    agree = d.fp[i] == d.truefp[0];
+  }
+  const unsigned long long t = block_sum(agree);
+  if (threadIdx.x == 0 && t) atomicAdd(&d.ctr[C_AGREE], (uint32_t)t);
+}
+
+__global__ void k_bcast_write(Dev d, BcastSlots bs, const uint32_t* join_off, const uint32_t* fail_off, BCast* bjoin,
+                              BCast* bfail) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.C) return;
+  uint32_t bseq = 0;
+  if (bs.join[i]) bjoin[join_off[i]] = BCast{i, i, bseq++, 0};
+  const uint32_t nfl = bs.nfail[i];
+  for (uint32_t q = 0; q < nfl; ++q) bfail[fail_off[i] + q] = BCast{i, bs.fail[(size_t)i * SLOTS + q], bseq++, 0};
+}
+
+__global__ void k_round_end(Dev d, int32_t r) {
+  if (threadIdx.x || blockIdx.x) return;
+  const uint32_t a = d.ctr[C_AGREE], al = d.ctr[C_ALIVE];
+  d.ctr[C_LASTAGREE] = a; d.ctr[C_LASTALIVE] = al;
+  if (al && a == al) {
+    if ((int32_t)d.ctr[C_FIRSTCONV] < 0) d.ctr[C_FIRSTCONV] = (uint32_t)r;
+    d.ctr[C_LASTCONV] = (uint32_t)r;
+  }
+  d.ctr[C_AGREE] = 0; d.ctr[C_ALIVE] = 0;
+}
+
+}  // namespace kb

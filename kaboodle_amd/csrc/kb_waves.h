@@ -1,0 +1,314 @@
+// kb_waves.h — unicast delivery waves: routing, the KnownPeers group (message-parallel), and the
+// per-node in-order handler for every other message kind (src/kaboodle.rs:394-548).
+#pragma once
+#include "kb_common.h"
+
+namespace kb {
+
+struct WaveCtl {
+  uint8_t* status;        // per outbox slot: 0 dropped, 1 delivered (in-order kinds), 2 delivered KnownPeers
+  uint32_t* cnt1; uint32_t* bnd; uint32_t* bpay; uint32_t* cursor;   // per destination
+  uint32_t* in_off; uint32_t* inbox; uint32_t* active;
+  uint32_t* kp_list; uint32_t* touched; uint32_t* touched_list;
+  uint32_t msg_cap; uint32_t pay_cap;
+};
+
+// messages a handler may emit per delivered message (next-wave outbox reservation)
+__device__ inline uint32_t out_bound(uint32_t kind) {
+  return kind == K_ACK ? NOBS + 1 : (kind == K_KPR ? 2u : (kind == K_KP ? 0u : 1u));
+}
+
+// delivery decisions for every message of the wave (thread per sender region): dead receiver,
+// partition, loss (Philox keyed on the message), else delivered; counts per destination.
+__global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int32_t r, uint32_t w, int last) {
+  __shared__ uint32_t s_kp[256];
+  __shared__ uint32_t s_base;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0;
+  uint32_t nkp = 0;
+  const uint32_t cnt = i < d.C ? ob.cnt[i] : 0;
+  const uint32_t base = i < d.C ? ob.off[i] : 0;
+  for (uint32_t q = 0; q < cnt; ++q) {
+    const uint32_t g = base + q;
+    const Msg m = ob.msgs[g];
+    ks[m.kind < 5 ? m.kind : 0]++;
+    uint8_t st = 0;
+    if (last) win++;
+    else if (!d.alive[m.dest]) dead++;
+    else if (part_blocks(d, r, m.sender, m.dest)) part++;
+    else if (faults(d, r) && d.loss_thr &&
+             philox(m.sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m.seq, d.k0, d.k1).x < d.loss_thr) loss++;
+    else if (m.kind == K_KP) { st = 2; nkp++; }
+    else {
+      st = 1;
+      atomicAdd(&wc.cnt1[m.dest], 1u);
+      atomicAdd(&wc.bnd[m.dest], out_bound(m.kind));
+      if (m.kind == K_KPR) atomicAdd(&wc.bpay[m.dest], d.paybound);
+    }
+    if (!last) wc.status[g] = st;
+  }
+  for (int k = 0; k < 5; ++k) stat_add(d, S_PING + k, ks[k]);
+  stat_add(d, S_DEAD, dead); stat_add(d, S_PART, part); stat_add(d, S_LOSS, loss); stat_add(d, S_WINDOW, win);
+  if (last) return;
+  s_kp[threadIdx.x] = nkp;                // one atomic per block reserves kp_list space
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (uint32_t t = 0; t < blockDim.x; ++t) { const uint32_t v = s_kp[t]; s_kp[t] = run; run += v; }
+    s_base = run ? atomicAdd(&d.ctr[C_KP], run) : 0;
+  }
+  __syncthreads();
+  uint32_t pos = s_base + s_kp[threadIdx.x];
+  if (nkp) for (uint32_t q = 0; q < cnt; ++q) if (wc.status[base + q] == 2) wc.kp_list[pos++] = base + q;
+}
+
+__global__ void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.C) return;
+  const uint32_t cnt = ob.cnt[i], base = ob.off[i];
+  for (uint32_t q = 0; q < cnt; ++q) {
+    const uint32_t g = base + q;
+    if (wc.status[g] != 1) continue;
+    const uint32_t dst = ob.msgs[g].dest;
+    wc.inbox[wc.in_off[dst] + atomicAdd(&wc.cursor[dst], 1u)] = g;
+  }
+}
+
+__device__ inline void mark_touched(const Dev& d, const WaveCtl& wc, uint32_t node) {
+  if (atomicExch(&wc.touched[node], 1u) == 0u) wc.touched_list[atomicAdd(&d.ctr[C_TOUCH], 1u)] = node;
+}
+
+// KnownPeers arm (:448-472): every listed unknown peer becomes Known(now - 10 s).  Message-parallel:
+// the group commutes, so all arms run before all prologues.
+__global__ __launch_bounds__(256) void k_kp_insert(Dev d, OutBuf ob, WaveCtl wc, int32_t r) {
+  const uint32_t nkp = d.ctr[C_KP];
+  const uint8_t old = enc(r - SHARE_AGE, r);
+  for (uint32_t it = blockIdx.x * 4 + (threadIdx.x >> 6); it < nkp; it += gridDim.x * 4) {
+    const Msg m = ob.msgs[wc.kp_list[it]];
+    uint8_t* rw = row_of(d, m.dest);
+    unsigned long long segs = 0;
+    for (uint32_t e = lane(); e < m.a; e += 64) {
+      const uint32_t p = ob.pay[m.off + e];
+      if (!is_mem(d, m.dest, p) && mem_set(d, m.dest, p)) { rw[p] = old; segs |= seg_bit(d, p); }
+    }
+    segs = (unsigned long long)wave_or((uint32_t)segs) | ((unsigned long long)wave_or((uint32_t)(segs >> 32)) << 32);
+    if (segs && lane() == 0) { mark(d, m.dest, segs); mark_touched(d, wc, m.dest); }
+  }
+}
+// prologue of every KnownPeers envelope (:406-415): the sender becomes Known(now)
+__global__ void k_kp_prologue(Dev d, OutBuf ob, WaveCtl wc, int32_t r) {
+  const uint32_t nkp = d.ctr[C_KP];
+  const uint8_t now = enc(r, r);
+  for (uint32_t it = blockIdx.x * blockDim.x + threadIdx.x; it < nkp; it += gridDim.x * blockDim.x) {
+    const Msg m = ob.msgs[wc.kp_list[it]];
+    uint8_t* rw = row_of(d, m.dest);
+    const bool was = is_mem(d, m.dest, m.sender);
+    const uint8_t b = was ? rw[m.sender] : ST_UNKNOWN;
+    rw[m.sender] = now;
+    if (!was && mem_set(d, m.dest, m.sender)) mark(d, m.dest, seg_bit(d, m.sender));
+    if (b <= ST_SUSPECT) mark_touched(d, wc, m.dest);
+  }
+}
+// recount membership of touched rows; drop suspect slots whose entry was overwritten to Known
+__global__ __launch_bounds__(256) void k_touch_fix(Dev d, WaveCtl wc) {
+  const uint32_t nt = d.ctr[C_TOUCH];
+  const uint32_t l = lane();
+  for (uint32_t it = blockIdx.x * 4 + (threadIdx.x >> 6); it < nt; it += gridDim.x * 4) {
+    const uint32_t i = wc.touched_list[it];
+    const uint32_t* bw = bits_of(d, i);
+    uint32_t c = 0;
+    for (uint32_t w = l; w < d.NWR; w += 64) c += __popc(bw[w]);
+    c = wave_sum(c);
+    if (l < SLOTS) {
+      Susp* s = d.susp + (size_t)i * SLOTS + l;
+      if (s->kind && row_of(d, i)[s->peer] != ST_SUSPECT) s->kind = 0;
+    }
+    if (l == 0) {
+      if (c != d.n[i]) { d.n[i] = c; d.dirty[i] = 1; }
+      wc.touched[i] = 0;
+    }
+  }
+}
+
+// ---- the per-node in-order program for Ping / PingRequest / Ack / KnownPeersRequest ---------------
+__global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r) {
+  __shared__ uint32_t ztab[ZT * 128];
+  __shared__ Susp s_susp[4][SLOTS];
+  __shared__ Cur s_cur[4][CSLOTS];
+  load_ztab(d, ztab);
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t l = lane();
+  const uint32_t nact = d.ctr[C_ACTIVE];
+  const uint8_t now = enc(r, r);
+  const uint8_t fresh_thr = enc(r - (SHARE_AGE - 1), r);
+  for (uint32_t it = blockIdx.x * 4 + wv; it < nact; it += gridDim.x * 4) {
+    const uint32_t i = wc.active[it];
+    uint8_t* rw = row_of(d, i);
+    const uint32_t* bw = bits_of(d, i);
+    uint32_t n = d.n[i], fp = d.fp[i], oseq = 0, pay_used = 0;
+    bool dirty = d.dirty[i] != 0, need_sync = false;
+    unsigned long long segs = 0;
+    if (l < SLOTS) s_susp[wv][l] = d.susp[(size_t)i * SLOTS + l];
+    if (l < CSLOTS) s_cur[wv][l] = d.cur[(size_t)i * CSLOTS + l];
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t ibase = wc.in_off[i], icnt = wc.cnt1[i];
+    // canonical order = ascending outbox index = (sender, seq)
+    uint32_t mine = l < icnt ? wc.inbox[ibase + l] : 0xFFFFFFFFu;
+    const bool small = icnt <= 64;
+    if (small) {
+#pragma unroll
+      for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          const uint32_t o = __shfl_xor(mine, j, 64);
+          const bool up = (l & k) == 0, lower = (l & j) == 0;
+          const uint32_t mn = o < mine ? o : mine, mx = o < mine ? mine : o;
+          mine = (lower == up) ? mn : mx;
+        }
+      }
+    }
+    auto fp_now = [&]() -> uint32_t {
+      if (dirty) {
+        if (need_sync) { wave_mem_sync(); need_sync = false; }
+        fp = wave_fp(d, ztab, i, segs);
+        segs = 0;
+        dirty = false;
+      }
+      return fp;
+    };
+    auto maybe_sync = [&](uint32_t peer, uint32_t their_fp, uint32_t their_n) {   // :707-740
+      const uint32_t f = fp_now();
+      if (f == their_fp || n > their_n) return;
+      emit_msg(ob, d, i, oseq, peer, K_KPR, 0, f, n, 0);
+    };
+    uint32_t last_g = 0xFFFFFFFFu, last_sender = 0xFFFFFFFFu;
+    for (uint32_t t = 0; t < icnt; ++t) {
+      uint32_t g;
+      if (small) g = bcast(mine, (int)t);
+      else {        // large inbox: next smallest index above the previous one
+        uint32_t best = 0xFFFFFFFFu;
+        for (uint32_t q = l; q < icnt; q += 64) {
+          const uint32_t v = wc.inbox[ibase + q];
+          if ((last_g == 0xFFFFFFFFu || v > last_g) && v < best) best = v;
+        }
+        g = wave_min(best);
+      }
+      last_g = g;
+      const Msg m = ib.msgs[g];
+      const uint32_t s = m.sender;
+      if (s != last_sender) {                         // prologue: insert(sender, Known(now)) (:406-415)
+        const bool was = (bw[s >> 5] >> (s & 31)) & 1u;
+        const uint8_t b = was ? rw[s] : ST_UNKNOWN;
+        if (b == ST_SUSPECT && l < SLOTS && s_susp[wv][l].kind && s_susp[wv][l].peer == s) s_susp[wv][l].kind = 0;
+        if (!was) {
+          n++; dirty = true; segs |= seg_bit(d, s);
+          if (l == 0) const_cast<uint32_t*>(bw)[s >> 5] |= 1u << (s & 31);   // single writer of this row
+        }
+        if (b != now) { if (l == 0) rw[s] = now; need_sync = true; }
+        last_sender = s;
+        __builtin_amdgcn_wave_barrier();
+      }
+      switch (m.kind) {
+        case K_PING: {                                               // :513-532
+          const uint32_t f = fp_now();
+          emit_msg(ob, d, i, oseq, s, K_ACK, i, f, n, 0);
+          break;
+        }
+        case K_PINGREQ: {                                            // :533-545
+          const unsigned long long hit = __ballot(l < CSLOTS && s_cur[wv][l].used && s_cur[wv][l].peer == m.a);
+          int e = hit ? __ffsll((long long)hit) - 1 : -1;
+          if (e < 0) {
+            const unsigned long long fr = __ballot(l < CSLOTS && !s_cur[wv][l].used);
+            e = fr ? __ffsll((long long)fr) - 1 : -1;
+            if (e >= 0 && l == 0) { s_cur[wv][e].used = 1; s_cur[wv][e].peer = m.a; s_cur[wv][e].nobs = 0; }
+          }
+          __builtin_amdgcn_s_waitcnt(0);
+          __builtin_amdgcn_wave_barrier();
+          if (e < 0) { if (l == 0) atomicAdd(&d.stats[S_CUROVF], 1ull); }
+          else if (l == 0) {
+            Cur& c = s_cur[wv][e];
+            bool dup = false;
+            for (uint32_t q = 0; q < c.nobs; ++q) dup |= c.obs[q] == s;
+            if (!dup) { if (c.nobs == NOBS) atomicAdd(&d.stats[S_CUROVF], 1ull); else c.obs[c.nobs++] = s; }
+          }
+          __builtin_amdgcn_s_waitcnt(0);
+          __builtin_amdgcn_wave_barrier();
+          emit_msg(ob, d, i, oseq, m.a, K_PING, 0, 0, 0, 0);
+          break;
+        }
+        case K_ACK: {                                                // :418-447
+          const unsigned long long hit = __ballot(l < CSLOTS && s_cur[wv][l].used && s_cur[wv][l].peer == m.a);
+          if (hit) {
+            const int e = __ffsll((long long)hit) - 1;
+            const uint32_t nobs = s_cur[wv][e].nobs;
+            uint32_t obs[NOBS];
+            for (int q = 0; q < NOBS; ++q) obs[q] = s_cur[wv][e].obs[q];
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+            if (l == 0) s_cur[wv][e].used = 0;
+            for (uint32_t q = 0; q < nobs; ++q) emit_msg(ob, d, i, oseq, obs[q], K_ACK, m.a, m.fp, m.n, 0);
+            __builtin_amdgcn_s_waitcnt(0);
+            __builtin_amdgcn_wave_barrier();
+          }
+          maybe_sync(m.a, m.fp, m.n);
+          break;
+        }
+        case K_KPR: {                                                // :473-512
+          if (need_sync) { wave_mem_sync(); need_sync = false; }
+          const uint32_t poff = ob.poff[i] + pay_used;
+          uint32_t total = 0;
+          uint64_t size = 8 + (d.seglen[i] - ADDR_LEN) + 4 + 8;
+          bool over = false;
+          for (uint32_t c = 0; c < d.W && !over; c += 1024) {
+            const uint32_t j0 = c + l * 16;
+            const uint4 v = *reinterpret_cast<const uint4*>(rw + j0);
+            const uint32_t mb = (bw[j0 >> 5] >> (j0 & 16)) & 0xFFFFu;
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+            uint32_t mask = 0;
+#pragma unroll
+            for (int t2 = 0; t2 < 16; ++t2) {
+              const uint32_t b = (w4[t2 >> 2] >> (8 * (t2 & 3))) & 0xFFu, j = j0 + t2;
+              mask |= (uint32_t)(((mb >> t2) & 1u) && b >= fresh_thr && j != i && j != s) << t2;
+            }
+            const uint32_t mc = __popc(mask);
+            uint32_t pos = total + wave_excl(mc);
+            if (!d.uniform) {
+              uint32_t sz = 0, mm = mask;
+              while (mm) { const int t2 = __ffs(mm) - 1; mm &= mm - 1; sz += 18 + d.seglen[j0 + t2] - ADDR_LEN; }
+              size += wave_sum(sz);
+            }
+            while (mask) {
+              const int t2 = __ffs(mask) - 1;
+              mask &= mask - 1;
+              if (pos < d.paybound) {
+                if (poff + pos < ob.pay_cap) ob.pay[poff + pos] = j0 + t2;
+                else set_err(d, DERR_PAYLOAD);
+              }
+              pos++;
+            }
+            total += wave_sum(mc);
+            if (d.uniform && total > d.capk) over = true;
+          }
+          over = d.uniform ? total > d.capk : size > (uint64_t)BUFSZ;
+          if (over) { if (l == 0) atomicAdd(&d.stats[S_OVERSIZE], 1ull); }
+          else { emit_msg(ob, d, i, oseq, s, K_KP, total, 0, 0, poff); pay_used += total; }
+          maybe_sync(s, m.fp, m.n);
+          break;
+        }
+        default: break;
+      }
+    }
+    if (l < SLOTS) d.susp[(size_t)i * SLOTS + l] = s_susp[wv][l];
+    if (l < CSLOTS) d.cur[(size_t)i * CSLOTS + l] = s_cur[wv][l];
+    if (l == 0) {
+      if (segs) atomicOr(&d.sdirty[i], segs);
+      d.n[i] = n; d.fp[i] = fp; d.dirty[i] = dirty ? 1 : 0;
+      ob.cnt[i] = oseq;
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+}  // namespace kb

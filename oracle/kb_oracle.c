@@ -396,9 +396,28 @@ static int should_respond(kbo_sim* s, uint32_t i, uint32_t joiner, int32_t r) {
   return (int64_t)o_mulhi(u, 100) < pct;
 }
 
+/* Keyed permutation of [0, n): 4-round Feistel network on the smallest even bit width b with 2^b >= n,
+ * round function lowbias32(R ^ key[k]) masked to b/2 bits, cycle-walked into [0, n). */
+static inline uint32_t o_mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+static uint32_t prp_walk(uint32_t x, uint32_t n, const uint32_t key[4]) {
+  uint32_t b = 2;
+  while ((1ull << b) < n) b += 2;
+  const uint32_t h = b / 2, mask = (1u << h) - 1u;
+  do {
+    uint32_t L = x >> h, R = x & mask;
+    for (int k = 0; k < 4; ++k) { uint32_t t = R; R = L ^ (o_mix32(R ^ key[k]) & mask); L = t; }
+    x = (L << h) | R;
+  } while (x >= n);
+  return x;
+}
+
 /* maybe_send_known_peers_to_peer (src/kaboodle.rs:356-392): every entry of the map (self, the joiner
  * and suspects included); while the encoding is >= 10240 B drop a uniformly random entry — restated
- * as a uniform random subset of the largest size that fits, drawn with Floyd's algorithm. */
+ * as a uniform random subset of the largest size that fits: the first `cap` images of a keyed
+ * pseudo-random permutation of the member ranks (prp_walk). */
 static void join_response(kbo_sim* s, uint32_t i, uint32_t joiner, int32_t r) {
   const uint8_t* rw = row(s, i);
   uint32_t n = s->n[i];
@@ -411,14 +430,10 @@ static void join_response(kbo_sim* s, uint32_t i, uint32_t joiner, int32_t r) {
   if (m <= cap || !s->uniform) {
     pay = members; plen = m;
   } else {
-    /* Floyd: for t in [0,cap): j = m-cap+t; v = uniform[0, j]; add v unless present, else add j */
+    /* first `cap` images of a keyed pseudo-random permutation of [0, m) */
+    o_u32x4 key = ph(s, i, (uint32_t)r, (uint32_t)P_TRUNC << 24, joiner);
     uint8_t* chosen = (uint8_t*)calloc(m, 1);
-    for (uint32_t t = 0; t < cap; ++t) {
-      uint32_t j = m - cap + t;
-      o_u32x4 w = ph(s, i, (uint32_t)r, ((uint32_t)P_TRUNC << 24) | (t >> 2), joiner);
-      uint32_t v = o_mulhi(w.v[t & 3], j + 1);
-      if (chosen[v]) chosen[j] = 1; else chosen[v] = 1;
-    }
+    for (uint32_t t = 0; t < cap; ++t) chosen[prp_walk(t, m, key.v)] = 1;
     pay = (uint32_t*)malloc(sizeof(uint32_t) * cap);
     plen = 0;
     for (uint32_t k = 0; k < m; ++k) if (chosen[k]) pay[plen++] = members[k];
@@ -921,7 +936,7 @@ int kbo_sim_dump_curious(kbo_sim* s, uint32_t node, int32_t* out, size_t cap, si
 }
 
 /* pure helpers */
-uint32_t kbo_fingerprint_of_ids(const uint32_t* ids, size_t n, const uint8_t* identities, size_t stride,
+uint32_t kbo_fingerprint_of_set(const uint32_t* ids, size_t n, const uint8_t* identities, size_t stride,
                                 const uint8_t* lens) {
   o_crc_init();
   uint32_t* v = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));

@@ -36,6 +36,31 @@ def mulhi(u, k):
     return (u * k) >> 32
 
 
+def mix32(x):
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & MASK
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & MASK
+    x ^= x >> 16
+    return x
+
+
+def prp_walk(x, n, key):
+    """x-th image of the keyed permutation of [0, n) (4-round Feistel, cycle walking)"""
+    b = 2
+    while (1 << b) < n:
+        b += 2
+    h = b // 2
+    mask = (1 << h) - 1
+    while True:
+        L, R = x >> h, x & mask
+        for k in range(4):
+            L, R = R, L ^ (mix32(R ^ key[k]) & mask)
+        x = (L << h) | R
+        if x < n:
+            return x
+
+
 def addr(i: int) -> str:
     return f"10.100.100.{100 + i // 50000}:{10000 + i % 50000}"
 
@@ -246,11 +271,8 @@ class PyMesh:
         cap = (BUFSZ - 20 - L - 1) // (18 + L)
         if len(members) > cap:
             n = len(members)
-            chosen = set()
-            for t in range(cap):
-                j = n - cap + t
-                v = mulhi(self.ph(p.id, r, (P_TRUNC << 24) | (t >> 2), joiner)[t & 3], j + 1)
-                chosen.add(j if v in chosen else v)
+            key = self.ph(p.id, r, P_TRUNC << 24, joiner)
+            chosen = {prp_walk(t, n, key) for t in range(cap)}
             members = [members[k] for k in sorted(chosen)]
         self.emit(p.id, joiner, "KnownPeers", peers=members)
         self.stats["join_responses"] += 1

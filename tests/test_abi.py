@@ -1,0 +1,88 @@
+"""The C-ABI boundary (include/kaboodle_sim.h): both implementations export every declared symbol, the
+HIP library loads without a GPU and fails loudly (KB_NO_DEVICE) instead of computing on the CPU, and the
+host-side mirror (kaboodle_amd) refuses to run without the HIP path."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import kaboodle_amd
+from kaboodle_amd._ffi import KB_ABI_VERSION, KB_NO_DEVICE, KbConfig, KbStats, SimConfig
+from parity import GPU_SO, ORACLE_SO
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "kaboodle_sim.h")
+
+
+def declared():
+    src = re.sub(r"/\*.*?\*/", "", open(HEADER).read(), flags=re.S)
+    return sorted(set(re.findall(r"\b(kb_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_the_surface():
+    names = declared()
+    for must in ("kb_sim_create", "kb_sim_destroy", "kb_sim_step", "kb_sim_fingerprint", "kb_sim_peers",
+                 "kb_sim_peer_states", "kb_sim_start_node", "kb_sim_stop_node", "kb_sim_ping_addrs",
+                 "kb_sim_set_identity", "kb_sim_stats", "kb_sim_is_running", "kb_format_addr"):
+        assert must in names
+    m = re.search(r"#define\s+KB_ABI_VERSION\s+(\d+)", open(HEADER).read())
+    assert int(m.group(1)) == KB_ABI_VERSION
+
+
+@pytest.mark.skipif(not os.path.exists(GPU_SO), reason="HIP library not built (run __graft_entry__.build())")
+def test_hip_library_exports_every_symbol():
+    lib = C.CDLL(GPU_SO)
+    missing = [n for n in declared() if not hasattr(lib, n)]
+    assert not missing
+
+
+def test_oracle_exports_every_symbol():
+    lib = C.CDLL(ORACLE_SO)
+    skip = {"kb_sim_kernel_time", "kb_sim_reset_kernel_time", "kb_sim_sweep_bytes"}   # GPU timing surface
+    missing = [n for n in declared() if n not in skip and not hasattr(lib, "kbo_" + n[3:])]
+    assert not missing
+
+
+def test_struct_layouts_match_header():
+    # kb_config: 15 scalar fields (seed is u64) + reserved[6]; kb_stats: 6 x 4-byte + 19 x u64 + reserved[8]
+    assert C.sizeof(KbConfig) == 4 * 4 + 8 + 4 * 10 + 4 * 6
+    assert C.sizeof(KbStats) == 6 * 4 + 19 * 8 + 8 * 8
+
+
+def test_config_default_matches_mirror():
+    for path, fn in ((GPU_SO, "kb_config_default"), (ORACLE_SO, "kbo_config_default")):
+        if not os.path.exists(path):
+            continue
+        c = KbConfig()
+        getattr(C.CDLL(path), fn)(C.byref(c))
+        d = SimConfig().to_c()
+        for f, _ in KbConfig._fields_:
+            if f != "reserved":
+                assert getattr(c, f) == getattr(d, f), f
+
+
+@pytest.mark.skipif(not os.path.exists(GPU_SO), reason="HIP library not built")
+def test_no_gpu_means_no_device_error():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is visible")
+    except ImportError:
+        pass
+    lib = C.CDLL(GPU_SO)
+    lib.kb_last_error.restype = C.c_char_p
+    c = SimConfig(capacity=8, initial_nodes=8).to_c()
+    h = C.c_void_p()
+    assert lib.kb_sim_create(C.byref(c), C.byref(h)) == KB_NO_DEVICE
+    assert b"device" in lib.kb_last_error()
+    with pytest.raises(Exception):
+        kaboodle_amd.require_gpu()
+    with pytest.raises(kaboodle_amd.KbError):
+        kaboodle_amd.Mesh(capacity=8, initial_nodes=8)
+
+
+def test_thresholds():
+    c = SimConfig(loss=0.01, churn=0.001).to_c()
+    assert c.loss_threshold == round(0.01 * 2**32) and c.churn_threshold == round(0.001 * 2**32)
+    assert SimConfig(loss=1.0).to_c().loss_threshold == 2**32 - 1

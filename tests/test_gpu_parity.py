@@ -1,0 +1,110 @@
+"""Parity of the HIP library with the CPU oracle, through the C ABI, on an MI355X.
+
+Bar: bit-exact (all state is integer/byte): stamp rows, per-node scalars, suspect and curious tables,
+fingerprints and every counter, after every round."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import parity
+import scenarios
+from kaboodle_amd._ffi import KB_INIT_CONVERGED, Sim, SimConfig
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    import kaboodle_amd
+    kaboodle_amd.require_gpu()
+    return parity.gpu_lib()
+
+
+@pytest.mark.parametrize("name,case,rounds", parity.standard_cases(), ids=[c[0] for c in parity.standard_cases()])
+def test_parity_every_round(gpu, name, case, rounds):
+    ok, msg, _ = parity.run_case(case, rounds)
+    assert ok, f"{name}: {msg}"
+
+
+@pytest.mark.parametrize("name", [s["name"] for s in scenarios.SCENARIOS])
+def test_gpu_matches_pyref_trace(gpu, name):
+    traces = json.load(open(os.path.join(HERE, "golden", "traces.json")))
+    sc = scenarios.BY_NAME[name]
+    with Sim(gpu, sc["cfg"]) as g:
+        scenarios.setup(g, sc)
+        for r in range(sc["rounds"]):
+            scenarios.apply_events(g, sc, r)
+            g.step(1)
+            assert scenarios.digest_sim(g) == traces[name]["rounds"][r], f"{name} round {r}"
+
+
+def test_full_size_64k_against_oracle(gpu):
+    """BASELINE configs[2] at full size (64K peers, 1% loss, 0.1% churn) for a few rounds: every
+    fingerprint, scalar and counter, and a sample of complete stamp rows, against the OpenMP oracle."""
+    cfg = SimConfig(capacity=65536 + 4096, initial_nodes=65536, init_mode=KB_INIT_CONVERGED, loss=0.01,
+                    churn=0.001, seed=1)
+    o = Sim(parity.oracle_lib(omp=True), cfg)
+    g = Sim(gpu, cfg)
+    rng = np.random.default_rng(0)
+    for r in range(4):
+        o.step(1)
+        g.step(1)
+        assert o.stats() == g.stats(), f"round {r}"
+        assert np.array_equal(o.fingerprints(), g.fingerprints()), f"round {r}"
+        assert np.array_equal(o.scalars(), g.scalars()), f"round {r}"
+        for i in rng.choice(cfg.capacity, 24, replace=False):
+            assert np.array_equal(o.row(int(i)), g.row(int(i))), f"round {r} node {i}"
+            assert o.suspects(int(i)) == g.suspects(int(i))
+    o.close()
+    g.close()
+
+
+def test_fingerprint_consistent_with_membership(gpu):
+    """Size-independent property at bench scale: each node's incremental fingerprint equals the
+    generate_fingerprint of the peer list the ABI reports for it (kb_fingerprint_of_set)."""
+    import ctypes as C
+    cfg = SimConfig(capacity=65536 + 4096, initial_nodes=65536, init_mode=KB_INIT_CONVERGED, loss=0.01,
+                    churn=0.001, seed=2)
+    lib = C.CDLL(parity.GPU_SO)
+    f = lib.kb_fingerprint_of_set
+    f.restype = C.c_uint32
+    f.argtypes = [C.POINTER(C.c_uint32), C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p]
+    with Sim(gpu, cfg) as g:
+        g.step(12)
+        fps = g.fingerprints()
+        st = g.stats()
+        assert st["alive"] == 65536 - st["churn_leaves"] + st["churn_joins"]
+        assert st["next_free_id"] == 65536 + st["churn_joins"]
+        for i in np.random.default_rng(1).choice(65536, 16, replace=False):
+            if not g.is_running(int(i)):
+                continue
+            p = g.peers(int(i))
+            assert f((C.c_uint32 * len(p))(*p), len(p), None, 0, None) == fps[i]
+
+
+def test_deterministic_replay(gpu):
+    cfg = SimConfig(capacity=5000, initial_nodes=4096, init_mode=KB_INIT_CONVERGED, loss=0.02, churn=0.002, seed=9)
+    out = []
+    for _ in range(2):
+        with Sim(gpu, cfg) as g:
+            g.step(20)
+            out.append((g.stats(), g.fingerprints().copy(), g.rows()[::97].copy()))
+    assert out[0][0] == out[1][0]
+    assert np.array_equal(out[0][1], out[1][1]) and np.array_equal(out[0][2], out[1][2])
+
+
+def test_kaboodle_view(gpu):
+    import kaboodle_amd
+    m = kaboodle_amd.Mesh(capacity=4, initial_nodes=0)
+    for i, ident in enumerate(scenarios.CONFIG1_IDS):
+        k = m.node(i)
+        k.set_identity(ident)
+        k.start()
+    m.step(6)
+    fps = {m.node(i).fingerprint() for i in range(4)}
+    assert fps == {0x981285C8}
+    assert m.node(0).self_addr() == "10.100.100.100:10000"
+    assert sorted(m.node(2).peers()) == [f"10.100.100.100:1000{i}" for i in range(4)]
