@@ -1,0 +1,90 @@
+// kaboodle_sim.hpp — thin header-only C++ wrapper over the C ABI (include/kaboodle_sim.h) with the
+// shape of the reference's `Kaboodle` surface (src/lib.rs:65-369): a `Mesh` owns one simulated mesh
+// on one GPU, `Mesh::Peer` is the per-instance view (start/stop/ping_addrs/fingerprint/peers/...).
+// Errors become `kb::Error` (status code + kb_last_error text), mirroring KaboodleError
+// (src/errors.rs:8-24).
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "kaboodle_sim.h"
+
+namespace kb {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& what) : std::runtime_error(what), code(c) {}
+};
+
+inline void check(int rc, const char* fn) {
+  if (rc != KB_OK) {
+    const char* e = kb_last_error();
+    throw Error(rc, std::string(fn) + ": " + (e ? e : ""));
+  }
+}
+
+inline std::string format_addr(uint32_t id) {                 // canonical simulated SocketAddr
+  char buf[32];
+  check(kb_format_addr(id, buf, sizeof buf), "kb_format_addr");
+  return buf;
+}
+
+class Mesh {
+ public:
+  explicit Mesh(const kb_config& cfg) { check(kb_sim_create(&cfg, &h_), "kb_sim_create"); }
+  static kb_config defaults() { kb_config c; kb_config_default(&c); return c; }
+  ~Mesh() { if (h_) kb_sim_destroy(h_); }
+  Mesh(const Mesh&) = delete;
+  Mesh& operator=(const Mesh&) = delete;
+  Mesh(Mesh&& o) noexcept : h_(std::exchange(o.h_, nullptr)) {}
+
+  void step(uint32_t rounds = 1) { check(kb_sim_step(h_, rounds), "kb_sim_step"); }
+  kb_stats stats() const { kb_stats s; check(kb_sim_stats(h_, &s), "kb_sim_stats"); return s; }
+  uint32_t true_fingerprint() const { uint32_t f; check(kb_sim_true_fingerprint(h_, &f), "kb_sim_true_fingerprint"); return f; }
+  kb_sim* handle() const { return h_; }
+
+  // the per-instance view: method names of src/lib.rs
+  class Peer {
+   public:
+    Peer(kb_sim* h, uint32_t id) : h_(h), id_(id) {}
+    void start() { check(kb_sim_start_node(h_, id_), "kb_sim_start_node"); }            // :136
+    void stop() { check(kb_sim_stop_node(h_, id_), "kb_sim_stop_node"); }               // :159
+    bool is_running() const { int r; check(kb_sim_is_running(h_, id_, &r), "kb_sim_is_running"); return r != 0; }
+    std::string self_addr() const { return format_addr(id_); }                          // :312
+    void ping_addrs(const std::vector<uint32_t>& ids) {                                 // :268
+      check(kb_sim_ping_addrs(h_, id_, ids.data(), ids.size()), "kb_sim_ping_addrs");
+    }
+    void set_identity(const std::vector<uint8_t>& ident) {                              // :323
+      check(kb_sim_set_identity(h_, id_, ident.data(), ident.size()), "kb_sim_set_identity");
+    }
+    uint32_t fingerprint() const { uint32_t f; check(kb_sim_fingerprint(h_, id_, &f), "kb_sim_fingerprint"); return f; }
+    std::vector<uint32_t> peers() const {                                               // :339
+      size_t n = 0;
+      check(kb_sim_peers(h_, id_, nullptr, 0, &n), "kb_sim_peers");
+      std::vector<uint32_t> v(n);
+      check(kb_sim_peers(h_, id_, v.data(), v.size(), &n), "kb_sim_peers");
+      v.resize(n);
+      return v;
+    }
+    std::vector<kb_peer_state> peer_states() const {                                   // :348
+      size_t n = 0;
+      check(kb_sim_peer_states(h_, id_, nullptr, 0, &n), "kb_sim_peer_states");
+      std::vector<kb_peer_state> v(n);
+      check(kb_sim_peer_states(h_, id_, v.data(), v.size(), &n), "kb_sim_peer_states");
+      v.resize(n);
+      return v;
+    }
+   private:
+    kb_sim* h_;
+    uint32_t id_;
+  };
+  Peer peer(uint32_t id) const { return Peer(h_, id); }
+
+ private:
+  kb_sim* h_ = nullptr;
+};
+
+}  // namespace kb

@@ -6,6 +6,8 @@
 //   segp   [C][64] {raw, cnt} crc0 of the members of each W/64-id segment (fingerprint checkpoints)
 //   sdirty [C] u64  segments whose checkpoint is stale; dirty[C] u8: cached fingerprint stale
 //   susp   [C][8]   WaitingForPing / WaitingForIndirectPing slots; cur [C][8] curious_peers entries
+//   flog   [C][LOGCAP] u32 freshness log: (peer << 8 | round & 255) each time a stamp becomes
+//          Known(now); flog_n [C] entries appended; fstart [C][16] flog_n at the start of each round
 #pragma once
 #include "kb_device.h"
 #include "../../include/kaboodle_sim.h"
@@ -14,7 +16,9 @@ namespace kb {
 
 enum StatIdx {
   S_PING, S_PINGREQ, S_ACK, S_KP, S_KPR, S_BJOIN, S_BFAIL, S_DEAD, S_LOSS, S_WINDOW, S_OVERSIZE, S_PART, S_BDROP,
-  S_RMTIMEOUT, S_RMFAILED, S_JRESP, S_CUROVF, S_CLEAVE, S_CJOIN, NSTAT
+  S_RMTIMEOUT, S_RMFAILED, S_JRESP, S_CUROVF, S_CLEAVE, S_CJOIN,
+  S_SWEEPB,                       // bytes the row sweep had to read (bench roofline; not a kb_stats field)
+  NSTAT
 };
 enum CtrIdx {
   C_KP, C_TOUCH, C_ACTIVE, C_AGREE, C_ALIVE, C_LEAVES, C_NEXTFREE, C_ERR, C_FIRSTCONV, C_LASTCONV, C_LASTAGREE,
@@ -22,6 +26,7 @@ enum CtrIdx {
 };
 constexpr int NSEG = 64;          // fingerprint checkpoints per row
 constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
+constexpr int ZB = 9 * 1024;      // LDS byte tables for Z^0..Z^8 (the sweep: 4 lookups per multiply)
 
 struct Dev {
   uint32_t C, W, SEGW, NWR;       // capacity, row stride, ids per segment (W/64), bitset words per row (W/32)
@@ -55,12 +60,24 @@ struct Dev {
   uint32_t* seglen;
   uint32_t* zpow;                 // Z^k, Z = x^(8L), k in [0, C+1]
   uint32_t* ztab;                 // [17][8][16] nibble tables of multiplication by Z^c
+  uint32_t* zbtab;                // [9][4][256] byte tables of multiplication by Z^c
   uint32_t* htab;                 // [(W/8)][256] crc0 of every member pattern of every 8-id half block
   unsigned long long* stats;
   uint32_t* ctr;
   uint32_t* truefp;
+  uint32_t* flog;
+  uint32_t* flog_n;
+  uint32_t* fstart;
 };
 
+// freshness log (the KnownPeersRequest reply set, :503-508, without scanning the row): an entry is
+// appended exactly when a stamp byte changes to Known(now); a (peer, t) entry is live iff the peer
+// is still a member whose stamp is exactly enc(t).  Window of round r = entries since fstart[r-9].
+__device__ inline uint32_t log_entry(uint32_t peer, int32_t r) { return (peer << 8) | ((uint32_t)r & 255u); }
+__device__ inline int32_t log_round(uint32_t e, int32_t r) { return r - (int32_t)(((uint32_t)r - (e & 255u)) & 255u); }
+__device__ inline uint32_t log_window_start(const Dev& d, uint32_t i, int32_t r) {
+  return r >= SHARE_AGE - 1 ? d.fstart[(size_t)i * 16 + ((uint32_t)(r - (SHARE_AGE - 1)) & 15u)] : 0u;
+}
 __device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }
 __device__ inline bool faults(const Dev& d, int32_t r) { return d.fault_end < 0 || r < d.fault_end; }
 __device__ inline bool part_blocks(const Dev& d, int32_t r, uint32_t a, uint32_t b) {
@@ -90,6 +107,14 @@ __device__ inline uint32_t mulzc(const uint32_t* tab, uint32_t x, uint32_t c) {
   const uint32_t* t = tab + c * 128;
   return t[x & 15] ^ t[16 + ((x >> 4) & 15)] ^ t[32 + ((x >> 8) & 15)] ^ t[48 + ((x >> 12) & 15)] ^
          t[64 + ((x >> 16) & 15)] ^ t[80 + ((x >> 20) & 15)] ^ t[96 + ((x >> 24) & 15)] ^ t[112 + (x >> 28)];
+}
+__device__ inline uint32_t mulzb(const uint32_t* tab, uint32_t x, uint32_t c) {
+  const uint32_t* t = tab + c * 1024;
+  return t[x & 255] ^ t[256 + ((x >> 8) & 255)] ^ t[512 + ((x >> 16) & 255)] ^ t[768 + (x >> 24)];
+}
+__device__ inline void load_zbtab(const Dev& d, uint32_t* lds) {
+  for (uint32_t k = threadIdx.x; k < ZB; k += blockDim.x) lds[k] = d.zbtab[k];
+  __syncthreads();
 }
 __device__ inline void load_ztab(const Dev& d, uint32_t* lds) {
   for (uint32_t k = threadIdx.x; k < ZT * 128; k += blockDim.x) lds[k] = d.ztab[k];

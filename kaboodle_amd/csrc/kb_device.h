@@ -25,6 +25,8 @@ constexpr int MAXID = 32;           // identity bytes
 constexpr int ADDR_LEN = 20;        // "10.100.100.ddd:ppppp"
 constexpr int TICK_MAX = 3 * SLOTS + 1 + PAQ;   // unicast emissions of one tick
 constexpr int FLOYD_MAX_N = 262144; // LDS bitmap bound for truncated Join responses
+constexpr uint32_t LOGCAP = 2048;    // freshness log entries per node (power of two)
+constexpr uint32_t LOG_INVALID = 0xFFFFFFFFu;
 // stamp byte encoding
 constexpr uint8_t ST_UNKNOWN = 0, ST_SUSPECT = 1, ST_ANCIENT = 2;
 constexpr int EPOCH = 64, EOFF = 192;
@@ -38,7 +40,7 @@ constexpr uint32_t CRC_POLY = 0xEDB88320u;
 
 // error codes raised on the device (checked by the host after each step)
 enum : uint32_t { DERR_NONE = 0, DERR_SLOTS = 1, DERR_OUTBOX = 2, DERR_PAYLOAD = 3, DERR_FLOYD = 4, DERR_INBOX = 5,
-                  DERR_RESP = 6 };
+                  DERR_RESP = 6, DERR_LOG = 7 };
 
 // ---- records ------------------------------------------------------------------------------------
 struct Msg {            // 32 B unicast record

@@ -100,6 +100,12 @@ __global__ __launch_bounds__(1024) void k_truefp(Dev d) {
   if (t == 0) d.truefp[0] = finish_fp(d, sraw[0], scnt[0]);
 }
 
+// round start of every node's freshness log window
+__global__ void k_log_mark(Dev d, int32_t r) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < d.C) d.fstart[(size_t)i * 16 + ((uint32_t)r & 15u)] = d.flog_n[i];
+}
+
 // ================================================================================================
 // Broadcast phase: Failed then Join deliveries of round r-1's broadcasts (src/kaboodle.rs:256-311)
 // ================================================================================================
@@ -163,23 +169,35 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r) {
   auto is_susp = [&](uint32_t x) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
   uint32_t n = d.n[i];
   const uint32_t n0 = n;
+  uint32_t fn = d.flog_n[i];
+  const uint8_t now = enc(r, r);
   uint32_t lost_cnt = 0, removed_cnt = 0;
   unsigned long long segs = 0;
   const bool honour = d.failed_mode == KB_FAILED_SIM_SENDER;
   // ---- Failed(p) group (src/kaboodle.rs:268-283) ----
-  // Entries are independent unless a sender was itself named as failed by an earlier entry (dep):
-  // chunks run in parallel (a repeated peer is removed once: the atomic returns whether it was set)
-  // until such an entry would act, then the exact in-order loop takes over.
-  uint32_t c0 = pb.nf;
+  // In-order semantics, 64 entries at a time.  An entry acts iff it is delivered, names neither the
+  // receiver nor comes from it, and its sender is still a member when it is reached.  Membership at the
+  // chunk start is in B (earlier chunks applied); inside the chunk only an entry whose sender is named
+  // by an earlier entry (dep) can change its mind: those are resolved in lane order with one ballot
+  // each (killed iff an earlier acting lane of the chunk names its sender).  The acting entries are
+  // then applied together: the atomic's return says whether the peer was still present (removed once).
   for (uint32_t c = 0; c < pb.nf; c += 64) {
     const uint32_t e = c + l;
     const bool valid = e < pb.nf;
     const BCast b = valid ? pb.bfail[e] : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
     const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
-    const bool cond = valid && b.sender != i && !lost && b.peer != i && honour && mem(b.sender) && mem(b.peer);
-    if (__ballot(cond && pb.dep[e])) { c0 = c; break; }
+    const bool base = valid && b.sender != i && !lost && b.peer != i && honour && mem(b.sender);
+    unsigned long long actm = __ballot(base);
+    unsigned long long depm = __ballot(base && pb.dep[e]);
+    while (depm) {
+      const uint32_t q = (uint32_t)(__ffsll((long long)depm) - 1);
+      depm &= depm - 1;
+      const uint32_t s_q = bcast(b.sender, q);
+      const unsigned long long killers = __ballot(((actm >> l) & 1ull) && b.peer == s_q) & ((1ull << q) - 1ull);
+      if (killers) actm &= ~(1ull << q);
+    }
     lost_cnt += __popcll(__ballot(lost));
-    if (cond) {
+    if ((actm >> l) & 1ull) {
       const uint32_t m = 1u << (b.peer & 31);
       if (atomicAnd(&B[b.peer >> 5], ~m) & m) {
         removed_cnt++;
@@ -191,25 +209,6 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r) {
     __builtin_amdgcn_wave_barrier();
   }
   removed_cnt = wave_sum(removed_cnt);
-  for (uint32_t c = c0; c < pb.nf; c += 64) {          // exact in-order tail
-    const uint32_t e = c + l;
-    const bool valid = e < pb.nf;
-    const BCast b = valid ? pb.bfail[e] : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
-    const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
-    lost_cnt += __popcll(__ballot(lost));
-    const uint32_t m = pb.nf - c < 64 ? pb.nf - c : 64;
-    for (uint32_t q = 0; q < m; ++q) {
-      const uint32_t s_q = bcast(b.sender, q), p_q = bcast(b.peer, q);
-      if (s_q == i || bcast((uint32_t)lost, q) || p_q == i || !honour) continue;
-      __builtin_amdgcn_s_waitcnt(0);
-      __builtin_amdgcn_wave_barrier();
-      if (!mem(s_q) || !mem(p_q)) continue;
-      if (l == 0) atomicAnd(&B[p_q >> 5], ~(1u << (p_q & 31)));
-      removed_cnt++;
-      if (is_susp(p_q) && l == 0) susp_clear(d, i, p_q);
-      segs |= seg_bit(d, p_q);
-    }
-  }
   n -= removed_cnt;
   __builtin_amdgcn_s_waitcnt(0);
   __builtin_amdgcn_wave_barrier();
@@ -238,9 +237,13 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r) {
       }
     }
     const unsigned long long respm = __ballot(resp);
+    const bool logit = deliver && (!known || rw[b.sender] != now);
+    const unsigned long long lgm = __ballot(logit);
+    if (logit) d.flog[(size_t)i * LOGCAP + ((fn + __popcll(lgm & ((1ull << l) - 1ull))) & (LOGCAP - 1))] = log_entry(b.sender, r);
+    fn += __popcll(lgm);
     if (deliver) {
       if (known && is_susp(b.sender)) susp_clear(d, i, b.sender);
-      rw[b.sender] = enc(r, r);
+      rw[b.sender] = now;
       if (isnew) { atomicOr(&B[b.sender >> 5], 1u << (b.sender & 31)); segs |= seg_bit(d, b.sender); }
     }
     const uint32_t sz = resp ? (d.uniform ? (nq < d.capj ? nq : d.capj) : nq) : 0;
@@ -262,6 +265,7 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r) {
   }
   if (l == 0) {
     d.n[i] = n;
+    d.flog_n[i] = fn;
     mark(d, i, segs);
     if (n != n0) d.dirty[i] = 1;
     pb.nresp[i] = nresp; pb.paysum[i] = paysum; pb.nbase[i] = nbase;
@@ -313,17 +317,42 @@ __device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint
   return w * 32 + (__ffs(x) - 1);
 }
 constexpr uint32_t RESP_LDS_W = 131072;   // rows up to this many ids keep their bitsets in LDS
+__host__ __device__ inline size_t resp_words(uint32_t NW, uint32_t NB) { return 2ull * NW + 2ull * (NB + 1); }
+
+// exclusive prefix of the member counts of X's 256-id blocks into XP[0..NB], XP[NB] = total (block-wide)
+__device__ uint32_t block_prefix(const uint32_t* X, uint32_t* XP, uint32_t NB, uint32_t* s_red) {
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  const uint32_t per = (NB + T - 1) / T;
+  uint32_t bc = 0;
+  for (uint32_t k = t * per; k < (t + 1) * per && k < NB; ++k) {
+    uint32_t c = 0;
+    for (uint32_t w = 0; w < 8; ++w) c += __popc(X[k * 8 + w]);
+    XP[k] = c; bc += c;
+  }
+  uint32_t ex = wave_excl(bc);
+  const uint32_t wt = wave_sum(bc);
+  __syncthreads();
+  if (lane() == 0) s_red[t >> 6] = wt;
+  __syncthreads();
+  for (uint32_t w = 0; w < (t >> 6); ++w) ex += s_red[w];
+  uint32_t tot = 0;
+  for (uint32_t w = 0; w < T / 64; ++w) tot += s_red[w];
+  for (uint32_t k = t * per; k < (t + 1) * per && k < NB; ++k) { const uint32_t c = XP[k]; XP[k] = ex; ex += c; }
+  if (t == 0) XP[NB] = tot;
+  __syncthreads();
+  return tot;
+}
 
 __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint32_t* nodes, const uint32_t* nnodes_p,
                                                    OutBuf ob, int32_t r, uint32_t* gscratch) {
   extern __shared__ uint32_t lds_dyn[];
-  // rows wider than RESP_LDS_W keep the three bitsets in a per-workgroup slice of global scratch
-  uint32_t* lds = gscratch ? gscratch + (size_t)blockIdx.x * (3 * d.NWR + d.W / 256 + 1) : lds_dyn;
   const uint32_t NW = d.NWR, NB = d.W / 256;
-  uint32_t* B = lds;                 // row membership         [NW]
-  uint32_t* S = B + NW;              // members at response    [NW]
-  uint32_t* SP = S + NW;             // block prefix of S      [NB + 1]
-  uint32_t* F = SP + NB + 1;         // kept-rank bitmap       [NW]
+  // rows wider than RESP_LDS_W keep their bitsets in a per-workgroup slice of global scratch
+  uint32_t* lds = gscratch ? gscratch + (size_t)blockIdx.x * resp_words(NW, NB) : lds_dyn;
+  uint32_t* B = lds;                 // row membership after the Join group   [NW]
+  uint32_t* BP = B + NW;             // block prefix of B                     [NB + 1]
+  uint32_t* S = BP + NB + 1;         // members at response (unsampled path)  [NW]
+  uint32_t* SP = S + NW;             // block prefix of S                     [NB + 1]
   __shared__ uint32_t s_red[16];
   const uint32_t t = threadIdx.x, T = blockDim.x;
   const uint32_t nnodes = *nnodes_p;
@@ -332,8 +361,11 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
     const uint32_t* bi = bits_of(d, i);
     for (uint32_t k = t; k < NW; k += T) B[k] = bi[k];
     __syncthreads();
+    const uint32_t nB = block_prefix(B, BP, NB, s_red);
     const unsigned long long* nm = pb.newmask + (size_t)i * pb.JW;
     const unsigned long long* rm = pb.respmask + (size_t)i * pb.JW;
+    uint32_t nnew = 0;
+    for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
     uint32_t poff = ob.poff[i], q = 0, ins_before = 0;
     for (uint32_t wj = 0; wj < pb.JW; ++wj) {
       unsigned long long rmw = rm[wj];
@@ -342,66 +374,43 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
         const uint32_t bit = (uint32_t)(__ffsll((long long)rmw) - 1);
         const uint32_t K = wj * 64 + bit;
         rmw &= rmw - 1;
-        const uint32_t expect = pb.nbase[i] + ins_before + __popcll(nmw & ((2ull << bit) - 1ull));
+        const uint32_t upto = ins_before + __popcll(nmw & ((2ull << bit) - 1ull));   // new joiners <= K
+        const uint32_t expect = pb.nbase[i] + upto;
         const uint32_t a = pb.bjoin[K].sender;
-        // S = B minus the joiners inserted after K
-        for (uint32_t k = t; k < NW; k += T) S[k] = B[k];
-        __syncthreads();
-        for (uint32_t e = K + 1 + t; e < pb.nj; e += T)
-          if (newbit(nm, e)) { const uint32_t x = pb.bjoin[e].sender; atomicAnd(&S[x >> 5], ~(1u << (x & 31))); }
-        __syncthreads();
-        // exclusive block prefix of S (8 words per block)
-        uint32_t bc = 0;
-        const uint32_t per = (NB + T - 1) / T;
-        for (uint32_t k = t * per; k < (t + 1) * per && k < NB; ++k) {
-          uint32_t c = 0;
-          for (uint32_t w = 0; w < 8; ++w) c += __popc(S[k * 8 + w]);
-          SP[k] = c; bc += c;
-        }
-        uint32_t ex = wave_excl(bc);
-        const uint32_t wt = wave_sum(bc);
-        if (lane() == 0) s_red[t >> 6] = wt;
-        __syncthreads();
-        for (uint32_t w = 0; w < (t >> 6); ++w) ex += s_red[w];
-        uint32_t nk = 0;
-        for (uint32_t w = 0; w < T / 64; ++w) nk += s_red[w];
-        for (uint32_t k = t * per; k < (t + 1) * per && k < NB; ++k) { const uint32_t c = SP[k]; SP[k] = ex; ex += c; }
-        if (t == 0) SP[NB] = nk;
-        __syncthreads();
+        // the member set at this response: B minus the joiners inserted after K
+        const uint32_t nk = nB - (nnew - upto);
         const bool sample = d.uniform && nk > d.capj;
         const uint32_t cap = sample ? d.capj : nk;
         uint32_t* pay = ob.pay + poff;
-        if (!sample) {
+        if (sample) {
+          // kept ranks = first cap images of the keyed permutation; rank -> id by select on B,
+          // stepping over later joiners (least fixed point of e = #later joiners <= select(y + e))
+          const U4 key = philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1);
+          for (uint32_t k = t; k < cap; k += T) {
+            const uint32_t y = prp_walk(k, nk, key);
+            uint32_t e = 0, x;
+            while (true) {
+              x = bm_select(B, BP, NB, y + e);
+              uint32_t c = 0;
+              for (uint32_t f = K + 1; f < pb.nj; ++f)
+                if (newbit(nm, f)) c += pb.bjoin[f].sender <= x;
+              if (c == e) break;
+              e = c;
+            }
+            pay[k] = x;
+          }
+        } else {
+          for (uint32_t k = t; k < NW; k += T) S[k] = B[k];
+          __syncthreads();
+          for (uint32_t f = K + 1 + t; f < pb.nj; f += T)
+            if (newbit(nm, f)) { const uint32_t x = pb.bjoin[f].sender; atomicAnd(&S[x >> 5], ~(1u << (x & 31))); }
+          __syncthreads();
+          block_prefix(S, SP, NB, s_red);
           for (uint32_t w = t; w < NW; w += T) {        // every member, position = rank
             uint32_t x = S[w];
             if (!x) continue;
             uint32_t pos = bm_rank(S, SP, w * 32);
             while (x) { const uint32_t b = __ffs(x) - 1; x &= x - 1; pay[pos++] = w * 32 + b; }
-          }
-        } else {
-          const uint32_t FW = (nk + 31) / 32;
-          for (uint32_t w = t; w < FW; w += T) F[w] = 0;
-          __syncthreads();
-          const U4 key = philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1);
-          for (uint32_t k = t; k < cap; k += T) {
-            const uint32_t y = prp_walk(k, nk, key);
-            atomicOr(&F[y >> 5], 1u << (y & 31));
-          }
-          __syncthreads();
-          // kept ranks in increasing order -> output slots
-          const uint32_t fper = (FW + T - 1) / T;
-          uint32_t fc = 0;
-          for (uint32_t w = t * fper; w < (t + 1) * fper && w < FW; ++w) fc += __popc(F[w]);
-          uint32_t fex = wave_excl(fc);
-          const uint32_t fwt = wave_sum(fc);
-          __syncthreads();
-          if (lane() == 0) s_red[t >> 6] = fwt;
-          __syncthreads();
-          for (uint32_t w = 0; w < (t >> 6); ++w) fex += s_red[w];
-          uint32_t o = fex;
-          for (uint32_t w = t * fper; w < (t + 1) * fper && w < FW; ++w) {
-            uint32_t x = F[w];
-            while (x) { const uint32_t b = __ffs(x) - 1; x &= x - 1; pay[o++] = bm_select(S, SP, NB, w * 32 + b); }
           }
         }
         if (t == 0) {

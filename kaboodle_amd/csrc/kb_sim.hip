@@ -274,9 +274,9 @@ static int upload_segments(kb_sim* s) {
   s->d.uniform = uniform ? 1 : 0;
   s->d.L = ADDR_LEN + s->cfg.id_len;
   const uint32_t Z = h_xpow8(s->d.L);
-  std::vector<uint32_t> zpow(C + 2);
+  std::vector<uint32_t> zpow(std::max<uint32_t>(C + 2, 17));     // the tables below need Z^0..Z^16
   zpow[0] = 0x80000000u;
-  for (uint32_t k = 1; k < C + 2; ++k) zpow[k] = multmodp(Z, zpow[k - 1]);
+  for (size_t k = 1; k < zpow.size(); ++k) zpow[k] = multmodp(Z, zpow[k - 1]);
   std::vector<uint32_t> ztab(17 * 128);
   for (uint32_t c = 0; c <= 16; ++c)
     for (uint32_t k = 0; k < 8; ++k)
@@ -286,6 +286,11 @@ static int upload_segments(kb_sim* s) {
   HIPCHK(hipMemcpy(s->d.seglen, seglen.data(), 4ull * C, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(s->d.zpow, zpow.data(), 4ull * (C + 2), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(s->d.ztab, ztab.data(), 4ull * ztab.size(), hipMemcpyHostToDevice));
+  std::vector<uint32_t> zb(9 * 1024);
+  for (uint32_t c = 0; c < 9; ++c)
+    for (uint32_t k = 0; k < 4; ++k)
+      for (uint32_t v = 0; v < 256; ++v) zb[c * 1024 + k * 256 + v] = multmodp(zpow[c], v << (8 * k));
+  HIPCHK(hipMemcpy(s->d.zbtab, zb.data(), 4ull * zb.size(), hipMemcpyHostToDevice));
   const size_t hn = (size_t)(s->W / 8) * 256;
   k_build_htab<<<(unsigned)((hn + 255) / 256), 256>>>(s->d);
   HIPCHK(hipDeviceSynchronize());
@@ -295,8 +300,8 @@ static int upload_segments(kb_sim* s) {
 static void free_all(kb_sim* s) {
   Dev& d = s->d;
   void* ptrs[] = {d.stamp, d.bits, d.segp, d.sdirty, d.dirty, d.alive, d.abits, d.start_round, d.n, d.fp,
-                  d.last_bcast, d.susp, d.cur, d.paq, d.paq_n, d.cseg, d.segmul, d.seglen, d.zpow, d.ztab, d.htab,
-                  d.stats, d.ctr, d.truefp,
+                  d.last_bcast, d.susp, d.cur, d.paq, d.paq_n, d.cseg, d.segmul, d.seglen, d.zpow, d.ztab, d.zbtab, d.htab,
+                  d.stats, d.ctr, d.truefp, d.flog, d.flog_n, d.fstart,
                   s->ob[0].msgs, s->ob[0].pay, s->ob[0].off, s->ob[0].cap, s->ob[0].cnt, s->ob[0].poff,
                   s->ob[1].msgs, s->ob[1].pay, s->ob[1].off, s->ob[1].cap, s->ob[1].cnt, s->ob[1].poff,
                   s->wc.status, s->wc.cnt1, s->wc.bnd, s->wc.bpay, s->wc.cursor, s->wc.in_off, s->wc.inbox,
@@ -346,8 +351,9 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
   A(d.stamp, (size_t)C * W); A(d.bits, (size_t)C * d.NWR); A(d.segp, (size_t)C * NSEG); A(d.sdirty, C);
   A(d.dirty, C); A(d.alive, C); A(d.abits, d.NWR); A(d.start_round, C); A(d.n, C); A(d.fp, C);
   A(d.last_bcast, C); A(d.susp, (size_t)C * SLOTS); A(d.cur, (size_t)C * CSLOTS); A(d.paq, (size_t)C * PAQ);
-  A(d.paq_n, C); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.ztab, 17 * 128);
+  A(d.paq_n, C); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1);
+  A(d.flog, (size_t)C * LOGCAP); A(d.flog_n, C); A(d.fstart, (size_t)C * 16);
   s->msg_cap = std::max<uint32_t>(8u * C + (uint32_t)TICK_MAX * C, 1u << 16);
   s->pay_cap = std::max<uint32_t>((d.capk + 1) * C, 1u << 24);
   for (int b = 0; b < 2; ++b) {
@@ -445,6 +451,7 @@ static int step_round(kb_sim* s) {
   }
   k_alive_bits<<<(d.NWR + tb - 1) / tb, tb, 0, st>>>(d);
   k_truefp<<<1, 1024, 0, st>>>(d);
+  k_log_mark<<<gnode, tb, 0, st>>>(d, r);
   // 2. broadcasts of round r-1
   OutBuf& o0 = s->ob[0];
   PhaseB pb;
@@ -491,7 +498,7 @@ static int step_round(kb_sim* s) {
     if (msg_tot > s->msg_cap || pay_tot > s->pay_cap) { seterr("wave-0 outbox exceeds preallocated capacity"); return KB_CAPACITY; }
     if (resp_nodes) {
       const uint32_t grid = std::min<uint32_t>(resp_nodes, 4096);
-      const size_t words = 3ull * d.NWR + s->W / 256 + 1;
+      const size_t words = resp_words(d.NWR, s->W / 256);
       uint32_t* scratch = nullptr;
       size_t lds = 4 * words;
       if (s->W > RESP_LDS_W) {
@@ -509,7 +516,7 @@ static int step_round(kb_sim* s) {
   // 3. tick
   k_tick_pre<<<gwave, 256, 0, st>>>(d, o0, s->bs, r);
   (void)hipEventRecord(s->ev0, st);
-  k_sweep<<<((C + 63) / 64 * s->S + 3) / 4, 256, 0, st>>>(d, s->so);
+  k_sweep<<<((C + 63) / 64 + 3) / 4 * s->S, 256, 0, st>>>(d, s->so);
   (void)hipEventRecord(s->ev1, st);
   k_tick_post<<<gnode, tb, 0, st>>>(d, s->so, o0, r);
   {
@@ -553,13 +560,11 @@ static int step_round(kb_sim* s) {
   }
   k_round_end<<<1, 1, 0, st>>>(d, r);
   (void)hipEventRecord(s->er1, st);
-  uint32_t tot[2], alive_now = 0;
+  uint32_t tot[2];
   HIPCHK(hipMemcpyAsync(tot, s->scan_tot, 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipMemcpyAsync(&alive_now, d.ctr + C_LASTALIVE, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   s->nj = tot[0]; s->nf = tot[1];
   s->bj_total += s->nj; s->bf_total += s->nf;
-  s->sweep_bytes += (uint64_t)alive_now * (C + C / 8);
   float ms = 0;
   (void)hipEventElapsedTime(&ms, s->ev0, s->ev1); s->sweep_ms += ms; s->sweep_launches++;
   (void)hipEventElapsedTime(&ms, s->er0, s->er1); s->round_ms += ms; s->round_launches++;
@@ -797,13 +802,20 @@ extern "C" int kb_sim_kernel_time(kb_sim* s, int kind, double* ms, uint64_t* lau
   else { *ms = s->round_ms; *launches = s->round_launches; }
   return KB_OK;
 }
+static uint64_t sweep_counter(kb_sim* s) {
+  unsigned long long v = 0;
+  if (hipMemcpy(&v, s->d.stats + S_SWEEPB, 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  return v;
+}
 extern "C" int kb_sim_reset_kernel_time(kb_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
-  s->sweep_ms = s->round_ms = 0; s->sweep_launches = s->round_launches = 0; s->sweep_bytes = 0;
+  s->sweep_ms = s->round_ms = 0; s->sweep_launches = s->round_launches = 0;
+  s->sweep_bytes = sweep_counter(s);            // baseline of the device-side byte counter
   return KB_OK;
 }
+// bytes of member bits and stamp lines the row sweep read since the last reset (counted in-kernel)
 extern "C" int kb_sim_sweep_bytes(kb_sim* s, uint64_t* bytes) {
   if (!s || !bytes) return KB_INVALID_ARGUMENT;
-  *bytes = s->sweep_bytes;
+  *bytes = sweep_counter(s) - s->sweep_bytes;
   return KB_OK;
 }

@@ -145,46 +145,66 @@ __device__ inline void top5_insert(uint32_t (&k)[5], uint32_t nk) {
 }
 __device__ inline uint32_t thr5(const uint32_t (&k)[5]) { return k[4] == 0xFFFFFFFFu ? 256u : (k[4] >> 24); }
 
+// One 128-id step of one lane's row.  The member bits (16 B) are read when the segment is refolded
+// or when the step can still change a top-5 list; the stamp bytes (128 B) only in the latter case.
+// A part's list is final once it holds five ancient (minimum-stamp) entries: later ids of that part
+// have larger rot and can never displace them.
 template <bool FOLD>
-__device__ inline void sweep_step(const Dev& d, const uint32_t* ztab, const uint8_t* rw, const uint32_t* bw,
+__device__ __attribute__((always_inline)) inline void sweep_step(const Dev& d, const uint32_t* zb, const uint8_t* rw, const uint32_t* bw,
                                   uint32_t i, uint32_t p, uint32_t col, uint32_t (&A)[5], uint32_t (&B)[5],
-                                  uint32_t& TA, uint32_t& TB, uint32_t& raw, uint32_t& cnt) {
+                                  uint32_t& raw, uint32_t& cnt, uint32_t& nbytes) {
+  // a part's threshold is the stamp of its 5th key (256 while it has fewer than five)
+  const bool need = !(d.ablate & 2) && ((thr5(A) > ST_ANCIENT && col < p) || (thr5(B) > ST_ANCIENT && col + 128 > p));
+  if (!FOLD && !need) return;
+  const uint4 mb = *reinterpret_cast<const uint4*>(bw + (col >> 5));
+  nbytes += 16;
+  if (FOLD) {
+    const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
+    const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      const uint32_t m8 = (mw[h >> 2] >> (8 * (h & 3))) & 0xFFu;
+      if (m8) {
+        const uint32_t c = __popc(m8);
+        raw = mulzb(zb, raw, c) ^ ht[h * 256 + m8];
+        cnt += c;
+      }
+    }
+  }
+  if (!need) return;
+  if (!(mb.x | mb.y | mb.z | mb.w)) return;        // no member in these 128 ids: stamps are irrelevant
+  nbytes += 128;
+  const uint32_t C = d.C;
   uint4 v[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const uint4*>(rw + col + 16 * q);
-  const uint4 mb = *reinterpret_cast<const uint4*>(bw + (col >> 5));
   const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
-  if (FOLD) {
-#pragma unroll
-    for (int h = 0; h < 16; ++h) fold_half(d, ztab, (col >> 3) + h, (mw[h >> 2] >> (8 * (h & 3))) & 0xFFu, raw, cnt);
-  }
-  // parts of this step: ids [col, col+128) below p belong to A, the rest to B
-  if (d.ablate & 2) return;
-  const bool needA = TA > ST_ANCIENT && col < p;
-  const bool needB = TB > ST_ANCIENT && col + 128 > p;
-  if (!(needA || needB)) return;
-  const uint32_t C = d.C;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const uint32_t w4[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-    const uint32_t mbits = (mw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const uint32_t b = (w4[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+    uint32_t cm = (nzmask4(v[q].x & 0xFEFEFEFEu) | (nzmask4(v[q].y & 0xFEFEFEFEu) << 4) |
+                   (nzmask4(v[q].z & 0xFEFEFEFEu) << 8) | (nzmask4(v[q].w & 0xFEFEFEFEu) << 12)) &
+                  ((mw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu);
+    while (cm) {
+      const uint32_t t = __ffs(cm) - 1;
+      cm &= cm - 1;
+      const uint32_t word = (t & 8) ? ((t & 4) ? v[q].w : v[q].z) : ((t & 4) ? v[q].y : v[q].x);
+      const uint32_t b = (word >> (8 * (t & 3))) & 0xFFu;
       const uint32_t j = col + 16 * q + t;
-      if (!((mbits >> t) & 1u) || b < ST_ANCIENT || j == i) continue;
-      if (j >= p) { if (b < TB) { top5_insert(B, (b << 24) | (j - p)); TB = thr5(B); } }
-      else if (b < TA) { top5_insert(A, (b << 24) | (j + C - p)); TA = thr5(A); }
+      if (j == i) continue;
+      if (j >= p) { if (b < thr5(B)) top5_insert(B, (b << 24) | (j - p)); }
+      else if (b < thr5(A)) top5_insert(A, (b << 24) | (j + C - p));
     }
   }
 }
 
 __global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
-  __shared__ uint32_t ztab[ZT * 128];
-  load_ztab(d, ztab);
+  __shared__ uint32_t zb[ZB];
+  load_zbtab(d, zb);
+  // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so split s = blockIdx % S keeps each
+  // XCD on 1/min(S,8) of the columns and its slice of the half-block CRC tables resident in its L2.
   const uint32_t S = so.S;
-  const uint32_t wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint32_t g = wave / S, s = wave % S;
+  const uint32_t s = blockIdx.x % S;
+  const uint32_t g = (blockIdx.x / S) * 4 + (threadIdx.x >> 6);
   const uint32_t i0 = g * 64 + lane();
   const bool act = i0 < d.C && d.alive[i0];
   // the ballot is taken once with the full wave active: inside the select below it would run
@@ -201,7 +221,7 @@ __global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
   uint32_t A[5], B[5];
 #pragma unroll
   for (int k = 0; k < 5; ++k) { A[k] = 0xFFFFFFFFu; B[k] = 0xFFFFFFFFu; }
-  uint32_t TA = 256, TB = 256;
+  uint32_t nbytes = 0;
   const uint32_t spp = NSEG / S;
   unsigned long long folded = 0;
   for (uint32_t k = s * spp; k < (s + 1) * spp; ++k) {
@@ -209,12 +229,18 @@ __global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
     uint32_t raw = 0, cnt = 0;
     const bool mine = ((sd >> k) & 1ull) && !(d.ablate & 1);
     if (__ballot(mine)) {                 // wave-uniform: one pass for the whole wave
-      for (uint32_t col = c0; col < c1; col += 128) sweep_step<true>(d, ztab, rw, bw, i, p, col, A, B, TA, TB, raw, cnt);
+      for (uint32_t col = c0; col < c1; col += 128)
+        sweep_step<true>(d, zb, rw, bw, i, p, col, A, B, raw, cnt, nbytes);
       if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; }
     } else {
-      for (uint32_t col = c0; col < c1; col += 128) sweep_step<false>(d, ztab, rw, bw, i, p, col, A, B, TA, TB, raw, cnt);
+      const bool need = (thr5(A) > ST_ANCIENT && c0 < p) || (thr5(B) > ST_ANCIENT && c1 > p);
+      if (!__ballot(act && need)) continue;   // no list of this wave can change in this segment
+      for (uint32_t col = c0; col < c1; col += 128)
+        sweep_step<false>(d, zb, rw, bw, i, p, col, A, B, raw, cnt, nbytes);
     }
   }
+  const uint32_t wb = wave_sum(act ? nbytes : 0u);
+  if (lane() == 0 && wb) atomicAdd(&d.stats[S_SWEEPB], (unsigned long long)wb);
   if (!act) return;
   if (folded) atomicAnd(&d.sdirty[i], ~folded);
   uint32_t* out = so.part + ((size_t)i * S + s) * 10;
@@ -245,7 +271,15 @@ __global__ void k_tick_post(Dev d, SweepOut so, OutBuf ob, int32_t r) {
       while (k < SLOTS && sl[k].kind) ++k;
       if (k == SLOTS) set_err(d, DERR_SLOTS);
       else { sl[k].peer = t; sl[k].kind = SK_WFP; sl[k].since = r; }
-      row_of(d, i)[t] = ST_SUSPECT;
+      uint8_t* tb = row_of(d, i) + t;
+      if (*tb == enc(r, r)) {            // stamped Known(now) earlier this round: retire its log entry
+        const uint32_t e = log_entry(t, r), fe = d.flog_n[i];
+        for (uint32_t q = d.fstart[(size_t)i * 16 + ((uint32_t)r & 15u)]; q < fe; ++q) {
+          uint32_t& slot = d.flog[(size_t)i * LOGCAP + (q & (LOGCAP - 1))];
+          if (slot == e) slot = LOG_INVALID;
+        }
+      }
+      *tb = ST_SUSPECT;
       if (oseq >= ob.cap[i]) set_err(d, DERR_OUTBOX);
       else ob.msgs[ob.off[i] + oseq] = Msg{t, i, oseq, K_PING, 0, 0, 0, 0};
       oseq++;

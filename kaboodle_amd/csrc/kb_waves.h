@@ -103,8 +103,21 @@ __global__ void k_kp_prologue(Dev d, OutBuf ob, WaveCtl wc, int32_t r) {
     const Msg m = ob.msgs[wc.kp_list[it]];
     uint8_t* rw = row_of(d, m.dest);
     const bool was = is_mem(d, m.dest, m.sender);
-    const uint8_t b = was ? rw[m.sender] : ST_UNKNOWN;
-    rw[m.sender] = now;
+    // byte update by CAS on its word: exactly one envelope per (dest, sender) sees the transition to
+    // Known(now) and appends it to the freshness log
+    uint32_t* wp = reinterpret_cast<uint32_t*>(rw + (m.sender & ~3u));
+    const uint32_t sh = 8 * (m.sender & 3u);
+    uint32_t old = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), prevb;
+    while (true) {
+      prevb = (old >> sh) & 0xFFu;
+      if (prevb == now) break;
+      const uint32_t res = atomicCAS(wp, old, (old & ~(0xFFu << sh)) | ((uint32_t)now << sh));
+      if (res == old) break;
+      old = res;
+    }
+    if (prevb != now)
+      d.flog[(size_t)m.dest * LOGCAP + (atomicAdd(&d.flog_n[m.dest], 1u) & (LOGCAP - 1))] = log_entry(m.sender, r);
+    const uint8_t b = was ? (uint8_t)prevb : ST_UNKNOWN;
     if (!was && mem_set(d, m.dest, m.sender)) mark(d, m.dest, seg_bit(d, m.sender));
     if (b <= ST_SUSPECT) mark_touched(d, wc, m.dest);
   }
@@ -145,7 +158,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     const uint32_t i = wc.active[it];
     uint8_t* rw = row_of(d, i);
     const uint32_t* bw = bits_of(d, i);
-    uint32_t n = d.n[i], fp = d.fp[i], oseq = 0, pay_used = 0;
+    uint32_t n = d.n[i], fp = d.fp[i], oseq = 0, pay_used = 0, fn = d.flog_n[i];
     bool dirty = d.dirty[i] != 0, need_sync = false;
     unsigned long long segs = 0;
     if (l < SLOTS) s_susp[wv][l] = d.susp[(size_t)i * SLOTS + l];
@@ -205,7 +218,11 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           n++; dirty = true; segs |= seg_bit(d, s);
           if (l == 0) const_cast<uint32_t*>(bw)[s >> 5] |= 1u << (s & 31);   // single writer of this row
         }
-        if (b != now) { if (l == 0) rw[s] = now; need_sync = true; }
+        if (b != now) {
+          if (l == 0) { rw[s] = now; d.flog[(size_t)i * LOGCAP + (fn & (LOGCAP - 1))] = log_entry(s, r); }
+          fn++;
+          need_sync = true;
+        }
         last_sender = s;
         __builtin_amdgcn_wave_barrier();
       }
@@ -255,40 +272,52 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           break;
         }
         case K_KPR: {                                                // :473-512
+          // reply = {p Known, p != self, p != sender, stamped within SHARE_AGE}, never truncated;
+          // > 10240 B is lost at the receiver (Q3), so only the count matters once it exceeds capk
           if (need_sync) { wave_mem_sync(); need_sync = false; }
           const uint32_t poff = ob.poff[i] + pay_used;
           uint32_t total = 0;
           uint64_t size = 8 + (d.seglen[i] - ADDR_LEN) + 4 + 8;
           bool over = false;
-          for (uint32_t c = 0; c < d.W && !over; c += 1024) {
-            const uint32_t j0 = c + l * 16;
-            const uint4 v = *reinterpret_cast<const uint4*>(rw + j0);
-            const uint32_t mb = (bw[j0 >> 5] >> (j0 & 16)) & 0xFFFFu;
-            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-            uint32_t mask = 0;
-#pragma unroll
-            for (int t2 = 0; t2 < 16; ++t2) {
-              const uint32_t b = (w4[t2 >> 2] >> (8 * (t2 & 3))) & 0xFFu, j = j0 + t2;
-              mask |= (uint32_t)(((mb >> t2) & 1u) && b >= fresh_thr && j != i && j != s) << t2;
+          auto take = [&](bool ok, uint32_t j) {
+            const unsigned long long okm = __ballot(ok);
+            const uint32_t pos = total + __popcll(okm & ((1ull << l) - 1ull));
+            if (!d.uniform) size += wave_sum(ok ? 18u + d.seglen[j] - ADDR_LEN : 0u);
+            if (ok && pos < d.paybound) {
+              if (poff + pos < ob.pay_cap) ob.pay[poff + pos] = j;
+              else set_err(d, DERR_PAYLOAD);
             }
-            const uint32_t mc = __popc(mask);
-            uint32_t pos = total + wave_excl(mc);
-            if (!d.uniform) {
-              uint32_t sz = 0, mm = mask;
-              while (mm) { const int t2 = __ffs(mm) - 1; mm &= mm - 1; sz += 18 + d.seglen[j0 + t2] - ADDR_LEN; }
-              size += wave_sum(sz);
-            }
-            while (mask) {
-              const int t2 = __ffs(mask) - 1;
-              mask &= mask - 1;
-              if (pos < d.paybound) {
-                if (poff + pos < ob.pay_cap) ob.pay[poff + pos] = j0 + t2;
-                else set_err(d, DERR_PAYLOAD);
-              }
-              pos++;
-            }
-            total += wave_sum(mc);
+            total += __popcll(okm);
             if (d.uniform && total > d.capk) over = true;
+          };
+          // the log ring holds the newest LOGCAP entries: the whole window when complete; otherwise
+          // those entries are still exact members of the reply, enough to prove it oversize
+          const uint32_t ws = log_window_start(d, i, r);
+          const bool complete = fn - ws <= LOGCAP;
+          for (uint32_t k0 = complete ? ws : fn - LOGCAP; k0 < fn && !over; k0 += 64) {
+            const uint32_t k = k0 + l;
+            const uint32_t e = k < fn ? d.flog[(size_t)i * LOGCAP + (k & (LOGCAP - 1))] : LOG_INVALID;
+            const uint32_t j = e >> 8;
+            bool ok = e != LOG_INVALID && j != i && j != s && r - log_round(e, r) < SHARE_AGE;
+            if (ok) ok = ((bw[j >> 5] >> (j & 31)) & 1u) && rw[j] == enc(log_round(e, r), r);
+            take(ok, j);
+          }
+          if (!complete && !over) {                   // rare: rescan the row itself
+            total = 0;
+            size = 8 + (d.seglen[i] - ADDR_LEN) + 4 + 8;
+            for (uint32_t c = 0; c < d.W && !over; c += 1024) {
+              const uint32_t j0 = c + l * 16;
+              const uint4 v = *reinterpret_cast<const uint4*>(rw + j0);
+              const uint32_t mb = (bw[j0 >> 5] >> (j0 & 16)) & 0xFFFFu;
+              const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+              uint32_t mask = 0;
+#pragma unroll
+              for (int t2 = 0; t2 < 16; ++t2) {
+                const uint32_t b = (w4[t2 >> 2] >> (8 * (t2 & 3))) & 0xFFu, j = j0 + t2;
+                mask |= (uint32_t)(((mb >> t2) & 1u) && b >= fresh_thr && j != i && j != s) << t2;
+              }
+              for (int t2 = 0; t2 < 16; ++t2) take((mask >> t2) & 1u, j0 + t2);
+            }
           }
           over = d.uniform ? total > d.capk : size > (uint64_t)BUFSZ;
           if (over) { if (l == 0) atomicAdd(&d.stats[S_OVERSIZE], 1ull); }
@@ -303,7 +332,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     if (l < CSLOTS) d.cur[(size_t)i * CSLOTS + l] = s_cur[wv][l];
     if (l == 0) {
       if (segs) atomicOr(&d.sdirty[i], segs);
-      d.n[i] = n; d.fp[i] = fp; d.dirty[i] = dirty ? 1 : 0;
+      d.n[i] = n; d.fp[i] = fp; d.dirty[i] = dirty ? 1 : 0; d.flog_n[i] = fn;
       ob.cnt[i] = oseq;
     }
     __builtin_amdgcn_s_waitcnt(0);

