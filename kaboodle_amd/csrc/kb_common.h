@@ -78,6 +78,16 @@ __device__ inline int32_t log_round(uint32_t e, int32_t r) { return r - (int32_t
 __device__ inline uint32_t log_window_start(const Dev& d, uint32_t i, int32_t r) {
   return r >= SHARE_AGE - 1 ? d.fstart[(size_t)i * 16 + ((uint32_t)(r - (SHARE_AGE - 1)) & 15u)] : 0u;
 }
+// copy n 16-byte words global -> LDS with `lanes` cooperating threads (index t), 8 loads in flight each
+__device__ inline void stage16(uint4* dst, const uint4* src, uint32_t n, uint32_t t, uint32_t lanes) {
+  for (uint32_t w0 = 0; w0 < n; w0 += lanes * 8) {
+    uint4 v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { const uint32_t w = w0 + k * lanes + t; if (w < n) v[k] = src[w]; }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { const uint32_t w = w0 + k * lanes + t; if (w < n) dst[w] = v[k]; }
+  }
+}
 __device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }
 __device__ inline bool faults(const Dev& d, int32_t r) { return d.fault_end < 0 || r < d.fault_end; }
 __device__ inline bool part_blocks(const Dev& d, int32_t r, uint32_t a, uint32_t b) {

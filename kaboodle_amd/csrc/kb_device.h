@@ -114,6 +114,8 @@ __device__ inline uint32_t wave_excl(uint32_t v) {
   for (int o = 1; o < 64; o <<= 1) { uint32_t t = __shfl_up(x, o, 64); if (l >= (uint32_t)o) x += t; }
   return x - v;
 }
+// s_waitcnt lgkmcnt(0) only (gfx9 encoding: vmcnt 63, expcnt 7): LDS/SMEM done, memory ops may fly
+__device__ inline void wait_lds() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 __device__ inline uint32_t bcast(uint32_t v, int src) { return __shfl(v, src, 64); }
 // Make this wave's earlier global stores visible to its own later loads (same CU; workgroup scope).
 __device__ inline void wave_mem_sync() {

@@ -138,140 +138,206 @@ __global__ void k_bfail_prep(const BCast* bf, uint32_t nf, uint32_t* gid, uint8_
   gid[q] = g; dep[q] = dp;
 }
 
-// One wave per node.  The node's member bitset is staged in LDS (coalesced read, LDS atomics, one
-// coalesced write-back) when it fits (W <= PB_LDS_W); wider rows work on the global bitset.
+// Same facts for lists up to 2048 entries: one workgroup, LDS hash of peer -> first index naming it.
+__global__ __launch_bounds__(1024) void k_bfail_prep_lds(const BCast* bf, uint32_t nf, uint32_t* gid, uint8_t* dep) {
+  constexpr uint32_t HS = 4096, EMPTY = 0xFFFFFFFFu;
+  __shared__ uint32_t hk[HS], hv[HS];
+  for (uint32_t t = threadIdx.x; t < HS; t += blockDim.x) { hk[t] = EMPTY; hv[t] = EMPTY; }
+  __syncthreads();
+  auto slot0 = [](uint32_t x) { return (x * 0x9E3779B1u) >> 20; };   // 12 bits
+  for (uint32_t e = threadIdx.x; e < nf; e += blockDim.x) {
+    const uint32_t key = bf[e].peer;
+    uint32_t h = slot0(key);
+    while (true) {
+      const uint32_t prev = atomicCAS(&hk[h], EMPTY, key);
+      if (prev == EMPTY || prev == key) { atomicMin(&hv[h], e); break; }
+      h = (h + 1) & (HS - 1);
+    }
+  }
+  __syncthreads();
+  auto first = [&](uint32_t x) -> uint32_t {
+    uint32_t h = slot0(x);
+    while (hk[h] != EMPTY) { if (hk[h] == x) return hv[h]; h = (h + 1) & (HS - 1); }
+    return EMPTY;
+  };
+  for (uint32_t e = threadIdx.x; e < nf; e += blockDim.x) {
+    gid[e] = first(bf[e].peer);
+    const uint32_t f = first(bf[e].sender);
+    dep[e] = f != EMPTY && f < e;
+  }
+}
+
+// Persistent waves, one node at a time.  Each workgroup first stages the broadcast lists in LDS
+// (shared by all its nodes: Failed as {sender | bseq << 23 | dep << 31, peer}, Join as
+// {sender | bseq << 23}); then every wave loops over nodes with the node's member bitset staged in
+// LDS (coalesced read, LDS atomics, write-back of the changed segments).  Lists longer than the LDS
+// budget, or rows wider than PB_LDS_W, are read from HBM instead.
 constexpr uint32_t PB_LDS_W = 524288;
+constexpr uint32_t PB_FMAX = 2048, PB_JMAX = 1024;
 
 template <bool LDSB>
-__global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r) {
+__global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uint32_t lf, uint32_t lj) {
   extern __shared__ uint32_t pb_dyn[];
   __shared__ uint32_t s_sp[4][SLOTS];
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t i = blockIdx.x * wpb + wv;
   const uint32_t l = lane();
-  if (i >= d.C) return;
-  if (!d.alive[i] || d.start_round[i] >= r) {
-    if (l == 0) { pb.nresp[i] = 0; pb.paysum[i] = 0; }
-    return;
+  uint32_t* FL = pb_dyn + (LDSB ? (size_t)wpb * d.NWR : 0);   // [2 * nf] when lf
+  uint32_t* JL = FL + (lf ? 2 * pb.nf : 0);                    // [nj] when lj
+  if (lf) for (uint32_t e = threadIdx.x; e < pb.nf; e += blockDim.x) {
+    const BCast b = pb.bfail[e];
+    FL[2 * e] = b.sender | (b.bseq << 23) | ((uint32_t)pb.dep[e] << 31);
+    FL[2 * e + 1] = b.peer;
   }
-  uint8_t* rw = row_of(d, i);
-  uint32_t* gB = bits_of(d, i);
-  uint32_t* B = LDSB ? pb_dyn + (size_t)wv * d.NWR : gB;
-  if (LDSB) for (uint32_t w = l; w < d.NWR; w += 64) B[w] = gB[w];
-  if (l < SLOTS) { const Susp sl = d.susp[(size_t)i * SLOTS + l]; s_sp[wv][l] = sl.kind ? sl.peer : 0xFFFFFFFFu; }
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  auto mem = [&](uint32_t x) -> bool {
-    const uint32_t w = LDSB ? B[x >> 5] : __hip_atomic_load(&B[x >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return (w >> (x & 31)) & 1u;
-  };
-  auto is_susp = [&](uint32_t x) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
-  uint32_t n = d.n[i];
-  const uint32_t n0 = n;
-  uint32_t fn = d.flog_n[i];
-  const uint8_t now = enc(r, r);
-  uint32_t lost_cnt = 0, removed_cnt = 0;
-  unsigned long long segs = 0;
-  const bool honour = d.failed_mode == KB_FAILED_SIM_SENDER;
-  // ---- Failed(p) group (src/kaboodle.rs:268-283) ----
-  // In-order semantics, 64 entries at a time.  An entry acts iff it is delivered, names neither the
-  // receiver nor comes from it, and its sender is still a member when it is reached.  Membership at the
-  // chunk start is in B (earlier chunks applied); inside the chunk only an entry whose sender is named
-  // by an earlier entry (dep) can change its mind: those are resolved in lane order with one ballot
-  // each (killed iff an earlier acting lane of the chunk names its sender).  The acting entries are
-  // then applied together: the atomic's return says whether the peer was still present (removed once).
-  for (uint32_t c = 0; c < pb.nf; c += 64) {
-    const uint32_t e = c + l;
-    const bool valid = e < pb.nf;
-    const BCast b = valid ? pb.bfail[e] : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
-    const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
-    const bool base = valid && b.sender != i && !lost && b.peer != i && honour && mem(b.sender);
-    unsigned long long actm = __ballot(base);
-    unsigned long long depm = __ballot(base && pb.dep[e]);
-    while (depm) {
-      const uint32_t q = (uint32_t)(__ffsll((long long)depm) - 1);
-      depm &= depm - 1;
-      const uint32_t s_q = bcast(b.sender, q);
-      const unsigned long long killers = __ballot(((actm >> l) & 1ull) && b.peer == s_q) & ((1ull << q) - 1ull);
-      if (killers) actm &= ~(1ull << q);
+  if (lj) for (uint32_t e = threadIdx.x; e < pb.nj; e += blockDim.x) JL[e] = pb.bjoin[e].sender | (pb.bjoin[e].bseq << 23);
+  __syncthreads();
+  auto fail_at = [&](uint32_t e, uint32_t& dep) -> BCast {
+    if (lf) {
+      const uint32_t x = FL[2 * e];
+      dep = x >> 31;
+      return BCast{x & 0x7FFFFFu, FL[2 * e + 1], (x >> 23) & 0xFFu, 0};
     }
-    lost_cnt += __popcll(__ballot(lost));
-    if ((actm >> l) & 1ull) {
-      const uint32_t m = 1u << (b.peer & 31);
-      if (atomicAnd(&B[b.peer >> 5], ~m) & m) {
-        removed_cnt++;
-        if (is_susp(b.peer)) susp_clear(d, i, b.peer);
-        segs |= seg_bit(d, b.peer);
+    dep = pb.dep[e];
+    return pb.bfail[e];
+  };
+  auto join_at = [&](uint32_t e) -> BCast {
+    if (lj) { const uint32_t x = JL[e]; return BCast{x & 0x7FFFFFu, x & 0x7FFFFFu, x >> 23, 0}; }
+    return pb.bjoin[e];
+  };
+  const bool honour = d.failed_mode == KB_FAILED_SIM_SENDER;
+  const uint8_t now = enc(r, r);
+  // counters stay in registers for the whole persistent loop: one atomic per wave at the end (same-
+  // address atomics from every node would serialise in L2 and stall the waves that wait on them)
+  unsigned long long w_lost = 0, w_removed = 0, w_resp = 0;
+  for (uint32_t i = blockIdx.x * wpb + wv; i < d.C; i += gridDim.x * wpb) {
+    if (!d.alive[i] || d.start_round[i] >= r) {
+      if (l == 0) { pb.nresp[i] = 0; pb.paysum[i] = 0; }
+      continue;
+    }
+    uint8_t* rw = row_of(d, i);
+    uint32_t* gB = bits_of(d, i);
+    uint32_t* B = LDSB ? pb_dyn + (size_t)wv * d.NWR : gB;
+    if (LDSB) stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB), d.NWR / 4, l, 64);
+    if (l < SLOTS) { const Susp sl = d.susp[(size_t)i * SLOTS + l]; s_sp[wv][l] = sl.kind ? sl.peer : 0xFFFFFFFFu; }
+    wait_lds();
+    __builtin_amdgcn_wave_barrier();
+    auto mem = [&](uint32_t x) -> bool {
+      const uint32_t w = LDSB ? B[x >> 5] : __hip_atomic_load(&B[x >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return (w >> (x & 31)) & 1u;
+    };
+    auto is_susp = [&](uint32_t x) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
+    uint32_t n = d.n[i];
+    const uint32_t n0 = n;
+    uint32_t fn = d.flog_n[i];
+    uint32_t lost_cnt = 0, removed_cnt = 0;
+    unsigned long long segs = 0;
+    // ---- Failed(p) group (src/kaboodle.rs:268-283) ----
+    // In-order semantics, 64 entries at a time.  An entry acts iff it is delivered, names neither the
+    // receiver nor comes from it, and its sender is still a member when it is reached.  Membership at
+    // the chunk start is in B (earlier chunks applied); inside the chunk only an entry whose sender is
+    // named by an earlier entry (dep) can change its mind: those are resolved in lane order with one
+    // ballot each (killed iff an earlier acting lane of the chunk names its sender).  The acting
+    // entries are then applied together: the atomic's return says whether the peer was still present.
+    for (uint32_t c = 0; c < pb.nf; c += 64) {
+      const uint32_t e = c + l;
+      const bool valid = e < pb.nf;
+      uint32_t dep = 0;
+      const BCast b = valid ? fail_at(e, dep) : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+      const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
+      const bool base = valid && b.sender != i && !lost && b.peer != i && honour && mem(b.sender);
+      unsigned long long actm = __ballot(base);
+      unsigned long long depm = __ballot(base && dep);
+      while (depm) {
+        const uint32_t q = (uint32_t)(__ffsll((long long)depm) - 1);
+        depm &= depm - 1;
+        const uint32_t s_q = bcast(b.sender, q);
+        const unsigned long long killers = __ballot(((actm >> l) & 1ull) && b.peer == s_q) & ((1ull << q) - 1ull);
+        if (killers) actm &= ~(1ull << q);
+      }
+      lost_cnt += __popcll(__ballot(lost));
+      if ((actm >> l) & 1ull) {
+        const uint32_t m = 1u << (b.peer & 31);
+        if (atomicAnd(&B[b.peer >> 5], ~m) & m) {
+          removed_cnt++;
+          if (is_susp(b.peer)) susp_clear(d, i, b.peer);
+          segs |= seg_bit(d, b.peer);
+        }
+      }
+      if (!LDSB) { __builtin_amdgcn_s_waitcnt(0); }
+      __builtin_amdgcn_wave_barrier();
+    }
+    removed_cnt = wave_sum(removed_cnt);
+    n -= removed_cnt;
+    if (!LDSB) { __builtin_amdgcn_s_waitcnt(0); }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t nbase = n;
+    // ---- Join{addr} group (src/kaboodle.rs:284-304) ----
+    uint32_t nresp = 0, paysum = 0;
+    for (uint32_t c = 0; c < pb.nj; c += 64) {
+      const uint32_t e = c + l;
+      const bool valid = e < pb.nj;
+      const BCast b = valid ? join_at(e) : BCast{0xFFFFFFFFu, 0, 0, 0};
+      const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
+      const bool deliver = valid && b.sender != i && !lost;
+      const bool known = deliver && mem(b.sender);
+      const unsigned long long newm = __ballot(deliver && !known);
+      const bool isnew = (newm >> l) & 1ull;
+      // n right after inserting this joiner = n before the chunk + new joiners up to and including it
+      const uint32_t nq = n + __popcll(newm & ((2ull << l) - 1ull));
+      bool resp = false;
+      if (isnew) {                                   // should_respond_to_broadcast :333-354
+        const int64_t o = (int64_t)nq - 2;
+        if (o <= 0) resp = true;
+        else {
+          int64_t pct = 100 - o * o; if (pct < 1) pct = 1;
+          const uint32_t u = philox(i, (uint32_t)r, (uint32_t)P_RESPOND << 24, b.sender, d.k0, d.k1).x;
+          resp = (int64_t)mulhi(u, 100) < pct;
+        }
+      }
+      const unsigned long long respm = __ballot(resp);
+      const bool logit = deliver && (!known || rw[b.sender] != now);
+      const unsigned long long lgm = __ballot(logit);
+      if (logit) d.flog[(size_t)i * LOGCAP + ((fn + __popcll(lgm & ((1ull << l) - 1ull))) & (LOGCAP - 1))] = log_entry(b.sender, r);
+      fn += __popcll(lgm);
+      if (deliver) {
+        if (known && is_susp(b.sender)) susp_clear(d, i, b.sender);
+        rw[b.sender] = now;
+        if (isnew) { atomicOr(&B[b.sender >> 5], 1u << (b.sender & 31)); segs |= seg_bit(d, b.sender); }
+      }
+      const uint32_t sz = resp ? (d.uniform ? (nq < d.capj ? nq : d.capj) : nq) : 0;
+      paysum += wave_sum(sz);
+      nresp += __popcll(respm);
+      n += __popcll(newm);
+      lost_cnt += __popcll(__ballot(lost));
+      if (l == 0) {
+        pb.newmask[(size_t)i * pb.JW + c / 64] = newm;
+        pb.respmask[(size_t)i * pb.JW + c / 64] = respm;
       }
     }
-    __builtin_amdgcn_s_waitcnt(0);
+    segs = (unsigned long long)wave_or((uint32_t)segs) | ((unsigned long long)wave_or((uint32_t)(segs >> 32)) << 32);
+    wait_lds();
+    __builtin_amdgcn_wave_barrier();
+    if (LDSB && segs) {                                 // write back the changed segments of the bitset
+      const uint32_t wps4 = d.SEGW / 128;             // 16-byte words per segment
+      const uint4* B4 = reinterpret_cast<const uint4*>(B);
+      uint4* g4 = reinterpret_cast<uint4*>(gB);
+      for (uint32_t w = l; w < d.NWR / 4; w += 64) if ((segs >> (w / wps4)) & 1ull) g4[w] = B4[w];
+    }
+    if (l == 0) {
+      d.n[i] = n;
+      d.flog_n[i] = fn;
+      mark(d, i, segs);
+      if (n != n0) d.dirty[i] = 1;
+      pb.nresp[i] = nresp; pb.paysum[i] = paysum; pb.nbase[i] = nbase;
+    }
+    w_lost += lost_cnt; w_removed += removed_cnt; w_resp += nresp;
+    wait_lds();                                       // LDS bitset is reused by the next node
     __builtin_amdgcn_wave_barrier();
   }
-  removed_cnt = wave_sum(removed_cnt);
-  n -= removed_cnt;
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  const uint32_t nbase = n;
-  // ---- Join{addr} group (src/kaboodle.rs:284-304) ----
-  uint32_t nresp = 0, paysum = 0;
-  for (uint32_t c = 0; c < pb.nj; c += 64) {
-    const uint32_t e = c + l;
-    const bool valid = e < pb.nj;
-    const BCast b = valid ? pb.bjoin[e] : BCast{0xFFFFFFFFu, 0, 0, 0};
-    const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
-    const bool deliver = valid && b.sender != i && !lost;
-    const bool known = deliver && mem(b.sender);
-    const unsigned long long newm = __ballot(deliver && !known);
-    const bool isnew = (newm >> l) & 1ull;
-    // n right after inserting this joiner = n before the chunk + new joiners up to and including it
-    const uint32_t nq = n + __popcll(newm & ((2ull << l) - 1ull));
-    bool resp = false;
-    if (isnew) {                                   // should_respond_to_broadcast :333-354
-      const int64_t o = (int64_t)nq - 2;
-      if (o <= 0) resp = true;
-      else {
-        int64_t pct = 100 - o * o; if (pct < 1) pct = 1;
-        const uint32_t u = philox(i, (uint32_t)r, (uint32_t)P_RESPOND << 24, b.sender, d.k0, d.k1).x;
-        resp = (int64_t)mulhi(u, 100) < pct;
-      }
-    }
-    const unsigned long long respm = __ballot(resp);
-    const bool logit = deliver && (!known || rw[b.sender] != now);
-    const unsigned long long lgm = __ballot(logit);
-    if (logit) d.flog[(size_t)i * LOGCAP + ((fn + __popcll(lgm & ((1ull << l) - 1ull))) & (LOGCAP - 1))] = log_entry(b.sender, r);
-    fn += __popcll(lgm);
-    if (deliver) {
-      if (known && is_susp(b.sender)) susp_clear(d, i, b.sender);
-      rw[b.sender] = now;
-      if (isnew) { atomicOr(&B[b.sender >> 5], 1u << (b.sender & 31)); segs |= seg_bit(d, b.sender); }
-    }
-    const uint32_t sz = resp ? (d.uniform ? (nq < d.capj ? nq : d.capj) : nq) : 0;
-    paysum += wave_sum(sz);
-    nresp += __popcll(respm);
-    n += __popcll(newm);
-    lost_cnt += __popcll(__ballot(lost));
-    if (l == 0) {
-      pb.newmask[(size_t)i * pb.JW + c / 64] = newm;
-      pb.respmask[(size_t)i * pb.JW + c / 64] = respm;
-    }
-  }
-  segs = (unsigned long long)wave_or((uint32_t)segs) | ((unsigned long long)wave_or((uint32_t)(segs >> 32)) << 32);
-  __builtin_amdgcn_s_waitcnt(0);
-  __builtin_amdgcn_wave_barrier();
-  if (LDSB && segs) {                                 // write back the changed segments of the bitset
-    const uint32_t wps = d.SEGW / 32;
-    for (uint32_t w = l; w < d.NWR; w += 64) if ((segs >> (w / wps)) & 1ull) gB[w] = B[w];
-  }
   if (l == 0) {
-    d.n[i] = n;
-    d.flog_n[i] = fn;
-    mark(d, i, segs);
-    if (n != n0) d.dirty[i] = 1;
-    pb.nresp[i] = nresp; pb.paysum[i] = paysum; pb.nbase[i] = nbase;
-    if (lost_cnt) atomicAdd(&d.stats[S_BDROP], lost_cnt);
-    if (removed_cnt) atomicAdd(&d.stats[S_RMFAILED], removed_cnt);
-    if (nresp) atomicAdd(&d.stats[S_JRESP], nresp);
+    if (w_lost) atomicAdd(&d.stats[S_BDROP], w_lost);
+    if (w_removed) atomicAdd(&d.stats[S_RMFAILED], w_removed);
+    if (w_resp) atomicAdd(&d.stats[S_JRESP], w_resp);
   }
 }
 
@@ -317,7 +383,10 @@ __device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint
   return w * 32 + (__ffs(x) - 1);
 }
 constexpr uint32_t RESP_LDS_W = 131072;   // rows up to this many ids keep their bitsets in LDS
-__host__ __device__ inline size_t resp_words(uint32_t NW, uint32_t NB) { return 2ull * NW + 2ull * (NB + 1); }
+constexpr uint32_t RESP_JCAP = 1024;      // new joiners of one receiver kept in LDS (more: read from HBM)
+__host__ __device__ inline size_t resp_words(uint32_t NW, uint32_t NB) {
+  return (2ull * NW + 2ull * (NB + 1) + 2ull * RESP_JCAP + 1 + 3) & ~3ull;
+}
 
 // exclusive prefix of the member counts of X's 256-id blocks into XP[0..NB], XP[NB] = total (block-wide)
 __device__ uint32_t block_prefix(const uint32_t* X, uint32_t* XP, uint32_t NB, uint32_t* s_red) {
@@ -353,19 +422,36 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
   uint32_t* BP = B + NW;             // block prefix of B                     [NB + 1]
   uint32_t* S = BP + NB + 1;         // members at response (unsampled path)  [NW]
   uint32_t* SP = S + NW;             // block prefix of S                     [NB + 1]
+  uint32_t* J = SP + NB + 1;         // ids of this receiver's new joiners    [RESP_JCAP]
+  uint32_t* JM = J + RESP_JCAP;      // suffix minima of J                    [RESP_JCAP + 1]
   __shared__ uint32_t s_red[16];
   const uint32_t t = threadIdx.x, T = blockDim.x;
   const uint32_t nnodes = *nnodes_p;
   for (uint32_t it = blockIdx.x; it < nnodes; it += gridDim.x) {
     const uint32_t i = nodes[it];
-    const uint32_t* bi = bits_of(d, i);
-    for (uint32_t k = t; k < NW; k += T) B[k] = bi[k];
+    stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(bits_of(d, i)), NW / 4, t, T);
     __syncthreads();
     const uint32_t nB = block_prefix(B, BP, NB, s_red);
     const unsigned long long* nm = pb.newmask + (size_t)i * pb.JW;
     const unsigned long long* rm = pb.respmask + (size_t)i * pb.JW;
     uint32_t nnew = 0;
     for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
+    const bool jl = nnew <= RESP_JCAP;
+    if (jl) {                            // new joiners in list order (parallel), then suffix minima
+      for (uint32_t e = t; e < pb.nj; e += T) {
+        if (!newbit(nm, e)) continue;
+        uint32_t pos = __popcll(nm[e >> 6] & ((1ull << (e & 63)) - 1ull));
+        for (uint32_t w2 = 0; w2 < (e >> 6); ++w2) pos += __popcll(nm[w2]);
+        J[pos] = pb.bjoin[e].sender;
+      }
+      __syncthreads();
+      if (t == 0) {
+        uint32_t m = 0xFFFFFFFFu;
+        JM[nnew] = m;
+        for (uint32_t q3 = nnew; q3 > 0; --q3) { m = J[q3 - 1] < m ? J[q3 - 1] : m; JM[q3 - 1] = m; }
+      }
+    }
+    __syncthreads();
     uint32_t poff = ob.poff[i], q = 0, ins_before = 0;
     for (uint32_t wj = 0; wj < pb.JW; ++wj) {
       unsigned long long rmw = rm[wj];
@@ -392,8 +478,12 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
             while (true) {
               x = bm_select(B, BP, NB, y + e);
               uint32_t c = 0;
-              for (uint32_t f = K + 1; f < pb.nj; ++f)
-                if (newbit(nm, f)) c += pb.bjoin[f].sender <= x;
+              if (jl) {                                  // later joiners = J[upto..nnew)
+                if (x >= JM[upto]) for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= x;
+              } else {
+                for (uint32_t f = K + 1; f < pb.nj; ++f)
+                  if (newbit(nm, f)) c += pb.bjoin[f].sender <= x;
+              }
               if (c == e) break;
               e = c;
             }

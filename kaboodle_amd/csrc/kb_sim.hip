@@ -231,6 +231,8 @@ struct kb_sim {
   hipEvent_t ev0, ev1, er0, er1;
   double sweep_ms, round_ms;
   uint64_t sweep_launches, round_launches, sweep_bytes, bj_total, bf_total;
+  uint32_t ncu = 256;
+  size_t lds_per_cu = 65536;
 };
 
 static ScanArgs scan_args(kb_sim* s, uint32_t n, uint32_t* totals) {
@@ -325,6 +327,12 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
   s->device = cfg->device >= 0 ? cfg->device : 0;
   if (cfg->device < 0) (void)hipGetDevice(&s->device);
   if (hipSetDevice(s->device) != hipSuccess) { delete s; seterr("hipSetDevice failed"); return KB_NO_DEVICE; }
+  {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, s->device) != hipSuccess) { delete s; seterr("hipGetDeviceProperties failed"); return KB_NO_DEVICE; }
+    s->ncu = (uint32_t)prop.multiProcessorCount;
+    s->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 65536;
+  }
   const uint32_t C = cfg->capacity;
   const uint32_t W = (C + 8191) / 8192 * 8192;       // 64 segments of whole 128-id steps
   s->C = C; s->W = W; s->round = 0;
@@ -470,14 +478,21 @@ static int step_round(kb_sim* s) {
   pb.newmask = s->newmask; pb.respmask = s->respmask;
   pb.gid = s->bf_gid; pb.dep = s->bf_dep;
   const bool have_b = s->nf + s->nj > 0;
-  if (s->nf) k_bfail_prep<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep);
+  if (s->nf > 2048) k_bfail_prep<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep);
+  else if (s->nf) k_bfail_prep_lds<<<1, 1024, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep);
   if (have_b) {
-    if (s->W <= PB_LDS_W) {
-      const uint32_t wpb = std::max<uint32_t>(1, std::min<uint32_t>(4, 65536 / (4 * d.NWR)));
-      k_phaseB<true><<<(C + wpb - 1) / wpb, 64 * wpb, 4ull * d.NWR * wpb, st>>>(d, pb, r);
-    } else {
-      k_phaseB<false><<<gwave, 256, 0, st>>>(d, pb, r);
-    }
+    // persistent waves; broadcast lists staged in LDS once per workgroup when they fit
+    const uint32_t budget = 65536 / 4;                 // dynamic LDS words per workgroup
+    uint32_t lf = s->nf <= PB_FMAX, lj = s->nj <= PB_JMAX;
+    uint32_t listw = (lf ? 2 * s->nf : 0) + (lj ? s->nj : 0);
+    if (listw > budget / 2) { lf = lj = 0; listw = 0; }
+    const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR;
+    const uint32_t wpb = ldsb ? std::min<uint32_t>(4, (budget - listw) / d.NWR) : 4;
+    const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
+    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)(s->lds_per_cu / std::max<size_t>(lds + 512, 1))));
+    const uint32_t blocks = std::min<uint32_t>((C + wpb - 1) / wpb, s->ncu * per_cu);
+    if (ldsb) k_phaseB<true><<<blocks, 64 * wpb, lds, st>>>(d, pb, r, lf, lj);
+    else k_phaseB<false><<<blocks, 64 * wpb, lds, st>>>(d, pb, r, lf, lj);
   }
   else { HIPCHK(hipMemsetAsync(s->nresp, 0, 4ull * C, st)); HIPCHK(hipMemsetAsync(s->paysum, 0, 4ull * C, st)); }
   {  // wave-0 outbox regions: responses first, then the tick's messages

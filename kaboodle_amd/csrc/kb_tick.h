@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
   const uint8_t* rw = row_of(d, i);
   uint32_t oseq = ob.cnt[i];
   if (npick) {                                            // choose_multiple over the candidate list
-    __builtin_amdgcn_s_waitcnt(0);
+    wait_lds();
     __builtin_amdgcn_wave_barrier();
     const uint32_t* bw = bits_of(d, i);
     const uint32_t lo = l * d.SEGW, hi = lo + d.SEGW;     // padding ids are never members
@@ -149,16 +149,47 @@ __device__ inline uint32_t thr5(const uint32_t (&k)[5]) { return k[4] == 0xFFFFF
 // or when the step can still change a top-5 list; the stamp bytes (128 B) only in the latter case.
 // A part's list is final once it holds five ancient (minimum-stamp) entries: later ids of that part
 // have larger rot and can never displace them.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// smallest (byte - 2) over the 16 bytes of x, computed on 16-bit lanes with packed ops (bytes 0 and 1
+// wrap to >= 0xFFFE): a byte b can enter a top-5 list with threshold T only if this is < T - 2
+__device__ inline uint32_t min_stamp16(const uint4& x) {
+  const u16x2 two = {2, 2};
+  u16x2 mn = {0xFFFF, 0xFFFF};
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    mn = __builtin_elementwise_min(mn, __builtin_bit_cast(u16x2, w[k] & 0x00FF00FFu) - two);
+    mn = __builtin_elementwise_min(mn, __builtin_bit_cast(u16x2, (w[k] >> 8) & 0x00FF00FFu) - two);
+  }
+  return mn.x < mn.y ? mn.x : mn.y;
+}
+
+// One 128-id step of one lane's row.  Stamp bytes (128 B) are read while either part's list can still
+// change: a part is final once it holds five ancient (minimum) stamps, since later ids of the part have
+// larger rot.  A packed-u16 filter rejects 16-byte groups with no stamp below the current threshold;
+// only surviving groups are examined byte by byte against the member bits.  Member bits (16 B) are
+// read to refold a stale checkpoint, or for a surviving group.
 template <bool FOLD>
 __device__ __attribute__((always_inline)) inline void sweep_step(const Dev& d, const uint32_t* zb, const uint8_t* rw, const uint32_t* bw,
                                   uint32_t i, uint32_t p, uint32_t col, uint32_t (&A)[5], uint32_t (&B)[5],
                                   uint32_t& raw, uint32_t& cnt, uint32_t& nbytes) {
-  // a part's threshold is the stamp of its 5th key (256 while it has fewer than five)
-  const bool need = !(d.ablate & 2) && ((thr5(A) > ST_ANCIENT && col < p) || (thr5(B) > ST_ANCIENT && col + 128 > p));
+  const uint32_t TA = thr5(A), TB = thr5(B);
+  const bool needA = TA > ST_ANCIENT && col < p, needB = TB > ST_ANCIENT && col + 128 > p;
+  const bool need = !(d.ablate & 2) && (needA || needB);
   if (!FOLD && !need) return;
-  const uint4 mb = *reinterpret_cast<const uint4*>(bw + (col >> 5));
-  nbytes += 16;
+  uint4 v[8];
+  if (need) {                                      // issued first: they overlap the fold's LDS chain
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const uint4*>(rw + col + 16 * q);
+    nbytes += 128;
+  }
+  uint4 mb = make_uint4(0, 0, 0, 0);
+  bool have_mb = false;
   if (FOLD) {
+    mb = *reinterpret_cast<const uint4*>(bw + (col >> 5));
+    have_mb = true;
+    nbytes += 16;
     const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
     const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
 #pragma unroll
@@ -172,18 +203,16 @@ __device__ __attribute__((always_inline)) inline void sweep_step(const Dev& d, c
     }
   }
   if (!need) return;
-  if (!(mb.x | mb.y | mb.z | mb.w)) return;        // no member in these 128 ids: stamps are irrelevant
-  nbytes += 128;
+  const uint32_t T = (needA && TA > (needB ? TB : 0u)) ? TA : TB;   // the larger relevant threshold
   const uint32_t C = d.C;
-  uint4 v[8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const uint4*>(rw + col + 16 * q);
-  const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
+    if (min_stamp16(v[q]) >= T - 2) continue;
+    if (!have_mb) { mb = *reinterpret_cast<const uint4*>(bw + (col >> 5)); have_mb = true; nbytes += 16; }
+    const uint32_t mwq = (q >> 1) == 0 ? mb.x : ((q >> 1) == 1 ? mb.y : ((q >> 1) == 2 ? mb.z : mb.w));
     uint32_t cm = (nzmask4(v[q].x & 0xFEFEFEFEu) | (nzmask4(v[q].y & 0xFEFEFEFEu) << 4) |
                    (nzmask4(v[q].z & 0xFEFEFEFEu) << 8) | (nzmask4(v[q].w & 0xFEFEFEFEu) << 12)) &
-                  ((mw[q >> 1] >> (16 * (q & 1))) & 0xFFFFu);
+                  ((mwq >> (16 * (q & 1))) & 0xFFFFu);
     while (cm) {
       const uint32_t t = __ffs(cm) - 1;
       cm &= cm - 1;

@@ -154,6 +154,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint8_t now = enc(r, r);
   const uint8_t fresh_thr = enc(r - (SHARE_AGE - 1), r);
+  unsigned long long w_over = 0, w_curovf = 0;      // flushed once per wave (see k_phaseB)
   for (uint32_t it = blockIdx.x * 4 + wv; it < nact; it += gridDim.x * 4) {
     const uint32_t i = wc.active[it];
     uint8_t* rw = row_of(d, i);
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     unsigned long long segs = 0;
     if (l < SLOTS) s_susp[wv][l] = d.susp[(size_t)i * SLOTS + l];
     if (l < CSLOTS) s_cur[wv][l] = d.cur[(size_t)i * CSLOTS + l];
-    __builtin_amdgcn_s_waitcnt(0);
+    wait_lds();
     __builtin_amdgcn_wave_barrier();
     const uint32_t ibase = wc.in_off[i], icnt = wc.cnt1[i];
     // canonical order = ascending outbox index = (sender, seq)
@@ -240,16 +241,16 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
             e = fr ? __ffsll((long long)fr) - 1 : -1;
             if (e >= 0 && l == 0) { s_cur[wv][e].used = 1; s_cur[wv][e].peer = m.a; s_cur[wv][e].nobs = 0; }
           }
-          __builtin_amdgcn_s_waitcnt(0);
+          wait_lds();
           __builtin_amdgcn_wave_barrier();
-          if (e < 0) { if (l == 0) atomicAdd(&d.stats[S_CUROVF], 1ull); }
+          if (e < 0) w_curovf++;
           else if (l == 0) {
             Cur& c = s_cur[wv][e];
             bool dup = false;
             for (uint32_t q = 0; q < c.nobs; ++q) dup |= c.obs[q] == s;
-            if (!dup) { if (c.nobs == NOBS) atomicAdd(&d.stats[S_CUROVF], 1ull); else c.obs[c.nobs++] = s; }
+            if (!dup) { if (c.nobs == NOBS) w_curovf++; else c.obs[c.nobs++] = s; }
           }
-          __builtin_amdgcn_s_waitcnt(0);
+          wait_lds();
           __builtin_amdgcn_wave_barrier();
           emit_msg(ob, d, i, oseq, m.a, K_PING, 0, 0, 0, 0);
           break;
@@ -261,11 +262,11 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
             const uint32_t nobs = s_cur[wv][e].nobs;
             uint32_t obs[NOBS];
             for (int q = 0; q < NOBS; ++q) obs[q] = s_cur[wv][e].obs[q];
-            __builtin_amdgcn_s_waitcnt(0);
+            wait_lds();
             __builtin_amdgcn_wave_barrier();
             if (l == 0) s_cur[wv][e].used = 0;
             for (uint32_t q = 0; q < nobs; ++q) emit_msg(ob, d, i, oseq, obs[q], K_ACK, m.a, m.fp, m.n, 0);
-            __builtin_amdgcn_s_waitcnt(0);
+            wait_lds();
             __builtin_amdgcn_wave_barrier();
           }
           maybe_sync(m.a, m.fp, m.n);
@@ -320,7 +321,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
             }
           }
           over = d.uniform ? total > d.capk : size > (uint64_t)BUFSZ;
-          if (over) { if (l == 0) atomicAdd(&d.stats[S_OVERSIZE], 1ull); }
+          if (over) w_over++;
           else { emit_msg(ob, d, i, oseq, s, K_KP, total, 0, 0, poff); pay_used += total; }
           maybe_sync(s, m.fp, m.n);
           break;
@@ -335,8 +336,12 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       d.n[i] = n; d.fp[i] = fp; d.dirty[i] = dirty ? 1 : 0; d.flog_n[i] = fn;
       ob.cnt[i] = oseq;
     }
-    __builtin_amdgcn_s_waitcnt(0);
+    wait_lds();                                       // the LDS slot caches are reused by the next node
     __builtin_amdgcn_wave_barrier();
+  }
+  if (l == 0) {
+    if (w_over) atomicAdd(&d.stats[S_OVERSIZE], w_over);
+    if (w_curovf) atomicAdd(&d.stats[S_CUROVF], w_curovf);
   }
 }
 
