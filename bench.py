@@ -46,7 +46,7 @@ def parse():
     ap.add_argument("--loss", type=float, default=0.01)
     ap.add_argument("--churn", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--conv-cap", type=int, default=150, help="max untimed quiescent rounds for convergence")
+    ap.add_argument("--conv-cap", type=int, default=100, help="max untimed quiescent rounds for convergence")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-conv", action="store_true")
@@ -94,6 +94,30 @@ def cpu_baseline(cfg, budget_s: float, nodes: int) -> dict:
                       f"(oracle/kb_oracle.c, OpenMP over peers, {dt:.1f} s)"}
 
 
+def rank_config(a, rank: int, world: int, local: int):
+    """The replica this rank simulates: the same workload with a rank-distinct seed."""
+    from kaboodle_amd._ffi import KB_INIT_CONVERGED, SimConfig
+    total = a.warmup + a.steps
+    reserve = max(4096, int(a.nodes * a.churn * (total + 8) * 1.5))
+    return SimConfig(capacity=a.nodes + reserve, initial_nodes=a.nodes, init_mode=KB_INIT_CONVERGED, loss=a.loss,
+                     churn=a.churn, fault_end_round=total, seed=a.seed + 1000 * rank,
+                     device=local if world > 1 else -1)
+
+
+def aggregate(dt: float, units: float, world: int, device="cpu"):
+    """Whole-job numbers: max wall time over ranks, units summed over ranks."""
+    if world == 1:
+        return dt, units
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([dt, units], dtype=torch.float64, device=device)
+    tm = t[:1].clone()
+    tu = t[1:].clone()
+    dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tu, op=dist.ReduceOp.SUM)
+    return float(tm[0]), float(tu[0])
+
+
 def main() -> int:
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,15 +129,12 @@ def main() -> int:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", init_method="env://")
     import kaboodle_amd
-    from kaboodle_amd._ffi import KB_INIT_CONVERGED, SimConfig
+    from kaboodle_amd._ffi import SimConfig
     kaboodle_amd.require_gpu()
 
     total = a.warmup + a.steps
-    reserve = max(4096, int(a.nodes * a.churn * (total + 8) * 1.5))
-    capacity = a.nodes + reserve
-    cfg = SimConfig(capacity=capacity, initial_nodes=a.nodes, init_mode=KB_INIT_CONVERGED, loss=a.loss,
-                    churn=a.churn, fault_end_round=total, seed=a.seed + 1000 * rank,
-                    device=local if world > 1 else -1)
+    cfg = rank_config(a, rank, world, local)
+    capacity = cfg.capacity
     workload = f"configs[2]: {a.nodes} peers, converged start, {a.loss:.0%} loss, {a.churn:.1%}/round churn"
     mesh = kaboodle_amd.Mesh(cfg)
 
@@ -138,31 +159,36 @@ def main() -> int:
     sweep_bytes = mesh.sweep_bytes() - bytes0
     st = mesh.stats()
 
-    if world > 1:
-        t = torch.tensor([dt, float(alive_sum)], dtype=torch.float64, device="cuda")
-        tm = t.clone()
-        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        dt, alive_total = float(tm[0]), float(t[1])
-    else:
-        alive_total = float(alive_sum)
+    dt, alive_total = aggregate(dt, float(alive_sum), world, device="cuda")
 
     conv = None
     if not a.no_conv:
-        # quiescent tail: faults ended at round `total`; step untimed until all live peers agree
-        r_conv = st["first_converged_round"] if st["first_converged_round"] >= total else -1
-        extra = 0
+        # (1) BASELINE configs[1]: 1024 peers all joining at round 0, no faults -> rounds to convergence
+        with kaboodle_amd.Mesh(SimConfig(capacity=1024, initial_nodes=1024, seed=a.seed + 1000 * rank,
+                                         device=local if world > 1 else -1)) as m2:
+            r2 = -1
+            for _ in range(64):
+                m2.step(1)
+                s2 = m2.stats()
+                if s2["first_converged_round"] >= 0:
+                    r2 = s2["first_converged_round"]
+                    break
+        # (2) this workload's quiescent tail: faults ended at round `total`; step untimed until every live
+        # peer agrees or the cap (Q2 + honoured Failed remove live peers mesh-wide)
+        r_conv, extra = -1, 0
         while r_conv < 0 and extra < a.conv_cap:
             mesh.step(1)
             extra += 1
-            s2 = mesh.stats()
-            if s2["agree"] == s2["alive"]:
-                r_conv = s2["round"] - 1
-        s2 = mesh.stats()
-        conv = {"fault_end_round": total, "converged_round": r_conv if r_conv >= 0 else None,
-                "rounds_to_converge": (r_conv - total + 1) if r_conv >= 0 else None,
-                "agree_frac_at_fault_end": round(st["agree"] / max(st["alive"], 1), 4),
-                "agree_frac_final": round(s2["agree"] / max(s2["alive"], 1), 4)}
+            s3 = mesh.stats()
+            if s3["agree"] == s3["alive"]:
+                r_conv = s3["round"] - 1
+        s3 = mesh.stats()
+        conv = {"config2_join_1k_converged_round": r2 if r2 >= 0 else None,
+                "workload_fault_end_round": total,
+                "workload_converged_round": r_conv if r_conv >= 0 else None,
+                "workload_tail_rounds_run": extra,
+                "workload_agree_frac_at_fault_end": round(st["agree"] / max(st["alive"], 1), 4),
+                "workload_agree_frac_final": round(s3["agree"] / max(s3["alive"], 1), 4)}
 
     out = None
     if rank == 0:

@@ -186,18 +186,58 @@ __device__ inline void l1_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "
 // fingerprint of row i by one wave: refold the stale checkpoints (lane k <-> segment k), then an
 // ordered tree combine of the 64 checkpoints.  `extra` = segments changed by the caller and not yet
 // recorded in sdirty.  Returns the same value in every lane.
+// Wave-wide combine of per-lane (raw, cnt) pieces in lane order; lane 0 ends with the total.  The
+// subtree counts of all six levels are formed first so the six Z^cnt loads are in flight together.
+__device__ inline void wave_combine(const Dev& d, uint32_t& raw, uint32_t& cnt) {
+  const uint32_t l = lane();
+  uint32_t oc[6], zp[6];
+  uint32_t c = cnt;
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const uint32_t st = 1u << t;
+    oc[t] = __shfl_down(c, st, 64);
+    if ((l & (2 * st - 1)) == 0 && l + st < 64) c += oc[t];
+  }
+#pragma unroll
+  for (int t = 0; t < 6; ++t) zp[t] = d.uniform ? d.zpow[oc[t] <= d.C ? oc[t] : 0] : 0u;
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const uint32_t st = 1u << t;
+    const uint32_t oraw = __shfl_down(raw, st, 64);
+    if ((l & (2 * st - 1)) == 0 && l + st < 64)
+      raw = multmodp(d.uniform ? zp[t] : xpow8_dev(oc[t]), raw) ^ oraw;
+  }
+  cnt = c;
+}
+
+// Current fingerprint of row i with the whole wave: stale checkpoints are refolded (one per lane
+// when many are stale; all 64 lanes on each one when few are — the in-order handlers typically
+// dirty one segment per newly heard sender), then the 64 checkpoints are combined.
 __device__ uint32_t wave_fp(const Dev& d, const uint32_t* ztab, uint32_t i, unsigned long long extra) {
   const uint32_t l = lane();
   const unsigned long long sd = d.sdirty[i] | extra;
-  uint2 sp;
-  if ((sd >> l) & 1ull) { sp = fold_segment(d, ztab, i, l); d.segp[(size_t)i * NSEG + l] = sp; }
-  else sp = d.segp[(size_t)i * NSEG + l];
-  uint32_t raw = sp.x, cnt = sp.y;
-#pragma unroll
-  for (int s = 1; s < 64; s <<= 1) {
-    const uint32_t oraw = __shfl_down(raw, s, 64), ocnt = __shfl_down(cnt, s, 64);
-    if ((l & (2 * s - 1)) == 0 && l + s < 64) { raw = comb(d, raw, oraw, ocnt); cnt += ocnt; }
+  uint2 sp = make_uint2(0, 0);
+  if (d.uniform && sd && __popcll(sd) <= 4) {
+    sp = d.segp[(size_t)i * NSEG + l];
+    const uint8_t* hb = reinterpret_cast<const uint8_t*>(bits_of(d, i));   // one byte per 8-id block
+    const uint32_t nh = d.SEGW / 8;
+    for (unsigned long long m = sd; m; m &= m - 1) {
+      const uint32_t k = (uint32_t)(__ffsll((long long)m) - 1);
+      uint32_t raw = 0, cnt = 0;
+      const uint32_t h0 = k * nh + (l * nh) / 64, h1 = k * nh + ((l + 1) * nh) / 64;
+      for (uint32_t h = h0; h < h1; ++h) fold_half(d, ztab, h, hb[h], raw, cnt);
+      wave_combine(d, raw, cnt);
+      raw = bcast(raw, 0); cnt = bcast(cnt, 0);
+      if (l == k) { sp = make_uint2(raw, cnt); d.segp[(size_t)i * NSEG + k] = sp; }
+    }
+  } else if ((sd >> l) & 1ull) {
+    sp = fold_segment(d, ztab, i, l);
+    d.segp[(size_t)i * NSEG + l] = sp;
+  } else {
+    sp = d.segp[(size_t)i * NSEG + l];
   }
+  uint32_t raw = sp.x, cnt = sp.y;
+  wave_combine(d, raw, cnt);
   raw = bcast(raw, 0); cnt = bcast(cnt, 0);
   if (l == 0 && sd) atomicAnd(&d.sdirty[i], ~sd);
   return finish_fp(d, raw, cnt);

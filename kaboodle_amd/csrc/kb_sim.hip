@@ -232,6 +232,7 @@ struct kb_sim {
   double sweep_ms, round_ms;
   uint64_t sweep_launches, round_launches, sweep_bytes, bj_total, bf_total;
   uint32_t ncu = 256;
+  bool debug_waves = false;
   size_t lds_per_cu = 65536;
 };
 
@@ -351,6 +352,7 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
   d.capj = (BUFSZ - 20 - Lid - 1) / (18 + Lid);       // 20 + L + k(18+L) <  10240
   d.paybound = C < d.capk ? C : d.capk;
   if (const char* ab = getenv("KB_ABLATE")) d.ablate = (uint32_t)atoi(ab);
+  s->debug_waves = getenv("KB_DEBUG_WAVES") != nullptr;
   s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid); s->h_ever.assign(C, 0);
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &s->h_ident[(size_t)j * MAXID]);
   for (uint32_t j = 0; j < cfg->initial_nodes; ++j) s->h_ever[j] = 1;
@@ -564,12 +566,22 @@ static int step_round(kb_sim* s) {
       a.list = s->wc.active; a.list_count = d.ctr + C_ACTIVE;
       launch_scan(a, st);
     }
+    if (s->debug_waves) {                               // KB_DEBUG_WAVES: inbox sizes per wave
+      std::vector<uint32_t> c1(C);
+      HIPCHK(hipMemcpyAsync(c1.data(), s->wc.cnt1, 4ull * C, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      uint64_t sum = 0; uint32_t mx = 0, arg = 0, big = 0;
+      for (uint32_t k = 0; k < C; ++k) { sum += c1[k]; if (c1[k] > mx) { mx = c1[k]; arg = k; } big += c1[k] > 64; }
+      fprintf(stderr, "[kb] round %d wave %u: in-order msgs %llu, max inbox %u (node %u), inboxes > 64: %u\n", r, w,
+              (unsigned long long)sum, mx, arg, big);
+    }
     HIPCHK(hipMemcpyAsync(nb.cap, s->wc.bnd, 4ull * C, hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemsetAsync(nb.cnt, 0, 4ull * C, st));
     k_scatter<<<gnode, tb, 0, st>>>(d, ib, s->wc);
     k_kp_insert<<<2048, 256, 0, st>>>(d, ib, s->wc, r);
     k_kp_prologue<<<1024, 256, 0, st>>>(d, ib, s->wc, r);
     k_touch_fix<<<1024, 256, 0, st>>>(d, s->wc);
+    k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc);
     k_proc<<<4096, 256, 0, st>>>(d, ib, nb, s->wc, r);
     cur ^= 1;
   }

@@ -145,10 +145,6 @@ __device__ inline void top5_insert(uint32_t (&k)[5], uint32_t nk) {
 }
 __device__ inline uint32_t thr5(const uint32_t (&k)[5]) { return k[4] == 0xFFFFFFFFu ? 256u : (k[4] >> 24); }
 
-// One 128-id step of one lane's row.  The member bits (16 B) are read when the segment is refolded
-// or when the step can still change a top-5 list; the stamp bytes (128 B) only in the latter case.
-// A part's list is final once it holds five ancient (minimum-stamp) entries: later ids of that part
-// have larger rot and can never displace them.
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // smallest (byte - 2) over the 16 bytes of x, computed on 16-bit lanes with packed ops (bytes 0 and 1
@@ -165,64 +161,105 @@ __device__ inline uint32_t min_stamp16(const uint4& x) {
   return mn.x < mn.y ? mn.x : mn.y;
 }
 
-// One 128-id step of one lane's row.  Stamp bytes (128 B) are read while either part's list can still
-// change: a part is final once it holds five ancient (minimum) stamps, since later ids of the part have
-// larger rot.  A packed-u16 filter rejects 16-byte groups with no stamp below the current threshold;
-// only surviving groups are examined byte by byte against the member bits.  Member bits (16 B) are
-// read to refold a stale checkpoint, or for a surviving group.
+// One 128-id step of one lane's row, software-pipelined: the loads of step k+1 are issued before
+// step k is processed.  Stamp bytes (128 B, plus the 16 B of member bits) are loaded while either
+// part's list can still change: a part is final once it holds five ancient (minimum) stamps, since
+// later ids of the part have larger rot.  Member bits are loaded alone to refold a stale checkpoint.
+struct StepIn { uint4 v[8]; uint4 mb; };
+
+__device__ inline bool step_need(const Dev& d, const uint32_t (&A)[5], const uint32_t (&B)[5], uint32_t p, uint32_t col) {
+  return !(d.ablate & 2) && ((thr5(A) > ST_ANCIENT && col < p) || (thr5(B) > ST_ANCIENT && col + 128 > p));
+}
+
 template <bool FOLD>
-__device__ __attribute__((always_inline)) inline void sweep_step(const Dev& d, const uint32_t* zb, const uint8_t* rw, const uint32_t* bw,
-                                  uint32_t i, uint32_t p, uint32_t col, uint32_t (&A)[5], uint32_t (&B)[5],
-                                  uint32_t& raw, uint32_t& cnt, uint32_t& nbytes) {
-  const uint32_t TA = thr5(A), TB = thr5(B);
-  const bool needA = TA > ST_ANCIENT && col < p, needB = TB > ST_ANCIENT && col + 128 > p;
-  const bool need = !(d.ablate & 2) && (needA || needB);
-  if (!FOLD && !need) return;
-  uint4 v[8];
-  if (need) {                                      // issued first: they overlap the fold's LDS chain
+__device__ __attribute__((always_inline)) inline void step_load(const uint8_t* rw, const uint32_t* bw, uint32_t col,
+                                                                bool need, StepIn& s, uint32_t& nbytes) {
+  if (need) {
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = *reinterpret_cast<const uint4*>(rw + col + 16 * q);
+    for (int q = 0; q < 8; ++q) s.v[q] = *reinterpret_cast<const uint4*>(rw + col + 16 * q);
     nbytes += 128;
   }
-  uint4 mb = make_uint4(0, 0, 0, 0);
-  bool have_mb = false;
+  if (FOLD || need) { s.mb = *reinterpret_cast<const uint4*>(bw + (col >> 5)); nbytes += 16; }
+}
+
+// A packed-u16 filter rejects 16-byte groups with no stamp below the current threshold; surviving
+// groups are examined byte by byte against the member bits (strict <: within a part ids arrive in
+// increasing rot, so an equal stamp seen later never displaces an earlier one).
+// The fold's 16 table reads are issued before the next step's prefetch: vmcnt retires in order,
+// so waiting for them must not also wait for the prefetch.
+template <bool FOLD>
+__device__ __attribute__((always_inline)) inline void fold_fetch(const Dev& d, const StepIn& s, uint32_t col,
+                                                                 uint32_t (&hv)[16]) {
+  if (!FOLD) return;
+  const uint32_t mw[4] = {s.mb.x, s.mb.y, s.mb.z, s.mb.w};
+  const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
+#pragma unroll
+  for (int h = 0; h < 16; ++h) hv[h] = ht[h * 256 + ((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu)];   // entry 0 is 0
+}
+
+// A packed-u16 filter rejects 16-byte groups with no stamp below the current threshold; surviving
+// groups are examined byte by byte against the member bits (strict <: within a part ids arrive in
+// increasing rot, so an equal stamp seen later never displaces an earlier one).
+template <bool FOLD>
+__device__ __attribute__((always_inline)) inline void step_proc(const Dev& d, const uint32_t* zb, const StepIn& s,
+                                                                const uint32_t (&hv)[16], bool loaded, uint32_t i,
+                                                                uint32_t p, uint32_t col, uint32_t (&A)[5],
+                                                                uint32_t (&B)[5], uint32_t& raw, uint32_t& cnt) {
   if (FOLD) {
-    mb = *reinterpret_cast<const uint4*>(bw + (col >> 5));
-    have_mb = true;
-    nbytes += 16;
-    const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
-    const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
+    const uint32_t mw[4] = {s.mb.x, s.mb.y, s.mb.z, s.mb.w};
 #pragma unroll
     for (int h = 0; h < 16; ++h) {
-      const uint32_t m8 = (mw[h >> 2] >> (8 * (h & 3))) & 0xFFu;
-      if (m8) {
-        const uint32_t c = __popc(m8);
-        raw = mulzb(zb, raw, c) ^ ht[h * 256 + m8];
-        cnt += c;
-      }
+      const uint32_t c = __popc((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu);   // Z^0 table is the identity
+      raw = mulzb(zb, raw, c) ^ hv[h];
+      cnt += c;
     }
   }
-  if (!need) return;
+  if (!loaded) return;
+  const uint32_t TA = thr5(A), TB = thr5(B);
+  const bool needA = TA > ST_ANCIENT && col < p, needB = TB > ST_ANCIENT && col + 128 > p;
+  if (!(needA || needB)) return;
   const uint32_t T = (needA && TA > (needB ? TB : 0u)) ? TA : TB;   // the larger relevant threshold
   const uint32_t C = d.C;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    if (min_stamp16(v[q]) >= T - 2) continue;
-    if (!have_mb) { mb = *reinterpret_cast<const uint4*>(bw + (col >> 5)); have_mb = true; nbytes += 16; }
-    const uint32_t mwq = (q >> 1) == 0 ? mb.x : ((q >> 1) == 1 ? mb.y : ((q >> 1) == 2 ? mb.z : mb.w));
-    uint32_t cm = (nzmask4(v[q].x & 0xFEFEFEFEu) | (nzmask4(v[q].y & 0xFEFEFEFEu) << 4) |
-                   (nzmask4(v[q].z & 0xFEFEFEFEu) << 8) | (nzmask4(v[q].w & 0xFEFEFEFEu) << 12)) &
+    if (min_stamp16(s.v[q]) >= T - 2) continue;
+    const uint32_t mwq = (q >> 1) == 0 ? s.mb.x : ((q >> 1) == 1 ? s.mb.y : ((q >> 1) == 2 ? s.mb.z : s.mb.w));
+    uint32_t cm = (nzmask4(s.v[q].x & 0xFEFEFEFEu) | (nzmask4(s.v[q].y & 0xFEFEFEFEu) << 4) |
+                   (nzmask4(s.v[q].z & 0xFEFEFEFEu) << 8) | (nzmask4(s.v[q].w & 0xFEFEFEFEu) << 12)) &
                   ((mwq >> (16 * (q & 1))) & 0xFFFFu);
     while (cm) {
       const uint32_t t = __ffs(cm) - 1;
       cm &= cm - 1;
-      const uint32_t word = (t & 8) ? ((t & 4) ? v[q].w : v[q].z) : ((t & 4) ? v[q].y : v[q].x);
+      const uint32_t word = (t & 8) ? ((t & 4) ? s.v[q].w : s.v[q].z) : ((t & 4) ? s.v[q].y : s.v[q].x);
       const uint32_t b = (word >> (8 * (t & 3))) & 0xFFu;
       const uint32_t j = col + 16 * q + t;
       if (j == i) continue;
       if (j >= p) { if (b < thr5(B)) top5_insert(B, (b << 24) | (j - p)); }
       else if (b < thr5(A)) top5_insert(A, (b << 24) | (j + C - p));
     }
+  }
+}
+
+template <bool FOLD>
+__device__ __attribute__((always_inline)) inline void sweep_segment(const Dev& d, const uint32_t* zb, const uint8_t* rw,
+                                                                    const uint32_t* bw, uint32_t i, uint32_t p,
+                                                                    uint32_t c0, uint32_t c1, uint32_t (&A)[5],
+                                                                    uint32_t (&B)[5], uint32_t& raw, uint32_t& cnt,
+                                                                    uint32_t& nbytes) {
+  if (c0 >= c1) return;
+  StepIn cur;
+  bool need_cur = step_need(d, A, B, p, c0);
+  step_load<FOLD>(rw, bw, c0, need_cur, cur, nbytes);
+  for (uint32_t col = c0; col < c1; col += 128) {
+    uint32_t hv[16];
+    fold_fetch<FOLD>(d, cur, col, hv);
+    StepIn nxt;
+    // thresholds only fall, so the need computed before processing this step is a superset
+    const bool need_nxt = col + 128 < c1 && step_need(d, A, B, p, col + 128);
+    if (col + 128 < c1) step_load<FOLD>(rw, bw, col + 128, need_nxt, nxt, nbytes);
+    step_proc<FOLD>(d, zb, cur, hv, need_cur, i, p, col, A, B, raw, cnt);
+    cur = nxt;
+    need_cur = need_nxt;
   }
 }
 
@@ -258,14 +295,12 @@ __global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
     uint32_t raw = 0, cnt = 0;
     const bool mine = ((sd >> k) & 1ull) && !(d.ablate & 1);
     if (__ballot(mine)) {                 // wave-uniform: one pass for the whole wave
-      for (uint32_t col = c0; col < c1; col += 128)
-        sweep_step<true>(d, zb, rw, bw, i, p, col, A, B, raw, cnt, nbytes);
+      sweep_segment<true>(d, zb, rw, bw, i, p, c0, c1, A, B, raw, cnt, nbytes);
       if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; }
     } else {
       const bool need = (thr5(A) > ST_ANCIENT && c0 < p) || (thr5(B) > ST_ANCIENT && c1 > p);
       if (!__ballot(act && need)) continue;   // no list of this wave can change in this segment
-      for (uint32_t col = c0; col < c1; col += 128)
-        sweep_step<false>(d, zb, rw, bw, i, p, col, A, B, raw, cnt, nbytes);
+      sweep_segment<false>(d, zb, rw, bw, i, p, c0, c1, A, B, raw, cnt, nbytes);
     }
   }
   const uint32_t wb = wave_sum(act ? nbytes : 0u);

@@ -18,18 +18,39 @@ __device__ inline uint32_t out_bound(uint32_t kind) {
   return kind == K_ACK ? NOBS + 1 : (kind == K_KPR ? 2u : (kind == K_KP ? 0u : 1u));
 }
 
-// delivery decisions for every message of the wave (thread per sender region): dead receiver,
-// partition, loss (Philox keyed on the message), else delivered; counts per destination.
+// Message-parallel walk over the outboxes of 64 consecutive senders per wave: lane k of each
+// iteration takes the k-th message of the 64 regions concatenated, so one sender with hundreds of
+// messages (a popular ping target's Acks) spreads over the wave instead of serialising a thread.
+struct SenderSpan {
+  uint32_t total;
+  __device__ void owner(const uint32_t* ex, uint32_t k, uint32_t& j, uint32_t& q) const {
+    uint32_t lo = 0, hi = 64;                   // largest j with ex[j] <= k
+    while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (ex[mid] <= k) lo = mid; else hi = mid; }
+    j = lo; q = k - ex[lo];
+  }
+};
+
+// delivery decisions for every message of the wave: dead receiver, partition, loss (Philox keyed on
+// the message), else delivered; counts per destination.
 __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int32_t r, uint32_t w, int last) {
-  __shared__ uint32_t s_kp[256];
-  __shared__ uint32_t s_base;
+  __shared__ uint32_t s_ex[4][64], s_base[4][64];
+  __shared__ uint32_t s_kp[4];
+  __shared__ uint32_t s_kpbase;
+  const uint32_t wv = threadIdx.x >> 6, l = lane();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0;
   uint32_t nkp = 0;
   const uint32_t cnt = i < d.C ? ob.cnt[i] : 0;
-  const uint32_t base = i < d.C ? ob.off[i] : 0;
-  for (uint32_t q = 0; q < cnt; ++q) {
-    const uint32_t g = base + q;
+  s_ex[wv][l] = wave_excl(cnt);
+  s_base[wv][l] = i < d.C ? ob.off[i] : 0;
+  const uint32_t T = wave_sum(cnt);
+  wait_lds();
+  __builtin_amdgcn_wave_barrier();
+  const SenderSpan sp{T};
+  for (uint32_t k = l; k < T; k += 64) {
+    uint32_t j, q;
+    sp.owner(s_ex[wv], k, j, q);
+    const uint32_t g = s_base[wv][j] + q;
     const Msg m = ob.msgs[g];
     ks[m.kind < 5 ? m.kind : 0]++;
     uint8_t st = 0;
@@ -50,24 +71,43 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
   for (int k = 0; k < 5; ++k) stat_add(d, S_PING + k, ks[k]);
   stat_add(d, S_DEAD, dead); stat_add(d, S_PART, part); stat_add(d, S_LOSS, loss); stat_add(d, S_WINDOW, win);
   if (last) return;
-  s_kp[threadIdx.x] = nkp;                // one atomic per block reserves kp_list space
+  // KnownPeers deliveries go to kp_list: one atomic per workgroup reserves the space
+  const uint32_t kex = wave_excl(nkp), ktot = wave_sum(nkp);
+  if (l == 0) s_kp[wv] = ktot;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t run = 0;
-    for (uint32_t t = 0; t < blockDim.x; ++t) { const uint32_t v = s_kp[t]; s_kp[t] = run; run += v; }
-    s_base = run ? atomicAdd(&d.ctr[C_KP], run) : 0;
+    for (uint32_t t = 0; t < blockDim.x / 64; ++t) { const uint32_t v = s_kp[t]; s_kp[t] = run; run += v; }
+    s_kpbase = run ? atomicAdd(&d.ctr[C_KP], run) : 0;
   }
   __syncthreads();
-  uint32_t pos = s_base + s_kp[threadIdx.x];
-  if (nkp) for (uint32_t q = 0; q < cnt; ++q) if (wc.status[base + q] == 2) wc.kp_list[pos++] = base + q;
+  if (ktot) {
+    uint32_t pos = s_kpbase + s_kp[wv] + kex;
+    __threadfence_block();
+    for (uint32_t k = l; k < T; k += 64) {
+      uint32_t j, q;
+      sp.owner(s_ex[wv], k, j, q);
+      const uint32_t g = s_base[wv][j] + q;
+      if (wc.status[g] == 2) wc.kp_list[pos++] = g;
+    }
+  }
 }
 
-__global__ void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
+__global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
+  __shared__ uint32_t s_ex[4][64], s_base[4][64];
+  const uint32_t wv = threadIdx.x >> 6, l = lane();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.C) return;
-  const uint32_t cnt = ob.cnt[i], base = ob.off[i];
-  for (uint32_t q = 0; q < cnt; ++q) {
-    const uint32_t g = base + q;
+  const uint32_t cnt = i < d.C ? ob.cnt[i] : 0;
+  s_ex[wv][l] = wave_excl(cnt);
+  s_base[wv][l] = i < d.C ? ob.off[i] : 0;
+  const uint32_t T = wave_sum(cnt);
+  wait_lds();
+  __builtin_amdgcn_wave_barrier();
+  const SenderSpan sp{T};
+  for (uint32_t k = l; k < T; k += 64) {
+    uint32_t j, q;
+    sp.owner(s_ex[wv], k, j, q);
+    const uint32_t g = s_base[wv][j] + q;
     if (wc.status[g] != 1) continue;
     const uint32_t dst = ob.msgs[g].dest;
     wc.inbox[wc.in_off[dst] + atomicAdd(&wc.cursor[dst], 1u)] = g;
@@ -143,6 +183,38 @@ __global__ __launch_bounds__(256) void k_touch_fix(Dev d, WaveCtl wc) {
   }
 }
 
+// ---- inboxes longer than one wave: sorted into canonical (sender, seq) order = ascending outbox
+// index, one workgroup per node, bitonic in LDS (up to SORT_MAX entries; longer ones keep the
+// selection path of k_proc)
+constexpr uint32_t SORT_MAX = 8192;
+__global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc) {
+  __shared__ uint32_t v[SORT_MAX];
+  const uint32_t nact = d.ctr[C_ACTIVE];
+  for (uint32_t it = blockIdx.x; it < nact; it += gridDim.x) {
+    const uint32_t i = wc.active[it];
+    const uint32_t n = wc.cnt1[i];
+    if (n <= 64 || n > SORT_MAX) continue;
+    uint32_t P = 128;
+    while (P < n) P <<= 1;
+    const uint32_t base = wc.in_off[i];
+    for (uint32_t k = threadIdx.x; k < P; k += blockDim.x) v[k] = k < n ? wc.inbox[base + k] : 0xFFFFFFFFu;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1)
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t x = threadIdx.x; x < P; x += blockDim.x) {
+          const uint32_t y = x ^ j;
+          if (y > x) {
+            const uint32_t a = v[x], b = v[y];
+            if (((x & k) == 0) == (a > b)) { v[x] = b; v[y] = a; }
+          }
+        }
+        __syncthreads();
+      }
+    for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) wc.inbox[base + k] = v[k];
+    __syncthreads();
+  }
+}
+
 // ---- the per-node in-order program for Ping / PingRequest / Ack / KnownPeersRequest ---------------
 __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r) {
   __shared__ uint32_t ztab[ZT * 128];
@@ -167,9 +239,10 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     wait_lds();
     __builtin_amdgcn_wave_barrier();
     const uint32_t ibase = wc.in_off[i], icnt = wc.cnt1[i];
-    // canonical order = ascending outbox index = (sender, seq)
+    // canonical order = ascending outbox index = (sender, seq): one wave sorts <= 64 entries in
+    // registers; k_sort_inbox has sorted longer inboxes up to SORT_MAX in place
     uint32_t mine = l < icnt ? wc.inbox[ibase + l] : 0xFFFFFFFFu;
-    const bool small = icnt <= 64;
+    const bool small = icnt <= 64, sorted = icnt <= SORT_MAX;
     if (small) {
 #pragma unroll
       for (int k = 2; k <= 64; k <<= 1) {
@@ -197,10 +270,19 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       emit_msg(ob, d, i, oseq, peer, K_KPR, 0, f, n, 0);
     };
     uint32_t last_g = 0xFFFFFFFFu, last_sender = 0xFFFFFFFFu;
+    // messages are fetched 64 at a time (lane k holds the record of message base + k) and handed to
+    // the wave one by one with cross-lane reads, so the in-order loop never waits on HBM per message
+    Msg lm;
     for (uint32_t t = 0; t < icnt; ++t) {
       uint32_t g;
-      if (small) g = bcast(mine, (int)t);
-      else {        // large inbox: next smallest index above the previous one
+      if (sorted) {
+        if ((t & 63) == 0) {
+          const uint32_t gl = small ? mine : (t + l < icnt ? wc.inbox[ibase + t + l] : 0xFFFFFFFFu);
+          if (gl != 0xFFFFFFFFu) lm = ib.msgs[gl];
+          if (!small) mine = gl;
+        }
+        g = bcast(mine, (int)(t & 63));
+      } else {      // beyond SORT_MAX: next smallest index above the previous one
         uint32_t best = 0xFFFFFFFFu;
         for (uint32_t q = l; q < icnt; q += 64) {
           const uint32_t v = wc.inbox[ibase + q];
@@ -209,7 +291,15 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
         g = wave_min(best);
       }
       last_g = g;
-      const Msg m = ib.msgs[g];
+      Msg m;
+      if (sorted) {
+        const int src = (int)(t & 63);
+        m.dest = bcast(lm.dest, src); m.sender = bcast(lm.sender, src); m.seq = bcast(lm.seq, src);
+        m.kind = bcast(lm.kind, src); m.a = bcast(lm.a, src); m.fp = bcast(lm.fp, src); m.n = bcast(lm.n, src);
+        m.off = bcast(lm.off, src);
+      } else {
+        m = ib.msgs[g];
+      }
       const uint32_t s = m.sender;
       if (s != last_sender) {                         // prologue: insert(sender, Known(now)) (:406-415)
         const bool was = (bw[s >> 5] >> (s & 31)) & 1u;

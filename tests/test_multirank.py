@@ -1,0 +1,55 @@
+"""The N > 1 bench path on CPU: world_size-2 gloo process groups (127.0.0.1).  Each rank runs its
+replica of the workload (here through the CPU oracle, since there is no GPU in this container) and the
+whole-job numbers are reduced exactly as bench.py does on RCCL: max wall time, summed peer-rounds."""
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import argparse
+    import bench
+    import parity
+    from kaboodle_amd._ffi import Sim
+    a = argparse.Namespace(nodes=96, loss=0.02, churn=0.01, seed=1, warmup=1, steps=4)
+    cfg = bench.rank_config(a, rank, world, rank)
+    with Sim(parity.oracle_lib(), cfg) as o:
+        o.step(a.warmup)
+        units = 0
+        for _ in range(a.steps):
+            o.step(1)
+            units += o.stats()["alive"]
+        fps = o.fingerprints().tolist()
+    dt = 1.0 + rank                    # a stand-in wall time per rank, to check the reduction
+    tot_dt, tot_units = bench.aggregate(dt, float(units), world)
+    out[rank] = (cfg.seed, units, tot_dt, tot_units, fps[:8])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_replicas_reduce_like_bench():
+    world, port = 2, _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
+    (s0, u0, dt0, tu0, fp0), (s1, u1, dt1, tu1, fp1) = out[0], out[1]
+    assert s0 != s1                                     # distinct replicas
+    assert fp0 != fp1
+    assert dt0 == dt1 == 2.0                            # max over ranks
+    assert tu0 == tu1 == float(u0 + u1)                 # summed units

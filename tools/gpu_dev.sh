@@ -12,7 +12,7 @@ for ab in 0 1 2 3; do
   KB_ABLATE=$ab timeout -k 10 200 python tools/quick_perf.py 65536 10 > gpurun_out/$TAG/perf_ab$ab.log 2>&1 || exit 1
   echo "ablate=$ab: $(grep N= gpurun_out/$TAG/perf_ab$ab.log)"
 done
-timeout -k 10 300 python tools/age_perf.py 65536 300 50 > gpurun_out/$TAG/age.log 2>&1 || exit 1
+timeout -k 10 400 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/gpurun_out/$TAG/age" -o run --output-format csv -- python3 tools/age_perf.py 65536 300 50 > gpurun_out/$TAG/age.log 2>&1 || exit 1
 cat gpurun_out/$TAG/age.log
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/$TAG/prof" -o run --output-format csv -- python3 bench.py --no-cpu --no-conv --steps 20 > gpurun_out/$TAG/prof_bench.json 2> gpurun_out/$TAG/prof_bench.err || exit $?
 cat gpurun_out/$TAG/prof_bench.json
