@@ -22,7 +22,7 @@ enum StatIdx {
 };
 enum CtrIdx {
   C_KP, C_TOUCH, C_ACTIVE, C_AGREE, C_ALIVE, C_LEAVES, C_NEXTFREE, C_ERR, C_FIRSTCONV, C_LASTCONV, C_LASTAGREE,
-  C_LASTALIVE, NCTR
+  C_LASTALIVE, C_DBG_INS, C_DBG_FP, C_DBG_MAXFP, NCTR
 };
 constexpr int NSEG = 64;          // fingerprint checkpoints per row
 constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
@@ -59,6 +59,7 @@ struct Dev {
   uint32_t* segmul;
   uint32_t* seglen;
   uint32_t* zpow;                 // Z^k, Z = x^(8L), k in [0, C+1]
+  uint32_t* zfin;                 // Z^k * 0xFFFFFFFF (the init term of a k-member fingerprint)
   uint32_t* ztab;                 // [17][8][16] nibble tables of multiplication by Z^c
   uint32_t* zbtab;                // [9][4][256] byte tables of multiplication by Z^c
   uint32_t* htab;                 // [(W/8)][256] crc0 of every member pattern of every 8-id half block
@@ -68,6 +69,7 @@ struct Dev {
   uint32_t* flog;
   uint32_t* flog_n;
   uint32_t* fstart;
+  int32_t* kpr_big;               // round in which the node's KPR reply was proven oversize for the round
 };
 
 // freshness log (the KnownPeersRequest reply set, :503-508, without scanning the row): an entry is

@@ -40,7 +40,7 @@ constexpr uint32_t CRC_POLY = 0xEDB88320u;
 
 // error codes raised on the device (checked by the host after each step)
 enum : uint32_t { DERR_NONE = 0, DERR_SLOTS = 1, DERR_OUTBOX = 2, DERR_PAYLOAD = 3, DERR_FLOYD = 4, DERR_INBOX = 5,
-                  DERR_RESP = 6, DERR_LOG = 7 };
+                  DERR_RESP = 6, DERR_LOG = 7, DERR_FP = 8 };
 
 // ---- records ------------------------------------------------------------------------------------
 struct Msg {            // 32 B unicast record

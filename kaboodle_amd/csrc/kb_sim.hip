@@ -288,6 +288,11 @@ static int upload_segments(kb_sim* s) {
   HIPCHK(hipMemcpy(s->d.segmul, segmul.data(), 4ull * C, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(s->d.seglen, seglen.data(), 4ull * C, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(s->d.zpow, zpow.data(), 4ull * (C + 2), hipMemcpyHostToDevice));
+  {
+    std::vector<uint32_t> zf(C + 2);
+    for (uint32_t k = 0; k < C + 2; ++k) zf[k] = multmodp(zpow[k], 0xFFFFFFFFu);
+    HIPCHK(hipMemcpy(s->d.zfin, zf.data(), 4ull * (C + 2), hipMemcpyHostToDevice));
+  }
   HIPCHK(hipMemcpy(s->d.ztab, ztab.data(), 4ull * ztab.size(), hipMemcpyHostToDevice));
   std::vector<uint32_t> zb(9 * 1024);
   for (uint32_t c = 0; c < 9; ++c)
@@ -303,8 +308,8 @@ static int upload_segments(kb_sim* s) {
 static void free_all(kb_sim* s) {
   Dev& d = s->d;
   void* ptrs[] = {d.stamp, d.bits, d.segp, d.sdirty, d.dirty, d.alive, d.abits, d.start_round, d.n, d.fp,
-                  d.last_bcast, d.susp, d.cur, d.paq, d.paq_n, d.cseg, d.segmul, d.seglen, d.zpow, d.ztab, d.zbtab, d.htab,
-                  d.stats, d.ctr, d.truefp, d.flog, d.flog_n, d.fstart,
+                  d.last_bcast, d.susp, d.cur, d.paq, d.paq_n, d.cseg, d.segmul, d.seglen, d.zpow, d.zfin, d.ztab, d.zbtab, d.htab,
+                  d.stats, d.ctr, d.truefp, d.flog, d.flog_n, d.fstart, d.kpr_big,
                   s->ob[0].msgs, s->ob[0].pay, s->ob[0].off, s->ob[0].cap, s->ob[0].cnt, s->ob[0].poff,
                   s->ob[1].msgs, s->ob[1].pay, s->ob[1].off, s->ob[1].cap, s->ob[1].cnt, s->ob[1].poff,
                   s->wc.status, s->wc.cnt1, s->wc.bnd, s->wc.bpay, s->wc.cursor, s->wc.in_off, s->wc.inbox,
@@ -361,9 +366,9 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
   A(d.stamp, (size_t)C * W); A(d.bits, (size_t)C * d.NWR); A(d.segp, (size_t)C * NSEG); A(d.sdirty, C);
   A(d.dirty, C); A(d.alive, C); A(d.abits, d.NWR); A(d.start_round, C); A(d.n, C); A(d.fp, C);
   A(d.last_bcast, C); A(d.susp, (size_t)C * SLOTS); A(d.cur, (size_t)C * CSLOTS); A(d.paq, (size_t)C * PAQ);
-  A(d.paq_n, C); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
+  A(d.paq_n, C); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2); A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1);
-  A(d.flog, (size_t)C * LOGCAP); A(d.flog_n, C); A(d.fstart, (size_t)C * 16);
+  A(d.flog, (size_t)C * LOGCAP); A(d.flog_n, C); A(d.fstart, (size_t)C * 16); A(d.kpr_big, C);
   s->msg_cap = std::max<uint32_t>(8u * C + (uint32_t)TICK_MAX * C, 1u << 16);
   s->pay_cap = std::max<uint32_t>((d.capk + 1) * C, 1u << 24);
   for (int b = 0; b < 2; ++b) {
@@ -383,6 +388,7 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
 #undef A
   if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); free_all(s); delete s; return KB_CAPACITY; }
   s->so.S = S;
+  (void)hipMemset(d.kpr_big, 0xFF, 4ull * C);          // no round yet
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   s->newmask = nullptr; s->respmask = nullptr; s->mask_words = 0;
   s->resp_scratch = nullptr; s->resp_scratch_words = 0;
@@ -582,7 +588,15 @@ static int step_round(kb_sim* s) {
     k_kp_prologue<<<1024, 256, 0, st>>>(d, ib, s->wc, r);
     k_touch_fix<<<1024, 256, 0, st>>>(d, s->wc);
     k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc);
+    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 12, st));
     k_proc<<<4096, 256, 0, st>>>(d, ib, nb, s->wc, r);
+    if (s->debug_waves) {
+      uint32_t dbg[3];
+      HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 12, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      fprintf(stderr, "[kb] round %d wave %u: prologue inserts %u, fingerprint refreshes %u (max per node %u)\n", r, w,
+              dbg[0], dbg[1], dbg[2]);
+    }
     cur ^= 1;
   }
   k_round_end<<<1, 1, 0, st>>>(d, r);

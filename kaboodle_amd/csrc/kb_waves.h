@@ -220,6 +220,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
   __shared__ uint32_t ztab[ZT * 128];
   __shared__ Susp s_susp[4][SLOTS];
   __shared__ Cur s_cur[4][CSLOTS];
+  __shared__ uint2 s_suf[4][NSEG + 1];
   load_ztab(d, ztab);
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t l = lane();
@@ -232,6 +233,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     uint8_t* rw = row_of(d, i);
     const uint32_t* bw = bits_of(d, i);
     uint32_t n = d.n[i], fp = d.fp[i], oseq = 0, pay_used = 0, fn = d.flog_n[i];
+    int32_t kbig = d.kpr_big[i];
     bool dirty = d.dirty[i] != 0, need_sync = false;
     unsigned long long segs = 0;
     if (l < SLOTS) s_susp[wv][l] = d.susp[(size_t)i * SLOTS + l];
@@ -255,8 +257,56 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
         }
       }
     }
+    uint32_t dbg_fp = 0, dbg_ins = 0;
+    // Incremental fingerprint (uniform identities, sorted inbox).  Prologue insertions arrive in
+    // ascending id order, so for an inserted x every member above x is still the base set's:
+    //   raw(S + x) = raw(S)·Z ⊕ B·(Z ⊕ 1) ⊕ c_x·Z^{n>x},  B = fold of the members above x, n>x their count
+    // B = (fold of x's segment above x)·Z^{cnt} ⊕ suffix combine of the later segments (taken once per
+    // node, s_suf).  Each batch precomputes K = B·(Z ⊕ 1) ⊕ c_x·Z^{n>x} lane-parallel; the in-order
+    // update is then one multiply by Z per insertion.
+    bool inc = false, fpstale = false;
+    uint32_t R = 0;
+    auto take_base = [&]() {
+      if (need_sync) { wave_mem_sync(); need_sync = false; }
+      const unsigned long long sd = d.sdirty[i] | segs;
+      uint2 sp;
+      if ((sd >> l) & 1ull) { sp = fold_segment(d, ztab, i, l); d.segp[(size_t)i * NSEG + l] = sp; }
+      else sp = d.segp[(size_t)i * NSEG + l];
+      uint32_t raw = sp.x, cnt = sp.y, c = sp.y;
+      uint32_t oc[6], zp[6];
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {               // inclusive suffix scan: lane k -> segments k..63
+        const uint32_t st = 1u << t;
+        oc[t] = __shfl_down(c, st, 64);
+        if (l + st >= 64) oc[t] = 0;
+        c += oc[t];
+      }
+#pragma unroll
+      for (int t = 0; t < 6; ++t) zp[t] = d.zpow[oc[t]];
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        const uint32_t st = 1u << t;
+        const uint32_t oraw = __shfl_down(raw, st, 64);
+        if (l + st < 64) raw = multmodp(zp[t], raw) ^ oraw;
+      }
+      cnt = c;
+      s_suf[wv][l] = make_uint2(raw, cnt);
+      if (l == 0) s_suf[wv][NSEG] = make_uint2(0, 0);
+      wait_lds();
+      __builtin_amdgcn_wave_barrier();
+      R = bcast(raw, 0);
+      if (bcast(cnt, 0) != n) set_err(d, DERR_FP);
+      if (l == 0 && sd) atomicAnd(&d.sdirty[i], ~sd);
+      segs = 0;
+      inc = true; dirty = false; fpstale = true;
+    };
     auto fp_now = [&]() -> uint32_t {
+      if (inc) {
+        if (fpstale) { fp = R ^ d.zfin[n] ^ 0xFFFFFFFFu; fpstale = false; }
+        return fp;
+      }
       if (dirty) {
+        dbg_fp++;
         if (need_sync) { wave_mem_sync(); need_sync = false; }
         fp = wave_fp(d, ztab, i, segs);
         segs = 0;
@@ -272,14 +322,69 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     uint32_t last_g = 0xFFFFFFFFu, last_sender = 0xFFFFFFFFu;
     // messages are fetched 64 at a time (lane k holds the record of message base + k) and handed to
     // the wave one by one with cross-lane reads, so the in-order loop never waits on HBM per message
+    // The prologue's row state (member bit, stamp) of each batch's senders is fetched with the batch:
+    // a handler changes only its own sender's entry, and equal senders are adjacent (sorted inbox), so
+    // the prefetched state of a later message of the batch is still current when it is reached.
     Msg lm;
+    uint32_t pre_was = 0, pre_b = 0, Kx = 0;
     for (uint32_t t = 0; t < icnt; ++t) {
       uint32_t g;
       if (sorted) {
         if ((t & 63) == 0) {
+          if (need_sync) { wave_mem_sync(); need_sync = false; }
           const uint32_t gl = small ? mine : (t + l < icnt ? wc.inbox[ibase + t + l] : 0xFFFFFFFFu);
-          if (gl != 0xFFFFFFFFu) lm = ib.msgs[gl];
+          if (gl != 0xFFFFFFFFu) {
+            lm = ib.msgs[gl];
+            pre_was = (bw[lm.sender >> 5] >> (lm.sender & 31)) & 1u;
+            pre_b = pre_was ? rw[lm.sender] : ST_UNKNOWN;
+          }
           if (!small) mine = gl;
+          // insertions of this batch: first message of a sender run whose sender is not a member
+          const uint32_t prev = __shfl_up(lm.sender, 1, 64);
+          const bool ins = gl != 0xFFFFFFFFu && !pre_was && lm.sender != (l == 0 ? last_sender : prev);
+          const unsigned long long insm = __ballot(ins);
+          if (d.uniform && insm) {
+            if (!inc) take_base();
+            const uint8_t* hb = reinterpret_cast<const uint8_t*>(bw);
+            if (__popcll(insm) >= 8) {              // many: one insertion per lane
+              if (ins) {
+                const uint32_t x = lm.sender, k = x / d.SEGW, hend = (k + 1) * (d.SEGW / 8);
+                uint32_t praw = 0, pcnt = 0;
+                fold_half(d, ztab, x >> 3, hb[x >> 3] & ~((2u << (x & 7)) - 1u) & 0xFFu, praw, pcnt);
+                for (uint32_t h0 = (x >> 3) + 1; h0 < hend; h0 += 16) {   // 16 blocks of loads in flight
+                  uint32_t m8v[16], hv[16];
+#pragma unroll
+                  for (int j = 0; j < 16; ++j) m8v[j] = h0 + j < hend ? hb[h0 + j] : 0u;
+#pragma unroll
+                  for (int j = 0; j < 16; ++j) hv[j] = m8v[j] ? d.htab[(size_t)(h0 + j) * 256 + m8v[j]] : 0u;
+#pragma unroll
+                  for (int j = 0; j < 16; ++j)
+                    if (m8v[j]) { const uint32_t c = __popc(m8v[j]); praw = mulzc(ztab, praw, c) ^ hv[j]; pcnt += c; }
+                }
+                const uint2 su = s_suf[wv][k + 1];
+                const uint32_t Bx = multmodp(d.zpow[su.y], praw) ^ su.x;
+                Kx = mulzc(ztab, Bx, 1) ^ Bx ^ multmodp(d.zpow[pcnt + su.y], d.cseg[x]);
+              }
+            } else {                                  // few: the whole wave on each insertion
+              for (unsigned long long mm = insm; mm; mm &= mm - 1) {
+                const int q = __ffsll((long long)mm) - 1;
+                const uint32_t x = bcast(lm.sender, q), k = x / d.SEGW;
+                const uint32_t hs = x >> 3, nh = (k + 1) * (d.SEGW / 8) - hs;
+                uint32_t praw = 0, pcnt = 0;
+                for (uint32_t h = hs + (l * nh) / 64; h < hs + ((l + 1) * nh) / 64; ++h) {
+                  uint32_t m8 = hb[h];
+                  if (h == hs) m8 &= ~((2u << (x & 7)) - 1u) & 0xFFu;
+                  fold_half(d, ztab, h, m8, praw, pcnt);
+                }
+                wave_combine(d, praw, pcnt);
+                praw = bcast(praw, 0); pcnt = bcast(pcnt, 0);
+                const uint2 su = s_suf[wv][k + 1];
+                const uint32_t Bx = multmodp(d.zpow[su.y], praw) ^ su.x;
+                const uint32_t K = mulzc(ztab, Bx, 1) ^ Bx ^ multmodp(d.zpow[pcnt + su.y], d.cseg[x]);
+                if (l == (uint32_t)q) Kx = K;
+              }
+            }
+          }
         }
         g = bcast(mine, (int)(t & 63));
       } else {      // beyond SORT_MAX: next smallest index above the previous one
@@ -302,11 +407,16 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       }
       const uint32_t s = m.sender;
       if (s != last_sender) {                         // prologue: insert(sender, Known(now)) (:406-415)
-        const bool was = (bw[s >> 5] >> (s & 31)) & 1u;
-        const uint8_t b = was ? rw[s] : ST_UNKNOWN;
+        bool was;
+        uint8_t b;
+        if (sorted) { was = bcast(pre_was, (int)(t & 63)) != 0; b = (uint8_t)bcast(pre_b, (int)(t & 63)); }
+        else { was = (bw[s >> 5] >> (s & 31)) & 1u; b = was ? rw[s] : ST_UNKNOWN; }
         if (b == ST_SUSPECT && l < SLOTS && s_susp[wv][l].kind && s_susp[wv][l].peer == s) s_susp[wv][l].kind = 0;
         if (!was) {
-          n++; dirty = true; segs |= seg_bit(d, s);
+          dbg_ins++;
+          n++; segs |= seg_bit(d, s);
+          if (inc) { R = mulzc(ztab, R, 1) ^ bcast(Kx, (int)(t & 63)); fpstale = true; }
+          else dirty = true;
           if (l == 0) const_cast<uint32_t*>(bw)[s >> 5] |= 1u << (s & 31);   // single writer of this row
         }
         if (b != now) {
@@ -365,11 +475,15 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
         case K_KPR: {                                                // :473-512
           // reply = {p Known, p != self, p != sender, stamped within SHARE_AGE}, never truncated;
           // > 10240 B is lost at the receiver (Q3), so only the count matters once it exceeds capk
+          // The fresh set only grows during a round (stamps rise to now; nothing is removed while
+          // messages are handled), so once a reply counted capk + 2 entries every later reply of
+          // this node in this round is oversize too: kpr_big[i] = r records that.
           if (need_sync) { wave_mem_sync(); need_sync = false; }
           const uint32_t poff = ob.poff[i] + pay_used;
           uint32_t total = 0;
           uint64_t size = 8 + (d.seglen[i] - ADDR_LEN) + 4 + 8;
-          bool over = false;
+          bool over = d.uniform && kbig == r;
+          if (over) { w_over++; maybe_sync(s, m.fp, m.n); break; }
           auto take = [&](bool ok, uint32_t j) {
             const unsigned long long okm = __ballot(ok);
             const uint32_t pos = total + __popcll(okm & ((1ull << l) - 1ull));
@@ -379,7 +493,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
               else set_err(d, DERR_PAYLOAD);
             }
             total += __popcll(okm);
-            if (d.uniform && total > d.capk) over = true;
+            if (d.uniform && total > d.capk + 1) over = true;
           };
           // the log ring holds the newest LOGCAP entries: the whole window when complete; otherwise
           // those entries are still exact members of the reply, enough to prove it oversize
@@ -410,6 +524,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
               for (int t2 = 0; t2 < 16; ++t2) take((mask >> t2) & 1u, j0 + t2);
             }
           }
+          if (d.uniform && total > d.capk + 1) kbig = r;
           over = d.uniform ? total > d.capk : size > (uint64_t)BUFSZ;
           if (over) w_over++;
           else { emit_msg(ob, d, i, oseq, s, K_KP, total, 0, 0, poff); pay_used += total; }
@@ -421,10 +536,13 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     }
     if (l < SLOTS) d.susp[(size_t)i * SLOTS + l] = s_susp[wv][l];
     if (l < CSLOTS) d.cur[(size_t)i * CSLOTS + l] = s_cur[wv][l];
+    if (inc) fp_now();                              // exact: the touched checkpoints stay marked stale
     if (l == 0) {
       if (segs) atomicOr(&d.sdirty[i], segs);
-      d.n[i] = n; d.fp[i] = fp; d.dirty[i] = dirty ? 1 : 0; d.flog_n[i] = fn;
+      d.n[i] = n; d.fp[i] = fp; d.dirty[i] = dirty ? 1 : 0; d.flog_n[i] = fn; d.kpr_big[i] = kbig;
       ob.cnt[i] = oseq;
+      if (dbg_fp) { atomicAdd(&d.ctr[C_DBG_FP], dbg_fp); atomicMax(&d.ctr[C_DBG_MAXFP], dbg_fp); }
+      if (dbg_ins) atomicAdd(&d.ctr[C_DBG_INS], dbg_ins);
     }
     wait_lds();                                       // the LDS slot caches are reused by the next node
     __builtin_amdgcn_wave_barrier();
