@@ -125,6 +125,28 @@ int  kb_sim_stats(kb_sim* sim, kb_stats* out);
 /* fingerprint of the true running set (what every converged node should report) */
 int  kb_sim_true_fingerprint(kb_sim* sim, uint32_t* fp);
 
+/* ---- sharding across GPUs --------------------------------------------------------
+ * A mesh of C ids can be split into `world` (1..8) contiguous row shards: shard k holds the observer
+ * state of ids [k*S, min(C, (k+1)*S)), S = ceil(C/world).  The reference's UDP transport between
+ * instances (src/kaboodle.rs:188-226, src/networking.rs:27-121) becomes, per round, an all-to-all-v
+ * of each delivery wave's records and an all-gather of the Join/Failed broadcast lists.  Results are
+ * bit-identical to the unsharded mesh (same Philox draws, same canonical orders).
+ *
+ * kb_sim_create_rank: one process per GPU.  Rank 0 makes the id with kb_rccl_unique_id and the host
+ *   broadcasts it (e.g. over torch.distributed); every rank then creates its shard.  Calls that change
+ *   the mesh (start/stop/set_identity/ping_addrs) and kb_sim_step / kb_sim_stats are collective: every
+ *   rank makes them alike.  Row inspection (fingerprint/peers/peer_states/dump_*) is answered by the
+ *   rank holding the row and returns KB_INVALID_ARGUMENT on the others; kb_sim_fingerprints and
+ *   kb_sim_dump_scalars fill this rank's rows (zeros elsewhere).
+ * kb_sim_create_local: all shards inside this process on one device (one host thread per shard and
+ *   step), exchanged by device copies — the whole ABI then behaves as for an unsharded mesh.       */
+#define KB_UNIQUE_ID_BYTES 128
+int  kb_rccl_unique_id(uint8_t* out, size_t cap);
+int  kb_sim_create_rank(const kb_config* cfg, int32_t rank, int32_t world, const uint8_t* unique_id,
+                        kb_sim** out);
+int  kb_sim_create_local(const kb_config* cfg, int32_t shards, kb_sim** out);
+int  kb_sim_shard_info(kb_sim* sim, int32_t* rank, int32_t* world, uint32_t* lo, uint32_t* hi);
+
 /* ---- parity / test surface ---------------------------------------------------------------------- */
 /* Raw stamp row of `node` (capacity bytes, DESIGN.md §2.2 encoding). */
 int  kb_sim_dump_row(kb_sim* sim, uint32_t node, uint8_t* row, size_t cap);

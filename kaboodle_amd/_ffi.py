@@ -115,6 +115,13 @@ _SIGS = {
     "last_error": (C.c_char_p, []),
 }
 _OPTIONAL = {
+    # sharding (HIP library only; the oracle is the unsharded mesh every shard layout must reproduce)
+    "rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8), C.c_size_t]),
+    "sim_create_rank": (C.c_int, [C.POINTER(KbConfig), C.c_int32, C.c_int32, C.POINTER(C.c_uint8),
+                                  C.POINTER(C.c_void_p)]),
+    "sim_create_local": (C.c_int, [C.POINTER(KbConfig), C.c_int32, C.POINTER(C.c_void_p)]),
+    "sim_shard_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_uint32),
+                                 C.POINTER(C.c_uint32)]),
     "sim_kernel_time": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "sim_reset_kernel_time": (C.c_int, [C.c_void_p]),
     "sim_sweep_bytes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
@@ -147,16 +154,47 @@ class SimLib:
             raise KbError(rc, f"{self.prefix}{name} ({err.decode(errors='replace') if err else ''})")
 
 
-class Sim:
-    """A simulated mesh (one handle) bound to a SimLib."""
+KB_UNIQUE_ID_BYTES = 128
 
-    def __init__(self, lib: SimLib, cfg: SimConfig):
+
+def rccl_unique_id(lib: SimLib) -> bytes:
+    """A fresh RCCL unique id (rank 0 makes it; the host broadcasts it to the other ranks)."""
+    buf = (C.c_uint8 * KB_UNIQUE_ID_BYTES)()
+    lib.call("rccl_unique_id", buf, KB_UNIQUE_ID_BYTES)
+    return bytes(buf)
+
+
+class Sim:
+    """A simulated mesh (one handle) bound to a SimLib.
+
+    shards=k (k >= 1): the mesh split into k row shards inside this process (kb_sim_create_local);
+    rank/world/uid: this process's shard of a mesh spread over `world` processes (kb_sim_create_rank).
+    A library without the sharding entry points (the oracle) always builds the unsharded mesh, which
+    every shard layout must reproduce bit for bit.
+    """
+
+    def __init__(self, lib: SimLib, cfg: SimConfig, shards: int = 0, rank: int | None = None,
+                 world: int | None = None, uid: bytes | None = None):
         self.lib, self.cfg = lib, cfg
         self._c = cfg.to_c()
         h = C.c_void_p()
-        lib.call("sim_create", C.byref(self._c), C.byref(h))
+        if world is not None and "sim_create_rank" in lib.fn:
+            ub = (C.c_uint8 * KB_UNIQUE_ID_BYTES).from_buffer_copy(uid)
+            lib.call("sim_create_rank", C.byref(self._c), rank, world, ub, C.byref(h))
+        elif shards and "sim_create_local" in lib.fn:
+            lib.call("sim_create_local", C.byref(self._c), shards, C.byref(h))
+        else:
+            lib.call("sim_create", C.byref(self._c), C.byref(h))
         self.h = h
         self.capacity = cfg.capacity
+
+    def shard_info(self):
+        """(rank, world, lo, hi): the rows this handle holds."""
+        if "sim_shard_info" not in self.lib.fn:
+            return 0, 1, 0, self.capacity
+        r, w, lo, hi = C.c_int32(), C.c_int32(), C.c_uint32(), C.c_uint32()
+        self.lib.call("sim_shard_info", self.h, C.byref(r), C.byref(w), C.byref(lo), C.byref(hi))
+        return r.value, w.value, lo.value, hi.value
 
     def close(self) -> None:
         if self.h:

@@ -12,14 +12,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "kb_sim.hip")
 OUT = os.path.join(HERE, "libkaboodle_sim.so")
 ARCH = os.environ.get("KB_OFFLOAD_ARCH", "gfx950")
-FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-Wno-unused-value"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-result", "-Wno-unused-value", "-lrccl", "-pthread"]
 
 
 def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = [SRC] + [os.path.join(HERE, "csrc", f) for f in ("kb_device.h", "kb_common.h", "kb_round.h", "kb_tick.h", "kb_waves.h")] + [
+    deps = [SRC] + [os.path.join(HERE, "csrc", f) for f in ("kb_device.h", "kb_common.h", "kb_round.h", "kb_tick.h", "kb_waves.h", "kb_xfer.h")] + [
             os.path.join(os.path.dirname(HERE), "include", "kaboodle_sim.h")]
     return any(os.path.getmtime(p) > t for p in deps)
 

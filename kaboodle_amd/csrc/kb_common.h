@@ -28,7 +28,12 @@ constexpr int NSEG = 64;          // fingerprint checkpoints per row
 constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
 constexpr int ZB = 9 * 1024;      // LDS byte tables for Z^0..Z^8 (the sweep: 4 lookups per multiply)
 
+// Row shards: a shard holds the rows of ids [lo, hi) — the observer state of those
+// peers.  Row-indexed tables are allocated for the local rows only and their pointers are biased by
+// -lo rows, so every kernel indexes them with the global id.  Per-id facts (alive, start_round,
+// identity CRCs) are replicated: every shard applies the same lifecycle events and churn draws.
 struct Dev {
+  uint32_t lo, hi;                // local rows (unsharded: 0, C)
   uint32_t C, W, SEGW, NWR;       // capacity, row stride, ids per segment (W/64), bitset words per row (W/32)
   uint32_t k0, k1;
   uint32_t loss_thr, churn_thr;
@@ -92,6 +97,7 @@ __device__ inline void stage16(uint4* dst, const uint4* src, uint32_t n, uint32_
 }
 __device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }
 __device__ inline bool faults(const Dev& d, int32_t r) { return d.fault_end < 0 || r < d.fault_end; }
+__device__ inline bool local(const Dev& d, uint32_t i) { return i >= d.lo && i < d.hi; }
 __device__ inline bool part_blocks(const Dev& d, int32_t r, uint32_t a, uint32_t b) {
   if (d.pgroups <= 1 || r < d.pstart || r >= d.pend) return false;
   return ((uint64_t)a * d.pgroups / d.C) != ((uint64_t)b * d.pgroups / d.C);
@@ -265,17 +271,24 @@ __device__ inline void susp_clear(const Dev& d, uint32_t i, uint32_t p) {
   Susp* s = d.susp + (size_t)i * SLOTS;
   for (int k = 0; k < SLOTS; ++k) if (s[k].kind && s[k].peer == p) s[k].kind = 0;
 }
+// lifecycle: the per-id part on every shard, the row part on the shard holding the row
 __device__ void node_start(const Dev& d, uint32_t i, int32_t r) {      // src/lib.rs:136-156
-  if (mem_set(d, i, i)) d.n[i] += 1;
-  else susp_clear(d, i, i);
-  row_of(d, i)[i] = enc(r, r);
-  mark(d, i, seg_bit(d, i));
-  d.alive[i] = 1; d.start_round[i] = r; d.last_bcast[i] = NONE_ROUND; d.paq_n[i] = 0;
-  for (int k = 0; k < CSLOTS; ++k) d.cur[(size_t)i * CSLOTS + k].used = 0;
+  if (local(d, i)) {
+    if (mem_set(d, i, i)) d.n[i] += 1;
+    else susp_clear(d, i, i);
+    row_of(d, i)[i] = enc(r, r);
+    mark(d, i, seg_bit(d, i));
+    d.last_bcast[i] = NONE_ROUND; d.paq_n[i] = 0;
+    for (int k = 0; k < CSLOTS; ++k) d.cur[(size_t)i * CSLOTS + k].used = 0;
+  }
+  d.alive[i] = 1; d.start_round[i] = r;
 }
 __device__ void node_stop(const Dev& d, uint32_t i) {                  // src/lib.rs:159-183
-  if (mem_clr(d, i, i)) { susp_clear(d, i, i); d.n[i] -= 1; mark(d, i, seg_bit(d, i)); }
-  d.alive[i] = 0; d.paq_n[i] = 0;
+  if (local(d, i)) {
+    if (mem_clr(d, i, i)) { susp_clear(d, i, i); d.n[i] -= 1; mark(d, i, seg_bit(d, i)); }
+    d.paq_n[i] = 0;
+  }
+  d.alive[i] = 0;
 }
 
 // block-wide sum (blockDim <= 1024), valid in thread 0

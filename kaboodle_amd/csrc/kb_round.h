@@ -7,8 +7,8 @@ namespace kb {
 
 // ---- stamp window: every 64 rounds known stamps shift down, saturating at "ancient"
 __global__ void k_rebase(Dev d) {
-  const size_t total = (size_t)d.C * d.W / 16;
-  uint4* p = reinterpret_cast<uint4*>(d.stamp);
+  const size_t total = (size_t)(d.hi - d.lo) * d.W / 16;     // the local rows
+  uint4* p = reinterpret_cast<uint4*>(d.stamp + (size_t)d.lo * d.W);
   for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (size_t)gridDim.x * blockDim.x) {
     const uint4 v = p[k];
     uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -54,7 +54,7 @@ __global__ void k_churn_join(Dev d, int32_t r) {
   __syncthreads();
   if (threadIdx.x == 0) {
     d.ctr[C_NEXTFREE] = nf + joins; d.ctr[C_LEAVES] = 0;
-    d.stats[S_CLEAVE] += leaves; d.stats[S_CJOIN] += joins;
+    if (d.lo == 0) { d.stats[S_CLEAVE] += leaves; d.stats[S_CJOIN] += joins; }   // replicated: counted once
   }
 }
 
@@ -102,8 +102,8 @@ __global__ __launch_bounds__(1024) void k_truefp(Dev d) {
 
 // round start of every node's freshness log window
 __global__ void k_log_mark(Dev d, int32_t r) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < d.C) d.fstart[(size_t)i * 16 + ((uint32_t)r & 15u)] = d.flog_n[i];
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < d.hi) d.fstart[(size_t)i * 16 + ((uint32_t)r & 15u)] = d.flog_n[i];
 }
 
 // ================================================================================================
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
   // counters stay in registers for the whole persistent loop: one atomic per wave at the end (same-
   // address atomics from every node would serialise in L2 and stall the waves that wait on them)
   unsigned long long w_lost = 0, w_removed = 0, w_resp = 0;
-  for (uint32_t i = blockIdx.x * wpb + wv; i < d.C; i += gridDim.x * wpb) {
+  for (uint32_t i = d.lo + blockIdx.x * wpb + wv; i < d.hi; i += gridDim.x * wpb) {
     if (!d.alive[i] || d.start_round[i] >= r) {
       if (l == 0) { pb.nresp[i] = 0; pb.paysum[i] = 0; }
       continue;

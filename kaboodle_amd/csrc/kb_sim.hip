@@ -22,10 +22,12 @@
 #include <vector>
 #include <array>
 #include <algorithm>
+#include <thread>
 #include "kb_common.h"
 #include "kb_round.h"
 #include "kb_tick.h"
 #include "kb_waves.h"
+#include "kb_xfer.h"
 
 using namespace kb;
 
@@ -36,7 +38,7 @@ using namespace kb;
 struct ScanArgs {
   const uint32_t* in[4]; uint32_t* out[4]; int narr; uint32_t n;
   uint32_t* totals;   // device, narr values (+ list count at totals[4] when list != null)
-  uint32_t* list; uint32_t* list_count;
+  uint32_t* list; uint32_t* list_count; uint32_t list_base;   // list entries are j + list_base
   uint32_t addc[4];   // constant added to every element of array q before scanning
   uint32_t* tiles;    // workspace [5 * ntiles]
   uint32_t ntiles;
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(1024) void k_scan_apply(ScanArgs a) {
   if (t < 5) { uint32_t run = 0; for (int w = 0; w < 16; ++w) { uint32_t x = wpre[t][w]; wpre[t][w] = run; run += x; } }
   __syncthreads();
   for (int q = 0; q < a.narr; ++q) if (j < a.n) a.out[q][j] = base[q] + wpre[q][t >> 6] + ex[q];
-  if (a.list && j < a.n && v[4]) a.list[base[4] + wpre[4][t >> 6] + ex[4]] = j;
+  if (a.list && j < a.n && v[4]) a.list[base[4] + wpre[4][t >> 6] + ex[4]] = j + a.list_base;
   if (tile == gridDim.x - 1 && t == 1023) {
     for (int q = 0; q < a.narr; ++q) a.totals[q] = base[q] + wpre[q][15] + ex[q] + v[q];
     if (a.list) { const uint32_t c = base[4] + wpre[4][15] + ex[4] + v[4]; a.totals[4] = c; if (a.list_count) *a.list_count = c; }
@@ -110,23 +112,25 @@ __global__ void k_build_htab(Dev d) {
   }
   d.htab[k] = raw;
 }
-__global__ void k_set_cap(uint32_t C, const uint32_t* nresp, uint32_t* cap, uint32_t* cnt) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < C) { cap[i] = nresp[i] + TICK_MAX; cnt[i] = nresp[i]; }
+__global__ void k_set_cap(Dev d, const uint32_t* nresp, uint32_t* cap, uint32_t* cnt) {
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < d.hi) { cap[i] = nresp[i] + TICK_MAX; cnt[i] = nresp[i]; }
 }
 __global__ void k_init_nodes(Dev d, uint32_t n0) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.C) return;
-  d.last_bcast[i] = NONE_ROUND;
+  if (local(d, i)) d.last_bcast[i] = NONE_ROUND;
   d.start_round[i] = NONE_ROUND;
   if (i < n0) node_start(d, i, 0);
 }
+// rows of the initial members (the local ones): every initial member known and "ancient", self now
 __global__ void k_init_converged_rows(Dev d, uint32_t n0) {
   const uint32_t wpr = d.W / 16;
-  const size_t words = (size_t)n0 * wpr;
+  const uint32_t r0 = d.lo, r1 = n0 < d.hi ? n0 : d.hi;
+  const size_t words = r1 > r0 ? (size_t)(r1 - r0) * wpr : 0;
   uint4* p = reinterpret_cast<uint4*>(d.stamp);
   for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < words; k += (size_t)gridDim.x * blockDim.x) {
-    const uint32_t i = (uint32_t)(k / wpr), c = (uint32_t)(k % wpr);
+    const uint32_t i = r0 + (uint32_t)(k / wpr), c = (uint32_t)(k % wpr);
     uint32_t w4[4];
     for (int q = 0; q < 4; ++q) {
       uint32_t y = 0;
@@ -140,27 +144,28 @@ __global__ void k_init_converged_rows(Dev d, uint32_t n0) {
     }
     p[(size_t)i * wpr + c] = make_uint4(w4[0], w4[1], w4[2], w4[3]);
   }
-  const size_t bw = (size_t)n0 * d.NWR;
+  const size_t bw = r1 > r0 ? (size_t)(r1 - r0) * d.NWR : 0;
   for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < bw; k += (size_t)gridDim.x * blockDim.x) {
     const uint32_t w = (uint32_t)(k % d.NWR);
     uint32_t x = 0;
     if (w * 32 + 32 <= n0) x = 0xFFFFFFFFu;
     else if (w * 32 < n0) x = (1u << (n0 - w * 32)) - 1u;
-    d.bits[k] = x;
+    d.bits[(size_t)r0 * d.NWR + k] = x;
   }
 }
 __global__ void k_init_converged_nodes(Dev d, uint32_t n0) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.C) return;
-  d.last_bcast[i] = NONE_ROUND;
+  const bool loc = local(d, i);
+  if (loc) d.last_bcast[i] = NONE_ROUND;
   d.start_round[i] = NONE_ROUND;
   if (i >= n0) return;
-  d.alive[i] = 1; d.start_round[i] = 0; d.dirty[i] = 1; d.n[i] = n0; d.last_bcast[i] = -1000; d.paq_n[i] = 0;
-  d.sdirty[i] = ~0ull;
+  d.alive[i] = 1; d.start_round[i] = 0;
+  if (loc) { d.dirty[i] = 1; d.n[i] = n0; d.last_bcast[i] = -1000; d.paq_n[i] = 0; d.sdirty[i] = ~0ull; }
 }
 __global__ void k_mark_all_dirty(Dev d) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < d.C) { d.dirty[i] = 1; d.sdirty[i] = ~0ull; }
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < d.hi) { d.dirty[i] = 1; d.sdirty[i] = ~0ull; }
 }
 __global__ __launch_bounds__(64) void k_fp_one(Dev d, uint32_t i) {
   __shared__ uint32_t ztab[ZT * 128];
@@ -172,8 +177,8 @@ __global__ __launch_bounds__(64) void k_fp_one(Dev d, uint32_t i) {
 __global__ __launch_bounds__(256) void k_fp_all(Dev d) {
   __shared__ uint32_t ztab[ZT * 128];
   load_ztab(d, ztab);
-  const uint32_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= d.C || !d.dirty[i]) return;
+  const uint32_t i = d.lo + blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= d.hi || !d.dirty[i]) return;
   const uint32_t f = wave_fp(d, ztab, i, 0);
   if (lane() == 0) { d.fp[i] = f; d.dirty[i] = 0; }
 }
@@ -210,37 +215,73 @@ struct kb_sim {
   Dev d;
   int device;
   hipStream_t st;
-  uint32_t C, W, S;
+  uint32_t C, W, S;                    // capacity, row stride, row-sweep column splits
+  // row shard: this handle holds rows [lo, hi) of the mesh, R = hi - lo
+  uint32_t lo, hi, R;
+  int rank, world;
+  Xfer* xf;                            // null: unsharded (no exchange at all)
+  bool in_group;                       // a shard of a kb_sim_create_local group
+  std::vector<void*> allocs;           // device memory owned by this handle
   int32_t round;
   std::vector<uint8_t> h_ident, h_idlen, h_ever;
   std::vector<Event> events;
   OutBuf ob[2];
   WaveCtl wc;
   uint32_t msg_cap, pay_cap;
-  BCast* bfail; BCast* bjoin;
+  BCast* bfail; BCast* bjoin;          // the round's broadcast lists (whole mesh, sender order)
+  BCast* bfail_loc; BCast* bjoin_loc;  // sharded: this shard's part, before the all-gather
   uint32_t nf, nj;
   BcastSlots bs;
   uint32_t* join_off; uint32_t* fail_off;
   uint32_t* scan_tot; uint32_t* scan_tiles;
   unsigned long long* newmask; unsigned long long* respmask; size_t mask_words;
+  unsigned long long* newmask_base; unsigned long long* respmask_base;
   uint32_t* nresp; uint32_t* paysum; uint32_t* nbase; uint32_t* resp_off;
   uint32_t* resp_nodes; uint32_t* bf_gid; uint8_t* bf_dep;
   uint32_t* resp_scratch; size_t resp_scratch_words;
   SweepOut so;
   Event* d_events; uint32_t events_cap;
+  // sharded waves: send side (xs), all-gathered counts, receive buffers (grown on demand)
+  XState xs;
+  uint32_t* xall; unsigned long long* xstats;
+  std::vector<uint32_t> h_xall;
+  Msg* rmsg; uint32_t* rpay; uint8_t* rstatus; uint32_t* rinbox; uint32_t* rkp;
+  size_t rmsg_cap, rpay_cap;
   hipEvent_t ev0, ev1, er0, er1;
   double sweep_ms, round_ms;
   uint64_t sweep_launches, round_launches, sweep_bytes, bj_total, bf_total;
   uint32_t ncu = 256;
   bool debug_waves = false;
   size_t lds_per_cu = 65536;
+  // kb_sim_create_local: a façade over `world` in-process shards (one host thread each per step)
+  std::vector<kb_sim*> shards;
+  LocalHub* hub;
 };
+
+// allocation of this handle's device memory; row tables hold the local rows only and their pointer
+// is biased by -lo rows so kernels index them with global ids
+template <class T> static hipError_t talloc(kb_sim* s, T** p, size_t n) {
+  hipError_t e = dalloc(p, n);
+  if (e == hipSuccess) s->allocs.push_back((void*)*p);
+  return e;
+}
+template <class T> static T* bias(T* base, size_t per_row, uint32_t lo) {
+  return reinterpret_cast<T*>(reinterpret_cast<uintptr_t>(base) - sizeof(T) * per_row * lo);
+}
+template <class T> static hipError_t ralloc(kb_sim* s, T** p, size_t per_row) {
+  T* base = nullptr;
+  hipError_t e = talloc(s, &base, per_row * s->R);
+  *p = bias(base, per_row, s->lo);
+  return e;
+}
+template <class T> static T* L(const kb_sim* s, T* p) { return p + s->lo; }   // biased row table -> local base
 
 static ScanArgs scan_args(kb_sim* s, uint32_t n, uint32_t* totals) {
   ScanArgs a; memset(&a, 0, sizeof a); a.n = n; a.totals = totals;
   a.tiles = s->scan_tiles; a.ntiles = (n + 1023) / 1024; return a;
 }
 static void launch_scan(const ScanArgs& a, hipStream_t st) {
+  if (!a.n) return;
   k_scan_tiles<<<a.ntiles, 1024, 0, st>>>(a);
   k_scan_apply<<<a.ntiles, 1024, 0, st>>>(a);
 }
@@ -306,47 +347,62 @@ static int upload_segments(kb_sim* s) {
 }
 
 static void free_all(kb_sim* s) {
-  Dev& d = s->d;
-  void* ptrs[] = {d.stamp, d.bits, d.segp, d.sdirty, d.dirty, d.alive, d.abits, d.start_round, d.n, d.fp,
-                  d.last_bcast, d.susp, d.cur, d.paq, d.paq_n, d.cseg, d.segmul, d.seglen, d.zpow, d.zfin, d.ztab, d.zbtab, d.htab,
-                  d.stats, d.ctr, d.truefp, d.flog, d.flog_n, d.fstart, d.kpr_big,
-                  s->ob[0].msgs, s->ob[0].pay, s->ob[0].off, s->ob[0].cap, s->ob[0].cnt, s->ob[0].poff,
-                  s->ob[1].msgs, s->ob[1].pay, s->ob[1].off, s->ob[1].cap, s->ob[1].cnt, s->ob[1].poff,
-                  s->wc.status, s->wc.cnt1, s->wc.bnd, s->wc.bpay, s->wc.cursor, s->wc.in_off, s->wc.inbox,
-                  s->wc.active, s->wc.kp_list, s->wc.touched, s->wc.touched_list, s->bfail, s->bjoin, s->bs.join,
-                  s->bs.nfail, s->bs.fail, s->join_off, s->fail_off, s->scan_tot, s->scan_tiles, s->newmask,
-                  s->respmask, s->nresp, s->paysum, s->nbase, s->resp_off, s->resp_nodes, s->bf_gid, s->bf_dep,
-                  s->resp_scratch, s->so.part, s->d_events};
-  for (void* p : ptrs) if (p) (void)hipFree(p);
+  for (void* p : s->allocs) (void)hipFree(p);
+  s->allocs.clear();
+  void* dyn[] = {s->newmask_base, s->respmask_base, s->resp_scratch, s->d_events, s->rmsg, s->rpay, s->rstatus,
+                 s->rinbox, s->rkp};
+  for (void* p : dyn) if (p) (void)hipFree(p);
+}
+static void destroy_shard(kb_sim* s) {
+  (void)hipSetDevice(s->device);
+  if (s->st) (void)hipStreamSynchronize(s->st);
+  free_all(s);
+  if (s->ev0) { (void)hipEventDestroy(s->ev0); (void)hipEventDestroy(s->ev1); (void)hipEventDestroy(s->er0); (void)hipEventDestroy(s->er1); }
+  if (s->st) (void)hipStreamDestroy(s->st);
+  delete s->xf;
+  delete s;
 }
 
-extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
+// One handle = rows [lo, hi) of a mesh; unsharded when xf is null (world 1, no exchange).
+static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_sim** out) {
   h_crc_init();
-  if (!cfg || !out || cfg->abi_version != KB_ABI_VERSION) { seterr("bad config"); return KB_INVALID_ARGUMENT; }
+  if (!cfg || !out || cfg->abi_version != KB_ABI_VERSION) { seterr("bad config"); delete xf; return KB_INVALID_ARGUMENT; }
   if (cfg->capacity == 0 || cfg->capacity > 7800000u || cfg->initial_nodes > cfg->capacity || cfg->id_len > MAXID ||
-      cfg->max_waves == 0 || cfg->max_waves > 64) { seterr("config out of range"); return KB_INVALID_ARGUMENT; }
+      cfg->max_waves == 0 || cfg->max_waves > 64) { seterr("config out of range"); delete xf; return KB_INVALID_ARGUMENT; }
+  const uint32_t C = cfg->capacity;
+  const uint32_t rows_per = (C + (uint32_t)world - 1) / (uint32_t)world;
+  if (world < 1 || world > (int)XMAX || rank < 0 || rank >= world || (uint64_t)(world - 1) * rows_per >= C) {
+    seterr("shard layout out of range (1..8 shards, each holding at least one row)"); delete xf; return KB_INVALID_ARGUMENT;
+  }
   int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { seterr("no HIP device"); return KB_NO_DEVICE; }
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { seterr("no HIP device"); delete xf; return KB_NO_DEVICE; }
   kb_sim* s = new kb_sim();
   memset((void*)&s->d, 0, sizeof s->d);
+  memset((void*)&s->xs, 0, sizeof s->xs);
   s->cfg = *cfg;
+  s->xf = xf;
+  s->rank = rank; s->world = world;
   s->device = cfg->device >= 0 ? cfg->device : 0;
   if (cfg->device < 0) (void)hipGetDevice(&s->device);
-  if (hipSetDevice(s->device) != hipSuccess) { delete s; seterr("hipSetDevice failed"); return KB_NO_DEVICE; }
+  if (hipSetDevice(s->device) != hipSuccess) { destroy_shard(s); seterr("hipSetDevice failed"); return KB_NO_DEVICE; }
   {
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, s->device) != hipSuccess) { delete s; seterr("hipGetDeviceProperties failed"); return KB_NO_DEVICE; }
+    if (hipGetDeviceProperties(&prop, s->device) != hipSuccess) { destroy_shard(s); seterr("hipGetDeviceProperties failed"); return KB_NO_DEVICE; }
     s->ncu = (uint32_t)prop.multiProcessorCount;
     s->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor ? prop.maxSharedMemoryPerMultiProcessor : 65536;
   }
-  const uint32_t C = cfg->capacity;
   const uint32_t W = (C + 8191) / 8192 * 8192;       // 64 segments of whole 128-id steps
   s->C = C; s->W = W; s->round = 0;
-  const uint32_t groups = (C + 63) / 64;
+  s->lo = (uint32_t)rank * rows_per;
+  s->hi = std::min<uint32_t>(C, s->lo + rows_per);
+  s->R = s->hi - s->lo;
+  const uint32_t R = s->R;
+  const uint32_t groups = (R + 63) / 64;
   uint32_t S = 1;
   while (S < 64 && groups * S < 8192) S <<= 1;        // enough sweep waves to fill the chip
   s->S = S;
   Dev& d = s->d;
+  d.lo = s->lo; d.hi = s->hi;
   d.C = C; d.W = W; d.SEGW = W / NSEG; d.NWR = W / 32;
   d.k0 = (uint32_t)cfg->seed; d.k1 = (uint32_t)(cfg->seed >> 32);
   d.loss_thr = cfg->loss_threshold; d.churn_thr = cfg->churn_threshold; d.fault_end = cfg->fault_end_round;
@@ -362,47 +418,55 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &s->h_ident[(size_t)j * MAXID]);
   for (uint32_t j = 0; j < cfg->initial_nodes; ++j) s->h_ever[j] = 1;
   hipError_t e = hipSuccess;
-#define A(ptr, n) if (e == hipSuccess) e = dalloc(&(ptr), (n))
-  A(d.stamp, (size_t)C * W); A(d.bits, (size_t)C * d.NWR); A(d.segp, (size_t)C * NSEG); A(d.sdirty, C);
-  A(d.dirty, C); A(d.alive, C); A(d.abits, d.NWR); A(d.start_round, C); A(d.n, C); A(d.fp, C);
-  A(d.last_bcast, C); A(d.susp, (size_t)C * SLOTS); A(d.cur, (size_t)C * CSLOTS); A(d.paq, (size_t)C * PAQ);
-  A(d.paq_n, C); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2); A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
+#define A(ptr, n) if (e == hipSuccess) e = talloc(s, &(ptr), (n))     // per-id / global tables
+#define AR(ptr, n) if (e == hipSuccess) e = ralloc(s, &(ptr), (n))   // row tables: n entries per local row
+  AR(d.stamp, W); AR(d.bits, d.NWR); AR(d.segp, NSEG); AR(d.sdirty, 1);
+  AR(d.dirty, 1); A(d.alive, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
+  AR(d.last_bcast, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
+  AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
+  A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1);
-  A(d.flog, (size_t)C * LOGCAP); A(d.flog_n, C); A(d.fstart, (size_t)C * 16); A(d.kpr_big, C);
-  s->msg_cap = std::max<uint32_t>(8u * C + (uint32_t)TICK_MAX * C, 1u << 16);
-  s->pay_cap = std::max<uint32_t>((d.capk + 1) * C, 1u << 24);
+  AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
+  s->msg_cap = std::max<uint32_t>(8u * R + (uint32_t)TICK_MAX * R, 1u << 16);
+  s->pay_cap = std::max<uint32_t>((d.capk + 1) * R, 1u << 24);
   for (int b = 0; b < 2; ++b) {
-    A(s->ob[b].msgs, s->msg_cap); A(s->ob[b].pay, s->pay_cap); A(s->ob[b].off, C); A(s->ob[b].cap, C);
-    A(s->ob[b].cnt, C); A(s->ob[b].poff, C);
+    A(s->ob[b].msgs, s->msg_cap); A(s->ob[b].pay, s->pay_cap); AR(s->ob[b].off, 1); AR(s->ob[b].cap, 1);
+    AR(s->ob[b].cnt, 1); AR(s->ob[b].poff, 1);
     s->ob[b].msg_cap = s->msg_cap; s->ob[b].pay_cap = s->pay_cap;
   }
-  A(s->wc.status, s->msg_cap); A(s->wc.cnt1, C); A(s->wc.bnd, C); A(s->wc.bpay, C); A(s->wc.cursor, C);
-  A(s->wc.in_off, C); A(s->wc.inbox, s->msg_cap); A(s->wc.active, C); A(s->wc.kp_list, s->msg_cap);
-  A(s->wc.touched, C); A(s->wc.touched_list, C);
+  AR(s->wc.cnt1, 1); AR(s->wc.bnd, 1); AR(s->wc.bpay, 1); AR(s->wc.cursor, 1);
+  AR(s->wc.in_off, 1); A(s->wc.active, R); AR(s->wc.touched, 1); A(s->wc.touched_list, R);
+  if (!xf) { A(s->wc.status, s->msg_cap); A(s->wc.inbox, s->msg_cap); A(s->wc.kp_list, s->msg_cap); }
   A(s->bfail, (size_t)C * SLOTS); A(s->bjoin, C);
-  A(s->bs.join, C); A(s->bs.nfail, C); A(s->bs.fail, (size_t)C * SLOTS); A(s->join_off, C); A(s->fail_off, C);
-  A(s->scan_tot, 16); A(s->scan_tiles, 5 * ((C + 1023) / 1024) + 5);
-  A(s->nresp, C); A(s->paysum, C); A(s->nbase, C); A(s->resp_off, C);
-  A(s->resp_nodes, C); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS);
-  A(s->so.part, (size_t)C * S * 10);
+  AR(s->bs.join, 1); AR(s->bs.nfail, 1); AR(s->bs.fail, SLOTS); AR(s->join_off, 1); AR(s->fail_off, 1);
+  A(s->scan_tot, 32); A(s->scan_tiles, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
+  AR(s->nresp, 1); AR(s->paysum, 1); AR(s->nbase, 1); AR(s->resp_off, 1);
+  A(s->resp_nodes, R); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS);
+  AR(s->so.part, (size_t)S * 10);
+  if (xf) {
+    XState& x = s->xs;
+    x.world = (uint32_t)world; x.R = R; x.S = rows_per;
+    A(x.ostatus, s->msg_cap); A(x.xcnt, (size_t)world * R); A(x.xpay, (size_t)world * R);
+    A(x.xoff, (size_t)world * R); A(x.xpoff, (size_t)world * R); A(x.xb, 2 * world);
+    A(x.smsg, s->msg_cap); A(x.spay, s->pay_cap);
+    A(s->xall, 2 * world * world); A(s->xstats, NSTAT);
+    A(s->bfail_loc, (size_t)R * SLOTS); A(s->bjoin_loc, R);
+    s->h_xall.assign(2 * world * world, 0);
+  }
 #undef A
-  if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); free_all(s); delete s; return KB_CAPACITY; }
+#undef AR
+  if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); destroy_shard(s); return KB_CAPACITY; }
   s->so.S = S;
-  (void)hipMemset(d.kpr_big, 0xFF, 4ull * C);          // no round yet
+  (void)hipMemset(L(s, d.kpr_big), 0xFF, 4ull * R);          // no round yet
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
-  s->newmask = nullptr; s->respmask = nullptr; s->mask_words = 0;
-  s->resp_scratch = nullptr; s->resp_scratch_words = 0;
-  s->d_events = nullptr; s->events_cap = 0; s->nf = 0; s->nj = 0;
-  if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { free_all(s); delete s; seterr("stream"); return KB_IO_ERROR; }
+  if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
   (void)hipEventCreate(&s->ev0); (void)hipEventCreate(&s->ev1); (void)hipEventCreate(&s->er0); (void)hipEventCreate(&s->er1);
-  s->sweep_ms = s->round_ms = 0; s->sweep_launches = s->round_launches = s->sweep_bytes = 0;
-  s->bj_total = s->bf_total = 0;
   int rc = upload_segments(s);
-  if (rc) { free_all(s); delete s; return rc; }
+  if (rc) { destroy_shard(s); return rc; }
   uint32_t ctr0[NCTR] = {0};
   ctr0[C_NEXTFREE] = cfg->initial_nodes;
   ctr0[C_FIRSTCONV] = 0xFFFFFFFFu; ctr0[C_LASTCONV] = 0xFFFFFFFFu;
-  if (hipMemcpy(d.ctr, ctr0, sizeof ctr0, hipMemcpyHostToDevice) != hipSuccess) { free_all(s); delete s; return KB_IO_ERROR; }
+  if (hipMemcpy(d.ctr, ctr0, sizeof ctr0, hipMemcpyHostToDevice) != hipSuccess) { destroy_shard(s); seterr("ctr upload"); return KB_IO_ERROR; }
   const uint32_t tb = 256, gb = (C + tb - 1) / tb;
   if (cfg->init_mode == KB_INIT_CONVERGED) {
     k_init_converged_rows<<<4096, 256, 0, s->st>>>(d, cfg->initial_nodes);
@@ -410,45 +474,176 @@ extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
   } else {
     k_init_nodes<<<gb, tb, 0, s->st>>>(d, cfg->initial_nodes);
   }
-  if (hipStreamSynchronize(s->st) != hipSuccess) { free_all(s); delete s; seterr("init failed"); return KB_IO_ERROR; }
+  if (hipStreamSynchronize(s->st) != hipSuccess) { destroy_shard(s); seterr("init failed"); return KB_IO_ERROR; }
   *out = s;
+  return KB_OK;
+}
+
+extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) { return create_shard(cfg, 0, 1, nullptr, out); }
+
+extern "C" int kb_rccl_unique_id(uint8_t* out, size_t cap) {
+  if (!out || cap < sizeof(ncclUniqueId)) { seterr("unique id buffer too small"); return KB_INVALID_ARGUMENT; }
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) { seterr(std::string("ncclGetUniqueId: ") + ncclGetErrorString(r)); return KB_IO_ERROR; }
+  memcpy(out, &id, sizeof id);
+  return KB_OK;
+}
+
+extern "C" int kb_sim_create_rank(const kb_config* cfg, int32_t rank, int32_t world, const uint8_t* unique_id, kb_sim** out) {
+  if (!cfg || !unique_id || !out || world < 1 || world > (int)XMAX || rank < 0 || rank >= world) {
+    seterr("bad rank/world"); return KB_INVALID_ARGUMENT;
+  }
+  if (hipSetDevice(cfg->device >= 0 ? cfg->device : 0) != hipSuccess) { seterr("hipSetDevice failed"); return KB_NO_DEVICE; }
+  RcclXfer* x = new RcclXfer();
+  if (!x->init(rank, world, unique_id)) { seterr(x->error()); delete x; return KB_IO_ERROR; }
+  return create_shard(cfg, rank, world, x, out);
+}
+
+extern "C" int kb_sim_create_local(const kb_config* cfg, int32_t shards, kb_sim** out) {
+  if (!cfg || !out || shards < 1 || shards > (int)XMAX) { seterr("shards out of range (1..8)"); return KB_INVALID_ARGUMENT; }
+  kb_sim* g = new kb_sim();
+  g->cfg = *cfg; g->C = cfg->capacity; g->world = shards; g->R = 0;
+  g->hub = new LocalHub(shards);
+  for (int k = 0; k < shards; ++k) {
+    LocalXfer* x = new LocalXfer();
+    x->rank = k; x->world = shards; x->hub = g->hub;
+    kb_sim* s = nullptr;
+    const int rc = create_shard(cfg, k, shards, x, &s);
+    if (rc) { for (kb_sim* t : g->shards) destroy_shard(t); delete g->hub; delete g; return rc; }
+    s->in_group = true;
+    g->shards.push_back(s);
+  }
+  g->device = g->shards[0]->device;
+  *out = g;
   return KB_OK;
 }
 
 extern "C" int kb_sim_destroy(kb_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
-  (void)hipSetDevice(s->device);
-  (void)hipStreamSynchronize(s->st);
-  free_all(s);
-  (void)hipEventDestroy(s->ev0); (void)hipEventDestroy(s->ev1); (void)hipEventDestroy(s->er0); (void)hipEventDestroy(s->er1);
-  (void)hipStreamDestroy(s->st);
-  delete s;
+  if (!s->shards.empty()) {
+    for (kb_sim* t : s->shards) destroy_shard(t);
+    delete s->hub;
+    delete s;
+    return KB_OK;
+  }
+  destroy_shard(s);
+  return KB_OK;
+}
+
+extern "C" int kb_sim_shard_info(kb_sim* s, int32_t* rank, int32_t* world, uint32_t* lo, uint32_t* hi) {
+  if (!s || !rank || !world || !lo || !hi) return KB_INVALID_ARGUMENT;
+  if (!s->shards.empty()) { *rank = 0; *world = s->world; *lo = 0; *hi = s->C; return KB_OK; }
+  *rank = s->rank; *world = s->world; *lo = s->lo; *hi = s->hi;
   return KB_OK;
 }
 
 static int check_err(kb_sim* s) {
   uint32_t e = 0;
+  if (s->xf && !s->xf->allreduce_max_u32(s->d.ctr + C_ERR, 1, s->st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
   HIPCHK(hipMemcpyAsync(&e, s->d.ctr + C_ERR, 4, hipMemcpyDeviceToHost, s->st));
   HIPCHK(hipStreamSynchronize(s->st));
   if (e) {
     const char* what[] = {"", "suspect slots exhausted", "outbox region overflow", "payload pool overflow",
-                          "truncated Join response too large", "inbox overflow", "Join response member count mismatch"};
-    seterr(std::string("device capacity error: ") + (e < 7 ? what[e] : "?"));
+                          "truncated Join response too large", "inbox overflow", "Join response member count mismatch",
+                          "freshness log", "fingerprint count mismatch", "wave-0 outbox exceeds preallocated capacity"};
+    seterr(std::string("device capacity error: ") + (e < 10 ? what[e] : "?"));
     return KB_CAPACITY;
   }
+  return KB_OK;
+}
+constexpr uint32_t HERR_WAVE0 = 9;   // raised by the host into C_ERR (kept symmetric across shards)
+
+// grow the receive side of the sharded waves to hold nm records and np payload ids
+static int ensure_recv(kb_sim* s, size_t nm, size_t np) {
+  if (nm > s->rmsg_cap || !s->rmsg) {
+    void* old[] = {s->rmsg, s->rstatus, s->rinbox, s->rkp};
+    for (void* p : old) if (p) (void)hipFree(p);
+    s->rmsg = nullptr; s->rstatus = nullptr; s->rinbox = nullptr; s->rkp = nullptr;
+    const size_t cap = std::max<size_t>(nm + nm / 2, 1u << 16);
+    HIPCHK(hipMalloc(&s->rmsg, sizeof(Msg) * cap)); HIPCHK(hipMalloc(&s->rstatus, cap));
+    HIPCHK(hipMalloc(&s->rinbox, 4 * cap)); HIPCHK(hipMalloc(&s->rkp, 4 * cap));
+    s->rmsg_cap = cap;
+    s->wc.status = s->rstatus; s->wc.inbox = s->rinbox; s->wc.kp_list = s->rkp;
+  }
+  if (np > s->rpay_cap || !s->rpay) {
+    if (s->rpay) (void)hipFree(s->rpay);
+    s->rpay = nullptr;
+    const size_t cap = std::max<size_t>(np + np / 2, 1u << 20);
+    HIPCHK(hipMalloc(&s->rpay, 4 * cap));
+    s->rpay_cap = cap;
+  }
+  return KB_OK;
+}
+
+// all-to-all-v of this wave's delivered records; returns the received record count
+static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb) {
+  const int W = s->world, me = s->rank;
+  XState& x = s->xs;
+  hipStream_t st = s->st;
+  {
+    ScanArgs a = scan_args(s, (uint32_t)W * s->R, s->scan_tot + 16);
+    a.narr = 2;
+    a.in[0] = x.xcnt; a.out[0] = x.xoff;
+    a.in[1] = x.xpay; a.out[1] = x.xpoff;
+    launch_scan(a, st);
+  }
+  k_xbound<<<1, 64, 0, st>>>(x, s->scan_tot + 16);
+  k_pack<<<(s->R + 3) / 4, 256, 0, st>>>(s->d, ob, x);
+  if (!s->xf->allgather_u32(x.xb, s->xall, 2 * W, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  HIPCHK(hipMemcpyAsync(s->h_xall.data(), s->xall, 4ull * 2 * W * W, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  size_t sc[XMAX], sd[XMAX], rc[XMAX], rd[XMAX], psc[XMAX], psd[XMAX], prc[XMAX], prd[XMAX];
+  size_t so = 0, pso = 0, ro = 0, pro = 0;
+  for (int k = 0; k < W; ++k) {
+    sc[k] = s->h_xall[(size_t)me * 2 * W + k]; psc[k] = s->h_xall[(size_t)me * 2 * W + W + k];
+    rc[k] = s->h_xall[(size_t)k * 2 * W + me]; prc[k] = s->h_xall[(size_t)k * 2 * W + W + me];
+    sd[k] = so; so += sc[k]; psd[k] = pso; pso += psc[k];
+    rd[k] = ro; ro += rc[k]; prd[k] = pro; pro += prc[k];
+  }
+  int rcode = ensure_recv(s, ro, pro);
+  if (rcode) return rcode;
+  if (!s->xf->alltoallv(x.smsg, sc, sd, s->rmsg, rc, rd, sizeof(Msg), st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  if (!s->xf->alltoallv(x.spay, psc, psd, s->rpay, prc, prd, 4, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  rb.world = (uint32_t)W;
+  for (int k = 0; k <= W && k <= (int)XMAX; ++k) {
+    rb.m0[k] = k < W ? (uint32_t)rd[k] : (uint32_t)ro;
+    rb.p0[k] = k < W ? (uint32_t)prd[k] : (uint32_t)pro;
+  }
+  nrecv = (uint32_t)ro;
+  return KB_OK;
+}
+
+// the round's broadcast lists of every shard, concatenated in shard order = sender order
+static int gather_broadcasts(kb_sim* s, uint32_t nj_loc, uint32_t nf_loc) {
+  const int W = s->world;
+  hipStream_t st = s->st;
+  if (!s->xf->allgather_u32(s->scan_tot, s->xall, 2, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  HIPCHK(hipMemcpyAsync(s->h_xall.data(), s->xall, 4ull * 2 * W, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  size_t sc[XMAX], sd[XMAX], rc[XMAX], rd[XMAX], fsc[XMAX], frc[XMAX], frd[XMAX];
+  size_t oj = 0, of = 0;
+  for (int k = 0; k < W; ++k) {
+    sc[k] = nj_loc; fsc[k] = nf_loc; sd[k] = 0;
+    rc[k] = s->h_xall[2 * k]; frc[k] = s->h_xall[2 * k + 1];
+    rd[k] = oj; oj += rc[k]; frd[k] = of; of += frc[k];
+  }
+  if (!s->xf->alltoallv(s->bjoin_loc, sc, sd, s->bjoin, rc, rd, sizeof(BCast), st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  if (!s->xf->alltoallv(s->bfail_loc, fsc, sd, s->bfail, frc, frd, sizeof(BCast), st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  s->nj = (uint32_t)oj; s->nf = (uint32_t)of;
   return KB_OK;
 }
 
 static int step_round(kb_sim* s) {
   Dev& d = s->d;
   const int32_t r = s->round;
-  const uint32_t C = s->C;
+  const uint32_t C = s->C, R = s->R;
   hipStream_t st = s->st;
-  const uint32_t tb = 256, gnode = (C + tb - 1) / tb, gwave = (C + 3) / 4;
+  const uint32_t tb = 256, gnode = (R + tb - 1) / tb, gwave = (R + 3) / 4, gall = (C + tb - 1) / tb;
   (void)hipEventRecord(s->er0, st);
   // 0. stamp window
   if (r > 0 && r % EPOCH == 0) k_rebase<<<8192, 256, 0, st>>>(d);
-  // 1. lifecycle
+  // 1. lifecycle (every shard applies the same events and churn draws to the replicated per-id state)
   if (!s->events.empty()) {
     if (s->events.size() > s->events_cap) {
       if (s->d_events) (void)hipFree(s->d_events);
@@ -462,7 +657,7 @@ static int step_round(kb_sim* s) {
   }
   const bool faults_on = s->cfg.fault_end_round < 0 || r < s->cfg.fault_end_round;
   if (faults_on && s->cfg.churn_threshold) {
-    k_churn_leave<<<gnode, tb, 0, st>>>(d, r);
+    k_churn_leave<<<gall, tb, 0, st>>>(d, r);
     k_churn_join<<<1, 1024, 0, st>>>(d, r);
   }
   k_alive_bits<<<(d.NWR + tb - 1) / tb, tb, 0, st>>>(d);
@@ -474,14 +669,16 @@ static int step_round(kb_sim* s) {
   pb.bfail = s->bfail; pb.nf = s->nf; pb.bjoin = s->bjoin; pb.nj = s->nj; pb.JW = (s->nj + 63) / 64;
   pb.nresp = s->nresp; pb.paysum = s->paysum; pb.nbase = s->nbase;
   if (pb.JW) {
-    const size_t words = (size_t)C * pb.JW;
+    const size_t words = (size_t)R * pb.JW;
     if (words > s->mask_words) {
-      if (s->newmask) (void)hipFree(s->newmask);
-      if (s->respmask) (void)hipFree(s->respmask);
-      s->newmask = nullptr; s->respmask = nullptr;
-      HIPCHK(hipMalloc(&s->newmask, 8 * words)); HIPCHK(hipMalloc(&s->respmask, 8 * words));
+      if (s->newmask_base) (void)hipFree(s->newmask_base);
+      if (s->respmask_base) (void)hipFree(s->respmask_base);
+      s->newmask_base = nullptr; s->respmask_base = nullptr;
+      HIPCHK(hipMalloc(&s->newmask_base, 8 * words)); HIPCHK(hipMalloc(&s->respmask_base, 8 * words));
       s->mask_words = words;
     }
+    s->newmask = bias(s->newmask_base, pb.JW, s->lo);
+    s->respmask = bias(s->respmask_base, pb.JW, s->lo);
   }
   pb.newmask = s->newmask; pb.respmask = s->respmask;
   pb.gid = s->bf_gid; pb.dep = s->bf_dep;
@@ -498,28 +695,32 @@ static int step_round(kb_sim* s) {
     const uint32_t wpb = ldsb ? std::min<uint32_t>(4, (budget - listw) / d.NWR) : 4;
     const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)(s->lds_per_cu / std::max<size_t>(lds + 512, 1))));
-    const uint32_t blocks = std::min<uint32_t>((C + wpb - 1) / wpb, s->ncu * per_cu);
+    const uint32_t blocks = std::min<uint32_t>((R + wpb - 1) / wpb, s->ncu * per_cu);
     if (ldsb) k_phaseB<true><<<blocks, 64 * wpb, lds, st>>>(d, pb, r, lf, lj);
     else k_phaseB<false><<<blocks, 64 * wpb, lds, st>>>(d, pb, r, lf, lj);
   }
-  else { HIPCHK(hipMemsetAsync(s->nresp, 0, 4ull * C, st)); HIPCHK(hipMemsetAsync(s->paysum, 0, 4ull * C, st)); }
+  else { HIPCHK(hipMemsetAsync(L(s, s->nresp), 0, 4ull * R, st)); HIPCHK(hipMemsetAsync(L(s, s->paysum), 0, 4ull * R, st)); }
   {  // wave-0 outbox regions: responses first, then the tick's messages
-    ScanArgs a = scan_args(s, C, s->scan_tot);
+    ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 3;
-    a.in[0] = s->nresp; a.out[0] = s->resp_off;
-    a.in[1] = s->paysum; a.out[1] = o0.poff;
-    a.in[2] = s->nresp; a.out[2] = o0.off; a.addc[2] = TICK_MAX;
-    a.list = s->resp_nodes;
+    a.in[0] = L(s, s->nresp); a.out[0] = L(s, s->resp_off);
+    a.in[1] = L(s, s->paysum); a.out[1] = L(s, o0.poff);
+    a.in[2] = L(s, s->nresp); a.out[2] = L(s, o0.off); a.addc[2] = TICK_MAX;
+    a.list = s->resp_nodes; a.list_base = s->lo;
     launch_scan(a, st);
   }
-  k_set_cap<<<gnode, tb, 0, st>>>(C, s->nresp, o0.cap, o0.cnt);
+  k_set_cap<<<gnode, tb, 0, st>>>(d, s->nresp, o0.cap, o0.cnt);
   if (have_b && s->nj) {
     uint32_t tot[5];
     HIPCHK(hipMemcpyAsync(tot, s->scan_tot, 20, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t pay_tot = tot[1], msg_tot = tot[2], resp_nodes = tot[4];
-    if (msg_tot > s->msg_cap || pay_tot > s->pay_cap) { seterr("wave-0 outbox exceeds preallocated capacity"); return KB_CAPACITY; }
-    if (resp_nodes) {
+    if (msg_tot > s->msg_cap || pay_tot > s->pay_cap) {
+      // no responses are written; the error surfaces on every shard at the round's end
+      const uint32_t he = HERR_WAVE0;
+      HIPCHK(hipMemcpyAsync(d.ctr + C_ERR, &he, 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemsetAsync(L(s, o0.cnt), 0, 4ull * R, st));
+    } else if (resp_nodes) {
       const uint32_t grid = std::min<uint32_t>(resp_nodes, 4096);
       const size_t words = resp_words(d.NWR, s->W / 256);
       uint32_t* scratch = nullptr;
@@ -539,51 +740,68 @@ static int step_round(kb_sim* s) {
   // 3. tick
   k_tick_pre<<<gwave, 256, 0, st>>>(d, o0, s->bs, r);
   (void)hipEventRecord(s->ev0, st);
-  k_sweep<<<((C + 63) / 64 + 3) / 4 * s->S, 256, 0, st>>>(d, s->so);
+  k_sweep<<<((R + 63) / 64 + 3) / 4 * s->S, 256, 0, st>>>(d, s->so);
   (void)hipEventRecord(s->ev1, st);
   k_tick_post<<<gnode, tb, 0, st>>>(d, s->so, o0, r);
   {
-    ScanArgs a = scan_args(s, C, s->scan_tot);
+    ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 2;
-    a.in[0] = s->bs.join; a.out[0] = s->join_off;
-    a.in[1] = s->bs.nfail; a.out[1] = s->fail_off;
+    a.in[0] = L(s, s->bs.join); a.out[0] = L(s, s->join_off);
+    a.in[1] = L(s, s->bs.nfail); a.out[1] = L(s, s->fail_off);
     launch_scan(a, st);
   }
-  k_bcast_write<<<gnode, tb, 0, st>>>(d, s->bs, s->join_off, s->fail_off, s->bjoin, s->bfail);
+  k_bcast_write<<<gnode, tb, 0, st>>>(d, s->bs, s->join_off, s->fail_off, s->xf ? s->bjoin_loc : s->bjoin,
+                                      s->xf ? s->bfail_loc : s->bfail);
   // 4. receive window: unicast waves
   int cur = 0;
   for (uint32_t w = 0; w <= s->cfg.max_waves; ++w) {
-    OutBuf& ib = s->ob[cur];
+    OutBuf& ob = s->ob[cur];
     OutBuf& nb = s->ob[cur ^ 1];
     const int last = w == s->cfg.max_waves;
-    HIPCHK(hipMemsetAsync(s->wc.cnt1, 0, 4ull * C, st));
-    HIPCHK(hipMemsetAsync(s->wc.bnd, 0, 4ull * C, st));
-    HIPCHK(hipMemsetAsync(s->wc.bpay, 0, 4ull * C, st));
-    HIPCHK(hipMemsetAsync(s->wc.cursor, 0, 4ull * C, st));
+    HIPCHK(hipMemsetAsync(L(s, s->wc.cnt1), 0, 4ull * R, st));
+    HIPCHK(hipMemsetAsync(L(s, s->wc.bnd), 0, 4ull * R, st));
+    HIPCHK(hipMemsetAsync(L(s, s->wc.bpay), 0, 4ull * R, st));
+    HIPCHK(hipMemsetAsync(L(s, s->wc.cursor), 0, 4ull * R, st));
     HIPCHK(hipMemsetAsync(d.ctr + C_KP, 0, 12, st));   // C_KP, C_TOUCH, C_ACTIVE
-    k_route<<<gnode, tb, 0, st>>>(d, ib, s->wc, r, w, last);
-    if (last) break;
+    OutBuf ib = ob;                                    // the wave's delivered records
+    uint32_t nrecv = 0;
+    if (!s->xf) {
+      k_route<<<gnode, tb, 0, st>>>(d, ob, s->wc, r, w, last);
+      if (last) break;
+    } else {
+      HIPCHK(hipMemsetAsync(s->xs.xcnt, 0, 4ull * s->world * R, st));
+      HIPCHK(hipMemsetAsync(s->xs.xpay, 0, 4ull * s->world * R, st));
+      k_route_x<<<gnode, tb, 0, st>>>(d, ob, s->xs, r, w, last);
+      if (last) break;
+      RecvBlocks rb;
+      memset(&rb, 0, sizeof rb);
+      int rc = exchange_wave(s, ob, nrecv, rb);
+      if (rc) return rc;
+      ib.msgs = s->rmsg; ib.pay = s->rpay;
+      if (nrecv) k_route_recv<<<(nrecv + 255) / 256, 256, 0, st>>>(d, ib, s->wc, rb, nrecv);
+    }
     {
-      ScanArgs a = scan_args(s, C, s->scan_tot + 8);
+      ScanArgs a = scan_args(s, R, s->scan_tot + 8);
       a.narr = 3;
-      a.in[0] = s->wc.cnt1; a.out[0] = s->wc.in_off;
-      a.in[1] = s->wc.bnd; a.out[1] = nb.off;
-      a.in[2] = s->wc.bpay; a.out[2] = nb.poff;
-      a.list = s->wc.active; a.list_count = d.ctr + C_ACTIVE;
+      a.in[0] = L(s, s->wc.cnt1); a.out[0] = L(s, s->wc.in_off);
+      a.in[1] = L(s, s->wc.bnd); a.out[1] = L(s, nb.off);
+      a.in[2] = L(s, s->wc.bpay); a.out[2] = L(s, nb.poff);
+      a.list = s->wc.active; a.list_count = d.ctr + C_ACTIVE; a.list_base = s->lo;
       launch_scan(a, st);
     }
     if (s->debug_waves) {                               // KB_DEBUG_WAVES: inbox sizes per wave
-      std::vector<uint32_t> c1(C);
-      HIPCHK(hipMemcpyAsync(c1.data(), s->wc.cnt1, 4ull * C, hipMemcpyDeviceToHost, st));
+      std::vector<uint32_t> c1(R);
+      HIPCHK(hipMemcpyAsync(c1.data(), L(s, s->wc.cnt1), 4ull * R, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       uint64_t sum = 0; uint32_t mx = 0, arg = 0, big = 0;
-      for (uint32_t k = 0; k < C; ++k) { sum += c1[k]; if (c1[k] > mx) { mx = c1[k]; arg = k; } big += c1[k] > 64; }
+      for (uint32_t k = 0; k < R; ++k) { sum += c1[k]; if (c1[k] > mx) { mx = c1[k]; arg = s->lo + k; } big += c1[k] > 64; }
       fprintf(stderr, "[kb] round %d wave %u: in-order msgs %llu, max inbox %u (node %u), inboxes > 64: %u\n", r, w,
               (unsigned long long)sum, mx, arg, big);
     }
-    HIPCHK(hipMemcpyAsync(nb.cap, s->wc.bnd, 4ull * C, hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemsetAsync(nb.cnt, 0, 4ull * C, st));
-    k_scatter<<<gnode, tb, 0, st>>>(d, ib, s->wc);
+    HIPCHK(hipMemcpyAsync(L(s, nb.cap), L(s, s->wc.bnd), 4ull * R, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemsetAsync(L(s, nb.cnt), 0, 4ull * R, st));
+    if (!s->xf) k_scatter<<<gnode, tb, 0, st>>>(d, ob, s->wc);
+    else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
     k_kp_insert<<<2048, 256, 0, st>>>(d, ib, s->wc, r);
     k_kp_prologue<<<1024, 256, 0, st>>>(d, ib, s->wc, r);
     k_touch_fix<<<1024, 256, 0, st>>>(d, s->wc);
@@ -599,12 +817,18 @@ static int step_round(kb_sim* s) {
     }
     cur ^= 1;
   }
+  if (s->xf && !s->xf->allreduce_sum_u32(d.ctr + C_AGREE, 1, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
   k_round_end<<<1, 1, 0, st>>>(d, r);
   (void)hipEventRecord(s->er1, st);
   uint32_t tot[2];
   HIPCHK(hipMemcpyAsync(tot, s->scan_tot, 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  s->nj = tot[0]; s->nf = tot[1];
+  if (s->xf) {
+    const int rc = gather_broadcasts(s, tot[0], tot[1]);
+    if (rc) return rc;
+  } else {
+    s->nj = tot[0]; s->nf = tot[1];
+  }
   s->bj_total += s->nj; s->bf_total += s->nf;
   float ms = 0;
   (void)hipEventElapsedTime(&ms, s->ev0, s->ev1); s->sweep_ms += ms; s->sweep_launches++;
@@ -613,15 +837,58 @@ static int step_round(kb_sim* s) {
   return check_err(s);
 }
 
+static bool is_group(const kb_sim* s) { return !s->shards.empty(); }
+static kb_sim* owner(kb_sim* g, uint32_t node) {                 // the shard holding node's row
+  for (kb_sim* t : g->shards) if (node >= t->lo && node < t->hi) return t;
+  return nullptr;
+}
+
+// every shard of a group steps in its own thread; a failing shard aborts the others' rendezvous
+static int group_step(kb_sim* g, uint32_t rounds) {
+  const size_t W = g->shards.size();
+  std::vector<int> rc(W, KB_OK);
+  std::vector<std::string> err(W);
+  g->hub->reset();
+  std::vector<std::thread> th;
+  for (size_t k = 0; k < W; ++k)
+    th.emplace_back([&, k] {
+      kb_sim* s = g->shards[k];
+      (void)hipSetDevice(s->device);
+      for (uint32_t q = 0; q < rounds && rc[k] == KB_OK; ++q) rc[k] = step_round(s);
+      if (rc[k] != KB_OK) { err[k] = g_err; g->hub->abort(); }
+    });
+  for (auto& t : th) t.join();
+  int first = KB_OK;
+  for (int pass = 0; pass < 2 && first == KB_OK; ++pass)     // the root cause first, released waiters last
+    for (size_t k = 0; k < W && first == KB_OK; ++k)
+      if (rc[k] != KB_OK && (pass == 1 || err[k].find("aborted by another shard") == std::string::npos)) {
+        first = rc[k];
+        seterr(err[k]);
+      }
+  return first;
+}
+
 extern "C" int kb_sim_step(kb_sim* s, uint32_t rounds) {
   if (!s) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) return group_step(s, rounds);
   (void)hipSetDevice(s->device);
-  for (uint32_t k = 0; k < rounds; ++k) { int rc = step_round(s); if (rc) return rc; }
+  for (uint32_t k = 0; k < rounds; ++k) {
+    int rc = step_round(s);
+    if (rc) { if (s->xf) s->xf->abort(); return rc; }
+  }
   return KB_OK;
 }
 
 // ---------------------------------------------------------------------------------- API surface
+// Sharded handles: calls that change the mesh (start/stop/set_identity/ping_addrs) are made on every
+// shard alike; row inspection is answered by the shard holding the row (KB_INVALID_ARGUMENT on the
+// others); kb_sim_stats is a collective over the ranks of kb_sim_create_rank.
 static int chk(kb_sim* s, uint32_t node) { return (!s || node >= s->C) ? KB_INVALID_ARGUMENT : KB_OK; }
+static int chk_row(kb_sim* s, uint32_t node) {
+  if (chk(s, node)) return KB_INVALID_ARGUMENT;
+  if (node < s->lo || node >= s->hi) { seterr("the node's row is held by another shard"); return KB_INVALID_ARGUMENT; }
+  return KB_OK;
+}
 static int read_row(kb_sim* s, uint32_t node, std::vector<uint8_t>& rw) {   // canonical bytes (0 = not a member)
   std::vector<uint32_t> bw(s->d.NWR);
   rw.resize(s->C);
@@ -631,19 +898,33 @@ static int read_row(kb_sim* s, uint32_t node, std::vector<uint8_t>& rw) {   // c
   return KB_OK;
 }
 
+#define GROUP_ALL(call)                                                   \
+  if (is_group(s)) {                                                      \
+    for (kb_sim* t_ : s->shards) { const int rc_ = call(t_); if (rc_) return rc_; } \
+    return KB_OK;                                                         \
+  }
+#define GROUP_OWNER(node, call)                                           \
+  if (is_group(s)) {                                                      \
+    if (chk(s, node)) return KB_INVALID_ARGUMENT;                         \
+    return call(owner(s, node));                                          \
+  }
+
 extern "C" int kb_sim_start_node(kb_sim* s, uint32_t node) {
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
+  GROUP_ALL([&](kb_sim* t) { return kb_sim_start_node(t, node); });
   s->events.push_back(Event{node, 0});
   s->h_ever[node] = 1;
   return KB_OK;
 }
 extern "C" int kb_sim_stop_node(kb_sim* s, uint32_t node) {
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
+  GROUP_ALL([&](kb_sim* t) { return kb_sim_stop_node(t, node); });
   s->events.push_back(Event{node, 1});
   return KB_OK;
 }
 extern "C" int kb_sim_is_running(kb_sim* s, uint32_t node, int* running) {
   if (chk(s, node) || !running) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) return kb_sim_is_running(s->shards[0], node, running);
   uint8_t a = 0;
   HIPCHK(hipMemcpy(&a, s->d.alive + node, 1, hipMemcpyDeviceToHost));
   *running = a;
@@ -651,16 +932,18 @@ extern "C" int kb_sim_is_running(kb_sim* s, uint32_t node, int* running) {
 }
 extern "C" int kb_sim_ping_addrs(kb_sim* s, uint32_t node, const uint32_t* peers, size_t n) {
   if (chk(s, node) || (n && !peers)) return KB_INVALID_ARGUMENT;
+  GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_ping_addrs(t, node, peers, n); });
+  for (size_t k = 0; k < n; ++k) if (peers[k] >= s->C) return KB_INVALID_ARGUMENT;
   uint8_t a = 0;
   HIPCHK(hipMemcpy(&a, s->d.alive + node, 1, hipMemcpyDeviceToHost));
   if (!a) { seterr("Cannot ping while we are not started"); return KB_INVALID_OPERATION; }
+  if (node < s->lo || node >= s->hi) return KB_OK;              // queued by the shard holding the row
   uint32_t qn = 0;
   HIPCHK(hipMemcpy(&qn, s->d.paq_n + node, 4, hipMemcpyDeviceToHost));
   std::vector<uint32_t> q(PAQ), bw(s->d.NWR);
   HIPCHK(hipMemcpy(q.data(), s->d.paq + (size_t)node * PAQ, 4 * PAQ, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(bw.data(), s->d.bits + (size_t)node * s->d.NWR, 4ull * s->d.NWR, hipMemcpyDeviceToHost));
   for (size_t k = 0; k < n; ++k) {
-    if (peers[k] >= s->C) return KB_INVALID_ARGUMENT;
     if ((bw[peers[k] >> 5] >> (peers[k] & 31)) & 1u) continue;      // already known: skipped (:277-282)
     if (qn == PAQ) { seterr("ping_addrs queue full"); return KB_CAPACITY; }
     q[qn++] = peers[k];
@@ -671,6 +954,7 @@ extern "C" int kb_sim_ping_addrs(kb_sim* s, uint32_t node, const uint32_t* peers
 }
 extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* identity, size_t len) {
   if (chk(s, node) || len > MAXID || (len && !identity)) return KB_INVALID_ARGUMENT;
+  GROUP_ALL([&](kb_sim* t) { return kb_sim_set_identity(t, node, identity, len); });
   uint8_t a = 0;
   HIPCHK(hipMemcpy(&a, s->d.alive + node, 1, hipMemcpyDeviceToHost));
   uint32_t nfree = 0;
@@ -682,22 +966,36 @@ extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* iden
   s->h_idlen[node] = (uint8_t)len;
   int rc = upload_segments(s);
   if (rc) return rc;
-  k_mark_all_dirty<<<(s->C + 255) / 256, 256, 0, s->st>>>(s->d);
+  k_mark_all_dirty<<<(s->R + 255) / 256, 256, 0, s->st>>>(s->d);
   HIPCHK(hipStreamSynchronize(s->st));
   return KB_OK;
 }
 extern "C" int kb_sim_fingerprint(kb_sim* s, uint32_t node, uint32_t* fp) {
   if (chk(s, node) || !fp) return KB_INVALID_ARGUMENT;
+  GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_fingerprint(t, node, fp); });
+  if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
   k_fp_one<<<1, 64, 0, s->st>>>(s->d, node);
   HIPCHK(hipMemcpyAsync(fp, s->d.fp + node, 4, hipMemcpyDeviceToHost, s->st));
   HIPCHK(hipStreamSynchronize(s->st));
   return KB_OK;
 }
+// all ids; 0 for non-running ids and (sharded ranks) for rows held by other shards
 extern "C" int kb_sim_fingerprints(kb_sim* s, uint32_t* fps, size_t cap) {
   if (!s || !fps || cap < s->C) return KB_INVALID_ARGUMENT;
-  k_fp_all<<<(s->C + 3) / 4, 256, 0, s->st>>>(s->d);
+  if (is_group(s)) {
+    std::vector<uint32_t> part(s->C);
+    memset(fps, 0, 4ull * s->C);
+    for (kb_sim* t : s->shards) {
+      const int rc = kb_sim_fingerprints(t, part.data(), part.size());
+      if (rc) return rc;
+      for (uint32_t j = t->lo; j < t->hi; ++j) fps[j] = part[j];
+    }
+    return KB_OK;
+  }
+  k_fp_all<<<(s->R + 3) / 4, 256, 0, s->st>>>(s->d);
   std::vector<uint8_t> al(s->C);
-  HIPCHK(hipMemcpyAsync(fps, s->d.fp, 4ull * s->C, hipMemcpyDeviceToHost, s->st));
+  memset(fps, 0, 4ull * s->C);
+  HIPCHK(hipMemcpyAsync(fps + s->lo, s->d.fp + s->lo, 4ull * s->R, hipMemcpyDeviceToHost, s->st));
   HIPCHK(hipMemcpyAsync(al.data(), s->d.alive, s->C, hipMemcpyDeviceToHost, s->st));
   HIPCHK(hipStreamSynchronize(s->st));
   for (uint32_t i = 0; i < s->C; ++i) if (!al[i]) fps[i] = 0;
@@ -705,6 +1003,7 @@ extern "C" int kb_sim_fingerprints(kb_sim* s, uint32_t* fps, size_t cap) {
 }
 extern "C" int kb_sim_true_fingerprint(kb_sim* s, uint32_t* fp) {
   if (!s || !fp) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) return kb_sim_true_fingerprint(s->shards[0], fp);
   k_alive_bits<<<(s->d.NWR + 255) / 256, 256, 0, s->st>>>(s->d);
   k_truefp<<<1, 1024, 0, s->st>>>(s->d);
   HIPCHK(hipMemsetAsync(s->d.ctr + C_ALIVE, 0, 4, s->st));
@@ -714,6 +1013,8 @@ extern "C" int kb_sim_true_fingerprint(kb_sim* s, uint32_t* fp) {
 }
 extern "C" int kb_sim_dump_row(kb_sim* s, uint32_t node, uint8_t* rw, size_t cap) {
   if (chk(s, node) || !rw || cap < s->C) return KB_INVALID_ARGUMENT;
+  GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_row(t, node, rw, cap); });
+  if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
   std::vector<uint8_t> v;
   int rc = read_row(s, node, v);
   if (rc) return rc;
@@ -722,6 +1023,8 @@ extern "C" int kb_sim_dump_row(kb_sim* s, uint32_t node, uint8_t* rw, size_t cap
 }
 extern "C" int kb_sim_peers(kb_sim* s, uint32_t node, uint32_t* peers, size_t cap, size_t* n) {
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
+  GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_peers(t, node, peers, cap, n); });
+  if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
   std::vector<uint8_t> rw;
   int rc = read_row(s, node, rw);
   if (rc) return rc;
@@ -732,6 +1035,8 @@ extern "C" int kb_sim_peers(kb_sim* s, uint32_t node, uint32_t* peers, size_t ca
 }
 extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, size_t cap, size_t* n) {
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
+  GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_peer_states(t, node, out, cap, n); });
+  if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
   std::vector<uint8_t> rw;
   int rc = read_row(s, node, rw);
   if (rc) return rc;
@@ -763,12 +1068,27 @@ extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
   if (!s || !out) return KB_INVALID_ARGUMENT;
   unsigned long long st[NSTAT];
   uint32_t ctr[NCTR];
-  HIPCHK(hipMemcpy(st, s->d.stats, sizeof st, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(ctr, s->d.ctr, sizeof ctr, hipMemcpyDeviceToHost));
-  std::vector<uint8_t> al(s->C);
-  HIPCHK(hipMemcpy(al.data(), s->d.alive, s->C, hipMemcpyDeviceToHost));
+  kb_sim* h = is_group(s) ? s->shards[0] : s;       // replicated facts come from any shard
+  if (is_group(s)) {
+    memset(st, 0, sizeof st);
+    for (kb_sim* t : s->shards) {
+      unsigned long long v[NSTAT];
+      HIPCHK(hipMemcpy(v, t->d.stats, sizeof v, hipMemcpyDeviceToHost));
+      for (int k = 0; k < NSTAT; ++k) st[k] += v[k];
+    }
+  } else if (s->xf && !s->in_group) {               // ranks: the counters summed over the mesh
+    HIPCHK(hipMemcpyAsync(s->xstats, s->d.stats, sizeof st, hipMemcpyDeviceToDevice, s->st));
+    if (!s->xf->allreduce_sum_u64(s->xstats, NSTAT, s->st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+    HIPCHK(hipMemcpyAsync(st, s->xstats, sizeof st, hipMemcpyDeviceToHost, s->st));
+    HIPCHK(hipStreamSynchronize(s->st));
+  } else {
+    HIPCHK(hipMemcpy(st, s->d.stats, sizeof st, hipMemcpyDeviceToHost));
+  }
+  HIPCHK(hipMemcpy(ctr, h->d.ctr, sizeof ctr, hipMemcpyDeviceToHost));
+  std::vector<uint8_t> al(h->C);
+  HIPCHK(hipMemcpy(al.data(), h->d.alive, h->C, hipMemcpyDeviceToHost));
   memset(out, 0, sizeof *out);
-  out->round = s->round;
+  out->round = h->round;
   uint32_t a = 0;
   for (uint8_t x : al) a += x;
   out->alive = a;
@@ -778,27 +1098,44 @@ extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
   out->next_free_id = ctr[C_NEXTFREE];
   out->sent_ping = st[S_PING]; out->sent_ping_req = st[S_PINGREQ]; out->sent_ack = st[S_ACK];
   out->sent_known_peers = st[S_KP]; out->sent_kpr = st[S_KPR];
-  out->bcast_join = s->bj_total; out->bcast_failed = s->bf_total;
+  out->bcast_join = h->bj_total; out->bcast_failed = h->bf_total;
   out->drop_dead = st[S_DEAD]; out->drop_loss = st[S_LOSS]; out->drop_window = st[S_WINDOW];
   out->drop_oversize = st[S_OVERSIZE]; out->drop_partition = st[S_PART]; out->drop_bcast = st[S_BDROP];
   out->removed_timeout = st[S_RMTIMEOUT]; out->removed_failed = st[S_RMFAILED]; out->join_responses = st[S_JRESP];
   out->curious_overflow = st[S_CUROVF]; out->churn_leaves = st[S_CLEAVE]; out->churn_joins = st[S_CJOIN];
   return KB_OK;
 }
+// per id: alive, n, last_bcast, start_round; n and last_bcast only for the rows this handle holds
 extern "C" int kb_sim_dump_scalars(kb_sim* s, int32_t* out, size_t cap) {
   if (!s || !out || cap < 4ull * s->C) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) {
+    std::vector<int32_t> part(4ull * s->C);
+    for (kb_sim* t : s->shards) {
+      const int rc = kb_sim_dump_scalars(t, part.data(), part.size());
+      if (rc) return rc;
+      for (uint32_t i = 0; i < s->C; ++i)
+        if ((i >= t->lo && i < t->hi) || t == s->shards[0]) memcpy(out + 4 * i, part.data() + 4 * i, 16);
+    }
+    return KB_OK;
+  }
   std::vector<uint8_t> al(s->C);
-  std::vector<uint32_t> n(s->C);
-  std::vector<int32_t> lb(s->C), sr(s->C);
+  std::vector<uint32_t> n(s->R);
+  std::vector<int32_t> lb(s->R), sr(s->C);
   HIPCHK(hipMemcpy(al.data(), s->d.alive, s->C, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(n.data(), s->d.n, 4ull * s->C, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemcpy(lb.data(), s->d.last_bcast, 4ull * s->C, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(n.data(), L(s, s->d.n), 4ull * s->R, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(lb.data(), L(s, s->d.last_bcast), 4ull * s->R, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(sr.data(), s->d.start_round, 4ull * s->C, hipMemcpyDeviceToHost));
-  for (uint32_t i = 0; i < s->C; ++i) { out[4 * i] = al[i]; out[4 * i + 1] = (int32_t)n[i]; out[4 * i + 2] = lb[i]; out[4 * i + 3] = sr[i]; }
+  for (uint32_t i = 0; i < s->C; ++i) {
+    const bool loc = i >= s->lo && i < s->hi;
+    out[4 * i] = al[i]; out[4 * i + 1] = loc ? (int32_t)n[i - s->lo] : 0;
+    out[4 * i + 2] = loc ? lb[i - s->lo] : 0; out[4 * i + 3] = sr[i];
+  }
   return KB_OK;
 }
 extern "C" int kb_sim_dump_suspects(kb_sim* s, uint32_t node, int32_t* out, size_t cap, size_t* n) {
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
+  GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_suspects(t, node, out, cap, n); });
+  if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
   Susp sl[SLOTS];
   HIPCHK(hipMemcpy(sl, s->d.susp + (size_t)node * SLOTS, sizeof sl, hipMemcpyDeviceToHost));
   std::vector<std::array<int32_t, 3>> v;
@@ -810,6 +1147,8 @@ extern "C" int kb_sim_dump_suspects(kb_sim* s, uint32_t node, int32_t* out, size
 }
 extern "C" int kb_sim_dump_curious(kb_sim* s, uint32_t node, int32_t* out, size_t cap, size_t* n) {
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
+  GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_curious(t, node, out, cap, n); });
+  if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
   Cur cu[CSLOTS];
   HIPCHK(hipMemcpy(cu, s->d.cur + (size_t)node * CSLOTS, sizeof cu, hipMemcpyDeviceToHost));
   std::vector<std::array<int32_t, 6>> v;
@@ -839,6 +1178,7 @@ extern "C" uint32_t kb_fingerprint_of_set(const uint32_t* ids, size_t n, const u
 }
 extern "C" int kb_sim_kernel_time(kb_sim* s, int kind, double* ms, uint64_t* launches) {
   if (!s || !ms || !launches) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) return kb_sim_kernel_time(s->shards[0], kind, ms, launches);
   if (kind == 0) { *ms = s->sweep_ms; *launches = s->sweep_launches; }
   else { *ms = s->round_ms; *launches = s->round_launches; }
   return KB_OK;
@@ -850,13 +1190,16 @@ static uint64_t sweep_counter(kb_sim* s) {
 }
 extern "C" int kb_sim_reset_kernel_time(kb_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
+  GROUP_ALL(kb_sim_reset_kernel_time);
   s->sweep_ms = s->round_ms = 0; s->sweep_launches = s->round_launches = 0;
   s->sweep_bytes = sweep_counter(s);            // baseline of the device-side byte counter
   return KB_OK;
 }
-// bytes of member bits and stamp lines the row sweep read since the last reset (counted in-kernel)
+// bytes of member bits and stamp lines the row sweep read since the last reset (counted in-kernel;
+// this handle's rows: shard 0's for a group, like kb_sim_kernel_time)
 extern "C" int kb_sim_sweep_bytes(kb_sim* s, uint64_t* bytes) {
   if (!s || !bytes) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) return kb_sim_sweep_bytes(s->shards[0], bytes);
   *bytes = sweep_counter(s) - s->sweep_bytes;
   return KB_OK;
 }

@@ -43,9 +43,9 @@ __device__ uint32_t select_known(const Dev& d, const uint8_t* rw, const uint32_t
 __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots bs, int32_t r) {
   __shared__ uint32_t s_pick_rank[4][SLOTS * 3], s_pick_peer[4][SLOTS * 3];
   const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t i = blockIdx.x * 4 + wv;
+  const uint32_t i = d.lo + blockIdx.x * 4 + wv;
   const uint32_t l = lane();
-  if (i >= d.C) return;
+  if (i >= d.hi) return;
   if (!d.alive[i]) { if (l == 0) { bs.join[i] = 0; bs.nfail[i] = 0; } return; }
   uint32_t n = d.n[i];
   if (l == 0) {
@@ -271,13 +271,13 @@ __global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
   const uint32_t S = so.S;
   const uint32_t s = blockIdx.x % S;
   const uint32_t g = (blockIdx.x / S) * 4 + (threadIdx.x >> 6);
-  const uint32_t i0 = g * 64 + lane();
-  const bool act = i0 < d.C && d.alive[i0];
+  const uint32_t i0 = d.lo + g * 64 + lane();
+  const bool act = i0 < d.hi && d.alive[i0];
   // the ballot is taken once with the full wave active: inside the select below it would run
   // under the idle lanes' exec mask only and see no live lane
   const unsigned long long actm = __ballot(act);
   if (!actm) return;
-  const uint32_t shadow = g * 64 + (uint32_t)(__ffsll((long long)actm) - 1);
+  const uint32_t shadow = d.lo + g * 64 + (uint32_t)(__ffsll((long long)actm) - 1);
   const uint32_t i = act ? i0 : shadow;                 // idle lanes shadow a live one
   const uint8_t* rw = row_of(d, i);
   const uint32_t* bw = bits_of(d, i);
@@ -315,9 +315,9 @@ __global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
 // ---- pick the ping target (one of the oldest 5), WaitingForPing(now), Ping; ping_addrs (:550-556);
 // ---- refresh the fingerprint from the checkpoints; agreement with the running set.  Thread per node.
 __global__ void k_tick_post(Dev d, SweepOut so, OutBuf ob, int32_t r) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long agree = 0;
-  if (i < d.C && d.alive[i]) {
+  if (i < d.hi && d.alive[i]) {
     const uint32_t C = d.C, S = so.S;
     const uint32_t p = (i + 1 == C) ? 0 : i + 1;
     uint32_t k5[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -375,8 +375,8 @@ __global__ void k_tick_post(Dev d, SweepOut so, OutBuf ob, int32_t r) {
 
 __global__ void k_bcast_write(Dev d, BcastSlots bs, const uint32_t* join_off, const uint32_t* fail_off, BCast* bjoin,
                               BCast* bfail) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.C) return;
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.hi) return;
   uint32_t bseq = 0;
   if (bs.join[i]) bjoin[join_off[i]] = BCast{i, i, bseq++, 0};
   const uint32_t nfl = bs.nfail[i];

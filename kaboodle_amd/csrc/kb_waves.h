@@ -37,12 +37,12 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
   __shared__ uint32_t s_kp[4];
   __shared__ uint32_t s_kpbase;
   const uint32_t wv = threadIdx.x >> 6, l = lane();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0;
   uint32_t nkp = 0;
-  const uint32_t cnt = i < d.C ? ob.cnt[i] : 0;
+  const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
   s_ex[wv][l] = wave_excl(cnt);
-  s_base[wv][l] = i < d.C ? ob.off[i] : 0;
+  s_base[wv][l] = i < d.hi ? ob.off[i] : 0;
   const uint32_t T = wave_sum(cnt);
   wait_lds();
   __builtin_amdgcn_wave_barrier();
@@ -96,10 +96,10 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
 __global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
   const uint32_t wv = threadIdx.x >> 6, l = lane();
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t cnt = i < d.C ? ob.cnt[i] : 0;
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
   s_ex[wv][l] = wave_excl(cnt);
-  s_base[wv][l] = i < d.C ? ob.off[i] : 0;
+  s_base[wv][l] = i < d.hi ? ob.off[i] : 0;
   const uint32_t T = wave_sum(cnt);
   wait_lds();
   __builtin_amdgcn_wave_barrier();
@@ -112,6 +112,159 @@ __global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
     const uint32_t dst = ob.msgs[g].dest;
     wc.inbox[wc.in_off[dst] + atomicAdd(&wc.cursor[dst], 1u)] = g;
   }
+}
+
+// ================================================================================================
+// Sharded waves.  The sender's shard decides every delivery (dead receiver,
+// partition, loss: the same Philox draws as the unsharded path, keyed on the message) and packs the
+// delivered records per destination shard, each block in (sender, seq) order, KnownPeers ids with
+// them.  After the all-to-all-v the receiver holds one flat buffer ordered by (source shard, sender,
+// seq) = (sender, seq): the canonical inbox order of the unsharded path, so the handlers below run
+// unchanged on it.
+// ================================================================================================
+constexpr uint32_t XMAX = 8;        // shards per mesh
+struct XState {
+  uint32_t world, R, S;             // shards, local rows, rows per shard
+  uint8_t* ostatus;                 // per outbox slot: 1 = delivered
+  uint32_t* xcnt; uint32_t* xpay;   // [world][R] delivered records / payload ids per (dest shard, sender)
+  uint32_t* xoff; uint32_t* xpoff;  // exclusive scans of xcnt / xpay (flattened) = send positions
+  uint32_t* xb;                     // [2 * world] records, payload ids sent to each shard
+  Msg* smsg; uint32_t* spay;        // send buffers
+};
+
+__global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int32_t r, uint32_t w, int last) {
+  __shared__ uint32_t s_ex[4][64], s_base[4][64];
+  const uint32_t wv = threadIdx.x >> 6, l = lane();
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0;
+  const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
+  s_ex[wv][l] = wave_excl(cnt);
+  s_base[wv][l] = i < d.hi ? ob.off[i] : 0;
+  const uint32_t T = wave_sum(cnt);
+  wait_lds();
+  __builtin_amdgcn_wave_barrier();
+  const SenderSpan sp{T};
+  for (uint32_t k = l; k < T; k += 64) {
+    uint32_t j, q;
+    sp.owner(s_ex[wv], k, j, q);
+    const uint32_t g = s_base[wv][j] + q;
+    const Msg m = ob.msgs[g];
+    ks[m.kind < 5 ? m.kind : 0]++;
+    uint8_t st = 0;
+    if (last) win++;
+    else if (!d.alive[m.dest]) dead++;
+    else if (part_blocks(d, r, m.sender, m.dest)) part++;
+    else if (faults(d, r) && d.loss_thr &&
+             philox(m.sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m.seq, d.k0, d.k1).x < d.loss_thr) loss++;
+    else {
+      st = 1;
+      const uint32_t slot = (m.dest / x.S) * x.R + (m.sender - d.lo);
+      atomicAdd(&x.xcnt[slot], 1u);
+      if (m.kind == K_KP && m.a) atomicAdd(&x.xpay[slot], m.a);
+    }
+    if (!last) x.ostatus[g] = st;
+  }
+  for (int k = 0; k < 5; ++k) stat_add(d, S_PING + k, ks[k]);
+  stat_add(d, S_DEAD, dead); stat_add(d, S_PART, part); stat_add(d, S_LOSS, loss); stat_add(d, S_WINDOW, win);
+}
+
+// records / payload ids this shard sends to each shard (from the scans' block starts and totals)
+__global__ void k_xbound(XState x, const uint32_t* tot) {
+  const uint32_t k = threadIdx.x;
+  if (k >= x.world) return;
+  const uint32_t a1 = k + 1 < x.world ? x.xoff[(k + 1) * x.R] : tot[0];
+  const uint32_t p1 = k + 1 < x.world ? x.xpoff[(k + 1) * x.R] : tot[1];
+  x.xb[k] = a1 - x.xoff[k * x.R];
+  x.xb[x.world + k] = p1 - x.xpoff[k * x.R];
+}
+
+// one wave per sender: its delivered records in seq order, 64 at a time, to their shard blocks;
+// a KnownPeers record's offset becomes relative to its block's payload (the receiver rebases it)
+__global__ __launch_bounds__(256) void k_pack(Dev d, OutBuf ob, XState x) {
+  const uint32_t l = lane();
+  const uint32_t i = d.lo + blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= d.hi) return;
+  const uint32_t il = i - d.lo, cnt = ob.cnt[i], base = ob.off[i];
+  uint32_t run[XMAX], prun[XMAX];
+#pragma unroll
+  for (uint32_t k = 0; k < XMAX; ++k) {
+    run[k] = k < x.world ? x.xoff[k * x.R + il] : 0u;
+    prun[k] = k < x.world ? x.xpoff[k * x.R + il] : 0u;
+  }
+  for (uint32_t c = 0; c < cnt; c += 64) {
+    const uint32_t q = c + l;
+    Msg m = Msg{0, 0, 0, 0, 0, 0, 0, 0};
+    bool del = false;
+    if (q < cnt) { m = ob.msgs[base + q]; del = x.ostatus[base + q] == 1; }
+    const uint32_t ds = del ? m.dest / x.S : XMAX;
+    const uint32_t pl = (del && m.kind == K_KP) ? m.a : 0u;
+    uint32_t pos = 0, ppos = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < XMAX; ++k) {
+      if (k >= x.world) break;
+      const bool mine = ds == k;
+      const unsigned long long bm = __ballot(mine);
+      if (!bm) continue;
+      const uint32_t pex = wave_excl(mine ? pl : 0u), ptot = wave_sum(mine ? pl : 0u);
+      if (mine) { pos = run[k] + __popcll(bm & ((1ull << l) - 1ull)); ppos = prun[k] + pex; }
+      run[k] += __popcll(bm);
+      prun[k] += ptot;
+    }
+    if (del) {
+      Msg o = m;
+      if (m.kind == K_KP) o.off = ppos - x.xpoff[ds * x.R];
+      x.smsg[pos] = o;
+    }
+    unsigned long long kpm = __ballot(pl != 0);
+    while (kpm) {                                    // payload ids: the whole wave on each list
+      const int src = __ffsll((long long)kpm) - 1;
+      kpm &= kpm - 1;
+      const uint32_t from = bcast(m.off, src), to = bcast(ppos, src), len = bcast(pl, src);
+      for (uint32_t e = l; e < len; e += 64) x.spay[to + e] = ob.pay[from + e];
+    }
+  }
+}
+
+// receiver: rebase KnownPeers offsets to the received payload, count the in-order records per local
+// destination (inbox sizes and next-wave outbox reservations), list the KnownPeers records
+struct RecvBlocks { uint32_t world; uint32_t m0[XMAX + 1]; uint32_t p0[XMAX + 1]; };
+__global__ __launch_bounds__(256) void k_route_recv(Dev d, OutBuf ib, WaveCtl wc, RecvBlocks rb, uint32_t n) {
+  __shared__ uint32_t s_kp[4];
+  __shared__ uint32_t s_kpbase;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t wv = threadIdx.x >> 6, l = lane();
+  bool kp = false;
+  if (g < n) {
+    const Msg m = ib.msgs[g];
+    if (m.kind == K_KP) {
+      uint32_t src = 0;
+      while (src + 1 < rb.world && rb.m0[src + 1] <= g) ++src;
+      ib.msgs[g].off = m.off + rb.p0[src];
+      wc.status[g] = 2;
+      kp = true;
+    } else {
+      wc.status[g] = 1;
+      atomicAdd(&wc.cnt1[m.dest], 1u);
+      atomicAdd(&wc.bnd[m.dest], out_bound(m.kind));
+      if (m.kind == K_KPR) atomicAdd(&wc.bpay[m.dest], d.paybound);
+    }
+  }
+  const unsigned long long km = __ballot(kp);
+  if (l == 0) s_kp[wv] = __popcll(km);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (uint32_t t = 0; t < blockDim.x / 64; ++t) { const uint32_t v = s_kp[t]; s_kp[t] = run; run += v; }
+    s_kpbase = run ? atomicAdd(&d.ctr[C_KP], run) : 0;
+  }
+  __syncthreads();
+  if (kp) wc.kp_list[s_kpbase + s_kp[wv] + __popcll(km & ((1ull << l) - 1ull))] = g;
+}
+__global__ void k_scatter_flat(OutBuf ib, WaveCtl wc, uint32_t n) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n || wc.status[g] != 1) return;
+  const uint32_t dst = ib.msgs[g].dest;
+  wc.inbox[wc.in_off[dst] + atomicAdd(&wc.cursor[dst], 1u)] = g;
 }
 
 __device__ inline void mark_touched(const Dev& d, const WaveCtl& wc, uint32_t node) {

@@ -1,0 +1,176 @@
+// kb_xfer.h — the cross-shard exchange of the sharded simulator, host side.
+//
+// A mesh of C peer ids can be split into `world` contiguous row shards: rank k holds the rows (the
+// observer state) of ids [k*S, min(C, (k+1)*S)), S = ceil(C / world).  Per round the shards exchange
+// exactly what the reference's UDP transport carries between instances (src/kaboodle.rs:188-226):
+// the unicast records of every delivery wave with the ids of KnownPeers lists (all-to-all-v), and
+// the Join / Failed broadcast lists (all-gather-v); plus two tiny reductions (agreement count, error
+// flag), and the counters when asked for.
+//
+// Two transports implement it:
+//   RcclXfer   one process per GPU: RCCL (ncclAllToAllv / ncclAllGather / ncclAllReduce) on the
+//              simulator's stream, over xGMI between the MI355X devices of a node;
+//   LocalXfer  the `world` shards of one mesh inside one process (one host thread and one HIP stream
+//              per shard): the same exchange as device-to-device copies.  It lets the sharded code
+//              path be tested bit-exact against the oracle on a single GPU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <stdint.h>
+#include <string.h>
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace kb {
+
+struct Xfer {
+  int rank = 0, world = 1;
+  virtual ~Xfer() {}
+  // all-to-all-v of `elem`-byte elements between device buffers; counts and displacements are in
+  // elements, indexed by peer rank (host arrays, the meaning of ncclAllToAllv's)
+  virtual bool alltoallv(const void* send, const size_t* scounts, const size_t* sdispls, void* recv,
+                         const size_t* rcounts, const size_t* rdispls, size_t elem, hipStream_t st) = 0;
+  // every rank contributes `count` u32 from `send`; `recv` gets world*count u32 in rank order
+  virtual bool allgather_u32(const uint32_t* send, uint32_t* recv, size_t count, hipStream_t st) = 0;
+  // in-place reductions of small device arrays
+  virtual bool allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t st) = 0;
+  virtual bool allreduce_max_u32(uint32_t* buf, size_t count, hipStream_t st) = 0;
+  virtual bool allreduce_sum_u64(unsigned long long* buf, size_t count, hipStream_t st) = 0;
+  virtual void abort() {}
+  virtual std::string error() const = 0;
+};
+
+// ---- RCCL ---------------------------------------------------------------------------------------
+struct RcclXfer : Xfer {
+  ncclComm_t comm = nullptr;
+  ncclResult_t last = ncclSuccess;
+  std::vector<size_t> sc, sd, rc, rd;
+  bool ok(ncclResult_t r) { last = r; return r == ncclSuccess; }
+  bool init(int r, int w, const void* uid) {
+    rank = r; world = w;
+    sc.resize(w); sd.resize(w); rc.resize(w); rd.resize(w);
+    ncclUniqueId id;
+    memcpy(&id, uid, sizeof id);
+    return ok(ncclCommInitRank(&comm, w, id, r));
+  }
+  ~RcclXfer() override { if (comm) ncclCommDestroy(comm); }
+  bool alltoallv(const void* send, const size_t* scounts, const size_t* sdispls, void* recv, const size_t* rcounts,
+                 const size_t* rdispls, size_t elem, hipStream_t st) override {
+    // moved as bytes: counts and displacements scale by the element size
+    for (int k = 0; k < world; ++k) {
+      sc[k] = scounts[k] * elem; sd[k] = sdispls[k] * elem; rc[k] = rcounts[k] * elem; rd[k] = rdispls[k] * elem;
+    }
+    return ok(ncclAllToAllv(send, sc.data(), sd.data(), recv, rc.data(), rd.data(), ncclUint8, comm, st));
+  }
+  bool allgather_u32(const uint32_t* send, uint32_t* recv, size_t count, hipStream_t st) override {
+    return ok(ncclAllGather(send, recv, count, ncclUint32, comm, st));
+  }
+  bool allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t st) override {
+    return ok(ncclAllReduce(buf, buf, count, ncclUint32, ncclSum, comm, st));
+  }
+  bool allreduce_max_u32(uint32_t* buf, size_t count, hipStream_t st) override {
+    return ok(ncclAllReduce(buf, buf, count, ncclUint32, ncclMax, comm, st));
+  }
+  bool allreduce_sum_u64(unsigned long long* buf, size_t count, hipStream_t st) override {
+    return ok(ncclAllReduce(buf, buf, count, ncclUint64, ncclSum, comm, st));
+  }
+  void abort() override { if (comm) { ncclCommAbort(comm); comm = nullptr; } }
+  std::string error() const override { return std::string("RCCL: ") + ncclGetErrorString(last); }
+};
+
+// ---- in-process shards --------------------------------------------------------------------------
+// Shared by the `world` shards of one mesh.  Every collective is a rendezvous: each shard drains its
+// stream (its send data is then complete), publishes its pointers and waits; each shard then pulls
+// what it needs from the others with device-to-device copies on its own stream, drains it, and waits
+// again before anyone may reuse a send buffer.  A shard that fails aborts the hub, which releases
+// every waiter with an error instead of a hang.
+struct LocalHub {
+  int world;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+  std::vector<const void*> src;
+  std::vector<const size_t*> sc, sd;
+  std::vector<std::vector<unsigned long long>> vals;
+  explicit LocalHub(int w) : world(w), src(w), sc(w), sd(w), vals(w) {}
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (aborted) return false;
+    const uint64_t g = gen;
+    if (++arrived == world) { arrived = 0; ++gen; cv.notify_all(); return true; }
+    cv.wait(lk, [&] { return gen != g || aborted; });
+    return !aborted;
+  }
+  void abort() { std::lock_guard<std::mutex> lk(mu); aborted = true; cv.notify_all(); }
+  void reset() { std::lock_guard<std::mutex> lk(mu); aborted = false; arrived = 0; }
+};
+
+struct LocalXfer : Xfer {
+  LocalHub* hub = nullptr;
+  std::string err;
+  bool fail(const char* what) { err = what; hub->abort(); return false; }
+  void abort() override { hub->abort(); }
+  bool alltoallv(const void* send, const size_t* scounts, const size_t* sdispls, void* recv, const size_t* rcounts,
+                 const size_t* rdispls, size_t elem, hipStream_t st) override {
+    if (hipStreamSynchronize(st) != hipSuccess) return fail("stream sync before exchange");
+    hub->src[rank] = send; hub->sc[rank] = scounts; hub->sd[rank] = sdispls;
+    if (!hub->barrier()) return fail("exchange aborted by another shard");
+    for (int k = 0; k < world; ++k) {
+      const size_t n = rcounts[k];
+      if (n != hub->sc[k][rank]) return fail("exchange counts disagree");
+      if (!n) continue;
+      const char* s = static_cast<const char*>(hub->src[k]) + hub->sd[k][rank] * elem;
+      if (hipMemcpyAsync(static_cast<char*>(recv) + rdispls[k] * elem, s, n * elem, hipMemcpyDeviceToDevice, st) !=
+          hipSuccess)
+        return fail("exchange copy");
+    }
+    if (hipStreamSynchronize(st) != hipSuccess) return fail("stream sync after exchange");
+    if (!hub->barrier()) return fail("exchange aborted by another shard");
+    return true;
+  }
+  // small arrays make a host round trip: every shard's values are gathered, combined, written back
+  template <class T, class F>
+  bool host_collective(const T* in, T* out, size_t count, bool gather, hipStream_t st, F comb) {
+    std::vector<T> mine(count);
+    if (hipMemcpyAsync(mine.data(), in, sizeof(T) * count, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return fail("collective copy");
+    hub->vals[rank].assign(mine.begin(), mine.end());
+    if (!hub->barrier()) return fail("collective aborted by another shard");
+    std::vector<T> res(gather ? count * world : count);
+    for (size_t q = 0; q < count; ++q) {
+      if (gather) {
+        for (int k = 0; k < world; ++k) res[k * count + q] = (T)hub->vals[k][q];
+      } else {
+        T a = (T)hub->vals[0][q];
+        for (int k = 1; k < world; ++k) a = comb(a, (T)hub->vals[k][q]);
+        res[q] = a;
+      }
+    }
+    if (!hub->barrier()) return fail("collective aborted by another shard");
+    if (hipMemcpyAsync(out, res.data(), sizeof(T) * res.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      return fail("collective copy back");
+    return true;
+  }
+  bool allgather_u32(const uint32_t* send, uint32_t* recv, size_t count, hipStream_t st) override {
+    return host_collective<uint32_t>(send, recv, count, true, st, [](uint32_t a, uint32_t) { return a; });
+  }
+  bool allreduce_sum_u32(uint32_t* buf, size_t count, hipStream_t st) override {
+    return host_collective<uint32_t>(buf, buf, count, false, st, [](uint32_t a, uint32_t b) { return a + b; });
+  }
+  bool allreduce_max_u32(uint32_t* buf, size_t count, hipStream_t st) override {
+    return host_collective<uint32_t>(buf, buf, count, false, st, [](uint32_t a, uint32_t b) { return a > b ? a : b; });
+  }
+  bool allreduce_sum_u64(unsigned long long* buf, size_t count, hipStream_t st) override {
+    return host_collective<unsigned long long>(buf, buf, count, false, st,
+                                               [](unsigned long long a, unsigned long long b) { return a + b; });
+  }
+  std::string error() const override { return "local exchange: " + err; }
+};
+
+}  // namespace kb

@@ -75,11 +75,14 @@ def setup(sim: Sim, case: dict) -> None:
         sim.start_node(i)
 
 
-def run_case(case: dict, rounds: int, check_every: int = 1, full_rows: bool = True, verbose: bool = False):
-    """Run `case` on both implementations; returns (ok, message, final gpu stats)."""
+def run_case(case: dict, rounds: int, check_every: int = 1, full_rows: bool = True, verbose: bool = False,
+             shards: int = 0, gpu: Sim | None = None):
+    """Run `case` on both implementations; returns (ok, message, final gpu stats).  shards=k runs the
+    GPU mesh as k row shards exchanging every wave (kb_sim_create_local); `gpu` = an already created
+    GPU handle for the case (e.g. an RCCL rank)."""
     cfg = case["cfg"]
     o = Sim(oracle_lib(), cfg)
-    g = Sim(gpu_lib(), cfg)
+    g = gpu if gpu is not None else Sim(gpu_lib(), cfg, shards=shards)
     setup(o, case)
     setup(g, case)
     events = case.get("events", {})

@@ -29,6 +29,61 @@ def test_parity_every_round(gpu, name, case, rounds):
     assert ok, f"{name}: {msg}"
 
 
+def _shard_cases():
+    """Every standard case as a sharded mesh (3 row shards, or as many as its capacity allows), plus
+    the 1K join case at the full 8 shards of a node."""
+    out = []
+    for name, case, rounds in parity.standard_cases():
+        C = case["cfg"].capacity
+        k = 3 if C >= 9 else 2
+        out.append((f"{name}-x{k}", case, rounds, k))
+        if name == "config2_join_1k":
+            out.append((f"{name}-x8", case, rounds, 8))
+        if name == "churn_loss_512":
+            out.append((f"{name}-x5", case, rounds, 5))
+    return out
+
+
+@pytest.mark.parametrize("name,case,rounds,shards", _shard_cases(), ids=[c[0] for c in _shard_cases()])
+def test_sharded_parity_every_round(gpu, name, case, rounds, shards):
+    """Row shards exchanging every wave (all-to-all-v of records, all-gather of broadcasts) reproduce
+    the unsharded oracle bit for bit, every round."""
+    ok, msg, _ = parity.run_case(case, rounds, shards=shards)
+    assert ok, f"{name}: {msg}"
+
+
+def test_rccl_rank_path_world1(gpu):
+    """The RCCL transport itself (kb_sim_create_rank: ncclAllToAllv / AllGather / AllReduce on the
+    simulator stream), as a 1-rank communicator on this GPU, against the oracle."""
+    from kaboodle_amd._ffi import rccl_unique_id
+    name, case, rounds = [c for c in parity.standard_cases() if c[0] == "churn_loss_512"][0]
+    g = Sim(gpu, case["cfg"], rank=0, world=1, uid=rccl_unique_id(gpu))
+    assert g.shard_info() == (0, 1, 0, case["cfg"].capacity)
+    ok, msg, _ = parity.run_case(case, rounds, gpu=g)
+    assert ok, f"{name} over RCCL: {msg}"
+
+
+def test_sharded_full_size_64k(gpu):
+    """BASELINE configs[2] at full size: 4 row shards against the unsharded GPU mesh, every counter,
+    fingerprint and per-node scalar, and sampled whole rows."""
+    cfg = SimConfig(capacity=65536 + 4096, initial_nodes=65536, init_mode=KB_INIT_CONVERGED, loss=0.01,
+                    churn=0.001, seed=3)
+    a = Sim(gpu, cfg)
+    b = Sim(gpu, cfg, shards=4)
+    assert b.shard_info()[1] == 4
+    rng = np.random.default_rng(2)
+    for r in range(4):
+        a.step(1)
+        b.step(1)
+        assert a.stats() == b.stats(), f"round {r}"
+        assert np.array_equal(a.fingerprints(), b.fingerprints()), f"round {r}"
+        assert np.array_equal(a.scalars(), b.scalars()), f"round {r}"
+        for i in rng.choice(cfg.capacity, 12, replace=False):
+            assert np.array_equal(a.row(int(i)), b.row(int(i))), f"round {r} node {i}"
+    a.close()
+    b.close()
+
+
 @pytest.mark.parametrize("name", [s["name"] for s in scenarios.SCENARIOS])
 def test_gpu_matches_pyref_trace(gpu, name):
     traces = json.load(open(os.path.join(HERE, "golden", "traces.json")))
