@@ -7,9 +7,12 @@ Workload (BASELINE.json configs[2]): 65,536 simulated Kaboodle peers on one MI35
 simulated round (lifecycle, broadcasts, tick A1-A4 for every live peer, and all receive waves) through
 the C ABI `kb_sim_step`; the timed region holds K steps with all state resident in HBM.
 
-value = peer-rounds/s summed over ranks (live peers x rounds / max-over-ranks wall time).
-N > 1: every rank simulates its own independent 64K mesh ("replicas", weak scaling, no collective on
-the data path), each with a distinct seed.
+value = live peers x rounds / max-over-ranks wall time, for the whole job.
+N > 1 (torchrun, one process per GPU): ONE mesh of nodes x N peers, row-sharded across the N GPUs
+(kb_sim_create_rank): every delivery wave is an RCCL all-to-all-v of the records between
+shards and the Join/Failed lists an all-gather.  Weak scaling: every GPU holds `nodes` rows of the
+mesh; the rows get wider with N (every peer tracks every peer), so the mesh is N x larger.
+--replicas runs N independent meshes instead (distinct seeds, no collective on the data path).
 
 Also reported, on the same JSON line:
   roofline      the dominant kernel (k_sweep, the per-round row sweep of ping_random_peer + fingerprint):
@@ -42,7 +45,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--nodes", type=int, default=65536)
+    ap.add_argument("--nodes", type=int, default=65536, help="peers per GPU (rows of the mesh each GPU holds)")
+    ap.add_argument("--replicas", action="store_true", help="N > 1: independent meshes instead of one sharded mesh")
+    ap.add_argument("--rank-mesh", action="store_true",
+                    help="N = 1: run the mesh through the RCCL rank path (a 1-rank communicator) to check it")
     ap.add_argument("--loss", type=float, default=0.01)
     ap.add_argument("--churn", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=1)
@@ -94,14 +100,31 @@ def cpu_baseline(cfg, budget_s: float, nodes: int) -> dict:
                       f"(oracle/kb_oracle.c, OpenMP over peers, {dt:.1f} s)"}
 
 
+def sharded(a, world: int) -> bool:
+    return (world > 1 and not getattr(a, "replicas", False)) or getattr(a, "rank_mesh", False)
+
+
 def rank_config(a, rank: int, world: int, local: int):
-    """The replica this rank simulates: the same workload with a rank-distinct seed."""
+    """This rank's mesh: one mesh of nodes x world peers shared by every rank (sharded), or a replica of
+    the nodes-peer workload with a rank-distinct seed (world 1, --replicas)."""
     from kaboodle_amd._ffi import KB_INIT_CONVERGED, SimConfig
     total = a.warmup + a.steps
-    reserve = max(4096, int(a.nodes * a.churn * (total + 8) * 1.5))
-    return SimConfig(capacity=a.nodes + reserve, initial_nodes=a.nodes, init_mode=KB_INIT_CONVERGED, loss=a.loss,
-                     churn=a.churn, fault_end_round=total, seed=a.seed + 1000 * rank,
+    shard = sharded(a, world)
+    peers = a.nodes * world if shard else a.nodes
+    reserve = max(4096, int(peers * a.churn * (total + 8) * 1.5))
+    return SimConfig(capacity=peers + reserve, initial_nodes=peers, init_mode=KB_INIT_CONVERGED, loss=a.loss,
+                     churn=a.churn, fault_end_round=total, seed=a.seed + (0 if shard else 1000 * rank),
                      device=local if world > 1 else -1)
+
+
+def share_uid(rank: int, make) -> bytes:
+    """Rank 0 makes the RCCL unique id of the mesh's communicator; every rank receives it."""
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        return make()
+    obj = [make() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
 
 
 def aggregate(dt: float, units: float, world: int, device="cpu"):
@@ -133,10 +156,17 @@ def main() -> int:
     kaboodle_amd.require_gpu()
 
     total = a.warmup + a.steps
+    shard = sharded(a, world)
     cfg = rank_config(a, rank, world, local)
     capacity = cfg.capacity
+    peers = cfg.initial_nodes
     workload = f"configs[2]: {a.nodes} peers, converged start, {a.loss:.0%} loss, {a.churn:.1%}/round churn"
-    mesh = kaboodle_amd.Mesh(cfg)
+    if shard:
+        workload = (f"configs[2] per GPU, one mesh: {peers} peers row-sharded {a.nodes}/GPU over {world} GPUs, "
+                    f"converged start, {a.loss:.0%} loss, {a.churn:.1%}/round churn")
+        mesh = kaboodle_amd.Mesh(cfg, rank=rank, world=world, uid=share_uid(rank, kaboodle_amd.rccl_unique_id))
+    else:
+        mesh = kaboodle_amd.Mesh(cfg)
 
     mesh.step(a.warmup)
     torch.cuda.synchronize()
@@ -149,7 +179,7 @@ def main() -> int:
     t0 = time.perf_counter()
     for _ in range(a.steps):
         mesh.step(1)                                 # synchronous: returns after the round's kernels
-        alive_sum += mesh.stats()["alive"]
+        alive_sum += mesh.stats()["alive"]           # sharded: the whole mesh (collective)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -159,20 +189,22 @@ def main() -> int:
     sweep_bytes = mesh.sweep_bytes() - bytes0
     st = mesh.stats()
 
-    dt, alive_total = aggregate(dt, float(alive_sum), world, device="cuda")
+    # sharded: every rank saw the whole mesh's count, so it enters the sum once
+    dt, alive_total = aggregate(dt, float(alive_sum if (rank == 0 or not shard) else 0), world, device="cuda")
 
     conv = None
     if not a.no_conv:
         # (1) BASELINE configs[1]: 1024 peers all joining at round 0, no faults -> rounds to convergence
-        with kaboodle_amd.Mesh(SimConfig(capacity=1024, initial_nodes=1024, seed=a.seed + 1000 * rank,
-                                         device=local if world > 1 else -1)) as m2:
-            r2 = -1
-            for _ in range(64):
-                m2.step(1)
-                s2 = m2.stats()
-                if s2["first_converged_round"] >= 0:
-                    r2 = s2["first_converged_round"]
-                    break
+        r2 = -1
+        if rank == 0 or not shard:
+            with kaboodle_amd.Mesh(SimConfig(capacity=1024, initial_nodes=1024, seed=a.seed + 1000 * rank,
+                                             device=local if world > 1 else -1)) as m2:
+                for _ in range(64):
+                    m2.step(1)
+                    s2 = m2.stats()
+                    if s2["first_converged_round"] >= 0:
+                        r2 = s2["first_converged_round"]
+                        break
         # (2) this workload's quiescent tail: faults ended at round `total`; step untimed until every live
         # peer agrees or the cap (Q2 + honoured Failed remove live peers mesh-wide)
         r_conv, extra = -1, 0
@@ -202,8 +234,9 @@ def main() -> int:
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (Philox-keyed loss/churn/targets, seed-determined)",
-            "config": {"workload": workload, "peers": a.nodes, "capacity": capacity, "loss": a.loss,
-                       "churn": a.churn, "parallelism": f"replicas{world}" if world > 1 else "single",
+            "config": {"workload": workload, "peers": peers, "peers_per_gpu": a.nodes, "capacity": capacity,
+                       "loss": a.loss, "churn": a.churn,
+                       "parallelism": (f"rowshard{world}" if shard else f"replicas{world}") if world > 1 else "single",
                        "max_waves": cfg.max_waves},
             "roofline": {"bound": "hbm", "kernel": "k_sweep", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -34,11 +34,23 @@ def require_gpu() -> None:
     lib()
 
 
-class Mesh(Sim):
-    """One simulated mesh on the GPU."""
+def rccl_unique_id() -> bytes:
+    """RCCL unique id for kb_sim_create_rank (made on rank 0, broadcast by the host)."""
+    from ._ffi import rccl_unique_id as _uid
+    return _uid(lib())
 
-    def __init__(self, cfg: SimConfig | None = None, **kw):
-        super().__init__(lib(), cfg or SimConfig(**kw))
+
+class Mesh(Sim):
+    """One simulated mesh on the GPU, or one row shard of it.
+
+    Mesh(cfg)                              the whole mesh on this process's GPU
+    Mesh(cfg, shards=k)                    k row shards inside this process (one GPU; exchange by copies)
+    Mesh(cfg, rank=r, world=w, uid=u)      this process's shard of a mesh over w GPUs (RCCL exchange)
+    """
+
+    def __init__(self, cfg: SimConfig | None = None, shards: int = 0, rank: int | None = None,
+                 world: int | None = None, uid: bytes | None = None, **kw):
+        super().__init__(lib(), cfg or SimConfig(**kw), shards=shards, rank=rank, world=world, uid=uid)
 
     def node(self, i: int) -> "Kaboodle":
         return Kaboodle(self, i)

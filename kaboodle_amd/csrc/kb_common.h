@@ -86,11 +86,12 @@ __device__ inline uint32_t log_window_start(const Dev& d, uint32_t i, int32_t r)
   return r >= SHARE_AGE - 1 ? d.fstart[(size_t)i * 16 + ((uint32_t)(r - (SHARE_AGE - 1)) & 15u)] : 0u;
 }
 // copy n 16-byte words global -> LDS with `lanes` cooperating threads (index t), 8 loads in flight each
-__device__ inline void stage16(uint4* dst, const uint4* src, uint32_t n, uint32_t t, uint32_t lanes) {
+__device__ __attribute__((always_inline)) inline void stage16(uint4* dst, const uint4* src, uint32_t n, uint32_t t,
+                                                             uint32_t lanes) {
   for (uint32_t w0 = 0; w0 < n; w0 += lanes * 8) {
     uint4 v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { const uint32_t w = w0 + k * lanes + t; if (w < n) v[k] = src[w]; }
+    for (int k = 0; k < 8; ++k) { const uint32_t w = w0 + k * lanes + t; v[k] = src[w < n ? w : 0]; }
 #pragma unroll
     for (int k = 0; k < 8; ++k) { const uint32_t w = w0 + k * lanes + t; if (w < n) dst[w] = v[k]; }
   }
@@ -221,7 +222,7 @@ __device__ inline void wave_combine(const Dev& d, uint32_t& raw, uint32_t& cnt) 
 // Current fingerprint of row i with the whole wave: stale checkpoints are refolded (one per lane
 // when many are stale; all 64 lanes on each one when few are — the in-order handlers typically
 // dirty one segment per newly heard sender), then the 64 checkpoints are combined.
-__device__ uint32_t wave_fp(const Dev& d, const uint32_t* ztab, uint32_t i, unsigned long long extra) {
+__device__ __attribute__((always_inline)) inline uint32_t wave_fp(const Dev& d, const uint32_t* ztab, uint32_t i, unsigned long long extra) {
   const uint32_t l = lane();
   const unsigned long long sd = d.sdirty[i] | extra;
   uint2 sp = make_uint2(0, 0);
@@ -272,7 +273,7 @@ __device__ inline void susp_clear(const Dev& d, uint32_t i, uint32_t p) {
   for (int k = 0; k < SLOTS; ++k) if (s[k].kind && s[k].peer == p) s[k].kind = 0;
 }
 // lifecycle: the per-id part on every shard, the row part on the shard holding the row
-__device__ void node_start(const Dev& d, uint32_t i, int32_t r) {      // src/lib.rs:136-156
+__device__ __attribute__((always_inline)) inline void node_start(const Dev& d, uint32_t i, int32_t r) {      // src/lib.rs:136-156
   if (local(d, i)) {
     if (mem_set(d, i, i)) d.n[i] += 1;
     else susp_clear(d, i, i);
@@ -283,7 +284,7 @@ __device__ void node_start(const Dev& d, uint32_t i, int32_t r) {      // src/li
   }
   d.alive[i] = 1; d.start_round[i] = r;
 }
-__device__ void node_stop(const Dev& d, uint32_t i) {                  // src/lib.rs:159-183
+__device__ __attribute__((always_inline)) inline void node_stop(const Dev& d, uint32_t i) {                  // src/lib.rs:159-183
   if (local(d, i)) {
     if (mem_clr(d, i, i)) { susp_clear(d, i, i); d.n[i] -= 1; mark(d, i, seg_bit(d, i)); }
     d.paq_n[i] = 0;

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(1024) void k_bfail_prep_lds(const BCast* bf, uint32
     }
   }
   __syncthreads();
-  auto first = [&](uint32_t x) -> uint32_t {
+  auto first = [&](uint32_t x) __attribute__((always_inline)) -> uint32_t {
     uint32_t h = slot0(x);
     while (hk[h] != EMPTY) { if (hk[h] == x) return hv[h]; h = (h + 1) & (HS - 1); }
     return EMPTY;
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
   }
   if (lj) for (uint32_t e = threadIdx.x; e < pb.nj; e += blockDim.x) JL[e] = pb.bjoin[e].sender | (pb.bjoin[e].bseq << 23);
   __syncthreads();
-  auto fail_at = [&](uint32_t e, uint32_t& dep) -> BCast {
+  auto fail_at = [&](uint32_t e, uint32_t& dep) __attribute__((always_inline)) -> BCast {
     if (lf) {
       const uint32_t x = FL[2 * e];
       dep = x >> 31;
@@ -200,7 +200,7 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
     dep = pb.dep[e];
     return pb.bfail[e];
   };
-  auto join_at = [&](uint32_t e) -> BCast {
+  auto join_at = [&](uint32_t e) __attribute__((always_inline)) -> BCast {
     if (lj) { const uint32_t x = JL[e]; return BCast{x & 0x7FFFFFu, x & 0x7FFFFFu, x >> 23, 0}; }
     return pb.bjoin[e];
   };
@@ -221,11 +221,11 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
     if (l < SLOTS) { const Susp sl = d.susp[(size_t)i * SLOTS + l]; s_sp[wv][l] = sl.kind ? sl.peer : 0xFFFFFFFFu; }
     wait_lds();
     __builtin_amdgcn_wave_barrier();
-    auto mem = [&](uint32_t x) -> bool {
+    auto mem = [&](uint32_t x) __attribute__((always_inline)) -> bool {
       const uint32_t w = LDSB ? B[x >> 5] : __hip_atomic_load(&B[x >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return (w >> (x & 31)) & 1u;
     };
-    auto is_susp = [&](uint32_t x) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
+    auto is_susp = [&](uint32_t x) __attribute__((always_inline)) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
     uint32_t n = d.n[i];
     const uint32_t n0 = n;
     uint32_t fn = d.flog_n[i];
@@ -353,7 +353,7 @@ __device__ inline uint32_t mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
-__device__ inline uint32_t prp_walk(uint32_t x, uint32_t n, const U4& key) {
+__device__ __attribute__((always_inline)) inline uint32_t prp_walk(uint32_t x, uint32_t n, const U4& key) {
   uint32_t b = 2;
   while ((1ull << b) < n) b += 2;
   const uint32_t h = b / 2, mask = (1u << h) - 1u;
@@ -389,7 +389,7 @@ __host__ __device__ inline size_t resp_words(uint32_t NW, uint32_t NB) {
 }
 
 // exclusive prefix of the member counts of X's 256-id blocks into XP[0..NB], XP[NB] = total (block-wide)
-__device__ uint32_t block_prefix(const uint32_t* X, uint32_t* XP, uint32_t NB, uint32_t* s_red) {
+__device__ __attribute__((always_inline)) inline uint32_t block_prefix(const uint32_t* X, uint32_t* XP, uint32_t NB, uint32_t* s_red) {
   const uint32_t t = threadIdx.x, T = blockDim.x;
   const uint32_t per = (NB + T - 1) / T;
   uint32_t bc = 0;

@@ -20,7 +20,7 @@ __device__ inline uint32_t cand16(const Dev& d, const uint8_t* rw, const uint32_
 }
 // rank -> id over the candidates of row i; lane l owns ids [lo, hi) holding candidate ranks
 // [lane_off, lane_off + lane_cnt).
-__device__ uint32_t select_known(const Dev& d, const uint8_t* rw, const uint32_t* bw, uint32_t i, uint32_t rank,
+__device__ __attribute__((always_inline)) inline uint32_t select_known(const Dev& d, const uint8_t* rw, const uint32_t* bw, uint32_t i, uint32_t rank,
                                  uint32_t lane_off, uint32_t lane_cnt, uint32_t lo, uint32_t hi) {
   uint32_t found = 0xFFFFFFFFu;
   if (rank >= lane_off && rank < lane_off + lane_cnt) {

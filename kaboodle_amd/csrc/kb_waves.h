@@ -419,7 +419,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     // update is then one multiply by Z per insertion.
     bool inc = false, fpstale = false;
     uint32_t R = 0;
-    auto take_base = [&]() {
+    auto take_base = [&]() __attribute__((always_inline)) {
       if (need_sync) { wave_mem_sync(); need_sync = false; }
       const unsigned long long sd = d.sdirty[i] | segs;
       uint2 sp;
@@ -453,7 +453,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       segs = 0;
       inc = true; dirty = false; fpstale = true;
     };
-    auto fp_now = [&]() -> uint32_t {
+    auto fp_now = [&]() __attribute__((always_inline)) -> uint32_t {
       if (inc) {
         if (fpstale) { fp = R ^ d.zfin[n] ^ 0xFFFFFFFFu; fpstale = false; }
         return fp;
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       }
       return fp;
     };
-    auto maybe_sync = [&](uint32_t peer, uint32_t their_fp, uint32_t their_n) {   // :707-740
+    auto maybe_sync = [&](uint32_t peer, uint32_t their_fp, uint32_t their_n) __attribute__((always_inline)) {   // :707-740
       const uint32_t f = fp_now();
       if (f == their_fp || n > their_n) return;
       emit_msg(ob, d, i, oseq, peer, K_KPR, 0, f, n, 0);
@@ -613,12 +613,11 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           if (hit) {
             const int e = __ffsll((long long)hit) - 1;
             const uint32_t nobs = s_cur[wv][e].nobs;
-            uint32_t obs[NOBS];
-            for (int q = 0; q < NOBS; ++q) obs[q] = s_cur[wv][e].obs[q];
+            // the entry's observers stay in LDS until a later PingRequest reuses the slot: read in place
+            for (uint32_t q = 0; q < nobs; ++q) emit_msg(ob, d, i, oseq, s_cur[wv][e].obs[q], K_ACK, m.a, m.fp, m.n, 0);
             wait_lds();
             __builtin_amdgcn_wave_barrier();
             if (l == 0) s_cur[wv][e].used = 0;
-            for (uint32_t q = 0; q < nobs; ++q) emit_msg(ob, d, i, oseq, obs[q], K_ACK, m.a, m.fp, m.n, 0);
             wait_lds();
             __builtin_amdgcn_wave_barrier();
           }
@@ -637,7 +636,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           uint64_t size = 8 + (d.seglen[i] - ADDR_LEN) + 4 + 8;
           bool over = d.uniform && kbig == r;
           if (over) { w_over++; maybe_sync(s, m.fp, m.n); break; }
-          auto take = [&](bool ok, uint32_t j) {
+          auto take = [&](bool ok, uint32_t j) __attribute__((always_inline)) {
             const unsigned long long okm = __ballot(ok);
             const uint32_t pos = total + __popcll(okm & ((1ull << l) - 1ull));
             if (!d.uniform) size += wave_sum(ok ? 18u + d.seglen[j] - ADDR_LEN : 0u);

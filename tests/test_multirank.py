@@ -27,7 +27,7 @@ def _worker(rank, world, port, out):
     import bench
     import parity
     from kaboodle_amd._ffi import Sim
-    a = argparse.Namespace(nodes=96, loss=0.02, churn=0.01, seed=1, warmup=1, steps=4)
+    a = argparse.Namespace(nodes=96, loss=0.02, churn=0.01, seed=1, warmup=1, steps=4, replicas=True)
     cfg = bench.rank_config(a, rank, world, rank)
     with Sim(parity.oracle_lib(), cfg) as o:
         o.step(a.warmup)
@@ -53,3 +53,36 @@ def test_replicas_reduce_like_bench():
     assert fp0 != fp1
     assert dt0 == dt1 == 2.0                            # max over ranks
     assert tu0 == tu1 == float(u0 + u1)                 # summed units
+
+
+def _shard_worker(rank, world, port, out):
+    """The sharded bench setup on gloo: the RCCL id made on rank 0 reaches every rank, and every rank
+    derives the same mesh (capacity, seed) of nodes x world peers."""
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import argparse
+    import bench
+    a = argparse.Namespace(nodes=96, loss=0.01, churn=0.001, seed=5, warmup=2, steps=3, replicas=False)
+    uid = bench.share_uid(rank, lambda: bytes(range(128)))
+    cfg = bench.rank_config(a, rank, world, rank)
+    ra = argparse.Namespace(**{**a.__dict__, "replicas": True})
+    rcfg = bench.rank_config(ra, rank, world, rank)
+    out[rank] = (uid, cfg.capacity, cfg.initial_nodes, cfg.seed, rcfg.initial_nodes, rcfg.seed,
+                 bench.sharded(a, world), bench.sharded(ra, world))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_setup_over_gloo():
+    world, port = 2, _free_port()
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_shard_worker, args=(world, port, out), nprocs=world, join=True)
+    r0, r1 = out[0], out[1]
+    assert r0[0] == r1[0] == bytes(range(128))          # rank 0's id on every rank
+    assert r0[1:4] == r1[1:4]                            # one mesh: same capacity, size and seed
+    assert r0[2] == 96 * world
+    assert r0[4] == r1[4] == 96 and r0[5] != r1[5]        # replicas: per-rank mesh, distinct seeds
+    assert r0[6] and not r0[7]
