@@ -11,7 +11,8 @@
 //   k_tick_pre                      maybe_broadcast_join + handle_suspected_peers  :228-251, :558-653
 //   k_sweep    <- dominant kernel   ping_random_peer row sweep + fingerprint checkpoints :655-703, :71-83
 //   k_tick_post                     ping target, handle_incoming_ping_requests     :655-703, :550-556
-//   waves: k_route, k_scan_*, k_scatter, k_kp_insert, k_kp_prologue, k_touch_fix, k_proc
+//   waves: k_wave_clear, k_route (k_route_x, k_pack, exchange, k_route_recv when sharded), k_scan_*,
+//          k_scatter, k_kp_group, k_sort_inbox, k_proc
 //                                   handle_incoming_messages                       src/kaboodle.rs:394-548
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,12 +40,13 @@ struct ScanArgs {
   const uint32_t* in[4]; uint32_t* out[4]; int narr; uint32_t n;
   uint32_t* totals;   // device, narr values (+ list count at totals[4] when list != null)
   uint32_t* list; uint32_t* list_count; uint32_t list_base;   // list entries are j + list_base
+  uint32_t list_or3;  // list flag: in[0][j] != 0, or also in[3][j] != 0 when set
   uint32_t addc[4];   // constant added to every element of array q before scanning
   uint32_t* tiles;    // workspace [5 * ntiles]
   uint32_t ntiles;
 };
 __device__ inline uint32_t scan_val(const ScanArgs& a, int q, uint32_t j) {
-  if (q == 4) return a.in[0][j] != 0;
+  if (q == 4) return a.in[0][j] != 0 || (a.list_or3 && a.in[3][j] != 0);
   return (a.in[q] ? a.in[q][j] : 0) + a.addc[q];
 }
 __global__ __launch_bounds__(1024) void k_scan_tiles(ScanArgs a) {
@@ -435,8 +437,9 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
     s->ob[b].msg_cap = s->msg_cap; s->ob[b].pay_cap = s->pay_cap;
   }
   AR(s->wc.cnt1, 1); AR(s->wc.bnd, 1); AR(s->wc.bpay, 1); AR(s->wc.cursor, 1);
-  AR(s->wc.in_off, 1); A(s->wc.active, R); AR(s->wc.touched, 1); A(s->wc.touched_list, R);
-  if (!xf) { A(s->wc.status, s->msg_cap); A(s->wc.inbox, s->msg_cap); A(s->wc.kp_list, s->msg_cap); }
+  AR(s->wc.in_off, 1); A(s->wc.active, R);
+  AR(s->wc.kcnt, 1); AR(s->wc.kpay, 1); AR(s->wc.kcur, 1); AR(s->wc.koff, 1);
+  if (!xf) { A(s->wc.status, s->msg_cap); A(s->wc.inbox, s->msg_cap); A(s->wc.kin, s->msg_cap); }
   A(s->bfail, (size_t)C * SLOTS); A(s->bjoin, C);
   AR(s->bs.join, 1); AR(s->bs.nfail, 1); AR(s->bs.fail, SLOTS); AR(s->join_off, 1); AR(s->fail_off, 1);
   A(s->scan_tot, 32); A(s->scan_tiles, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
@@ -564,7 +567,7 @@ static int ensure_recv(kb_sim* s, size_t nm, size_t np) {
     HIPCHK(hipMalloc(&s->rmsg, sizeof(Msg) * cap)); HIPCHK(hipMalloc(&s->rstatus, cap));
     HIPCHK(hipMalloc(&s->rinbox, 4 * cap)); HIPCHK(hipMalloc(&s->rkp, 4 * cap));
     s->rmsg_cap = cap;
-    s->wc.status = s->rstatus; s->wc.inbox = s->rinbox; s->wc.kp_list = s->rkp;
+    s->wc.status = s->rstatus; s->wc.inbox = s->rinbox; s->wc.kin = s->rkp;
   }
   if (np > s->rpay_cap || !s->rpay) {
     if (s->rpay) (void)hipFree(s->rpay);
@@ -758,11 +761,7 @@ static int step_round(kb_sim* s) {
     OutBuf& ob = s->ob[cur];
     OutBuf& nb = s->ob[cur ^ 1];
     const int last = w == s->cfg.max_waves;
-    HIPCHK(hipMemsetAsync(L(s, s->wc.cnt1), 0, 4ull * R, st));
-    HIPCHK(hipMemsetAsync(L(s, s->wc.bnd), 0, 4ull * R, st));
-    HIPCHK(hipMemsetAsync(L(s, s->wc.bpay), 0, 4ull * R, st));
-    HIPCHK(hipMemsetAsync(L(s, s->wc.cursor), 0, 4ull * R, st));
-    HIPCHK(hipMemsetAsync(d.ctr + C_KP, 0, 12, st));   // C_KP, C_TOUCH, C_ACTIVE
+    k_wave_clear<<<gnode, tb, 0, st>>>(d, s->wc);
     OutBuf ib = ob;                                    // the wave's delivered records
     uint32_t nrecv = 0;
     if (!s->xf) {
@@ -782,11 +781,12 @@ static int step_round(kb_sim* s) {
     }
     {
       ScanArgs a = scan_args(s, R, s->scan_tot + 8);
-      a.narr = 3;
+      a.narr = 4;
       a.in[0] = L(s, s->wc.cnt1); a.out[0] = L(s, s->wc.in_off);
       a.in[1] = L(s, s->wc.bnd); a.out[1] = L(s, nb.off);
       a.in[2] = L(s, s->wc.bpay); a.out[2] = L(s, nb.poff);
-      a.list = s->wc.active; a.list_count = d.ctr + C_ACTIVE; a.list_base = s->lo;
+      a.in[3] = L(s, s->wc.kcnt); a.out[3] = L(s, s->wc.koff);
+      a.list = s->wc.active; a.list_count = d.ctr + C_ACTIVE; a.list_base = s->lo; a.list_or3 = 1;
       launch_scan(a, st);
     }
     if (s->debug_waves) {                               // KB_DEBUG_WAVES: inbox sizes per wave
@@ -802,9 +802,8 @@ static int step_round(kb_sim* s) {
     HIPCHK(hipMemsetAsync(L(s, nb.cnt), 0, 4ull * R, st));
     if (!s->xf) k_scatter<<<gnode, tb, 0, st>>>(d, ob, s->wc);
     else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
-    k_kp_insert<<<2048, 256, 0, st>>>(d, ib, s->wc, r);
-    k_kp_prologue<<<1024, 256, 0, st>>>(d, ib, s->wc, r);
-    k_touch_fix<<<1024, 256, 0, st>>>(d, s->wc);
+    k_kp_group<false><<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r);
+    k_kp_group<true><<<std::min<uint32_t>((R + 1023) / 1024, 512), 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
     k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc);
     if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 12, st));
     k_proc<<<4096, 256, 0, st>>>(d, ib, nb, s->wc, r);

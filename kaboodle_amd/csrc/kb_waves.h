@@ -7,11 +7,22 @@ namespace kb {
 
 struct WaveCtl {
   uint8_t* status;        // per outbox slot: 0 dropped, 1 delivered (in-order kinds), 2 delivered KnownPeers
-  uint32_t* cnt1; uint32_t* bnd; uint32_t* bpay; uint32_t* cursor;   // per destination
+  uint32_t* cnt1; uint32_t* bnd; uint32_t* bpay; uint32_t* cursor;   // per destination: in-order inbox
+  uint32_t* kcnt; uint32_t* kpay; uint32_t* kcur; uint32_t* koff;    // per destination: KnownPeers group
   uint32_t* in_off; uint32_t* inbox; uint32_t* active;
-  uint32_t* kp_list; uint32_t* touched; uint32_t* touched_list;
+  uint32_t* kin;          // KnownPeers deliveries grouped by destination (koff / kcnt)
   uint32_t msg_cap; uint32_t pay_cap;
 };
+
+// per-wave counters of the local rows back to zero (one launch instead of a memset per array)
+__global__ void k_wave_clear(Dev d, WaveCtl wc) {
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < d.hi) {
+    wc.cnt1[i] = 0; wc.bnd[i] = 0; wc.bpay[i] = 0; wc.cursor[i] = 0;
+    wc.kcnt[i] = 0; wc.kpay[i] = 0; wc.kcur[i] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 3) d.ctr[C_KP + threadIdx.x] = 0;     // C_KP, C_TOUCH, C_ACTIVE
+}
 
 // messages a handler may emit per delivered message (next-wave outbox reservation)
 __device__ inline uint32_t out_bound(uint32_t kind) {
@@ -34,12 +45,9 @@ struct SenderSpan {
 // the message), else delivered; counts per destination.
 __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int32_t r, uint32_t w, int last) {
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
-  __shared__ uint32_t s_kp[4];
-  __shared__ uint32_t s_kpbase;
   const uint32_t wv = threadIdx.x >> 6, l = lane();
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0;
-  uint32_t nkp = 0;
   const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
   s_ex[wv][l] = wave_excl(cnt);
   s_base[wv][l] = i < d.hi ? ob.off[i] : 0;
@@ -59,8 +67,11 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
     else if (part_blocks(d, r, m.sender, m.dest)) part++;
     else if (faults(d, r) && d.loss_thr &&
              philox(m.sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m.seq, d.k0, d.k1).x < d.loss_thr) loss++;
-    else if (m.kind == K_KP) { st = 2; nkp++; }
-    else {
+    else if (m.kind == K_KP) {
+      st = 2;
+      atomicAdd(&wc.kcnt[m.dest], 1u);
+      if (m.a) atomicAdd(&wc.kpay[m.dest], m.a);
+    } else {
       st = 1;
       atomicAdd(&wc.cnt1[m.dest], 1u);
       atomicAdd(&wc.bnd[m.dest], out_bound(m.kind));
@@ -70,27 +81,6 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
   }
   for (int k = 0; k < 5; ++k) stat_add(d, S_PING + k, ks[k]);
   stat_add(d, S_DEAD, dead); stat_add(d, S_PART, part); stat_add(d, S_LOSS, loss); stat_add(d, S_WINDOW, win);
-  if (last) return;
-  // KnownPeers deliveries go to kp_list: one atomic per workgroup reserves the space
-  const uint32_t kex = wave_excl(nkp), ktot = wave_sum(nkp);
-  if (l == 0) s_kp[wv] = ktot;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t run = 0;
-    for (uint32_t t = 0; t < blockDim.x / 64; ++t) { const uint32_t v = s_kp[t]; s_kp[t] = run; run += v; }
-    s_kpbase = run ? atomicAdd(&d.ctr[C_KP], run) : 0;
-  }
-  __syncthreads();
-  if (ktot) {
-    uint32_t pos = s_kpbase + s_kp[wv] + kex;
-    __threadfence_block();
-    for (uint32_t k = l; k < T; k += 64) {
-      uint32_t j, q;
-      sp.owner(s_ex[wv], k, j, q);
-      const uint32_t g = s_base[wv][j] + q;
-      if (wc.status[g] == 2) wc.kp_list[pos++] = g;
-    }
-  }
 }
 
 __global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
@@ -108,9 +98,11 @@ __global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
     uint32_t j, q;
     sp.owner(s_ex[wv], k, j, q);
     const uint32_t g = s_base[wv][j] + q;
-    if (wc.status[g] != 1) continue;
+    const uint8_t st = wc.status[g];
+    if (!st) continue;
     const uint32_t dst = ob.msgs[g].dest;
-    wc.inbox[wc.in_off[dst] + atomicAdd(&wc.cursor[dst], 1u)] = g;
+    if (st == 1) wc.inbox[wc.in_off[dst] + atomicAdd(&wc.cursor[dst], 1u)] = g;
+    else wc.kin[wc.koff[dst] + atomicAdd(&wc.kcur[dst], 1u)] = g;
   }
 }
 
@@ -229,11 +221,7 @@ __global__ __launch_bounds__(256) void k_pack(Dev d, OutBuf ob, XState x) {
 // destination (inbox sizes and next-wave outbox reservations), list the KnownPeers records
 struct RecvBlocks { uint32_t world; uint32_t m0[XMAX + 1]; uint32_t p0[XMAX + 1]; };
 __global__ __launch_bounds__(256) void k_route_recv(Dev d, OutBuf ib, WaveCtl wc, RecvBlocks rb, uint32_t n) {
-  __shared__ uint32_t s_kp[4];
-  __shared__ uint32_t s_kpbase;
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t wv = threadIdx.x >> 6, l = lane();
-  bool kp = false;
   if (g < n) {
     const Msg m = ib.msgs[g];
     if (m.kind == K_KP) {
@@ -241,7 +229,8 @@ __global__ __launch_bounds__(256) void k_route_recv(Dev d, OutBuf ib, WaveCtl wc
       while (src + 1 < rb.world && rb.m0[src + 1] <= g) ++src;
       ib.msgs[g].off = m.off + rb.p0[src];
       wc.status[g] = 2;
-      kp = true;
+      atomicAdd(&wc.kcnt[m.dest], 1u);
+      if (m.a) atomicAdd(&wc.kpay[m.dest], m.a);
     } else {
       wc.status[g] = 1;
       atomicAdd(&wc.cnt1[m.dest], 1u);
@@ -249,90 +238,143 @@ __global__ __launch_bounds__(256) void k_route_recv(Dev d, OutBuf ib, WaveCtl wc
       if (m.kind == K_KPR) atomicAdd(&wc.bpay[m.dest], d.paybound);
     }
   }
-  const unsigned long long km = __ballot(kp);
-  if (l == 0) s_kp[wv] = __popcll(km);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t run = 0;
-    for (uint32_t t = 0; t < blockDim.x / 64; ++t) { const uint32_t v = s_kp[t]; s_kp[t] = run; run += v; }
-    s_kpbase = run ? atomicAdd(&d.ctr[C_KP], run) : 0;
-  }
-  __syncthreads();
-  if (kp) wc.kp_list[s_kpbase + s_kp[wv] + __popcll(km & ((1ull << l) - 1ull))] = g;
 }
 __global__ void k_scatter_flat(OutBuf ib, WaveCtl wc, uint32_t n) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= n || wc.status[g] != 1) return;
+  if (g >= n) return;
+  const uint8_t st = wc.status[g];
   const uint32_t dst = ib.msgs[g].dest;
-  wc.inbox[wc.in_off[dst] + atomicAdd(&wc.cursor[dst], 1u)] = g;
+  if (st == 1) wc.inbox[wc.in_off[dst] + atomicAdd(&wc.cursor[dst], 1u)] = g;
+  else if (st == 2) wc.kin[wc.koff[dst] + atomicAdd(&wc.kcur[dst], 1u)] = g;
 }
 
-__device__ inline void mark_touched(const Dev& d, const WaveCtl& wc, uint32_t node) {
-  if (atomicExch(&wc.touched[node], 1u) == 0u) wc.touched_list[atomicAdd(&d.ctr[C_TOUCH], 1u)] = node;
+// ---- KnownPeers group of one destination: the arms (:448-472) and the envelope prologues (:406-415)
+// One workgroup per destination with KnownPeers deliveries in the wave.  First every arm inserts
+// each listed absent peer as Known(now - 10 s) — message-parallel, the group commutes (DESIGN.md
+// §2.5) — then every envelope's prologue makes its sender Known(now).  The member count follows
+// from the bits the atomics newly set, and suspect slots whose entry became Known are freed.
+// BIG = the groups of at least KP_BIG ids (a joiner's hundreds of Join responses, all on one row):
+// 1024 threads on the row's member bitset staged in LDS, a wave per message with KP_UNROLL
+// independent id loads in flight per lane.  The other groups take 256 threads on the bitset in place.
+constexpr uint32_t KP_BIG = 4096;          // payload ids from which a group takes the BIG kernel
+constexpr uint32_t KP_LDS_WORDS = 16384;   // BIG: rows up to 512K ids keep their bitset in LDS (64 KB)
+constexpr int KP_UNROLL = 10;            // 640 ids per wave step: a whole Join response (<= 567)
+__host__ __device__ constexpr size_t kp_lds_bytes(uint32_t nwr) {
+  return 4ull * (nwr <= KP_LDS_WORDS ? nwr : 4);
 }
 
-// KnownPeers arm (:448-472): every listed unknown peer becomes Known(now - 10 s).  Message-parallel:
-// the group commutes, so all arms run before all prologues.
-__global__ __launch_bounds__(256) void k_kp_insert(Dev d, OutBuf ob, WaveCtl wc, int32_t r) {
-  const uint32_t nkp = d.ctr[C_KP];
-  const uint8_t old = enc(r - SHARE_AGE, r);
-  for (uint32_t it = blockIdx.x * 4 + (threadIdx.x >> 6); it < nkp; it += gridDim.x * 4) {
-    const Msg m = ob.msgs[wc.kp_list[it]];
-    uint8_t* rw = row_of(d, m.dest);
+template <bool BIG>
+__global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib, WaveCtl wc, int32_t r) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t kp_lds[];
+  __shared__ unsigned long long s_segs;
+  __shared__ uint32_t s_add, s_nl;
+  __shared__ uint32_t s_list[BIG ? 1024 : 256];
+  const uint32_t t = threadIdx.x, T = blockDim.x;
+  const uint32_t nact = d.ctr[C_ACTIVE];
+  const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
+  const bool lds = BIG && d.NWR <= KP_LDS_WORDS;
+  // the active list T entries per workgroup at a time, interleaved over the workgroups (consecutive
+  // ids, e.g. the round's joiners, go to different workgroups): the destinations of this kind are
+  // listed in LDS by all threads at once, then served one by one
+  for (uint32_t c0 = 0; c0 < nact; c0 += gridDim.x * T) {
+  const uint32_t it = c0 + t * gridDim.x + blockIdx.x;
+  if (t == 0) s_nl = 0;
+  __syncthreads();
+  if (it < nact) {
+    const uint32_t x = wc.active[it];
+    if (wc.kcnt[x] && (wc.kpay[x] >= KP_BIG) == BIG) s_list[atomicAdd(&s_nl, 1u)] = x;
+  }
+  __syncthreads();
+  const uint32_t nl = s_nl;
+  for (uint32_t li = 0; li < nl; ++li) {
+    const uint32_t i = s_list[li];
+    const uint32_t nk = wc.kcnt[i];
+    const uint32_t k0 = wc.koff[i];
+    uint32_t* gB = bits_of(d, i);
+    uint32_t* B = lds ? kp_lds : gB;
+    uint8_t* rw = row_of(d, i);
+    if (t == 0) { s_segs = 0; s_add = 0; }
+    if (lds) stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB), d.NWR / 4, t, T);
     unsigned long long segs = 0;
-    for (uint32_t e = lane(); e < m.a; e += 64) {
-      const uint32_t p = ob.pay[m.off + e];
-      if (!is_mem(d, m.dest, p) && mem_set(d, m.dest, p)) { rw[p] = old; segs |= seg_bit(d, p); }
+    uint32_t added = 0;
+    auto arm = [&](uint32_t p) __attribute__((always_inline)) {
+      const uint32_t bit = 1u << (p & 31);
+      const uint32_t w = lds ? B[p >> 5] : __hip_atomic_load(&B[p >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w & bit) return;
+      if (!(atomicOr(&B[p >> 5], bit) & bit)) { rw[p] = old; segs |= seg_bit(d, p); added++; }
+    };
+    if (BIG) {
+      // wave per message: the records of up to 64 of this wave's messages are fetched at once (lane
+      // j holds message wv + j * waves), then each message's ids are read KP_UNROLL per lane at once
+      __syncthreads();
+      const uint32_t nwv = T >> 6, wv = t >> 6, l = lane();
+      for (uint32_t q0 = wv; q0 < nk; q0 += 64 * nwv) {
+        const uint32_t qm = q0 + l * nwv;
+        uint32_t moff = 0, mlen = 0;
+        if (qm < nk) { const Msg m = ib.msgs[wc.kin[k0 + qm]]; moff = m.off; mlen = m.a; }
+        const uint32_t cnt = q0 + 64 * nwv <= nk ? 64u : (nk - q0 + nwv - 1) / nwv;
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const uint32_t off = bcast(moff, (int)j), len = bcast(mlen, (int)j);
+          for (uint32_t e0 = 0; e0 < len; e0 += 64 * KP_UNROLL) {
+            uint32_t pv[KP_UNROLL];
+#pragma unroll
+            for (int u = 0; u < KP_UNROLL; ++u) {
+              const uint32_t e = e0 + 64u * u + l;
+              pv[u] = e < len ? ib.pay[off + e] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int u = 0; u < KP_UNROLL; ++u) if (pv[u] != 0xFFFFFFFFu) arm(pv[u]);
+          }
+        }
+      }
+    } else {
+      __syncthreads();
+      for (uint32_t q = 0; q < nk; ++q) {              // message by message
+        const Msg m = ib.msgs[wc.kin[k0 + q]];
+        for (uint32_t e = t; e < m.a; e += T) arm(ib.pay[m.off + e]);
+      }
     }
-    segs = (unsigned long long)wave_or((uint32_t)segs) | ((unsigned long long)wave_or((uint32_t)(segs >> 32)) << 32);
-    if (segs && lane() == 0) { mark(d, m.dest, segs); mark_touched(d, wc, m.dest); }
+    __syncthreads();
+    for (uint32_t q = t; q < nk; q += T) {             // prologues
+      const Msg m = ib.msgs[wc.kin[k0 + q]];
+      const uint32_t s = m.sender;
+      // byte update by CAS on its word: exactly one envelope per (dest, sender) sees the transition to
+      // Known(now) and appends it to the freshness log
+      uint32_t* wp = reinterpret_cast<uint32_t*>(rw + (s & ~3u));
+      const uint32_t sh = 8 * (s & 3u);
+      uint32_t ow = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), prevb;
+      while (true) {
+        prevb = (ow >> sh) & 0xFFu;
+        if (prevb == now) break;
+        const uint32_t res = atomicCAS(wp, ow, (ow & ~(0xFFu << sh)) | ((uint32_t)now << sh));
+        if (res == ow) break;
+        ow = res;
+      }
+      if (prevb != now) d.flog[(size_t)i * LOGCAP + (atomicAdd(&d.flog_n[i], 1u) & (LOGCAP - 1))] = log_entry(s, r);
+      const uint32_t bit = 1u << (s & 31);
+      if (!(atomicOr(&B[s >> 5], bit) & bit)) { segs |= seg_bit(d, s); added++; }
+    }
+    if (segs) atomicOr(&s_segs, segs);
+    if (added) atomicAdd(&s_add, added);
+    __syncthreads();
+    const unsigned long long sg = s_segs;
+    if (lds && sg) {                                   // write back the changed segments of the bitset
+      const uint32_t wps4 = d.SEGW / 128;
+      const uint4* B4 = reinterpret_cast<const uint4*>(B);
+      uint4* g4 = reinterpret_cast<uint4*>(gB);
+      for (uint32_t w = t; w < d.NWR / 4; w += T) if ((sg >> (w / wps4)) & 1ull) g4[w] = B4[w];
+    }
+    if (t < SLOTS) {                                   // a prologue overwrote a WaitingFor* entry to Known
+      Susp* sl = d.susp + (size_t)i * SLOTS + t;
+      if (sl->kind) {
+        const uint32_t pw = __hip_atomic_load(reinterpret_cast<uint32_t*>(rw + (sl->peer & ~3u)), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        if (((pw >> (8 * (sl->peer & 3u))) & 0xFFu) != ST_SUSPECT) sl->kind = 0;
+      }
+    }
+    if (t == 0 && (s_add || sg)) { d.n[i] += s_add; mark(d, i, sg); }
+    __syncthreads();                                   // LDS reused by the next destination
   }
-}
-// prologue of every KnownPeers envelope (:406-415): the sender becomes Known(now)
-__global__ void k_kp_prologue(Dev d, OutBuf ob, WaveCtl wc, int32_t r) {
-  const uint32_t nkp = d.ctr[C_KP];
-  const uint8_t now = enc(r, r);
-  for (uint32_t it = blockIdx.x * blockDim.x + threadIdx.x; it < nkp; it += gridDim.x * blockDim.x) {
-    const Msg m = ob.msgs[wc.kp_list[it]];
-    uint8_t* rw = row_of(d, m.dest);
-    const bool was = is_mem(d, m.dest, m.sender);
-    // byte update by CAS on its word: exactly one envelope per (dest, sender) sees the transition to
-    // Known(now) and appends it to the freshness log
-    uint32_t* wp = reinterpret_cast<uint32_t*>(rw + (m.sender & ~3u));
-    const uint32_t sh = 8 * (m.sender & 3u);
-    uint32_t old = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), prevb;
-    while (true) {
-      prevb = (old >> sh) & 0xFFu;
-      if (prevb == now) break;
-      const uint32_t res = atomicCAS(wp, old, (old & ~(0xFFu << sh)) | ((uint32_t)now << sh));
-      if (res == old) break;
-      old = res;
-    }
-    if (prevb != now)
-      d.flog[(size_t)m.dest * LOGCAP + (atomicAdd(&d.flog_n[m.dest], 1u) & (LOGCAP - 1))] = log_entry(m.sender, r);
-    const uint8_t b = was ? (uint8_t)prevb : ST_UNKNOWN;
-    if (!was && mem_set(d, m.dest, m.sender)) mark(d, m.dest, seg_bit(d, m.sender));
-    if (b <= ST_SUSPECT) mark_touched(d, wc, m.dest);
-  }
-}
-// recount membership of touched rows; drop suspect slots whose entry was overwritten to Known
-__global__ __launch_bounds__(256) void k_touch_fix(Dev d, WaveCtl wc) {
-  const uint32_t nt = d.ctr[C_TOUCH];
-  const uint32_t l = lane();
-  for (uint32_t it = blockIdx.x * 4 + (threadIdx.x >> 6); it < nt; it += gridDim.x * 4) {
-    const uint32_t i = wc.touched_list[it];
-    const uint32_t* bw = bits_of(d, i);
-    uint32_t c = 0;
-    for (uint32_t w = l; w < d.NWR; w += 64) c += __popc(bw[w]);
-    c = wave_sum(c);
-    if (l < SLOTS) {
-      Susp* s = d.susp + (size_t)i * SLOTS + l;
-      if (s->kind && row_of(d, i)[s->peer] != ST_SUSPECT) s->kind = 0;
-    }
-    if (l == 0) {
-      if (c != d.n[i]) { d.n[i] = c; d.dirty[i] = 1; }
-      wc.touched[i] = 0;
-    }
   }
 }
 
@@ -342,11 +384,24 @@ __global__ __launch_bounds__(256) void k_touch_fix(Dev d, WaveCtl wc) {
 constexpr uint32_t SORT_MAX = 8192;
 __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc) {
   __shared__ uint32_t v[SORT_MAX];
+  __shared__ uint32_t s_list[1024], s_nl;
   const uint32_t nact = d.ctr[C_ACTIVE];
-  for (uint32_t it = blockIdx.x; it < nact; it += gridDim.x) {
-    const uint32_t i = wc.active[it];
+  // the active list 1024 entries per workgroup at a time, interleaved over the workgroups: its long
+  // inboxes are listed in LDS by all threads at once
+  for (uint32_t c0 = 0; c0 < nact; c0 += gridDim.x * 1024) {
+  const uint32_t it = c0 + threadIdx.x * gridDim.x + blockIdx.x;
+  if (threadIdx.x == 0) s_nl = 0;
+  __syncthreads();
+  if (it < nact) {
+    const uint32_t x = wc.active[it];
+    const uint32_t c = wc.cnt1[x];
+    if (c > 64 && c <= SORT_MAX) s_list[atomicAdd(&s_nl, 1u)] = x;
+  }
+  __syncthreads();
+  const uint32_t nl = s_nl;
+  for (uint32_t li = 0; li < nl; ++li) {
+    const uint32_t i = s_list[li];
     const uint32_t n = wc.cnt1[i];
-    if (n <= 64 || n > SORT_MAX) continue;
     uint32_t P = 128;
     while (P < n) P <<= 1;
     const uint32_t base = wc.in_off[i];
@@ -366,6 +421,7 @@ __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc) {
     for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) wc.inbox[base + k] = v[k];
     __syncthreads();
   }
+  }
 }
 
 // ---- the per-node in-order program for Ping / PingRequest / Ack / KnownPeersRequest ---------------
@@ -374,15 +430,17 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
   __shared__ Susp s_susp[4][SLOTS];
   __shared__ Cur s_cur[4][CSLOTS];
   __shared__ uint2 s_suf[4][NSEG + 1];
+  const uint32_t nact = d.ctr[C_ACTIVE];
+  if (blockIdx.x * 4 >= nact) return;                 // no node for this workgroup (before the table load)
   load_ztab(d, ztab);
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t l = lane();
-  const uint32_t nact = d.ctr[C_ACTIVE];
   const uint8_t now = enc(r, r);
   const uint8_t fresh_thr = enc(r - (SHARE_AGE - 1), r);
   unsigned long long w_over = 0, w_curovf = 0;      // flushed once per wave (see k_phaseB)
   for (uint32_t it = blockIdx.x * 4 + wv; it < nact; it += gridDim.x * 4) {
     const uint32_t i = wc.active[it];
+    if (!wc.cnt1[i]) continue;                        // KnownPeers deliveries only (k_kp_group)
     uint8_t* rw = row_of(d, i);
     const uint32_t* bw = bits_of(d, i);
     uint32_t n = d.n[i], fp = d.fp[i], oseq = 0, pay_used = 0, fn = d.flog_n[i];
@@ -651,13 +709,30 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           // those entries are still exact members of the reply, enough to prove it oversize
           const uint32_t ws = log_window_start(d, i, r);
           const bool complete = fn - ws <= LOGCAP;
-          for (uint32_t k0 = complete ? ws : fn - LOGCAP; k0 < fn && !over; k0 += 64) {
-            const uint32_t k = k0 + l;
-            const uint32_t e = k < fn ? d.flog[(size_t)i * LOGCAP + (k & (LOGCAP - 1))] : LOG_INVALID;
-            const uint32_t j = e >> 8;
-            bool ok = e != LOG_INVALID && j != i && j != s && r - log_round(e, r) < SHARE_AGE;
-            if (ok) ok = ((bw[j >> 5] >> (j & 31)) & 1u) && rw[j] == enc(log_round(e, r), r);
-            take(ok, j);
+          // KPR_BATCH x 64 entries per step: all their log, member-bit and stamp loads in flight at once,
+          // then taken in log order (the early exit stays between steps)
+          constexpr int KPR_BATCH = 4;
+          for (uint32_t k0 = complete ? ws : fn - LOGCAP; k0 < fn && !over; k0 += 64 * KPR_BATCH) {
+            uint32_t ev[KPR_BATCH], wv4[KPR_BATCH], bv[KPR_BATCH];
+#pragma unroll
+            for (int u = 0; u < KPR_BATCH; ++u) {
+              const uint32_t k = k0 + 64u * u + l;
+              ev[u] = k < fn ? d.flog[(size_t)i * LOGCAP + (k & (LOGCAP - 1))] : LOG_INVALID;
+            }
+#pragma unroll
+            for (int u = 0; u < KPR_BATCH; ++u) {
+              const uint32_t j = ev[u] == LOG_INVALID ? 0u : ev[u] >> 8;
+              wv4[u] = bw[j >> 5];
+              bv[u] = rw[j];
+            }
+#pragma unroll
+            for (int u = 0; u < KPR_BATCH; ++u) {
+              if (over) break;                          // wave-uniform
+              const uint32_t e = ev[u], j = e >> 8;
+              const bool ok = e != LOG_INVALID && j != i && j != s && r - log_round(e, r) < SHARE_AGE &&
+                              ((wv4[u] >> (j & 31)) & 1u) && bv[u] == enc(log_round(e, r), r);
+              take(ok, j);
+            }
           }
           if (!complete && !over) {                   // rare: rescan the row itself
             total = 0;
