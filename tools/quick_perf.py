@@ -5,7 +5,9 @@ from kaboodle_amd._ffi import SimConfig, KB_INIT_CONVERGED
 import kaboodle_amd
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 R = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-cfg = SimConfig(capacity=N + N // 4, initial_nodes=N, init_mode=KB_INIT_CONVERGED, loss=0.01, churn=0.001, seed=1)
+# the bench's sizing (bench.rank_config): capacity = peers + churn reserve for the run
+cfg = SimConfig(capacity=N + max(4096, int(N * 0.001 * (R + 10) * 1.5)), initial_nodes=N, init_mode=KB_INIT_CONVERGED,
+                loss=0.01, churn=0.001, seed=1)
 t = time.time(); m = kaboodle_amd.Mesh(cfg); print("create", round(time.time() - t, 2), flush=True)
 m.step(2)
 m.reset_kernel_time()
