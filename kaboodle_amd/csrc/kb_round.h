@@ -412,8 +412,114 @@ __device__ __attribute__((always_inline)) inline uint32_t block_prefix(const uin
   return tot;
 }
 
+// The common case of a large mesh — every response of the node is truncated (sampled), at most
+// RW_JCAP new joiners — takes one WAVE per responder instead of a workgroup: four responders per
+// workgroup at once, each with its own LDS slice (bitset, block prefix, joiners, suffix minima), and
+// only wave-level synchronisation.  Same arithmetic as k_resp_node's sampled path.
+constexpr uint32_t RW_JCAP = 128;
+__host__ __device__ inline uint32_t rwave_words(uint32_t NW, uint32_t NB) {
+  return (NW + NB + 1 + 2 * RW_JCAP + 1 + 3) & ~3u;
+}
+__device__ inline bool resp_by_wave(const Dev& d, uint32_t i, uint32_t nnew, bool on) {
+  return on && d.uniform && nnew <= RW_JCAP && d.n[i] - nnew > d.capj;
+}
+__global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint32_t* nodes, const uint32_t* nnodes_p,
+                                                   OutBuf ob, int32_t r) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t rw_lds[];
+  const uint32_t NW = d.NWR, NB = d.W / 256;
+  const uint32_t wv = threadIdx.x >> 6, l = lane();
+  uint32_t* B = rw_lds + (size_t)wv * rwave_words(NW, NB);   // row membership after the Join group [NW]
+  uint32_t* BP = B + NW;                                        // block prefix of B                 [NB + 1]
+  uint32_t* J = BP + NB + 1;                                    // this receiver's new joiners       [RW_JCAP]
+  uint32_t* JM = J + RW_JCAP;                                   // suffix minima of J                [RW_JCAP + 1]
+  const uint32_t nnodes = *nnodes_p;
+  for (uint32_t it = blockIdx.x * 4 + wv; it < nnodes; it += gridDim.x * 4) {
+    const uint32_t i = nodes[it];
+    const unsigned long long* nm = pb.newmask + (size_t)i * pb.JW;
+    const unsigned long long* rm = pb.respmask + (size_t)i * pb.JW;
+    uint32_t nnew = 0;
+    for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
+    if (!resp_by_wave(d, i, nnew, true)) continue;          // wave-uniform: k_resp_node serves it
+    stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(bits_of(d, i)), NW / 4, l, 64);
+    wait_lds();
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
+    uint32_t bc = 0;
+    for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) c += __popc(B[k * 8 + w]);
+      BP[k] = c; bc += c;
+    }
+    uint32_t ex = wave_excl(bc);
+    const uint32_t nB = wave_sum(bc);
+    for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) { const uint32_t c = BP[k]; BP[k] = ex; ex += c; }
+    if (l == 0) BP[NB] = nB;
+    for (uint32_t e = l; e < pb.nj; e += 64) {              // new joiners in list order
+      if (!newbit(nm, e)) continue;
+      uint32_t pos = __popcll(nm[e >> 6] & ((1ull << (e & 63)) - 1ull));
+      for (uint32_t w2 = 0; w2 < (e >> 6); ++w2) pos += __popcll(nm[w2]);
+      J[pos] = pb.bjoin[e].sender;
+    }
+    wait_lds();
+    __builtin_amdgcn_wave_barrier();
+    {                                                       // suffix minima of J[0..nnew), nnew <= 128
+      uint32_t v0 = l < nnew ? J[l] : 0xFFFFFFFFu, v1 = l + 64 < nnew ? J[l + 64] : 0xFFFFFFFFu;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u0 = __shfl_down(v0, o, 64), u1 = __shfl_down(v1, o, 64);
+        if (l + o < 64) { v0 = u0 < v0 ? u0 : v0; v1 = u1 < v1 ? u1 : v1; }
+      }
+      const uint32_t m1 = bcast(v1, 0);
+      v0 = m1 < v0 ? m1 : v0;
+      if (l < nnew) JM[l] = v0;
+      if (l + 64 < nnew) JM[l + 64] = v1;
+      if (l == 0) JM[nnew] = 0xFFFFFFFFu;
+    }
+    wait_lds();
+    __builtin_amdgcn_wave_barrier();
+    uint32_t poff = ob.poff[i], q = 0, ins_before = 0;
+    for (uint32_t wj = 0; wj < pb.JW; ++wj) {
+      unsigned long long rmw = rm[wj];
+      const unsigned long long nmw = nm[wj];
+      while (rmw) {
+        const uint32_t bit = (uint32_t)(__ffsll((long long)rmw) - 1);
+        const uint32_t K = wj * 64 + bit;
+        rmw &= rmw - 1;
+        const uint32_t upto = ins_before + __popcll(nmw & ((2ull << bit) - 1ull));   // new joiners <= K
+        const uint32_t expect = pb.nbase[i] + upto;
+        const uint32_t a = pb.bjoin[K].sender;
+        const uint32_t nk = nB - (nnew - upto), cap = d.capj;
+        uint32_t* pay = ob.pay + poff;
+        const U4 key = philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1);
+        for (uint32_t k = l; k < cap; k += 64) {
+          const uint32_t y = prp_walk(k, nk, key);
+          uint32_t e = 0, x;
+          while (true) {                                  // step over the joiners inserted after K
+            x = bm_select(B, BP, NB, y + e);
+            uint32_t c = 0;
+            if (x >= JM[upto]) for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= x;
+            if (c == e) break;
+            e = c;
+          }
+          pay[k] = x;
+        }
+        if (l == 0) {
+          Msg m; m.dest = a; m.sender = i; m.seq = q; m.kind = K_KP; m.a = cap; m.fp = 0; m.n = 0; m.off = poff;
+          ob.msgs[ob.off[i] + q] = m;
+          if (nk != expect) set_err(d, DERR_RESP);
+        }
+        poff += cap; q++;
+      }
+      ins_before += __popcll(nmw);
+    }
+    wait_lds();                                           // the LDS slice is reused by the next responder
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint32_t* nodes, const uint32_t* nnodes_p,
-                                                   OutBuf ob, int32_t r, uint32_t* gscratch) {
+                                                   OutBuf ob, int32_t r, uint32_t* gscratch, bool wave_on) {
   extern __shared__ uint32_t lds_dyn[];
   const uint32_t NW = d.NWR, NB = d.W / 256;
   // rows wider than RESP_LDS_W keep their bitsets in a per-workgroup slice of global scratch
@@ -429,13 +535,14 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
   const uint32_t nnodes = *nnodes_p;
   for (uint32_t it = blockIdx.x; it < nnodes; it += gridDim.x) {
     const uint32_t i = nodes[it];
-    stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(bits_of(d, i)), NW / 4, t, T);
-    __syncthreads();
-    const uint32_t nB = block_prefix(B, BP, NB, s_red);
     const unsigned long long* nm = pb.newmask + (size_t)i * pb.JW;
     const unsigned long long* rm = pb.respmask + (size_t)i * pb.JW;
     uint32_t nnew = 0;
     for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
+    if (resp_by_wave(d, i, nnew, wave_on)) continue;        // uniform: served by k_resp_wave
+    stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(bits_of(d, i)), NW / 4, t, T);
+    __syncthreads();
+    const uint32_t nB = block_prefix(B, BP, NB, s_red);
     const bool jl = nnew <= RESP_JCAP;
     if (jl) {                            // new joiners in list order (parallel), then suffix minima
       for (uint32_t e = t; e < pb.nj; e += T) {
@@ -445,7 +552,19 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
         J[pos] = pb.bjoin[e].sender;
       }
       __syncthreads();
-      if (t == 0) {
+      if (nnew <= T) {                     // suffix minima by a block scan (one joiner per thread)
+        uint32_t v = t < nnew ? J[t] : 0xFFFFFFFFu;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t u = __shfl_down(v, o, 64);
+          if (lane() + o < 64) v = u < v ? u : v;
+        }
+        if (lane() == 0) s_red[t >> 6] = v;
+        __syncthreads();
+        for (uint32_t w = (t >> 6) + 1; w < T / 64; ++w) v = s_red[w] < v ? s_red[w] : v;
+        if (t < nnew) JM[t] = v;
+        if (t == 0) JM[nnew] = 0xFFFFFFFFu;
+      } else if (t == 0) {
         uint32_t m = 0xFFFFFFFFu;
         JM[nnew] = m;
         for (uint32_t q3 = nnew; q3 > 0; --q3) { m = J[q3 - 1] < m ? J[q3 - 1] : m; JM[q3 - 1] = m; }

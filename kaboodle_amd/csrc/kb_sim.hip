@@ -737,7 +737,13 @@ static int step_round(kb_sim* s) {
         scratch = s->resp_scratch;
         lds = 0;
       }
-      k_resp_node<<<grid, 256, lds, st>>>(d, pb, s->resp_nodes, s->scan_tot + 4, o0, r, scratch);
+      // a wave per responder where its LDS slice fits (4 responders per 64 KB workgroup), else a workgroup
+      const size_t wlds = 16ull * rwave_words(d.NWR, s->W / 256);
+      const bool wave_on = wlds <= 65536;
+      if (wave_on)
+        k_resp_wave<<<std::min<uint32_t>((resp_nodes + 3) / 4, 4096), 256, wlds, st>>>(d, pb, s->resp_nodes,
+                                                                                     s->scan_tot + 4, o0, r);
+      k_resp_node<<<grid, 256, lds, st>>>(d, pb, s->resp_nodes, s->scan_tot + 4, o0, r, scratch, wave_on);
     }
   }
   // 3. tick
@@ -802,7 +808,7 @@ static int step_round(kb_sim* s) {
     HIPCHK(hipMemsetAsync(L(s, nb.cnt), 0, 4ull * R, st));
     if (!s->xf) k_scatter<<<gnode, tb, 0, st>>>(d, ob, s->wc);
     else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
-    k_kp_group<false><<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r);
+    k_kp_small<<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r);
     k_kp_group<true><<<std::min<uint32_t>((R + 1023) / 1024, 512), 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
     k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc);
     if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 12, st));

@@ -378,6 +378,74 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
   }
 }
 
+// The groups under KP_BIG ids (KnownPeersRequest replies, small Join lists): a wave per destination,
+// in place on the row's bitset, the same arms-then-prologues order as k_kp_group.
+__global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, int32_t r) {
+  __shared__ uint32_t s_list[256], s_nl;
+  const uint32_t t = threadIdx.x, wv = t >> 6, l = lane();
+  const uint32_t nact = d.ctr[C_ACTIVE];
+  const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
+  for (uint32_t c0 = 0; c0 < nact; c0 += gridDim.x * 256) {
+    const uint32_t it = c0 + t * gridDim.x + blockIdx.x;   // interleaved over the workgroups
+    if (t == 0) s_nl = 0;
+    __syncthreads();
+    if (it < nact) {
+      const uint32_t x = wc.active[it];
+      if (wc.kcnt[x] && wc.kpay[x] < KP_BIG) s_list[atomicAdd(&s_nl, 1u)] = x;
+    }
+    __syncthreads();
+    const uint32_t nl = s_nl;
+    for (uint32_t li = wv; li < nl; li += 4) {
+      const uint32_t i = s_list[li], nk = wc.kcnt[i], k0 = wc.koff[i];
+      uint32_t* B = bits_of(d, i);
+      uint8_t* rw = row_of(d, i);
+      unsigned long long segs = 0;
+      uint32_t added = 0;
+      for (uint32_t q = 0; q < nk; ++q) {                  // arms
+        const Msg m = ib.msgs[wc.kin[k0 + q]];
+        for (uint32_t e = l; e < m.a; e += 64) {
+          const uint32_t p = ib.pay[m.off + e], bit = 1u << (p & 31);
+          if (__hip_atomic_load(&B[p >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit) continue;
+          if (!(atomicOr(&B[p >> 5], bit) & bit)) { rw[p] = old; segs |= seg_bit(d, p); added++; }
+        }
+      }
+      wave_mem_sync();
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t q = l; q < nk; q += 64) {             // prologues (as k_kp_group)
+        const uint32_t s = ib.msgs[wc.kin[k0 + q]].sender;
+        uint32_t* wp = reinterpret_cast<uint32_t*>(rw + (s & ~3u));
+        const uint32_t sh = 8 * (s & 3u);
+        uint32_t ow = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), prevb;
+        while (true) {
+          prevb = (ow >> sh) & 0xFFu;
+          if (prevb == now) break;
+          const uint32_t res = atomicCAS(wp, ow, (ow & ~(0xFFu << sh)) | ((uint32_t)now << sh));
+          if (res == ow) break;
+          ow = res;
+        }
+        if (prevb != now) d.flog[(size_t)i * LOGCAP + (atomicAdd(&d.flog_n[i], 1u) & (LOGCAP - 1))] = log_entry(s, r);
+        const uint32_t bit = 1u << (s & 31);
+        if (!(atomicOr(&B[s >> 5], bit) & bit)) { segs |= seg_bit(d, s); added++; }
+      }
+      segs = (unsigned long long)wave_or((uint32_t)segs) | ((unsigned long long)wave_or((uint32_t)(segs >> 32)) << 32);
+      added = wave_sum(added);
+      __builtin_amdgcn_s_waitcnt(0);
+      __builtin_amdgcn_wave_barrier();
+      if (l < SLOTS) {                                   // a prologue overwrote a WaitingFor* entry to Known
+        Susp* sl = d.susp + (size_t)i * SLOTS + l;
+        if (sl->kind) {
+          const uint32_t pw = __hip_atomic_load(reinterpret_cast<uint32_t*>(rw + (sl->peer & ~3u)), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+          if (((pw >> (8 * (sl->peer & 3u))) & 0xFFu) != ST_SUSPECT) sl->kind = 0;
+        }
+      }
+      if (l == 0 && (added || segs)) { d.n[i] += added; mark(d, i, segs); }
+    }
+    __syncthreads();                                       // s_list reused by the next chunk
+  }
+}
+
 // ---- inboxes longer than one wave: sorted into canonical (sender, seq) order = ascending outbox
 // index, one workgroup per node, bitonic in LDS (up to SORT_MAX entries; longer ones keep the
 // selection path of k_proc)
