@@ -240,6 +240,7 @@ struct kb_sim {
   unsigned long long* newmask_base; unsigned long long* respmask_base;
   uint32_t* nresp; uint32_t* paysum; uint32_t* nbase; uint32_t* resp_off;
   uint32_t* resp_nodes; uint32_t* bf_gid; uint8_t* bf_dep;
+  uint32_t* slow;                      // the nodes of a wave k_proc_fast leaves to k_proc
   uint32_t* resp_scratch; size_t resp_scratch_words;
   SweepOut so;
   Event* d_events; uint32_t events_cap;
@@ -444,7 +445,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   AR(s->bs.join, 1); AR(s->bs.nfail, 1); AR(s->bs.fail, SLOTS); AR(s->join_off, 1); AR(s->fail_off, 1);
   A(s->scan_tot, 32); A(s->scan_tiles, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
   AR(s->nresp, 1); AR(s->paysum, 1); AR(s->nbase, 1); AR(s->resp_off, 1);
-  A(s->resp_nodes, R); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS);
+  A(s->resp_nodes, R); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS); A(s->slow, R);
   AR(s->so.part, (size_t)S * 10);
   if (xf) {
     XState& x = s->xs;
@@ -812,7 +813,8 @@ static int step_round(kb_sim* s) {
     k_kp_group<true><<<std::min<uint32_t>((R + 1023) / 1024, 512), 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
     k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc);
     if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 12, st));
-    k_proc<<<4096, 256, 0, st>>>(d, ib, nb, s->wc, r);
+    k_proc_fast<<<gnode, tb, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
+    k_proc<<<4096, 256, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
     if (s->debug_waves) {
       uint32_t dbg[3];
       HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 12, hipMemcpyDeviceToHost, st));

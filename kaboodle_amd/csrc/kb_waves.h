@@ -21,7 +21,7 @@ __global__ void k_wave_clear(Dev d, WaveCtl wc) {
     wc.cnt1[i] = 0; wc.bnd[i] = 0; wc.bpay[i] = 0; wc.cursor[i] = 0;
     wc.kcnt[i] = 0; wc.kpay[i] = 0; wc.kcur[i] = 0;
   }
-  if (blockIdx.x == 0 && threadIdx.x < 3) d.ctr[C_KP + threadIdx.x] = 0;     // C_KP, C_TOUCH, C_ACTIVE
+  if (blockIdx.x == 0 && threadIdx.x < 3) d.ctr[C_KP + threadIdx.x] = 0;     // C_KP, C_SLOW, C_ACTIVE
 }
 
 // messages a handler may emit per delivered message (next-wave outbox reservation)
@@ -493,12 +493,117 @@ __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc) {
 }
 
 // ---- the per-node in-order program for Ping / PingRequest / Ack / KnownPeersRequest ---------------
-__global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r) {
+// ---- fast lane of the in-order handlers: a THREAD per node --------------------------------------
+// The common inbox — at most FAST_MAX Ping / PingRequest / Ack envelopes, every sender already a
+// member, the node's fingerprint current — changes no membership, so no fingerprint work: the
+// handlers reduce to stamp/log/slot updates and emissions.  Such nodes are handled here, one per
+// thread, in canonical (sender, seq) order; every other node with in-order deliveries goes to the
+// `slow` list for k_proc (same semantics: prologue :406-415, Ping :513-532, PingRequest :533-545,
+// Ack :418-447, maybe_sync :707-740).
+constexpr uint32_t FAST_MAX = 8;
+__device__ __attribute__((always_inline)) inline void emit_t(const OutBuf& ob, const Dev& d, uint32_t i, uint32_t& oseq,
+                                                             uint32_t dest, uint32_t kind, uint32_t a, uint32_t fp,
+                                                             uint32_t n) {
+  if (oseq >= ob.cap[i] || ob.off[i] + oseq >= ob.msg_cap) set_err(d, DERR_OUTBOX);
+  else ob.msgs[ob.off[i] + oseq] = Msg{dest, i, oseq, kind, a, fp, n, 0};
+  oseq++;
+}
+__global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r, uint32_t* slow) {
+  const uint32_t nact = d.ctr[C_ACTIVE];
+  const uint32_t it = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint8_t now = enc(r, r);
+  unsigned long long curovf = 0;
+  bool to_slow = false;
+  uint32_t i = 0;
+  if (it < nact) {
+    i = wc.active[it];
+    const uint32_t icnt = wc.cnt1[i];
+    bool fast = icnt && icnt <= FAST_MAX && !d.dirty[i];
+    uint32_t g[FAST_MAX];
+    if (fast) {
+      const uint32_t base = wc.in_off[i];
+#pragma unroll
+      for (uint32_t k = 0; k < FAST_MAX; ++k) g[k] = k < icnt ? wc.inbox[base + k] : 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t a = 1; a < FAST_MAX; ++a)        // canonical order = ascending record index
+#pragma unroll
+        for (uint32_t b = a; b > 0; --b)
+          if (g[b - 1] > g[b]) { const uint32_t x = g[b]; g[b] = g[b - 1]; g[b - 1] = x; }
+      const uint32_t* bw = bits_of(d, i);
+#pragma unroll
+      for (uint32_t k = 0; k < FAST_MAX; ++k) {
+        if (k >= icnt) break;
+        const Msg m = ib.msgs[g[k]];
+        if (m.kind == K_KPR || !((bw[m.sender >> 5] >> (m.sender & 31)) & 1u)) fast = false;
+      }
+    }
+    to_slow = icnt && !fast;
+    if (fast) {
+      const uint32_t n = d.n[i], fp = d.fp[i];
+      uint32_t fn = d.flog_n[i], oseq = 0, last_sender = 0xFFFFFFFFu;
+      uint8_t* rw = row_of(d, i);
+      Susp* sl = d.susp + (size_t)i * SLOTS;
+      Cur* cu = d.cur + (size_t)i * CSLOTS;
+#pragma unroll
+      for (uint32_t k = 0; k < FAST_MAX; ++k) {
+        if (k >= icnt) break;
+        const Msg m = ib.msgs[g[k]];
+        const uint32_t s = m.sender;
+        if (s != last_sender) {                        // prologue: insert(sender, Known(now))
+          const uint8_t b = rw[s];
+          if (b == ST_SUSPECT)
+            for (int j = 0; j < SLOTS; ++j) if (sl[j].kind && sl[j].peer == s) sl[j].kind = 0;
+          if (b != now) { rw[s] = now; d.flog[(size_t)i * LOGCAP + (fn & (LOGCAP - 1))] = log_entry(s, r); fn++; }
+          last_sender = s;
+        }
+        if (m.kind == K_PING) {
+          emit_t(ob, d, i, oseq, s, K_ACK, i, fp, n);
+        } else if (m.kind == K_PINGREQ) {
+          int e = -1;
+          for (int j = 0; j < CSLOTS && e < 0; ++j) if (cu[j].used && cu[j].peer == m.a) e = j;
+          if (e < 0) {
+            for (int j = 0; j < CSLOTS && e < 0; ++j) if (!cu[j].used) e = j;
+            if (e >= 0) { cu[e].used = 1; cu[e].peer = m.a; cu[e].nobs = 0; }
+          }
+          if (e < 0) curovf++;
+          else {
+            const uint32_t nobs = cu[e].nobs;
+            bool dup = false;
+            for (uint32_t q = 0; q < nobs; ++q) dup |= cu[e].obs[q] == s;
+            if (!dup) { if (nobs == NOBS) curovf++; else { cu[e].obs[nobs] = s; cu[e].nobs = nobs + 1; } }
+          }
+          emit_t(ob, d, i, oseq, m.a, K_PING, 0, 0, 0);
+        } else if (m.kind == K_ACK) {
+          int e = -1;
+          for (int j = 0; j < CSLOTS && e < 0; ++j) if (cu[j].used && cu[j].peer == m.a) e = j;
+          if (e >= 0) {
+            const uint32_t nobs = cu[e].nobs;
+            for (uint32_t q = 0; q < nobs; ++q) emit_t(ob, d, i, oseq, cu[e].obs[q], K_ACK, m.a, m.fp, m.n);
+            cu[e].used = 0;
+          }
+          if (fp != m.fp && !(n > m.n)) emit_t(ob, d, i, oseq, m.a, K_KPR, 0, fp, n);
+        }
+      }
+      ob.cnt[i] = oseq;
+      d.flog_n[i] = fn;
+    }
+  }
+  const unsigned long long sm = __ballot(to_slow);  // the rest goes to k_proc
+  if (sm) {
+    uint32_t base = 0;
+    if (lane() == (uint32_t)(__ffsll((long long)sm) - 1)) base = atomicAdd(&d.ctr[C_SLOW], (uint32_t)__popcll(sm));
+    base = bcast(base, __ffsll((long long)sm) - 1);
+    if (to_slow) slow[base + __popcll(sm & ((1ull << lane()) - 1ull))] = i;
+  }
+  stat_add(d, S_CUROVF, curovf);
+}
+
+__global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r, const uint32_t* list) {
   __shared__ uint32_t ztab[ZT * 128];
   __shared__ Susp s_susp[4][SLOTS];
   __shared__ Cur s_cur[4][CSLOTS];
   __shared__ uint2 s_suf[4][NSEG + 1];
-  const uint32_t nact = d.ctr[C_ACTIVE];
+  const uint32_t nact = d.ctr[C_SLOW];                // the nodes k_proc_fast left (list)
   if (blockIdx.x * 4 >= nact) return;                 // no node for this workgroup (before the table load)
   load_ztab(d, ztab);
   const uint32_t wv = threadIdx.x >> 6;
@@ -507,8 +612,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
   const uint8_t fresh_thr = enc(r - (SHARE_AGE - 1), r);
   unsigned long long w_over = 0, w_curovf = 0;      // flushed once per wave (see k_phaseB)
   for (uint32_t it = blockIdx.x * 4 + wv; it < nact; it += gridDim.x * 4) {
-    const uint32_t i = wc.active[it];
-    if (!wc.cnt1[i]) continue;                        // KnownPeers deliveries only (k_kp_group)
+    const uint32_t i = list[it];
     uint8_t* rw = row_of(d, i);
     const uint32_t* bw = bits_of(d, i);
     uint32_t n = d.n[i], fp = d.fp[i], oseq = 0, pay_used = 0, fn = d.flog_n[i];
