@@ -101,6 +101,11 @@ __device__ inline uint32_t wave_min(uint32_t v) {
   for (int o = 32; o > 0; o >>= 1) { uint32_t t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
   return v;
 }
+__device__ inline uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { uint32_t t = __shfl_xor(v, o, 64); v = t > v ? t : v; }
+  return v;
+}
 __device__ inline uint32_t wave_or(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);

@@ -372,15 +372,43 @@ __device__ inline uint32_t bm_rank(const uint32_t* S, const uint32_t* SP, uint32
   for (uint32_t k = blk * 8; k < w; ++k) r += __popc(S[k]);
   return r + __popc(S[w] & ((1u << (id & 31)) - 1u));
 }
-__device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint32_t nblk, uint32_t b) {  // b-th member
+// position of the rem-th (0-based) set bit of x: a five-step popcount descent, no loop
+__device__ inline uint32_t select_in_word(uint32_t x, uint32_t rem) {
+  uint32_t pos = 0, c;
+  c = __popc(x & 0xFFFFu); if (rem >= c) { rem -= c; x >>= 16; pos += 16; }
+  c = __popc(x & 0xFFu);   if (rem >= c) { rem -= c; x >>= 8;  pos += 8; }
+  c = __popc(x & 0xFu);    if (rem >= c) { rem -= c; x >>= 4;  pos += 4; }
+  c = __popc(x & 0x3u);    if (rem >= c) { rem -= c; x >>= 2;  pos += 2; }
+  if (rem >= (x & 1u)) pos += 1;
+  return pos;
+}
+// b-th member (0-based) of bitset S with 256-id block prefix SP[0..nblk] (SP[nblk] = total > b).
+// The block is bracketed around the density guess b * nbu / total (nbu = blocks up to the last
+// non-empty one; rows are dense below it), falling back to the whole range when the guess misses;
+// the word and bit come from one 32-byte read of the block.  Any nbu gives the same answer.
+__device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint32_t nblk, uint32_t nbu, uint32_t b) {
   uint32_t lo = 0, hi = nblk;
+  {
+    uint32_t g = (uint32_t)(((uint64_t)b * nbu) / SP[nblk]);
+    g = g < nblk ? g : nblk - 1;
+    const uint32_t l2 = g >= 2 ? g - 2 : 0, h2 = g + 3 < nblk ? g + 3 : nblk;
+    if (SP[l2] <= b && b < SP[h2]) { lo = l2; hi = h2; }
+  }
   while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (SP[mid] <= b) lo = mid; else hi = mid; }
   uint32_t rem = b - SP[lo];
-  uint32_t w = lo * 8;
-  for (;; ++w) { const uint32_t c = __popc(S[w]); if (rem < c) break; rem -= c; }
-  uint32_t x = S[w];
-  for (uint32_t t = 0; t < rem; ++t) x &= x - 1;
-  return w * 32 + (__ffs(x) - 1);
+  const uint4 q0 = *reinterpret_cast<const uint4*>(S + lo * 8), q1 = *reinterpret_cast<const uint4*>(S + lo * 8 + 4);
+  const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+  uint32_t wi = 7, x = w[7];
+  bool found = false;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t c = __popc(w[k]);
+    if (!found) {
+      if (rem < c) { found = true; wi = k; x = w[k]; }
+      else rem -= c;
+    }
+  }
+  return (lo * 8 + wi) * 32 + select_in_word(x, rem);
 }
 constexpr uint32_t RESP_LDS_W = 131072;   // rows up to this many ids keep their bitsets in LDS
 constexpr uint32_t RESP_JCAP = 1024;      // new joiners of one receiver kept in LDS (more: read from HBM)
@@ -444,15 +472,17 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     wait_lds();
     __builtin_amdgcn_wave_barrier();
     const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
-    uint32_t bc = 0;
+    uint32_t bc = 0, last = 0;
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) {
       uint32_t c = 0;
 #pragma unroll
       for (int w = 0; w < 8; ++w) c += __popc(B[k * 8 + w]);
       BP[k] = c; bc += c;
+      if (c) last = k + 1;
     }
     uint32_t ex = wave_excl(bc);
     const uint32_t nB = wave_sum(bc);
+    const uint32_t nbu = wave_max(last);
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) { const uint32_t c = BP[k]; BP[k] = ex; ex += c; }
     if (l == 0) BP[NB] = nB;
     for (uint32_t e = l; e < pb.nj; e += 64) {              // new joiners in list order
@@ -496,7 +526,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
           const uint32_t y = prp_walk(k, nk, key);
           uint32_t e = 0, x;
           while (true) {                                  // step over the joiners inserted after K
-            x = bm_select(B, BP, NB, y + e);
+            x = bm_select(B, BP, NB, nbu, y + e);
             uint32_t c = 0;
             if (x >= JM[upto]) for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= x;
             if (c == e) break;
@@ -595,7 +625,7 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
             const uint32_t y = prp_walk(k, nk, key);
             uint32_t e = 0, x;
             while (true) {
-              x = bm_select(B, BP, NB, y + e);
+              x = bm_select(B, BP, NB, NB, y + e);
               uint32_t c = 0;
               if (jl) {                                  // later joiners = J[upto..nnew)
                 if (x >= JM[upto]) for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= x;

@@ -215,13 +215,15 @@ __device__ __attribute__((always_inline)) inline void step_proc(const Dev& d, co
     }
   }
   if (!loaded) return;
-  const uint32_t TA = thr5(A), TB = thr5(B);
-  const bool needA = TA > ST_ANCIENT && col < p, needB = TB > ST_ANCIENT && col + 128 > p;
-  if (!(needA || needB)) return;
-  const uint32_t T = (needA && TA > (needB ? TB : 0u)) ? TA : TB;   // the larger relevant threshold
   const uint32_t C = d.C;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
+    // thresholds are re-read per 16-id group: once a part holds five ancient stamps (typically
+    // within the first group of a step) the rest of the step is rejected by the packed filter
+    const uint32_t TA = thr5(A), TB = thr5(B);
+    const bool needA = TA > ST_ANCIENT && col < p, needB = TB > ST_ANCIENT && col + 128 > p;
+    if (!(needA || needB)) break;
+    const uint32_t T = (needA && TA > (needB ? TB : 0u)) ? TA : TB;   // the larger relevant threshold
     if (min_stamp16(s.v[q]) >= T - 2) continue;
     const uint32_t mwq = (q >> 1) == 0 ? s.mb.x : ((q >> 1) == 1 ? s.mb.y : ((q >> 1) == 2 ? s.mb.z : s.mb.w));
     uint32_t cm = (nzmask4(s.v[q].x & 0xFEFEFEFEu) | (nzmask4(s.v[q].y & 0xFEFEFEFEu) << 4) |
