@@ -256,15 +256,39 @@ __device__ __attribute__((always_inline)) inline uint32_t wave_fp(const Dev& d, 
   return finish_fp(d, raw, cnt);
 }
 // fingerprint of row i from its checkpoints by one thread (checkpoints must be fresh)
+// (16 checkpoints and their Z^cnt per batch: the loads of a batch are in flight together)
 __device__ inline uint32_t thread_fp(const Dev& d, uint32_t i) {
   uint32_t raw = 0, cnt = 0;
-  for (int k = 0; k < NSEG; ++k) {
-    const uint2 sp = d.segp[(size_t)i * NSEG + k];
-    if (sp.y) { raw = comb(d, raw, sp.x, sp.y); cnt += sp.y; }
+  const uint4* sp4 = reinterpret_cast<const uint4*>(d.segp + (size_t)i * NSEG);   // two checkpoints per 16 B
+  for (int k0 = 0; k0 < NSEG; k0 += 16) {
+    uint4 q[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) q[t] = sp4[k0 / 2 + t];
+    uint32_t z[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const uint32_t c = (t & 1) ? q[t >> 1].w : q[t >> 1].y;
+      z[t] = c ? (d.uniform ? d.zpow[c] : xpow8_dev(c)) : 0u;
+    }
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const uint32_t x = (t & 1) ? q[t >> 1].z : q[t >> 1].x, c = (t & 1) ? q[t >> 1].w : q[t >> 1].y;
+      if (c) { raw = multmodp(z[t], raw) ^ x; cnt += c; }
+    }
   }
   return finish_fp(d, raw, cnt);
 }
 
+// position of the rem-th (0-based) set bit of x: a five-step popcount descent, no loop
+__device__ inline uint32_t select_in_word(uint32_t x, uint32_t rem) {
+  uint32_t pos = 0, c;
+  c = __popc(x & 0xFFFFu); if (rem >= c) { rem -= c; x >>= 16; pos += 16; }
+  c = __popc(x & 0xFFu);   if (rem >= c) { rem -= c; x >>= 8;  pos += 8; }
+  c = __popc(x & 0xFu);    if (rem >= c) { rem -= c; x >>= 4;  pos += 4; }
+  c = __popc(x & 0x3u);    if (rem >= c) { rem -= c; x >>= 2;  pos += 2; }
+  if (rem >= (x & 1u)) pos += 1;
+  return pos;
+}
 // 4-bit "byte != 0" mask of a little-endian dword (SWAR)
 __device__ inline uint32_t nzmask4(uint32_t x) {
   const uint32_t y = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;

@@ -372,16 +372,6 @@ __device__ inline uint32_t bm_rank(const uint32_t* S, const uint32_t* SP, uint32
   for (uint32_t k = blk * 8; k < w; ++k) r += __popc(S[k]);
   return r + __popc(S[w] & ((1u << (id & 31)) - 1u));
 }
-// position of the rem-th (0-based) set bit of x: a five-step popcount descent, no loop
-__device__ inline uint32_t select_in_word(uint32_t x, uint32_t rem) {
-  uint32_t pos = 0, c;
-  c = __popc(x & 0xFFFFu); if (rem >= c) { rem -= c; x >>= 16; pos += 16; }
-  c = __popc(x & 0xFFu);   if (rem >= c) { rem -= c; x >>= 8;  pos += 8; }
-  c = __popc(x & 0xFu);    if (rem >= c) { rem -= c; x >>= 4;  pos += 4; }
-  c = __popc(x & 0x3u);    if (rem >= c) { rem -= c; x >>= 2;  pos += 2; }
-  if (rem >= (x & 1u)) pos += 1;
-  return pos;
-}
 // b-th member (0-based) of bitset S with 256-id block prefix SP[0..nblk] (SP[nblk] = total > b).
 // The block is bracketed around the density guess b * nbu / total (nbu = blocks up to the last
 // non-empty one; rows are dense below it), falling back to the whole range when the guess misses;

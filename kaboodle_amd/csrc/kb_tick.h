@@ -18,30 +18,9 @@ __device__ inline uint32_t cand16(const Dev& d, const uint8_t* rw, const uint32_
   if (i >= j0 && i < j0 + 16) c &= ~(1u << (i - j0));
   return c;
 }
-// rank -> id over the candidates of row i; lane l owns ids [lo, hi) holding candidate ranks
-// [lane_off, lane_off + lane_cnt).
-__device__ __attribute__((always_inline)) inline uint32_t select_known(const Dev& d, const uint8_t* rw, const uint32_t* bw, uint32_t i, uint32_t rank,
-                                 uint32_t lane_off, uint32_t lane_cnt, uint32_t lo, uint32_t hi) {
-  uint32_t found = 0xFFFFFFFFu;
-  if (rank >= lane_off && rank < lane_off + lane_cnt) {
-    uint32_t c = lane_off;
-    for (uint32_t j0 = lo; j0 < hi; j0 += 16) {
-      uint32_t m = cand16(d, rw, bw, i, j0);
-      const uint32_t pc = __popc(m);
-      if (rank < c + pc) {
-        for (uint32_t t = c; t < rank; ++t) m &= m - 1;
-        found = j0 + (__ffs(m) - 1);
-        break;
-      }
-      c += pc;
-    }
-  }
-  return wave_min(found);
-}
-
 // ---- A1 maybe_broadcast_join (:228-251) + A2 handle_suspected_peers (:558-653), one wave per node
 __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots bs, int32_t r) {
-  __shared__ uint32_t s_pick_rank[4][SLOTS * 3], s_pick_peer[4][SLOTS * 3];
+  __shared__ uint32_t s_pick_rank[4][SLOTS * 3], s_pick_peer[4][SLOTS * 3], s_pick_id[4][SLOTS * 3];
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t i = d.lo + blockIdx.x * 4 + wv;
   const uint32_t l = lane();
@@ -86,7 +65,7 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
         if (c >= hi) c++;
         pk[2] = c;
       }
-      if (l == 0) for (uint32_t q = 0; q < kk; ++q) { s_pick_rank[wv][npick + q] = pk[q]; s_pick_peer[wv][npick + q] = peer; }
+      if (l == 0) for (uint32_t q = 0; q < kk; ++q) { s_pick_rank[wv][npick + q] = pk[q]; s_pick_peer[wv][npick + q] = peer; s_pick_id[wv][npick + q] = 0xFFFFFFFFu; }
       npick += kk;
       indirect[nind++] = peer;
     } else {
@@ -96,17 +75,33 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
   const uint8_t* rw = row_of(d, i);
   uint32_t oseq = ob.cnt[i];
   if (npick) {                                            // choose_multiple over the candidate list
+    // rank -> id for every pick in coalesced passes over the row: lane l takes ids [j0 + 16 l, +16)
+    // of each 1024-id pass, four passes' loads in flight; a pass resolves the picks whose rank
+    // falls in its candidate range (ranks are in address order, :571-577)
     wait_lds();
     __builtin_amdgcn_wave_barrier();
     const uint32_t* bw = bits_of(d, i);
-    const uint32_t lo = l * d.SEGW, hi = lo + d.SEGW;     // padding ids are never members
-    uint32_t cnt = 0;
-    for (uint32_t j0 = lo; j0 < hi; j0 += 16) cnt += __popc(cand16(d, rw, bw, i, j0));
-    const uint32_t off = wave_excl(cnt);
-    for (uint32_t q = 0; q < npick; ++q) {
-      const uint32_t id = select_known(d, rw, bw, i, s_pick_rank[wv][q], off, cnt, lo, hi);
-      emit_msg(ob, d, i, oseq, id, K_PINGREQ, s_pick_peer[wv][q], 0, 0, 0);
+    uint32_t maxrank = 0;
+    for (uint32_t q = 0; q < npick; ++q) maxrank = s_pick_rank[wv][q] > maxrank ? s_pick_rank[wv][q] : maxrank;
+    uint32_t base = 0;
+    for (uint32_t j0 = 0; j0 < d.W && base <= maxrank; j0 += 4096) {
+      uint32_t mk[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { const uint32_t j = j0 + 1024 * u + 16 * l; mk[u] = j < d.W ? cand16(d, rw, bw, i, j) : 0u; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t j = j0 + 1024 * u + 16 * l;
+        const uint32_t pc = __popc(mk[u]), ex = wave_excl(pc), tot = wave_sum(pc);
+        for (uint32_t q = 0; q < npick; ++q) {
+          const uint32_t rk = s_pick_rank[wv][q];
+          if (rk >= base + ex && rk < base + ex + pc) s_pick_id[wv][q] = j + select_in_word(mk[u], rk - base - ex);
+        }
+        base += tot;
+      }
     }
+    wait_lds();
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t q = 0; q < npick; ++q) emit_msg(ob, d, i, oseq, s_pick_id[wv][q], K_PINGREQ, s_pick_peer[wv][q], 0, 0, 0);
   }
   if (l == 0) {                                           // :631-652
     for (uint32_t q = 0; q < nind; ++q)
@@ -330,8 +325,13 @@ __global__ void k_tick_post(Dev d, SweepOut so, OutBuf ob, int32_t r) {
     const uint32_t C = d.C, S = so.S;
     const uint32_t p = (i + 1 == C) ? 0 : i + 1;
     uint32_t k5[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    const uint32_t* part = so.part + (size_t)i * S * 10;
-    for (uint32_t q = 0; q < S * 10; ++q) { const uint32_t x = part[q]; if (x < k5[4]) top5_insert(k5, x); }
+    const uint2* part = reinterpret_cast<const uint2*>(so.part + (size_t)i * S * 10);   // S * 10 is even
+#pragma unroll 8
+    for (uint32_t q = 0; q < S * 5; ++q) {
+      const uint2 x = part[q];
+      if (x.x < k5[4]) top5_insert(k5, x.x);
+      if (x.y < k5[4]) top5_insert(k5, x.y);
+    }
     uint32_t nc = 0;
     while (nc < 5 && k5[nc] != 0xFFFFFFFFu) nc++;
     uint32_t oseq = ob.cnt[i];
