@@ -8,11 +8,13 @@ simulated round (lifecycle, broadcasts, tick A1-A4 for every live peer, and all 
 the C ABI `kb_sim_step`; the timed region holds K steps with all state resident in HBM.
 
 value = live peers x rounds / max-over-ranks wall time, for the whole job.
-N > 1 (torchrun, one process per GPU): ONE mesh of nodes x N peers, row-sharded across the N GPUs
+N > 1 (torchrun, one process per GPU): the same `nodes`-peer mesh row-sharded across the N GPUs
 (kb_sim_create_rank): every delivery wave is an RCCL all-to-all-v of the records between
-shards and the Join/Failed lists an all-gather.  Weak scaling: every GPU holds `nodes` rows of the
-mesh; the rows get wider with N (every peer tracks every peer), so the mesh is N x larger.
---replicas runs N independent meshes instead (distinct seeds, no collective on the data path).
+shards and the Join/Failed lists an all-gather.  Strong scaling: the workload is fixed (configs[2]) and
+each GPU holds nodes/N rows.  --weak makes `nodes` the rows per GPU (a mesh of nodes x N peers, e.g.
+configs[3]: --weak --nodes 131072 on 8 GPUs = 1M peers); its rows get wider with N, because every peer
+tracks every peer, so per-GPU work grows with N.  --replicas runs N independent meshes instead
+(distinct seeds, no collective on the data path).
 
 Also reported, on the same JSON line:
   roofline      the dominant kernel (k_sweep, the per-round row sweep of ping_random_peer + fingerprint):
@@ -45,7 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--nodes", type=int, default=65536, help="peers per GPU (rows of the mesh each GPU holds)")
+    ap.add_argument("--nodes", type=int, default=65536, help="peers of the mesh (per GPU with --weak)")
+    ap.add_argument("--weak", action="store_true", help="N > 1: nodes rows per GPU, a mesh of nodes x N peers")
     ap.add_argument("--replicas", action="store_true", help="N > 1: independent meshes instead of one sharded mesh")
     ap.add_argument("--rank-mesh", action="store_true",
                     help="N = 1: run the mesh through the RCCL rank path (a 1-rank communicator) to check it")
@@ -110,7 +113,7 @@ def rank_config(a, rank: int, world: int, local: int):
     from kaboodle_amd._ffi import KB_INIT_CONVERGED, SimConfig
     total = a.warmup + a.steps
     shard = sharded(a, world)
-    peers = a.nodes * world if shard else a.nodes
+    peers = a.nodes * world if (shard and getattr(a, "weak", False)) else a.nodes
     reserve = max(4096, int(peers * a.churn * (total + 8) * 1.5))
     return SimConfig(capacity=peers + reserve, initial_nodes=peers, init_mode=KB_INIT_CONVERGED, loss=a.loss,
                      churn=a.churn, fault_end_round=total, seed=a.seed + (0 if shard else 1000 * rank),
@@ -162,7 +165,9 @@ def main() -> int:
     peers = cfg.initial_nodes
     workload = f"configs[2]: {a.nodes} peers, converged start, {a.loss:.0%} loss, {a.churn:.1%}/round churn"
     if shard:
-        workload = (f"configs[2] per GPU, one mesh: {peers} peers row-sharded {a.nodes}/GPU over {world} GPUs, "
+        weak = getattr(a, "weak", False)
+        workload = (f"{'configs[2] per GPU' if weak else 'configs[2]'}, one mesh: {peers} peers row-sharded "
+                    f"{(peers + world - 1) // world}/GPU over {world} GPUs, "
                     f"converged start, {a.loss:.0%} loss, {a.churn:.1%}/round churn")
         mesh = kaboodle_amd.Mesh(cfg, rank=rank, world=world, uid=share_uid(rank, kaboodle_amd.rccl_unique_id))
     else:
@@ -232,9 +237,11 @@ def main() -> int:
             "metric": "simulated peer-rounds/sec (whole node) + rounds to fingerprint convergence",
             "value": alive_total / dt, "unit": "peer-rounds/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": dt / a.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "scaling": "weak" if (getattr(a, "weak", False) or (world > 1 and not shard)) else "strong",
+            "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (Philox-keyed loss/churn/targets, seed-determined)",
-            "config": {"workload": workload, "peers": peers, "peers_per_gpu": a.nodes, "capacity": capacity,
+            "config": {"workload": workload, "peers": peers, "peers_per_gpu": (peers + world - 1) // world if shard else peers,
+                       "capacity": capacity,
                        "loss": a.loss, "churn": a.churn,
                        "parallelism": (f"rowshard{world}" if shard else f"replicas{world}") if world > 1 else "single",
                        "max_waves": cfg.max_waves},

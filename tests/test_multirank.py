@@ -64,13 +64,15 @@ def _shard_worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import argparse
     import bench
-    a = argparse.Namespace(nodes=96, loss=0.01, churn=0.001, seed=5, warmup=2, steps=3, replicas=False)
+    a = argparse.Namespace(nodes=96, loss=0.01, churn=0.001, seed=5, warmup=2, steps=3, replicas=False, weak=False)
     uid = bench.share_uid(rank, lambda: bytes(range(128)))
     cfg = bench.rank_config(a, rank, world, rank)
     ra = argparse.Namespace(**{**a.__dict__, "replicas": True})
     rcfg = bench.rank_config(ra, rank, world, rank)
+    wa = argparse.Namespace(**{**a.__dict__, "weak": True})
+    wcfg = bench.rank_config(wa, rank, world, rank)
     out[rank] = (uid, cfg.capacity, cfg.initial_nodes, cfg.seed, rcfg.initial_nodes, rcfg.seed,
-                 bench.sharded(a, world), bench.sharded(ra, world))
+                 bench.sharded(a, world), bench.sharded(ra, world), wcfg.initial_nodes, wcfg.seed)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -83,6 +85,7 @@ def test_sharded_setup_over_gloo():
     r0, r1 = out[0], out[1]
     assert r0[0] == r1[0] == bytes(range(128))          # rank 0's id on every rank
     assert r0[1:4] == r1[1:4]                            # one mesh: same capacity, size and seed
-    assert r0[2] == 96 * world
+    assert r0[2] == 96                                   # strong: the same mesh split over the ranks
+    assert r0[8] == r1[8] == 96 * world and r0[9] == r1[9]  # --weak: nodes rows per rank, one mesh
     assert r0[4] == r1[4] == 96 and r0[5] != r1[5]        # replicas: per-rank mesh, distinct seeds
     assert r0[6] and not r0[7]
