@@ -156,8 +156,8 @@ __device__ inline uint32_t min_stamp16(const uint4& x) {
   return mn.x < mn.y ? mn.x : mn.y;
 }
 
-// One 128-id step of one lane's row, software-pipelined: the member bits of step k+1 are loaded
-// before step k is processed.  Stamp bytes (128 B, plus the 16 B of member bits) are loaded while either
+// One 128-id step of one lane's row, software-pipelined: the loads of step k+1 are issued before
+// step k is processed.  Stamp bytes (128 B, plus the 16 B of member bits) are loaded while either
 // part's list can still change: a part is final once it holds five ancient (minimum) stamps, since
 // later ids of the part have larger rot.  Member bits are loaded alone to refold a stale checkpoint.
 struct StepIn { uint4 v[8]; uint4 mb; };
@@ -166,18 +166,15 @@ __device__ inline bool step_need(const Dev& d, const uint32_t (&A)[5], const uin
   return !(d.ablate & 2) && ((thr5(A) > ST_ANCIENT && col < p) || (thr5(B) > ST_ANCIENT && col + 128 > p));
 }
 
-// stamps of a step (when a list can still change) and its member bits (for the fold or the stamps)
-__device__ __attribute__((always_inline)) inline void load_stamps(const uint8_t* rw, uint32_t col, bool need, StepIn& s,
-                                                                  uint32_t& nbytes) {
-  if (!need) return;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) s.v[q] = *reinterpret_cast<const uint4*>(rw + col + 16 * q);
-  nbytes += 128;
-}
 template <bool FOLD>
-__device__ __attribute__((always_inline)) inline void load_bits(const uint32_t* bw, uint32_t col, bool need, uint4& mb,
-                                                                uint32_t& nbytes) {
-  if (FOLD || need) { mb = *reinterpret_cast<const uint4*>(bw + (col >> 5)); nbytes += 16; }
+__device__ __attribute__((always_inline)) inline void step_load(const uint8_t* rw, const uint32_t* bw, uint32_t col,
+                                                                bool need, StepIn& s, uint32_t& nbytes) {
+  if (need) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s.v[q] = *reinterpret_cast<const uint4*>(rw + col + 16 * q);
+    nbytes += 128;
+  }
+  if (FOLD || need) { s.mb = *reinterpret_cast<const uint4*>(bw + (col >> 5)); nbytes += 16; }
 }
 
 // A packed-u16 filter rejects 16-byte groups with no stamp below the current threshold; surviving
@@ -247,27 +244,26 @@ __device__ __attribute__((always_inline)) inline void sweep_segment(const Dev& d
                                                                     uint32_t (&B)[5], uint32_t& raw, uint32_t& cnt,
                                                                     uint32_t& nbytes) {
   if (c0 >= c1) return;
-  // Only the member bits are prefetched a step ahead; a step's stamps are issued after its fold
-  // gathers and before the next bits (vmcnt retires in order), so they never share a live range
-  // with the next step's: that keeps the kernel at 4 waves per SIMD without spills.
+  // Measured: prefetching only the bits (stamps loaded in-step) fits 4 waves/SIMD and is 3 % faster,
+  // but the extra waves evict each row's bit line between its 8 steps: HBM traffic 1.71x the
+  // algorithmic bytes instead of 1.14x.  The full prefetch is kept.
   StepIn cur;
   bool need_cur = step_need(d, A, B, p, c0);
-  load_bits<FOLD>(bw, c0, need_cur, cur.mb, nbytes);
+  step_load<FOLD>(rw, bw, c0, need_cur, cur, nbytes);
   for (uint32_t col = c0; col < c1; col += 128) {
     uint32_t hv[16];
     fold_fetch<FOLD>(d, cur, col, hv);
-    load_stamps(rw, col, need_cur, cur, nbytes);
+    StepIn nxt;
     // thresholds only fall, so the need computed before processing this step is a superset
     const bool need_nxt = col + 128 < c1 && step_need(d, A, B, p, col + 128);
-    uint4 nmb = cur.mb;
-    if (col + 128 < c1) load_bits<FOLD>(bw, col + 128, need_nxt, nmb, nbytes);
+    if (col + 128 < c1) step_load<FOLD>(rw, bw, col + 128, need_nxt, nxt, nbytes);
     step_proc<FOLD>(d, zb, cur, hv, need_cur, i, p, col, A, B, raw, cnt);
-    cur.mb = nmb;
+    cur = nxt;
     need_cur = need_nxt;
   }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void k_sweep(Dev d, SweepOut so) {
+__global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
   __shared__ uint32_t zb[ZB];
   load_zbtab(d, zb);
   // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so split s = blockIdx % S keeps each
