@@ -26,7 +26,7 @@ enum CtrIdx {
 };
 constexpr int NSEG = 64;          // fingerprint checkpoints per row
 constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
-constexpr int ZB = 9 * 1024;      // LDS byte tables for Z^0..Z^8 (the sweep: 4 lookups per multiply)
+constexpr int ZB = 9 * 1024;      // byte tables for Z^0..Z^8 (4 lookups per multiply)
 
 // Row shards: a shard holds the rows of ids [lo, hi) — the observer state of those
 // peers.  Row-indexed tables are allocated for the local rows only and their pointers are biased by
@@ -86,15 +86,18 @@ __device__ inline uint32_t log_window_start(const Dev& d, uint32_t i, int32_t r)
   return r >= SHARE_AGE - 1 ? d.fstart[(size_t)i * 16 + ((uint32_t)(r - (SHARE_AGE - 1)) & 15u)] : 0u;
 }
 // copy n 16-byte words global -> LDS with `lanes` cooperating threads (index t), 8 loads in flight each
-template <int NF = 4>   // loads in flight per lane before their LDS stores
 __device__ __attribute__((always_inline)) inline void stage16(uint4* dst, const uint4* src, uint32_t n, uint32_t t,
                                                              uint32_t lanes) {
-  for (uint32_t w0 = t; w0 < n; w0 += lanes * NF) {
-    uint4 v[NF];
-#pragma unroll
-    for (int k = 0; k < NF; ++k) { const uint32_t w = w0 + k * lanes; v[k] = src[w < n ? w : w0]; }
-#pragma unroll
-    for (int k = 0; k < NF; ++k) { const uint32_t w = w0 + k * lanes; if (w < n) dst[w] = v[k]; }
+  for (uint32_t w0 = t; w0 < n; w0 += lanes * 4) {     // four independent loads in flight, then the stores
+    const uint32_t w1 = w0 + lanes, w2 = w1 + lanes, w3 = w2 + lanes;
+    const uint4 v0 = src[w0];
+    const uint4 v1 = src[w1 < n ? w1 : w0];
+    const uint4 v2 = src[w2 < n ? w2 : w0];
+    const uint4 v3 = src[w3 < n ? w3 : w0];
+    dst[w0] = v0;
+    if (w1 < n) dst[w1] = v1;
+    if (w2 < n) dst[w2] = v2;
+    if (w3 < n) dst[w3] = v3;
   }
 }
 __device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }

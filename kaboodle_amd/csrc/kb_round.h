@@ -217,7 +217,6 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
     uint8_t* rw = row_of(d, i);
     uint32_t* gB = bits_of(d, i);
     uint32_t* B = LDSB ? pb_dyn + (size_t)wv * d.NWR : gB;
-    const uint32_t n_ld = d.n[i], fn_ld = d.flog_n[i];   // issued with the staging loads
     if (LDSB) stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB), d.NWR / 4, l, 64);
     if (l < SLOTS) { const Susp sl = d.susp[(size_t)i * SLOTS + l]; s_sp[wv][l] = sl.kind ? sl.peer : 0xFFFFFFFFu; }
     wait_lds();
@@ -227,9 +226,9 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
       return (w >> (x & 31)) & 1u;
     };
     auto is_susp = [&](uint32_t x) __attribute__((always_inline)) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
-    uint32_t n = n_ld;
+    uint32_t n = d.n[i];
     const uint32_t n0 = n;
-    uint32_t fn = fn_ld;
+    uint32_t fn = d.flog_n[i];
     uint32_t lost_cnt = 0, removed_cnt = 0;
     unsigned long long segs = 0;
     // ---- Failed(p) group (src/kaboodle.rs:268-283) ----
@@ -296,10 +295,7 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
         }
       }
       const unsigned long long respm = __ballot(resp);
-      bool logit = deliver && !known;
-      if (__ballot(deliver && known)) {          // a known joiner (rare): log it unless stamped now already
-        if (deliver && known) logit = rw[b.sender] != now;
-      }
+      const bool logit = deliver && (!known || rw[b.sender] != now);
       const unsigned long long lgm = __ballot(logit);
       if (logit) d.flog[(size_t)i * LOGCAP + ((fn + __popcll(lgm & ((1ull << l) - 1ull))) & (LOGCAP - 1))] = log_entry(b.sender, r);
       fn += __popcll(lgm);
