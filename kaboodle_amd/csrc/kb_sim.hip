@@ -15,6 +15,7 @@
 //          k_scatter, k_kp_group, k_sort_inbox, k_proc
 //                                   handle_incoming_messages                       src/kaboodle.rs:394-548
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -464,12 +465,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   (void)hipMemset(L(s, d.kpr_big), 0xFF, 4ull * R);          // no round yet
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
-  // timing-only events: no system-scope fence, so recording them does not add an L2 write-back to
-  // the interval they bracket (with the fence the sweep's event time read ~12 % above rocprof's)
-  (void)hipEventCreateWithFlags(&s->ev0, hipEventDisableSystemFence);
-  (void)hipEventCreateWithFlags(&s->ev1, hipEventDisableSystemFence);
-  (void)hipEventCreateWithFlags(&s->er0, hipEventDisableSystemFence);
-  (void)hipEventCreateWithFlags(&s->er1, hipEventDisableSystemFence);
+  (void)hipEventCreate(&s->ev0); (void)hipEventCreate(&s->ev1); (void)hipEventCreate(&s->er0); (void)hipEventCreate(&s->er1);
   int rc = upload_segments(s);
   if (rc) { destroy_shard(s); return rc; }
   uint32_t ctr0[NCTR] = {0};
@@ -754,9 +750,10 @@ static int step_round(kb_sim* s) {
   }
   // 3. tick
   k_tick_pre<<<gwave, 256, 0, st>>>(d, o0, s->bs, r);
-  (void)hipEventRecord(s->ev0, st);
-  k_sweep<<<((R + 63) / 64 + 3) / 4 * s->S, 256, 0, st>>>(d, s->so);
-  (void)hipEventRecord(s->ev1, st);
+  // the sweep's events are taken by its own dispatch packet (hipExtLaunchKernel), so they time the
+  // kernel itself: a marker recorded before the launch can run while k_tick_pre is still executing
+  // and read ~12 % above rocprof's duration
+  hipExtLaunchKernelGGL(k_sweep, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, st, s->ev0, s->ev1, 0, d, s->so);
   k_tick_post<<<gnode, tb, 0, st>>>(d, s->so, o0, r);
   {
     ScanArgs a = scan_args(s, R, s->scan_tot);

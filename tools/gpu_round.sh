@@ -11,5 +11,5 @@ rc=$?; echo "pytest gpu rc=$rc"; tail -5 gpurun_out/$TAG/pytest_gpu.log
 timeout -k 10 600 python bench.py > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || { echo bench failed; tail gpurun_out/$TAG/bench.err; exit 1; }
 cat gpurun_out/$TAG/bench.json
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/$TAG/prof" -o run --output-format csv -- python3 bench.py --no-cpu --no-conv --steps 20 > gpurun_out/$TAG/prof_bench.json 2> gpurun_out/$TAG/prof_bench.err || exit $?
-python3 tools/prof_summary.py stats gpurun_out/$TAG/prof | head -30
+python3 tools/prof_summary.py stats gpurun_out/$TAG/prof 20 > gpurun_out/$TAG/kernel_stats.txt; head -30 gpurun_out/$TAG/kernel_stats.txt; tail -1 gpurun_out/$TAG/kernel_stats.txt
 bash tools/gpu_pmc.sh $TAG/pmc --steps 10 --warmup 3

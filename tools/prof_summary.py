@@ -1,6 +1,8 @@
 """Summaries of rocprofv3 CSV output (dev tool).
 
-  prof_summary.py stats <dir>            kernel_stats.csv -> compact table (name, calls, avg us, total %)
+  prof_summary.py stats <dir> [K]        kernel_stats.csv -> compact table (name, calls, avg us, total %), and
+                                         k_sweep's average over its last K launches of the kernel trace
+                                         (bench's timed steps; the table's average includes the warmup)
   prof_summary.py pmc <dir> [bench args] counter_collection.csv of the FETCH_SIZE / WRITE_SIZE passes ->
                                          JSON with HBM bytes per k_sweep launch (FETCH_SIZE x2, gfx950)
 """
@@ -26,12 +28,18 @@ def short(name):
     return n
 
 
-def stats(d):
+def stats(d, k_last=0):
     rs = rows(os.path.join(d, "**", "*kernel_stats.csv"))
     rs.sort(key=lambda r: -float(r["TotalDurationNs"]))
     print(f"{'kernel':40s} {'calls':>7s} {'avg_us':>10s} {'pct':>6s}")
     for r in rs:
         print(f"{short(r['Name'])[:40]:40s} {r['Calls']:>7s} {float(r['AverageNs'])/1e3:10.2f} {float(r['Percentage']):6.2f}")
+    if k_last:
+        tr = [r for r in rows(os.path.join(d, "**", "*kernel_trace.csv")) if short(r["Kernel_Name"]) == "k_sweep"]
+        tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+        dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in tr][-k_last:]
+        if dur:
+            print(f"k_sweep over its last {len(dur)} launches (the timed steps): avg {sum(dur) / len(dur):.2f} us")
 
 
 def pmc(d, args):
@@ -72,7 +80,7 @@ def sq(d):
 
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
-        stats(sys.argv[2])
+        stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 0)
     elif sys.argv[1] == "sq":
         sq(sys.argv[2])
     else:
