@@ -816,7 +816,10 @@ static int step_round(kb_sim* s) {
     k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc);
     if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 12, st));
     k_proc_fast<<<gnode, tb, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
-    k_proc<<<4096, 256, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
+    // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
+    // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
+    // on the late waves with few nodes.
+    k_proc<<<std::min<uint32_t>(4096, 2 * s->ncu), 256, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
     if (s->debug_waves) {
       uint32_t dbg[3];
       HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 12, hipMemcpyDeviceToHost, st));
