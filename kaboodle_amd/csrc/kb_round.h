@@ -435,8 +435,11 @@ __device__ __attribute__((always_inline)) inline uint32_t block_prefix(const uin
 // workgroup at once, each with its own LDS slice (bitset, block prefix, joiners, suffix minima), and
 // only wave-level synchronisation.  Same arithmetic as k_resp_node's sampled path.
 constexpr uint32_t RW_JCAP = 128;
+// The row bitset is read in place (L2/L1-resident while its wave works on it), so the LDS slice holds
+// only the block prefix and the joiner lists: more responder waves fit per CU.
 __host__ __device__ inline uint32_t rwave_words(uint32_t NW, uint32_t NB) {
-  return (NW + NB + 1 + 2 * RW_JCAP + 1 + 3) & ~3u;
+  (void)NW;
+  return (NB + 1 + 2 * RW_JCAP + 1 + 3) & ~3u;
 }
 __device__ inline bool resp_by_wave(const Dev& d, uint32_t i, uint32_t nnew, bool on) {
   return on && d.uniform && nnew <= RW_JCAP && d.n[i] - nnew > d.capj;
@@ -446,8 +449,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
   extern __shared__ __attribute__((aligned(16))) uint32_t rw_lds[];
   const uint32_t NW = d.NWR, NB = d.W / 256;
   const uint32_t wv = threadIdx.x >> 6, l = lane();
-  uint32_t* B = rw_lds + (size_t)wv * rwave_words(NW, NB);   // row membership after the Join group [NW]
-  uint32_t* BP = B + NW;                                        // block prefix of B                 [NB + 1]
+  uint32_t* BP = rw_lds + (size_t)wv * rwave_words(NW, NB);  // block prefix of the row's bitset    [NB + 1]
   uint32_t* J = BP + NB + 1;                                    // this receiver's new joiners       [RW_JCAP]
   uint32_t* JM = J + RW_JCAP;                                   // suffix minima of J                [RW_JCAP + 1]
   const uint32_t nnodes = *nnodes_p;
@@ -458,15 +460,14 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     uint32_t nnew = 0;
     for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
     if (!resp_by_wave(d, i, nnew, true)) continue;          // wave-uniform: k_resp_node serves it
-    stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(bits_of(d, i)), NW / 4, l, 64);
-    wait_lds();
-    __builtin_amdgcn_wave_barrier();
+    const uint32_t* B = bits_of(d, i);                      // row membership after the Join group
+    const uint4* B4 = reinterpret_cast<const uint4*>(B);
     const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
     uint32_t bc = 0, last = 0;
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) {
-      uint32_t c = 0;
-#pragma unroll
-      for (int w = 0; w < 8; ++w) c += __popc(B[k * 8 + w]);
+      const uint4 q0 = B4[2 * k], q1 = B4[2 * k + 1];
+      const uint32_t c = __popc(q0.x) + __popc(q0.y) + __popc(q0.z) + __popc(q0.w) + __popc(q1.x) + __popc(q1.y) +
+                         __popc(q1.z) + __popc(q1.w);
       BP[k] = c; bc += c;
       if (c) last = k + 1;
     }
