@@ -256,9 +256,14 @@ __global__ void k_scatter_flat(OutBuf ib, WaveCtl wc, uint32_t n) {
 // BIG = the groups of at least KP_BIG ids (a joiner's hundreds of Join responses, all on one row):
 // 1024 threads on the row's member bitset staged in LDS, a wave per message with KP_UNROLL
 // independent id loads in flight per lane.  The other groups take 256 threads on the bitset in place.
+// A BIG group whose bitset fits in LDS is served by KP_COLS workgroups, each owning a quarter of the
+// row's ids: every one reads all the group's ids and applies those in its quarter, arms then
+// prologues.  An arm and a prologue conflict only on the same id, which one workgroup owns, so the
+// quarters need no synchronisation with each other.
 constexpr uint32_t KP_BIG = 4096;          // payload ids from which a group takes the BIG kernel
 constexpr uint32_t KP_LDS_WORDS = 16384;   // BIG: rows up to 512K ids keep their bitset in LDS (64 KB)
 constexpr int KP_UNROLL = 10;            // 640 ids per wave step: a whole Join response (<= 567)
+constexpr uint32_t KP_COLS = 4;          // BIG groups in LDS: workgroups per destination, one per column quarter
 __host__ __device__ constexpr size_t kp_lds_bytes(uint32_t nwr) {
   return 4ull * (nwr <= KP_LDS_WORDS ? nwr : 4);
 }
@@ -273,11 +278,13 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
   const bool lds = BIG && d.NWR <= KP_LDS_WORDS;
-  // the active list T entries per workgroup at a time, interleaved over the workgroups (consecutive
-  // ids, e.g. the round's joiners, go to different workgroups): the destinations of this kind are
+  const uint32_t KS = lds ? KP_COLS : 1u, part = blockIdx.x % KS, G = gridDim.x / KS, g = blockIdx.x / KS;
+  const uint32_t w0 = part * (d.NWR / KS), w1 = w0 + d.NWR / KS;   // this workgroup's bitset words
+  // the active list T entries per workgroup group at a time, interleaved over the groups (consecutive
+  // ids, e.g. the round's joiners, go to different groups): the destinations of this kind are
   // listed in LDS by all threads at once, then served one by one
-  for (uint32_t c0 = 0; c0 < nact; c0 += gridDim.x * T) {
-  const uint32_t it = c0 + t * gridDim.x + blockIdx.x;
+  for (uint32_t c0 = 0; c0 < nact; c0 += G * T) {
+  const uint32_t it = c0 + t * G + g;
   if (t == 0) s_nl = 0;
   __syncthreads();
   if (it < nact) {
@@ -294,14 +301,16 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     uint32_t* B = lds ? kp_lds : gB;
     uint8_t* rw = row_of(d, i);
     if (t == 0) { s_segs = 0; s_add = 0; }
-    if (lds) stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB), d.NWR / 4, t, T);
+    if (lds) stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB + w0), (w1 - w0) / 4, t, T);
     unsigned long long segs = 0;
     uint32_t added = 0;
     auto arm = [&](uint32_t p) __attribute__((always_inline)) {
+      const uint32_t wi = p >> 5;
+      if (wi < w0 || wi >= w1) return;                  // another workgroup's quarter
       const uint32_t bit = 1u << (p & 31);
-      const uint32_t w = lds ? B[p >> 5] : __hip_atomic_load(&B[p >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t w = lds ? B[wi - w0] : __hip_atomic_load(&B[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (w & bit) return;
-      if (!(atomicOr(&B[p >> 5], bit) & bit)) { rw[p] = old; segs |= seg_bit(d, p); added++; }
+      if (!(atomicOr(&B[wi - w0], bit) & bit)) { rw[p] = old; segs |= seg_bit(d, p); added++; }
     };
     if (BIG) {
       // wave per message: the records of up to 64 of this wave's messages are fetched at once (lane
@@ -338,6 +347,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     for (uint32_t q = t; q < nk; q += T) {             // prologues
       const Msg m = ib.msgs[wc.kin[k0 + q]];
       const uint32_t s = m.sender;
+      if ((s >> 5) < w0 || (s >> 5) >= w1) continue;     // another workgroup's quarter
       // byte update by CAS on its word: exactly one envelope per (dest, sender) sees the transition to
       // Known(now) and appends it to the freshness log
       uint32_t* wp = reinterpret_cast<uint32_t*>(rw + (s & ~3u));
@@ -352,7 +362,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
       }
       if (prevb != now) d.flog[(size_t)i * LOGCAP + (atomicAdd(&d.flog_n[i], 1u) & (LOGCAP - 1))] = log_entry(s, r);
       const uint32_t bit = 1u << (s & 31);
-      if (!(atomicOr(&B[s >> 5], bit) & bit)) { segs |= seg_bit(d, s); added++; }
+      if (!(atomicOr(&B[(s >> 5) - w0], bit) & bit)) { segs |= seg_bit(d, s); added++; }
     }
     if (segs) atomicOr(&s_segs, segs);
     if (added) atomicAdd(&s_add, added);
@@ -362,17 +372,20 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
       const uint32_t wps4 = d.SEGW / 128;
       const uint4* B4 = reinterpret_cast<const uint4*>(B);
       uint4* g4 = reinterpret_cast<uint4*>(gB);
-      for (uint32_t w = t; w < d.NWR / 4; w += T) if ((sg >> (w / wps4)) & 1ull) g4[w] = B4[w];
+      for (uint32_t w = w0 / 4 + t; w < w1 / 4; w += T) if ((sg >> (w / wps4)) & 1ull) g4[w] = B4[w - w0 / 4];
     }
     if (t < SLOTS) {                                   // a prologue overwrote a WaitingFor* entry to Known
       Susp* sl = d.susp + (size_t)i * SLOTS + t;
-      if (sl->kind) {
+      if (sl->kind && (sl->peer >> 5) >= w0 && (sl->peer >> 5) < w1) {
         const uint32_t pw = __hip_atomic_load(reinterpret_cast<uint32_t*>(rw + (sl->peer & ~3u)), __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
         if (((pw >> (8 * (sl->peer & 3u))) & 0xFFu) != ST_SUSPECT) sl->kind = 0;
       }
     }
-    if (t == 0 && (s_add || sg)) { d.n[i] += s_add; mark(d, i, sg); }
+    if (t == 0 && (s_add || sg)) {
+      if (KS > 1) atomicAdd(&d.n[i], s_add); else d.n[i] += s_add;
+      mark(d, i, sg);
+    }
     __syncthreads();                                   // LDS reused by the next destination
   }
   }
