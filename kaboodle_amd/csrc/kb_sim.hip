@@ -807,11 +807,9 @@ static int step_round(kb_sim* s) {
       fprintf(stderr, "[kb] round %d wave %u: in-order msgs %llu, max inbox %u (node %u), inboxes > 64: %u\n", r, w,
               (unsigned long long)sum, mx, arg, big);
     }
-    HIPCHK(hipMemcpyAsync(L(s, nb.cap), L(s, s->wc.bnd), 4ull * R, hipMemcpyDeviceToDevice, st));
-    HIPCHK(hipMemsetAsync(L(s, nb.cnt), 0, 4ull * R, st));
     if (!s->xf) k_scatter<<<gnode, tb, 0, st>>>(d, ob, s->wc);
     else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
-    k_kp_small<<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r);
+    k_kp_small<<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r, nb);   // also sets up nb.cap / nb.cnt
     {  // BIG groups in LDS: KP_COLS workgroups per destination group, one per column quarter
       const uint32_t ks = d.NWR <= KP_LDS_WORDS ? KP_COLS : 1u;
       const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));

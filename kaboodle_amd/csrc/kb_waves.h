@@ -393,9 +393,13 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
 
 // The groups under KP_BIG ids (KnownPeersRequest replies, small Join lists): a wave per destination,
 // in place on the row's bitset, the same arms-then-prologues order as k_kp_group.
-__global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, int32_t r) {
+__global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, int32_t r, OutBuf nb) {
   __shared__ uint32_t s_list[256], s_nl;
   const uint32_t t = threadIdx.x, wv = t >> 6, l = lane();
+  {  // the next outbox of every local row: capacity = the wave's reservation, empty (was a copy + memset)
+    const uint32_t i = d.lo + blockIdx.x * blockDim.x + t;
+    if (i < d.hi) { nb.cap[i] = wc.bnd[i]; nb.cnt[i] = 0; }
+  }
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
   for (uint32_t c0 = 0; c0 < nact; c0 += gridDim.x * 256) {
