@@ -22,7 +22,7 @@ enum StatIdx {
 };
 enum CtrIdx {
   C_KP, C_SLOW, C_ACTIVE, C_AGREE, C_ALIVE, C_LEAVES, C_NEXTFREE, C_ERR, C_FIRSTCONV, C_LASTCONV, C_LASTAGREE,
-  C_LASTALIVE, C_DBG_INS, C_DBG_FP, C_DBG_MAXFP, NCTR
+  C_LASTALIVE, C_DBG_INS, C_DBG_FP, C_DBG_MAXFP, C_TICK, NCTR
 };
 constexpr int NSEG = 64;          // fingerprint checkpoints per row
 constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8

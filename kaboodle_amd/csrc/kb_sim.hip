@@ -749,7 +749,8 @@ static int step_round(kb_sim* s) {
     }
   }
   // 3. tick
-  k_tick_pre<<<gwave, 256, 0, st>>>(d, o0, s->bs, r);
+  k_tick_scan<<<gnode, tb, 0, st>>>(d, s->bs, r, s->slow);                       // A1; list the A2 nodes
+  k_tick_pre<<<std::min<uint32_t>(gwave, 1024), 256, 0, st>>>(d, o0, s->bs, r, s->slow);   // A2 per listed node
   // the sweep's events are taken by its own dispatch packet (hipExtLaunchKernel), so they time the
   // kernel itself: a marker recorded before the launch can run while k_tick_pre is still executing
   // and read ~12 % above rocprof's duration

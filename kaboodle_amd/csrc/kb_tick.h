@@ -18,21 +18,10 @@ __device__ inline uint32_t cand16(const Dev& d, const uint8_t* rw, const uint32_
   if (i >= j0 && i < j0 + 16) c &= ~(1u << (i - j0));
   return c;
 }
-// ---- A1 maybe_broadcast_join (:228-251) + A2 handle_suspected_peers (:558-653), one wave per node
-__global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots bs, int32_t r) {
-  __shared__ uint32_t s_pick_rank[4][SLOTS * 3], s_pick_peer[4][SLOTS * 3], s_pick_id[4][SLOTS * 3];
-  const uint32_t wv = threadIdx.x >> 6;
-  const uint32_t i = d.lo + blockIdx.x * 4 + wv;
-  const uint32_t l = lane();
-  if (i >= d.hi) return;
-  if (!d.alive[i]) { if (l == 0) { bs.join[i] = 0; bs.nfail[i] = 0; } return; }
+__device__ __attribute__((always_inline)) inline void tick_a2(const Dev& d, const OutBuf& ob, const BcastSlots& bs, int32_t r,
+                                                              uint32_t i, uint32_t l, uint32_t* pr, uint32_t* pp,
+                                                              uint32_t* pid) {
   uint32_t n = d.n[i];
-  if (l == 0) {
-    const int32_t lb = d.last_bcast[i];
-    uint32_t j = 0;
-    if (lb == NONE_ROUND || (r - lb >= REBROADCAST && n <= 1)) { j = 1; d.last_bcast[i] = r; }
-    bs.join[i] = j;
-  }
   Susp* sl = d.susp + (size_t)i * SLOTS;
   const Susp me = l < SLOTS ? sl[l] : Susp{0, 0, 0, 0};
   const bool occ = l < SLOTS && me.kind != 0;
@@ -65,7 +54,7 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
         if (c >= hi) c++;
         pk[2] = c;
       }
-      if (l == 0) for (uint32_t q = 0; q < kk; ++q) { s_pick_rank[wv][npick + q] = pk[q]; s_pick_peer[wv][npick + q] = peer; s_pick_id[wv][npick + q] = 0xFFFFFFFFu; }
+      if (l == 0) for (uint32_t q = 0; q < kk; ++q) { pr[npick + q] = pk[q]; pp[npick + q] = peer; pid[npick + q] = 0xFFFFFFFFu; }
       npick += kk;
       indirect[nind++] = peer;
     } else {
@@ -82,7 +71,7 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
     __builtin_amdgcn_wave_barrier();
     const uint32_t* bw = bits_of(d, i);
     uint32_t maxrank = 0;
-    for (uint32_t q = 0; q < npick; ++q) maxrank = s_pick_rank[wv][q] > maxrank ? s_pick_rank[wv][q] : maxrank;
+    for (uint32_t q = 0; q < npick; ++q) maxrank = pr[q] > maxrank ? pr[q] : maxrank;
     uint32_t base = 0;
     for (uint32_t j0 = 0; j0 < d.W && base <= maxrank; j0 += 4096) {
       uint32_t mk[4];
@@ -93,15 +82,15 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
         const uint32_t j = j0 + 1024 * u + 16 * l;
         const uint32_t pc = __popc(mk[u]), ex = wave_excl(pc), tot = wave_sum(pc);
         for (uint32_t q = 0; q < npick; ++q) {
-          const uint32_t rk = s_pick_rank[wv][q];
-          if (rk >= base + ex && rk < base + ex + pc) s_pick_id[wv][q] = j + select_in_word(mk[u], rk - base - ex);
+          const uint32_t rk = pr[q];
+          if (rk >= base + ex && rk < base + ex + pc) pid[q] = j + select_in_word(mk[u], rk - base - ex);
         }
         base += tot;
       }
     }
     wait_lds();
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t q = 0; q < npick; ++q) emit_msg(ob, d, i, oseq, s_pick_id[wv][q], K_PINGREQ, s_pick_peer[wv][q], 0, 0, 0);
+    for (uint32_t q = 0; q < npick; ++q) emit_msg(ob, d, i, oseq, pid[q], K_PINGREQ, pp[q], 0, 0, 0);
   }
   if (l == 0) {                                           // :631-652
     for (uint32_t q = 0; q < nind; ++q)
@@ -122,6 +111,37 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
     ob.cnt[i] = oseq;
   }
 }
+
+// ---- A1 maybe_broadcast_join (:228-251), thread per node; the nodes with a timed-out suspect slot
+// (A2's only work) are listed for k_tick_pre, a wave per listed node
+__global__ __launch_bounds__(256) void k_tick_scan(Dev d, BcastSlots bs, int32_t r, uint32_t* list) {
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= d.hi) return;
+  if (!d.alive[i]) { bs.join[i] = 0; bs.nfail[i] = 0; return; }
+  const int32_t lb = d.last_bcast[i];
+  uint32_t j = 0;
+  if (lb == NONE_ROUND || (r - lb >= REBROADCAST && d.n[i] <= 1)) { j = 1; d.last_bcast[i] = r; }
+  bs.join[i] = j;
+  const Susp* sl = d.susp + (size_t)i * SLOTS;
+  bool tim = false;
+#pragma unroll
+  for (int k = 0; k < SLOTS; ++k) { const Susp x = sl[k]; tim |= x.kind != 0 && r - x.since >= PING_TIMEOUT; }
+  if (!tim) { bs.nfail[i] = 0; return; }
+  list[atomicAdd(&d.ctr[C_TICK], 1u)] = i;
+}
+
+// ---- A2 handle_suspected_peers (:558-653) for the nodes k_tick_scan listed, one wave per node
+// (persistent grid over the list)
+__global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots bs, int32_t r, const uint32_t* list) {
+  __shared__ uint32_t s_pick_rank[4][SLOTS * 3], s_pick_peer[4][SLOTS * 3], s_pick_id[4][SLOTS * 3];
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t l = lane();
+  const uint32_t nlist = d.ctr[C_TICK];
+  for (uint32_t it = blockIdx.x * 4 + wv; it < nlist; it += gridDim.x * 4) {
+    tick_a2(d, ob, bs, r, list[it], l, s_pick_rank[wv], s_pick_peer[wv], s_pick_id[wv]);
+  }
+}
+
 
 // ================================================================================================
 // THE ROW SWEEP (dominant kernel).  ping_random_peer (:655-703) keeps the 5 oldest Known peers by
@@ -396,7 +416,7 @@ __global__ void k_round_end(Dev d, int32_t r) {
     if ((int32_t)d.ctr[C_FIRSTCONV] < 0) d.ctr[C_FIRSTCONV] = (uint32_t)r;
     d.ctr[C_LASTCONV] = (uint32_t)r;
   }
-  d.ctr[C_AGREE] = 0; d.ctr[C_ALIVE] = 0;
+  d.ctr[C_AGREE] = 0; d.ctr[C_ALIVE] = 0; d.ctr[C_TICK] = 0;
 }
 
 }  // namespace kb
