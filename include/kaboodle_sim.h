@@ -125,6 +125,21 @@ int  kb_sim_stats(kb_sim* sim, kb_stats* out);
 /* fingerprint of the true running set (what every converged node should report) */
 int  kb_sim_true_fingerprint(kb_sim* sim, uint32_t* fp);
 
+/* ---- event streams (src/events.rs:18-125; Kaboodle::discover_peers / discover_departures /
+ * discover_fingerprint_changes, src/lib.rs:186-263) -------------------------------------------------
+ * kb_sim_watch attaches an observer to `node`'s known_peers, empty, as Kaboodle::new does
+ * (src/lib.rs:112).  kb_sim_events drains one batch: the NET change since the previous drain, ids
+ * ascending.  discovered = known now and not at the last drain (Event::Added, events.rs:59-79);
+ * departed = known then and not now (Event::Removed, :88-99).  *fp is the node's fingerprint and
+ * *fp_changed = 1 when the node knows at least one peer and *fp differs from the last fingerprint
+ * reported as changed (initially 0, :103-122).  A peer added and removed inside one batch yields no
+ * event (the reference may emit a lone departure for it).  Buffers are caller-owned: with both
+ * pointers NULL the call only reports the counts and drains nothing; a buffer too small for its
+ * count gives KB_CAPACITY and drains nothing.  Not watched: KB_INVALID_OPERATION.               */
+int  kb_sim_watch(kb_sim* sim, uint32_t node);
+int  kb_sim_events(kb_sim* sim, uint32_t node, uint32_t* discovered, size_t cap_d, size_t* n_d,
+                   uint32_t* departed, size_t cap_p, size_t* n_p, uint32_t* fp, int* fp_changed);
+
 /* ---- sharding across GPUs --------------------------------------------------------
  * A mesh of C ids can be split into `world` (1..8) contiguous row shards: shard k holds the observer
  * state of ids [k*S, min(C, (k+1)*S)), S = ceil(C/world).  The reference's UDP transport between

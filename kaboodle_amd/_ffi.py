@@ -111,6 +111,10 @@ _SIGS = {
                                     C.POINTER(C.c_size_t)]),
     "sim_dump_curious": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_int32), C.c_size_t,
                                    C.POINTER(C.c_size_t)]),
+    "sim_watch": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sim_events": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t),
+                             C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_uint32),
+                             C.POINTER(C.c_int)]),
     "format_addr": (C.c_int, [C.c_uint32, C.c_char_p, C.c_size_t]),
     "last_error": (C.c_char_p, []),
 }
@@ -258,6 +262,22 @@ class Sim:
         arr = (C.c_uint32 * max(n.value, 1))()
         self.lib.call("sim_peers", self.h, node, arr, n.value, C.byref(n))
         return list(arr[: n.value])
+
+    # -- event streams (src/events.rs:18-125) --
+    def watch(self, node: int) -> None:
+        """Attach an observer to `node` (empty, as Kaboodle::new does, src/lib.rs:112)."""
+        self.lib.call("sim_watch", self.h, node)
+
+    def events(self, node: int):
+        """Drain one batch: (discovered, departed, fingerprint, fingerprint_changed)."""
+        nd, npp, fp, ch = C.c_size_t(), C.c_size_t(), C.c_uint32(), C.c_int()
+        self.lib.call("sim_events", self.h, node, None, 0, C.byref(nd), None, 0, C.byref(npp), C.byref(fp),
+                      C.byref(ch))
+        d = (C.c_uint32 * max(nd.value, 1))()
+        p = (C.c_uint32 * max(npp.value, 1))()
+        self.lib.call("sim_events", self.h, node, d, nd.value, C.byref(nd), p, npp.value, C.byref(npp),
+                      C.byref(fp), C.byref(ch))
+        return list(d[: nd.value]), list(p[: npp.value]), fp.value, bool(ch.value)
 
     def peer_states(self, node: int):
         n = C.c_size_t()

@@ -213,6 +213,57 @@ static uint32_t h_xpow8(uint64_t n) {
   return res;
 }
 
+// Event streams (src/events.rs:57-100): the net difference between `node`'s membership bitset and
+// the observer's snapshot.  One workgroup walks the row 1024 words at a time; the ids of each pass
+// are compacted in ascending order by a wave scan plus a scan over the 16 wave totals.
+// out = [discovered: C][departed: C][n_discovered, n_departed, n_known]
+__global__ __launch_bounds__(1024) void k_events_diff(const uint32_t* __restrict__ row,
+                                                      const uint32_t* __restrict__ snap, uint32_t C,
+                                                      uint32_t* __restrict__ out) {
+  __shared__ uint32_t wa[16], wr[16], base[2], known;
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6, nw = (C + 31) / 32;
+  uint32_t* add = out;
+  uint32_t* rem = out + C;
+  if (t == 0) { base[0] = 0; base[1] = 0; known = 0; }
+  __syncthreads();
+  uint32_t kn = 0;
+  for (uint32_t w0 = 0; w0 < nw; w0 += 1024) {
+    const uint32_t w = w0 + t;
+    uint32_t cur = 0, old = 0;
+    if (w < nw) {
+      const uint32_t valid = (C - w * 32 >= 32) ? ~0u : ((1u << (C - w * 32)) - 1u);
+      cur = row[w] & valid;
+      old = snap[w] & valid;
+    }
+    const uint32_t a = cur & ~old, r = old & ~cur;
+    kn += __popc(cur);
+    uint32_t pa = __popc(a), pr = __popc(r);
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t xa = __shfl_up(pa, o, 64), xr = __shfl_up(pr, o, 64);
+      if (lane >= (uint32_t)o) { pa += xa; pr += xr; }
+    }
+    if (lane == 63) { wa[wv] = pa; wr[wv] = pr; }
+    __syncthreads();
+    uint32_t oa = base[0] + pa - __popc(a), orr = base[1] + pr - __popc(r);
+    for (uint32_t k = 0; k < wv; ++k) { oa += wa[k]; orr += wr[k]; }
+    for (uint32_t m = a; m; m &= m - 1) add[oa++] = w * 32 + __ffs(m) - 1;
+    for (uint32_t m = r; m; m &= m - 1) rem[orr++] = w * 32 + __ffs(m) - 1;
+    __syncthreads();
+    if (t == 1023) { base[0] = oa; base[1] = orr; }
+    __syncthreads();
+  }
+  for (int o = 32; o > 0; o >>= 1) kn += __shfl_down(kn, o, 64);
+  if (lane == 0) atomicAdd(&known, kn);
+  __syncthreads();
+  if (t == 0) { out[2 * C] = base[0]; out[2 * C + 1] = base[1]; out[2 * C + 2] = known; }
+}
+// the drain: the snapshot becomes the current row
+__global__ __launch_bounds__(256) void k_events_commit(const uint32_t* __restrict__ row, uint32_t* __restrict__ snap,
+                                                       uint32_t nw) {
+  const uint32_t w = blockIdx.x * 256 + threadIdx.x;
+  if (w < nw) snap[w] = row[w];
+}
+
 struct kb_sim {
   kb_config cfg;
   Dev d;
@@ -260,6 +311,11 @@ struct kb_sim {
   // kb_sim_create_local: a façade over `world` in-process shards (one host thread each per step)
   std::vector<kb_sim*> shards;
   LocalHub* hub;
+  // event observers (kb_sim_watch): a watched node and the device snapshot of its membership bitset
+  // at the last drain, plus the fingerprint last reported for it
+  std::vector<uint32_t> watch_node, watch_fp;
+  std::vector<uint32_t*> watch_snap;
+  uint32_t* ev_out = nullptr;          // [2*C + 4]: discovered ids, departed ids, counters
 };
 
 // allocation of this handle's device memory; row tables hold the local rows only and their pointer
@@ -1078,6 +1134,50 @@ extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, 
   }
   *n = c;
   return (out && cap < c) ? KB_CAPACITY : KB_OK;
+}
+extern "C" int kb_sim_watch(kb_sim* s, uint32_t node) {
+  if (chk(s, node)) return KB_INVALID_ARGUMENT;
+  GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_watch(t, node); });
+  if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
+  for (uint32_t w : s->watch_node) if (w == node) return KB_OK;      // one observer per node
+  if (!s->ev_out) HIPCHK(talloc(s, &s->ev_out, 2ull * s->C + 4));
+  uint32_t* snap = nullptr;
+  HIPCHK(talloc(s, &snap, (size_t)s->d.NWR));
+  HIPCHK(hipMemsetAsync(snap, 0, 4ull * s->d.NWR, s->st));          // attached empty, as in Kaboodle::new
+  HIPCHK(hipStreamSynchronize(s->st));
+  s->watch_node.push_back(node); s->watch_fp.push_back(0); s->watch_snap.push_back(snap);
+  return KB_OK;
+}
+extern "C" int kb_sim_events(kb_sim* s, uint32_t node, uint32_t* discovered, size_t cap_d, size_t* n_d,
+                             uint32_t* departed, size_t cap_p, size_t* n_p, uint32_t* fp, int* fp_changed) {
+  if (chk(s, node) || !n_d || !n_p || !fp || !fp_changed) return KB_INVALID_ARGUMENT;
+  GROUP_OWNER(node, [&](kb_sim* t) {
+    return kb_sim_events(t, node, discovered, cap_d, n_d, departed, cap_p, n_p, fp, fp_changed); });
+  if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
+  size_t k = 0;
+  while (k < s->watch_node.size() && s->watch_node[k] != node) ++k;
+  if (k == s->watch_node.size()) { seterr("node is not watched (kb_sim_watch)"); return KB_INVALID_OPERATION; }
+  const uint32_t* row = s->d.bits + (size_t)node * s->d.NWR;
+  uint32_t ctr[3];
+  k_events_diff<<<1, 1024, 0, s->st>>>(row, s->watch_snap[k], s->C, s->ev_out);
+  k_fp_one<<<1, 64, 0, s->st>>>(s->d, node);
+  HIPCHK(hipMemcpyAsync(ctr, s->ev_out + 2ull * s->C, 12, hipMemcpyDeviceToHost, s->st));
+  HIPCHK(hipMemcpyAsync(fp, s->d.fp + node, 4, hipMemcpyDeviceToHost, s->st));
+  HIPCHK(hipStreamSynchronize(s->st));
+  *n_d = ctr[0]; *n_p = ctr[1];
+  // the fingerprint batch rule (src/events.rs:103-122): only with a non-empty map, only on change
+  *fp_changed = ctr[2] > 0 && *fp != s->watch_fp[k];
+  const bool fit = (!ctr[0] || (discovered && cap_d >= ctr[0])) && (!ctr[1] || (departed && cap_p >= ctr[1]));
+  if (!fit) {
+    if (discovered || departed) { seterr("event buffer too small"); return KB_CAPACITY; }
+    return KB_OK;                                                    // size query: nothing drained
+  }
+  if (ctr[0]) HIPCHK(hipMemcpyAsync(discovered, s->ev_out, 4ull * ctr[0], hipMemcpyDeviceToHost, s->st));
+  if (ctr[1]) HIPCHK(hipMemcpyAsync(departed, s->ev_out + s->C, 4ull * ctr[1], hipMemcpyDeviceToHost, s->st));
+  k_events_commit<<<(s->d.NWR + 255) / 256, 256, 0, s->st>>>(row, s->watch_snap[k], s->d.NWR);
+  HIPCHK(hipStreamSynchronize(s->st));
+  if (*fp_changed) s->watch_fp[k] = *fp;
+  return KB_OK;
 }
 extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
   if (!s || !out) return KB_INVALID_ARGUMENT;

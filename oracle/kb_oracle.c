@@ -102,6 +102,8 @@ struct kbo_sim {
   uint32_t* oseq;             /* per-node emission counter for the wave being produced */
   int32_t* a3fp;              /* unused */
   kb_stats st;
+  /* event observers (kbo_sim_watch): watched node, its membership at the last drain, last reported fp */
+  uint32_t* wnode; uint8_t** wsnap; uint32_t* wfp; size_t nwatch;
 };
 typedef struct kbo_sim kbo_sim;
 
@@ -370,6 +372,8 @@ int kbo_sim_destroy(kbo_sim* s) {
   free(s->stamp); free(s->alive); free(s->ever); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
   free(s->last_bcast); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
+  for (size_t k = 0; k < s->nwatch; ++k) free(s->wsnap[k]);
+  free(s->wnode); free(s->wsnap); free(s->wfp);
   free(s->ev); free(s);
   return KB_OK;
 }
@@ -858,6 +862,54 @@ int kbo_sim_peers(kbo_sim* s, uint32_t node, uint32_t* peers, size_t cap, size_t
   for (uint32_t j = 0; j < s->C; ++j) if (rw[j]) { if (peers && c < cap) peers[c] = j; c++; }
   *n = c;
   return (peers && cap < c) ? KB_CAPACITY : KB_OK;
+}
+/* Event streams, src/events.rs:18-125 (observer attached empty in Kaboodle::new, src/lib.rs:112).
+ * One drain = one batch: discovered = members now and not at the last drain (Added, :59-79),
+ * departed = members then and not now (Removed, :88-99), both ascending; the fingerprint is reported
+ * as changed when the map is non-empty and it differs from the last reported one (:103-122). */
+int kbo_sim_watch(kbo_sim* s, uint32_t node) {
+  if (check(s, node)) return KB_INVALID_ARGUMENT;
+  for (size_t k = 0; k < s->nwatch; ++k) if (s->wnode[k] == node) return KB_OK;
+  s->wnode = (uint32_t*)realloc(s->wnode, (s->nwatch + 1) * sizeof(uint32_t));
+  s->wfp = (uint32_t*)realloc(s->wfp, (s->nwatch + 1) * sizeof(uint32_t));
+  s->wsnap = (uint8_t**)realloc(s->wsnap, (s->nwatch + 1) * sizeof(uint8_t*));
+  s->wnode[s->nwatch] = node; s->wfp[s->nwatch] = 0;
+  s->wsnap[s->nwatch] = (uint8_t*)calloc(s->C, 1);
+  s->nwatch++;
+  return KB_OK;
+}
+int kbo_sim_events(kbo_sim* s, uint32_t node, uint32_t* discovered, size_t cap_d, size_t* n_d,
+                   uint32_t* departed, size_t cap_p, size_t* n_p, uint32_t* fp, int* fp_changed) {
+  if (check(s, node) || !n_d || !n_p || !fp || !fp_changed) return KB_INVALID_ARGUMENT;
+  size_t k = 0;
+  while (k < s->nwatch && s->wnode[k] != node) ++k;
+  if (k == s->nwatch) { seterr("node is not watched (kbo_sim_watch)"); return KB_INVALID_OPERATION; }
+  const uint8_t* rw = row(s, node);
+  uint8_t* snap = s->wsnap[k];
+  size_t a = 0, r = 0, known = 0;
+  for (uint32_t j = 0; j < s->C; ++j) {
+    const int now = rw[j] != 0, then = snap[j] != 0;
+    known += now;
+    a += now && !then;
+    r += then && !now;
+  }
+  *n_d = a; *n_p = r;
+  *fp = cur_fp(s, node);
+  *fp_changed = known > 0 && *fp != s->wfp[k];
+  const int fit = (!a || (discovered && cap_d >= a)) && (!r || (departed && cap_p >= r));
+  if (!fit) {
+    if (discovered || departed) { seterr("event buffer too small"); return KB_CAPACITY; }
+    return KB_OK;
+  }
+  a = r = 0;
+  for (uint32_t j = 0; j < s->C; ++j) {
+    const int now = rw[j] != 0, then = snap[j] != 0;
+    if (now && !then) discovered[a++] = j;
+    if (then && !now) departed[r++] = j;
+    snap[j] = (uint8_t)now;
+  }
+  if (*fp_changed) s->wfp[k] = *fp;
+  return KB_OK;
 }
 int kbo_sim_peer_states(kbo_sim* s, uint32_t node, kb_peer_state* out, size_t cap, size_t* n) {
   if (check(s, node) || !n) return KB_INVALID_ARGUMENT;

@@ -85,16 +85,8 @@ def run_case(case: dict, rounds: int, check_every: int = 1, full_rows: bool = Tr
     g = gpu if gpu is not None else Sim(gpu_lib(), cfg, shards=shards)
     setup(o, case)
     setup(g, case)
-    events = case.get("events", {})
     for r in range(rounds):
-        for kind, node, arg in events.get(r, []):
-            for s in (o, g):
-                if kind == "stop":
-                    s.stop_node(node)
-                elif kind == "start":
-                    s.start_node(node)
-                elif kind == "ping":
-                    s.ping_addrs(node, arg)
+        apply_events((o, g), case, r)
         o.step(1)
         g.step(1)
         if (r + 1) % check_every == 0 or r == rounds - 1:
@@ -105,6 +97,57 @@ def run_case(case: dict, rounds: int, check_every: int = 1, full_rows: bool = Tr
                 st = g.stats()
                 print(f"  round {r}: agree {st['agree']}/{st['alive']} ok", flush=True)
     return True, "ok", g.stats()
+
+
+def apply_events(sims, case: dict, r: int) -> None:
+    for kind, node, arg in case.get("events", {}).get(r, []):
+        for s in sims:
+            if kind == "stop":
+                s.stop_node(node)
+            elif kind == "start":
+                s.start_node(node)
+            elif kind == "ping":
+                s.ping_addrs(node, arg)
+
+
+def run_events_case(case: dict, rounds: int, watched, drain_every: int = 1, shards: int = 0,
+                    libs=None):
+    """Event streams (src/events.rs:18-125) on both implementations: every node in `watched` is
+    observed from creation and drained every `drain_every` rounds.  Each batch must be identical
+    across implementations and equal to the net diff of the oracle's peer lists.  libs = (oracle,
+    other) SimLibs; default (oracle, HIP library).  Returns (ok, message, batches compared)."""
+    cfg = case["cfg"]
+    la, lb = libs if libs is not None else (oracle_lib(), gpu_lib())
+    o = Sim(la, cfg)
+    g = Sim(lb, cfg, shards=shards)
+    for s in (o, g):
+        for i in watched:
+            s.watch(i)
+    setup(o, case)
+    setup(g, case)
+    prev = {i: set() for i in watched}
+    last_fp = {i: 0 for i in watched}
+    n = 0
+    for r in range(rounds):
+        apply_events((o, g), case, r)
+        o.step(1)
+        g.step(1)
+        if (r + 1) % drain_every and r != rounds - 1:
+            continue
+        for i in watched:
+            eo, eg = o.events(i), g.events(i)
+            if eo != eg:
+                return False, f"round {r} node {i}: oracle {eo[:2]} fp {eo[2]:#x}/{eo[3]} != {eg[:2]} fp {eg[2]:#x}/{eg[3]}", n
+            now = set(o.peers(i))
+            want_d, want_p = sorted(now - prev[i]), sorted(prev[i] - now)
+            want_ch = bool(now) and eo[2] != last_fp[i]
+            if (eo[0], eo[1], eo[3]) != (want_d, want_p, want_ch):
+                return False, f"round {r} node {i}: events {eo} != peer-list diff {want_d} {want_p} {want_ch}", n
+            if want_ch:
+                last_fp[i] = eo[2]
+            prev[i] = now
+            n += 1
+    return True, "ok", n
 
 
 def standard_cases() -> list[tuple[str, dict, int]]:

@@ -1,0 +1,106 @@
+"""Event streams — `handle_known_peers_events` (src/events.rs:18-125) behind Kaboodle::discover_peers /
+discover_departures / discover_fingerprint_changes (src/lib.rs:186-263), as kb_sim_watch +
+kb_sim_events (include/kaboodle_sim.h).
+
+One drain is one batch: discovered / departed are the NET membership change of the watched node since
+the previous drain (ascending ids), the fingerprint is reported when the map is non-empty and it
+differs from the last one reported (events.rs:103-122).  The CPU tests pin the oracle's batches to
+the diff of its own peer lists; the GPU tests require the HIP library's batches to equal the
+oracle's, unsharded and as row shards."""
+import ctypes as C
+
+import pytest
+
+import parity
+from kaboodle_amd._ffi import KB_INIT_CONVERGED, KbError, Sim, SimConfig
+
+
+def _cases():
+    by = {name: (case, rounds) for name, case, rounds in parity.standard_cases()}
+    return [
+        ("config1_2x2", *by["config1_2x2"], [0, 1, 2, 3], 1),
+        ("join_64", *by["join_64"], [0, 13, 63], 1),
+        ("churn_loss_512", *by["churn_loss_512"], [0, 1, 200, 511, 600], 1),
+        ("churn_loss_512_every3", *by["churn_loss_512"], [7, 300], 3),
+        ("stop_start", *by["stop_start"], [5, 17, 120, 0], 1),
+        ("partition_heal", *by["partition_heal"], [0, 128, 255], 2),
+    ]
+
+
+CASES = _cases()
+
+
+@pytest.mark.parametrize("name,case,rounds,watched,every", CASES, ids=[c[0] for c in CASES])
+def test_oracle_events_are_peer_list_diffs(name, case, rounds, watched, every):
+    lib = parity.oracle_lib()
+    ok, msg, n = parity.run_events_case(case, rounds, watched, every, libs=(lib, lib))
+    assert ok, f"{name}: {msg}"
+    assert n > 0
+
+
+def test_oracle_first_drain_reports_everything():
+    """Attached empty at creation (src/lib.rs:112): the first drain discovers every member, self
+    included, and reports the fingerprint (initial previous fingerprint 0)."""
+    with Sim(parity.oracle_lib(), SimConfig(capacity=64, initial_nodes=64, init_mode=KB_INIT_CONVERGED)) as s:
+        s.watch(3)
+        s.step(1)
+        d, p, fp, ch = s.events(3)
+        assert d == s.peers(3) and 3 in d and p == []
+        assert ch and fp == s.fingerprint(3)
+        # nothing changed since: empty batch, no fingerprint event
+        d, p, fp2, ch = s.events(3)
+        assert (d, p, ch) == ([], [], False) and fp2 == fp
+
+
+def test_oracle_events_errors_and_size_query():
+    lib = parity.oracle_lib()
+    with Sim(lib, SimConfig(capacity=32, initial_nodes=32, init_mode=KB_INIT_CONVERGED)) as s:
+        s.step(1)
+        nd, npp, fp, ch = C.c_size_t(), C.c_size_t(), C.c_uint32(), C.c_int()
+        with pytest.raises(KbError):                       # not watched
+            lib.call("sim_events", s.h, 1, None, 0, C.byref(nd), None, 0, C.byref(npp), C.byref(fp), C.byref(ch))
+        s.watch(1)
+        s.watch(1)                                         # idempotent
+        # size query drains nothing
+        lib.call("sim_events", s.h, 1, None, 0, C.byref(nd), None, 0, C.byref(npp), C.byref(fp), C.byref(ch))
+        assert nd.value == 32 and npp.value == 0 and ch.value == 1
+        small = (C.c_uint32 * 4)()
+        with pytest.raises(KbError):                       # too small: KB_CAPACITY, nothing drained
+            lib.call("sim_events", s.h, 1, small, 4, C.byref(nd), None, 0, C.byref(npp), C.byref(fp), C.byref(ch))
+        d, p, _, ch2 = s.events(1)
+        assert d == list(range(32)) and p == [] and ch2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", [0, 3], ids=["unsharded", "x3"])
+@pytest.mark.parametrize("name,case,rounds,watched,every", CASES, ids=[c[0] for c in CASES])
+def test_gpu_events_match_oracle(name, case, rounds, watched, every, shards):
+    import kaboodle_amd
+    kaboodle_amd.require_gpu()
+    if shards and case["cfg"].capacity < 9:
+        pytest.skip("too few ids for 3 shards")
+    ok, msg, n = parity.run_events_case(case, rounds, watched, every, shards=shards)
+    assert ok, f"{name}: {msg}"
+    assert n > 0
+
+
+@pytest.mark.gpu
+def test_gpu_events_64k_drain():
+    """Full workload width (capacity 71729, 2242 bitset words: three passes of the 1024-thread diff):
+    the first drain of a converged row is the whole row; after churn rounds the batch equals the
+    oracle-free peer-list diff of the HIP library itself."""
+    import kaboodle_amd
+    kaboodle_amd.require_gpu()
+    cfg = SimConfig(capacity=71729, initial_nodes=65536, init_mode=KB_INIT_CONVERGED, loss=0.01, churn=0.001,
+                    seed=1)
+    with Sim(parity.gpu_lib(), cfg) as g:
+        g.watch(12345)
+        g.step(1)
+        d, p, fp, ch = g.events(12345)
+        before = g.peers(12345)
+        assert d == before and p == [] and ch and fp == g.fingerprint(12345)
+        g.step(3)
+        d, p, fp2, ch = g.events(12345)
+        after = g.peers(12345)
+        assert d == sorted(set(after) - set(before)) and p == sorted(set(before) - set(after))
+        assert ch == (fp2 != fp)
