@@ -77,6 +77,22 @@ class Mesh {
       v.resize(n);
       return v;
     }
+    // events.rs:18-125 behind discover_peers / discover_departures / discover_fingerprint_changes
+    // (:186-263): watch() once, then events() after each step drains one batch
+    struct Events { std::vector<uint32_t> discovered, departed; bool fingerprint_changed; uint32_t fingerprint; };
+    void watch() { check(kb_sim_watch(h_, id_), "kb_sim_watch"); }
+    Events events() {
+      Events e;
+      size_t nd = 0, np = 0;
+      int ch = 0;
+      check(kb_sim_events(h_, id_, nullptr, 0, &nd, nullptr, 0, &np, &e.fingerprint, &ch), "kb_sim_events");
+      e.discovered.resize(nd);
+      e.departed.resize(np);
+      check(kb_sim_events(h_, id_, e.discovered.data(), nd, &nd, e.departed.data(), np, &np, &e.fingerprint, &ch),
+            "kb_sim_events");
+      e.fingerprint_changed = ch != 0;
+      return e;
+    }
    private:
     kb_sim* h_;
     uint32_t id_;

@@ -20,7 +20,11 @@ int main(int argc, char** argv) {
       p.set_identity(std::vector<uint8_t>(names[i], names[i] + strlen(names[i])));
       p.start();
     }
+    m.peer(0).watch();
     m.step(6);
+    auto ev = m.peer(0).events();                 // first batch: all four discovered (events.rs:59-79)
+    printf("events 0: disc %zu dep %zu changed %d fp %08x\n", ev.discovered.size(), ev.departed.size(),
+           (int)ev.fingerprint_changed, ev.fingerprint);
     for (uint32_t i = 0; i < 4; ++i) printf("peer %u fp %08x n %zu\n", i, m.peer(i).fingerprint(), m.peer(i).peers().size());
     printf("mesh ok\n");
   } catch (const kb::Error& e) {

@@ -40,4 +40,5 @@ def test_wrapper_host_side(tmp_path):
 @pytest.mark.gpu
 def test_wrapper_on_gpu(tmp_path):
     out = subprocess.run([build(tmp_path), "--gpu"], capture_output=True, text=True, check=True).stdout
-    assert out.count("fp 981285c8") == 4 and "mesh ok" in out
+    assert out.count("fp 981285c8") == 5 and "mesh ok" in out
+    assert "events 0: disc 4 dep 0 changed 1 fp 981285c8" in out
