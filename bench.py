@@ -226,6 +226,14 @@ def main() -> int:
                 "workload_tail_rounds_run": extra,
                 "workload_agree_frac_at_fault_end": round(st["agree"] / max(st["alive"], 1), 4),
                 "workload_agree_frac_final": round(s3["agree"] / max(s3["alive"], 1), 4)}
+        if not shard:
+            # how far the views are from agreement: |known_i| against the running count (0 = right size)
+            import numpy as np
+            sc = mesh.scalars()
+            live = sc[:, 0] != 0
+            gap = np.abs(sc[live, 1].astype(np.int64) - int(live.sum()))
+            conv["workload_view_size_match_frac_final"] = round(float((gap == 0).mean()), 4)
+            conv["workload_view_size_mean_gap_final"] = round(float(gap.mean()), 2)
 
     out = None
     if rank == 0:
