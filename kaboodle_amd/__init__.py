@@ -7,6 +7,7 @@ a GPU every entry point raises.
 """
 from __future__ import annotations
 
+import collections
 import os
 
 from ._ffi import (KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL, KB_INIT_CONVERGED, KB_INIT_JOIN,  # noqa: F401
@@ -51,9 +52,69 @@ class Mesh(Sim):
     def __init__(self, cfg: SimConfig | None = None, shards: int = 0, rank: int | None = None,
                  world: int | None = None, uid: bytes | None = None, **kw):
         super().__init__(lib(), cfg or SimConfig(**kw), shards=shards, rank=rank, world=world, uid=uid)
+        self._subs: dict[int, dict[str, list[Channel]]] = {}
 
     def node(self, i: int) -> "Kaboodle":
         return Kaboodle(self, i)
+
+    def subscribe(self, node: int, kind: str, ch: "Channel") -> "Channel":
+        """Add a discover_* channel of `node` (kind: peers | departures | fingerprints).  The first one
+        attaches the device observer and drains it, so channels see only later changes, as a channel
+        created on a running Kaboodle does (src/lib.rs:186-263)."""
+        if node not in self._subs:
+            self.watch(node)
+            self.events(node)
+            self._subs[node] = {"peers": [], "departures": [], "fingerprints": []}
+        self._subs[node][kind].append(ch)
+        return ch
+
+    def step(self, rounds: int = 1) -> None:
+        """Advance `rounds` rounds, then fan one event batch per observed node out to its channels
+        (handle_known_peers_events, src/events.rs:49-123)."""
+        super().step(rounds)
+        for node, subs in self._subs.items():
+            if not any(subs.values()):
+                continue
+            disc, dep, fp, changed = self.events(node)
+            for x in disc:
+                for c in subs["peers"]:
+                    c.send((self.format_addr(x), x))
+            for x in dep:
+                for c in subs["departures"]:
+                    c.send(self.format_addr(x))
+            if changed:
+                for c in subs["fingerprints"]:
+                    c.send(fp)
+            for k in subs:                        # closed channels are dropped (events.rs:29-38)
+                subs[k] = [c for c in subs[k] if not c.closed]
+
+
+class Channel:
+    """The receiving end of a discover_* channel (tokio UnboundedReceiver / oneshot Receiver in the
+    reference, src/lib.rs:186-263), filled by Mesh.step."""
+
+    def __init__(self, oneshot: bool = False):
+        self._q: collections.deque = collections.deque()
+        self.oneshot, self.closed = oneshot, False
+
+    def send(self, item) -> None:
+        if self.closed:
+            return
+        self._q.append(item)
+        if self.oneshot:
+            self.closed = True
+
+    def try_recv(self):
+        """The next item, or None when nothing is pending."""
+        return self._q.popleft() if self._q else None
+
+    def drain(self) -> list:
+        out = list(self._q)
+        self._q.clear()
+        return out
+
+    def close(self) -> None:
+        self.closed = True
 
 
 class Kaboodle:
@@ -85,6 +146,18 @@ class Kaboodle:
 
     def peers(self) -> dict:                      # src/lib.rs:339-345: addr -> identity
         return {self.mesh.format_addr(p): p for p in self.mesh.peers(self.id)}
+
+    def discover_peers(self) -> Channel:          # src/lib.rs:221-236: (addr, id) per new peer
+        return self.mesh.subscribe(self.id, "peers", Channel())
+
+    def discover_next_peer(self) -> Channel:      # src/lib.rs:238-263: the next one only
+        return self.mesh.subscribe(self.id, "peers", Channel(oneshot=True))
+
+    def discover_departures(self) -> Channel:     # src/lib.rs:185-199: addr per departed peer
+        return self.mesh.subscribe(self.id, "departures", Channel())
+
+    def discover_fingerprint_changes(self) -> Channel:   # src/lib.rs:201-219
+        return self.mesh.subscribe(self.id, "fingerprints", Channel())
 
     def peer_states(self) -> dict:                # src/lib.rs:348-354
         return {self.mesh.format_addr(p): (STATE_NAMES[s], since) for p, s, since in self.mesh.peer_states(self.id)}

@@ -104,3 +104,38 @@ def test_gpu_events_64k_drain():
         after = g.peers(12345)
         assert d == sorted(set(after) - set(before)) and p == sorted(set(before) - set(after))
         assert ch == (fp2 != fp)
+
+
+@pytest.mark.gpu
+def test_gpu_discover_channels_2x2():
+    """The Python mirror of discover_peers / discover_next_peer / discover_departures /
+    discover_fingerprint_changes (src/lib.rs:186-263) on the config-1 2x2 mesh: every peer is
+    discovered once, the last fingerprint reported is the golden 0x981285c8, and a stopped peer
+    (silent stop, src/lib.rs:159-183) arrives on the departure channel once it is removed."""
+    import kaboodle_amd
+    kaboodle_amd.require_gpu()
+    with kaboodle_amd.Mesh(SimConfig(capacity=4, initial_nodes=0)) as m:
+        names = [b"top-left", b"top-right", b"bottom-left", b"bottom-right"]
+        k = [m.node(i) for i in range(4)]
+        for i, n in enumerate(names):
+            k[i].set_identity(n)
+        peers, nxt = k[0].discover_peers(), k[0].discover_next_peer()
+        deps, fps = k[0].discover_departures(), k[0].discover_fingerprint_changes()
+        for x in k:
+            x.start()
+        m.step(6)
+        got = peers.drain()
+        assert sorted(i for _, i in got) == [0, 1, 2, 3]
+        assert got[0][0] == m.format_addr(got[0][1])
+        assert len(nxt.drain()) == 1 and nxt.closed
+        f = fps.drain()
+        assert f and f[-1] == 0x981285C8 == k[0].fingerprint()
+        k[3].stop()
+        for _ in range(30):
+            m.step(1)
+            if 3 not in m.peers(0):
+                break
+        assert 3 not in m.peers(0)
+        assert deps.drain() == [m.format_addr(3)]
+        assert peers.drain() == []
+        assert fps.drain()[-1] == k[0].fingerprint()
