@@ -111,15 +111,16 @@ def apply_events(sims, case: dict, r: int) -> None:
 
 
 def run_events_case(case: dict, rounds: int, watched, drain_every: int = 1, shards: int = 0,
-                    libs=None):
+                    libs=None, gpu: Sim | None = None):
     """Event streams (src/events.rs:18-125) on both implementations: every node in `watched` is
     observed from creation and drained every `drain_every` rounds.  Each batch must be identical
     across implementations and equal to the net diff of the oracle's peer lists.  libs = (oracle,
-    other) SimLibs; default (oracle, HIP library).  Returns (ok, message, batches compared)."""
+    other) SimLibs; default (oracle, HIP library); `gpu` = an already created handle (e.g. an RCCL
+    rank).  Returns (ok, message, batches compared)."""
     cfg = case["cfg"]
     la, lb = libs if libs is not None else (oracle_lib(), gpu_lib())
     o = Sim(la, cfg)
-    g = Sim(lb, cfg, shards=shards)
+    g = gpu if gpu is not None else Sim(lb, cfg, shards=shards)
     for s in (o, g):
         for i in watched:
             s.watch(i)

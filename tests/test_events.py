@@ -139,3 +139,17 @@ def test_gpu_discover_channels_2x2():
         assert deps.drain() == [m.format_addr(3)]
         assert peers.drain() == []
         assert fps.drain()[-1] == k[0].fingerprint()
+
+
+@pytest.mark.gpu
+def test_gpu_events_rccl_rank_world1():
+    """Event drains on the RCCL transport's handle (kb_sim_create_rank, 1-rank communicator)."""
+    import kaboodle_amd
+    kaboodle_amd.require_gpu()
+    from kaboodle_amd._ffi import rccl_unique_id
+    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}["churn_loss_512"]
+    lib = parity.gpu_lib()
+    g = Sim(lib, case["cfg"], rank=0, world=1, uid=rccl_unique_id(lib))
+    ok, msg, n = parity.run_events_case(case, rounds, [0, 300, 600], gpu=g)
+    assert ok, msg
+    assert n > 0
