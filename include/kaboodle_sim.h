@@ -73,8 +73,22 @@ typedef struct kb_config {
   int32_t  partition_start;  /* cross-group deliveries dropped for partition_start <= r < partition_end */
   int32_t  partition_end;
   int32_t  device;           /* HIP device ordinal, -1 = current device (ignored by the oracle)      */
-  uint32_t reserved[6];
+  uint32_t debug_flags;      /* KB_DBG_*: force the wide-row (HBM) kernel variants at any size; results
+                                are identical with any value (test surface, ignored by the oracle)   */
+  uint32_t track_latency;    /* 1: keep the per-(node, peer) ping latency EWMA of peer_states
+                                (src/kaboodle.rs:789-817); 0: latency reported as none (no table)    */
+  uint32_t reserved[4];
 } kb_config;
+
+/* debug_flags: each forces the code path a mesh of >= 1M ids takes, so that path is
+   parity-tested at sizes the oracle finishes in seconds. */
+enum {
+  KB_DBG_PHASEB_HBM = 1u,    /* broadcast phase on the HBM bitset (rows > PB_LDS_W ids), lists from HBM */
+  KB_DBG_RESP_HBM = 2u,      /* Join responses by workgroup with HBM scratch (rows > RESP_LDS_W ids)     */
+  KB_DBG_KP_HBM = 4u,        /* KnownPeers groups on the HBM bitset, one workgroup per destination      */
+  KB_DBG_KP_BIG_SMALL = 8u,  /* every KnownPeers group takes the BIG (1024-thread) kernel                */
+  KB_DBG_PROC_UNSORTED = 16u /* inboxes > 64 taken by k_proc's selection path (inboxes > SORT_MAX)       */
+};
 
 /* Per-peer state as reported by peer_states() (PeerState, src/structs.rs:27-41). */
 enum { KB_STATE_KNOWN = 0, KB_STATE_WAITING_FOR_PING = 1, KB_STATE_WAITING_FOR_INDIRECT_PING = 2 };
@@ -82,8 +96,10 @@ typedef struct kb_peer_state {
   uint32_t peer;             /* peer id                                                             */
   uint32_t state;            /* KB_STATE_*                                                          */
   int32_t  since;            /* round of the state's Instant; INT32_MIN = older than the stamp window */
-  uint32_t reserved;
+  uint32_t latency_ms;       /* PeerInfo.latency in simulated ms; KB_LATENCY_NONE =
+                                None (never measured, or track_latency off)                          */
 } kb_peer_state;
+#define KB_LATENCY_NONE 0xFFFFFFFFu
 
 /* Cumulative counters since creation (all ranks summed when sharded). */
 typedef struct kb_stats {
@@ -169,6 +185,11 @@ int  kb_sim_dump_row(kb_sim* sim, uint32_t node, uint8_t* row, size_t cap);
 int  kb_sim_dump_scalars(kb_sim* sim, int32_t* out, size_t cap);
 /* Canonical suspect table: sorted (peer, kind, since) triples for `node`; n = triples written.      */
 int  kb_sim_dump_suspects(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, size_t* n);
+/* OR of the kernel-variant bits that did work since creation (PATH_* in kaboodle_amd/csrc/kb_common.h:
+   1 broadcast phase on the HBM bitset, 2/4 Join responses from HBM scratch (sampled / complete),
+   8 KnownPeers BIG group on the HBM bitset, 16 k_proc unsorted selection path, 32 Failed-list prep
+   from HBM, 64 Join responses by wave, 128 KnownPeers BIG group in LDS).  Test surface.           */
+int  kb_sim_debug_paths(kb_sim* sim, uint32_t* mask);
 /* Canonical curious table: for each entry sorted by peer: peer, nobs, obs[0..3] (6 x int32).       */
 int  kb_sim_dump_curious(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, size_t* n);
 

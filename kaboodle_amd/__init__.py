@@ -159,5 +159,11 @@ class Kaboodle:
     def discover_fingerprint_changes(self) -> Channel:   # src/lib.rs:201-219
         return self.mesh.subscribe(self.id, "fingerprints", Channel())
 
-    def peer_states(self) -> dict:                # src/lib.rs:348-354
-        return {self.mesh.format_addr(p): (STATE_NAMES[s], since) for p, s, since in self.mesh.peer_states(self.id)}
+    def peer_states(self) -> dict:                # src/lib.rs:348-354: addr -> (state, since, latency)
+        """PeerInfo per known peer: state name, round of its Instant (None = older than the stamp window),
+        latency in simulated ms (None = never measured, as PeerInfo.latency, src/structs.rs:18-22)."""
+        out = {}
+        for p, s, since, lat in self.mesh.peer_states(self.id):
+            out[self.mesh.format_addr(p)] = (STATE_NAMES[s], None if since == -2**31 else since,
+                                             None if lat == 0xFFFFFFFF else lat)
+        return out

@@ -14,6 +14,9 @@ KB_ABI_VERSION = 1
 KB_OK, KB_INVALID_OPERATION, KB_IO_ERROR, KB_NO_DEVICE, KB_STOPPING_FAILED, KB_INVALID_ARGUMENT, KB_CAPACITY = range(7)
 KB_INIT_JOIN, KB_INIT_CONVERGED = 0, 1
 KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL = 0, 1
+KB_DBG_PHASEB_HBM, KB_DBG_RESP_HBM, KB_DBG_KP_HBM, KB_DBG_KP_BIG_SMALL, KB_DBG_PROC_UNSORTED = 1, 2, 4, 8, 16
+KB_DBG_ALL = 31
+KB_LATENCY_NONE = 0xFFFFFFFF
 STATE_NAMES = {0: "Known", 1: "WaitingForPing", 2: "WaitingForIndirectPing"}
 
 
@@ -24,12 +27,12 @@ class KbConfig(C.Structure):
         ("churn_threshold", C.c_uint32), ("fault_end_round", C.c_int32), ("max_waves", C.c_uint32),
         ("failed_mode", C.c_uint32), ("id_len", C.c_uint32), ("partition_groups", C.c_uint32),
         ("partition_start", C.c_int32), ("partition_end", C.c_int32), ("device", C.c_int32),
-        ("reserved", C.c_uint32 * 6),
+        ("debug_flags", C.c_uint32), ("track_latency", C.c_uint32), ("reserved", C.c_uint32 * 4),
     ]
 
 
 class KbPeerState(C.Structure):
-    _fields_ = [("peer", C.c_uint32), ("state", C.c_uint32), ("since", C.c_int32), ("reserved", C.c_uint32)]
+    _fields_ = [("peer", C.c_uint32), ("state", C.c_uint32), ("since", C.c_int32), ("latency_ms", C.c_uint32)]
 
 
 class KbStats(C.Structure):
@@ -73,6 +76,8 @@ class SimConfig:
     partition_start: int = 0
     partition_end: int = 0
     device: int = -1
+    debug_flags: int = 0         # KB_DBG_*: force the wide-row kernel variants (test surface)
+    track_latency: int = 0       # 1: keep the ping-latency EWMA reported by peer_states
 
     def to_c(self) -> KbConfig:
         c = KbConfig()
@@ -86,6 +91,7 @@ class SimConfig:
         c.partition_groups, c.partition_start, c.partition_end = (
             self.partition_groups, self.partition_start, self.partition_end)
         c.device = self.device
+        c.debug_flags, c.track_latency = self.debug_flags, self.track_latency
         return c
 
 
@@ -129,6 +135,7 @@ _OPTIONAL = {
     "sim_kernel_time": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "sim_reset_kernel_time": (C.c_int, [C.c_void_p]),
     "sim_sweep_bytes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "sim_debug_paths": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
 }
 
 
@@ -284,7 +291,7 @@ class Sim:
         self.lib.call("sim_peer_states", self.h, node, None, 0, C.byref(n))
         arr = (KbPeerState * max(n.value, 1))()
         self.lib.call("sim_peer_states", self.h, node, arr, n.value, C.byref(n))
-        return [(a.peer, a.state, a.since) for a in arr[: n.value]]
+        return [(a.peer, a.state, a.since, a.latency_ms) for a in arr[: n.value]]
 
     def stats(self) -> dict:
         st = KbStats()
@@ -332,6 +339,14 @@ class Sim:
 
     def reset_kernel_time(self) -> None:
         self.lib.call("sim_reset_kernel_time", self.h)
+
+    def debug_paths(self) -> int:
+        """OR of the kernel-variant bits (PATH_* of kb_common.h) that did work; 0 for the oracle."""
+        if "sim_debug_paths" not in self.lib.fn:
+            return 0
+        v = C.c_uint32()
+        self.lib.call("sim_debug_paths", self.h, C.byref(v))
+        return v.value
 
     def sweep_bytes(self) -> int:
         v = C.c_uint64()

@@ -22,8 +22,13 @@ enum StatIdx {
 };
 enum CtrIdx {
   C_KP, C_SLOW, C_ACTIVE, C_AGREE, C_ALIVE, C_LEAVES, C_NEXTFREE, C_ERR, C_FIRSTCONV, C_LASTCONV, C_LASTAGREE,
-  C_LASTALIVE, C_DBG_INS, C_DBG_FP, C_DBG_MAXFP, C_TICK, NCTR
+  C_LASTALIVE, C_DBG_INS, C_DBG_FP, C_DBG_MAXFP, C_TICK,
+  C_PATHS,                        // OR of the PATH_* bits of the kernel variants that did work (test surface)
+  NCTR
 };
+// kernel-variant coverage bits (kb_sim_debug_paths): the wide-row paths a >= 1M-id mesh takes
+enum : uint32_t { PATH_PHASEB_HBM = 1, PATH_RESP_SCRATCH_SAMPLED = 2, PATH_RESP_SCRATCH_FULL = 4, PATH_KP_BIG_HBM = 8,
+                  PATH_PROC_UNSORTED = 16, PATH_BFAIL_PREP_HBM = 32, PATH_RESP_WAVE = 64, PATH_KP_BIG_LDS = 128 };
 constexpr int NSEG = 64;          // fingerprint checkpoints per row
 constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
 constexpr int ZB = 9 * 1024;      // byte tables for Z^0..Z^8 (4 lookups per multiply)
@@ -45,6 +50,7 @@ struct Dev {
   uint32_t capk, capj;            // KnownPeers caps: KPR reply (size <= 10240), Join response (size < 10240)
   uint32_t paybound;              // payload entries reserved per KPR reply
   uint32_t ablate;                // timing experiments only (env KB_ABLATE): 1 = no fold in sweep, 2 = no A3
+  uint32_t dbg;                   // kb_config.debug_flags (KB_DBG_*): force the wide-row kernel variants
   uint8_t* stamp;
   uint32_t* bits;
   uint2* segp;
@@ -71,6 +77,7 @@ struct Dev {
   unsigned long long* stats;
   uint32_t* ctr;
   uint32_t* truefp;
+  uint2* tfpart;                  // [64] ordered partials of the running set's fingerprint
   uint32_t* flog;
   uint32_t* flog_n;
   uint32_t* fstart;
@@ -101,6 +108,7 @@ __device__ __attribute__((always_inline)) inline void stage16(uint4* dst, const 
   }
 }
 __device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }
+__device__ inline void path_hit(const Dev& d, uint32_t bit) { atomicOr(&d.ctr[C_PATHS], bit); }
 __device__ inline bool faults(const Dev& d, int32_t r) { return d.fault_end < 0 || r < d.fault_end; }
 __device__ inline bool local(const Dev& d, uint32_t i) { return i >= d.lo && i < d.hi; }
 __device__ inline bool part_blocks(const Dev& d, int32_t r, uint32_t a, uint32_t b) {

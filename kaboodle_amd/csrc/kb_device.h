@@ -24,7 +24,6 @@ constexpr int PAQ = 8;              // queued ping_addrs per node
 constexpr int MAXID = 32;           // identity bytes
 constexpr int ADDR_LEN = 20;        // "10.100.100.ddd:ppppp"
 constexpr int TICK_MAX = 3 * SLOTS + 1 + PAQ;   // unicast emissions of one tick
-constexpr int FLOYD_MAX_N = 262144; // LDS bitmap bound for truncated Join responses
 constexpr uint32_t LOGCAP = 2048;    // freshness log entries per node (power of two)
 constexpr uint32_t LOG_INVALID = 0xFFFFFFFFu;
 // stamp byte encoding

@@ -71,14 +71,19 @@ __global__ void k_alive_bits(Dev d) {
   const unsigned long long t = block_sum(cnt);
   if (threadIdx.x == 0 && t) atomicAdd(&d.ctr[C_ALIVE], (uint32_t)t);
 }
-__global__ __launch_bounds__(1024) void k_truefp(Dev d) {
+// The running set's fingerprint in two launches: TRUEFP_G workgroups fold consecutive word ranges of
+// `abits` into ordered partials (thread folds, then a tree combine in LDS), one wave combines them.
+constexpr uint32_t TRUEFP_G = 64;
+__global__ __launch_bounds__(256) void k_truefp_part(Dev d, uint2* part) {
   __shared__ uint32_t ztab[ZT * 128];
-  __shared__ uint32_t sraw[1024], scnt[1024];
+  __shared__ uint32_t sraw[256], scnt[256];
   load_ztab(d, ztab);
-  const uint32_t T = blockDim.x, t = threadIdx.x;
+  const uint32_t T = blockDim.x, t = threadIdx.x, g = blockIdx.x;
+  const uint32_t wpg = (d.NWR + TRUEFP_G - 1) / TRUEFP_G, wg0 = g * wpg;
+  const uint32_t wg1 = wg0 + wpg < d.NWR ? wg0 + wpg : d.NWR;
   uint32_t raw = 0, cnt = 0;
-  const uint32_t per = (d.NWR + T - 1) / T;
-  for (uint32_t w = t * per; w < (t + 1) * per && w < d.NWR; ++w) {
+  const uint32_t per = wg1 > wg0 ? (wg1 - wg0 + T - 1) / T : 0;
+  for (uint32_t w = wg0 + t * per; w < wg0 + (t + 1) * per && w < wg1; ++w) {
     uint32_t x = d.abits[w];
     if (!x) continue;
     if (d.uniform) {
@@ -97,8 +102,15 @@ __global__ __launch_bounds__(1024) void k_truefp(Dev d) {
     if (w) { sraw[t] = nr; scnt[t] = nc; }
     __syncthreads();
   }
-  if (t == 0) d.truefp[0] = finish_fp(d, sraw[0], scnt[0]);
+  if (t == 0) part[g] = make_uint2(sraw[0], scnt[0]);
 }
+__global__ __launch_bounds__(64) void k_truefp_fin(Dev d, const uint2* part) {
+  const uint2 p = part[lane()];                       // TRUEFP_G == 64: one partial per lane
+  uint32_t raw = p.x, cnt = p.y;
+  wave_combine(d, raw, cnt);
+  if (lane() == 0) d.truefp[0] = finish_fp(d, raw, cnt);
+}
+static_assert(TRUEFP_G == 64, "k_truefp_fin combines one partial per lane");
 
 // round start of every node's freshness log window
 __global__ void k_log_mark(Dev d, int32_t r) {
@@ -125,9 +137,10 @@ __device__ inline bool bcast_lost(const Dev& d, uint32_t recv, const BCast& b, i
 }
 
 // Per-list facts about the Failed broadcasts (identical for every receiver).
-__global__ void k_bfail_prep(const BCast* bf, uint32_t nf, uint32_t* gid, uint8_t* dep) {
+__global__ void k_bfail_prep(const BCast* bf, uint32_t nf, uint32_t* gid, uint8_t* dep, uint32_t* paths) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= nf) return;
+  if (q == 0) atomicOr(paths, PATH_BFAIL_PREP_HBM);
   const uint32_t p = bf[q].peer, sn = bf[q].sender;
   uint32_t g = q; uint8_t dp = 0;
   for (uint32_t k = 0; k < q; ++k) {
@@ -208,7 +221,7 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
   const uint8_t now = enc(r, r);
   // counters stay in registers for the whole persistent loop: one atomic per wave at the end (same-
   // address atomics from every node would serialise in L2 and stall the waves that wait on them)
-  unsigned long long w_lost = 0, w_removed = 0, w_resp = 0;
+  unsigned long long w_lost = 0, w_removed = 0, w_resp = 0, w_nodes = 0;
   for (uint32_t i = d.lo + blockIdx.x * wpb + wv; i < d.hi; i += gridDim.x * wpb) {
     if (!d.alive[i] || d.start_round[i] >= r) {
       if (l == 0) { pb.nresp[i] = 0; pb.paysum[i] = 0; }
@@ -330,7 +343,7 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
       if (n != n0) d.dirty[i] = 1;
       pb.nresp[i] = nresp; pb.paysum[i] = paysum; pb.nbase[i] = nbase;
     }
-    w_lost += lost_cnt; w_removed += removed_cnt; w_resp += nresp;
+    w_lost += lost_cnt; w_removed += removed_cnt; w_resp += nresp; w_nodes++;
     wait_lds();                                       // LDS bitset is reused by the next node
     __builtin_amdgcn_wave_barrier();
   }
@@ -338,6 +351,7 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
     if (w_lost) atomicAdd(&d.stats[S_BDROP], w_lost);
     if (w_removed) atomicAdd(&d.stats[S_RMFAILED], w_removed);
     if (w_resp) atomicAdd(&d.stats[S_JRESP], w_resp);
+    if (!LDSB && w_nodes) path_hit(d, PATH_PHASEB_HBM);
   }
 }
 
@@ -460,6 +474,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     uint32_t nnew = 0;
     for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
     if (!resp_by_wave(d, i, nnew, true)) continue;          // wave-uniform: k_resp_node serves it
+    if (l == 0) path_hit(d, PATH_RESP_WAVE);
     const uint32_t* B = bits_of(d, i);                      // row membership after the Join group
     const uint4* B4 = reinterpret_cast<const uint4*>(B);
     const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
@@ -647,6 +662,7 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
           Msg m; m.dest = a; m.sender = i; m.seq = q; m.kind = K_KP; m.a = cap; m.fp = 0; m.n = 0; m.off = poff;
           ob.msgs[ob.off[i] + q] = m;
           if (nk != expect) set_err(d, DERR_RESP);
+          if (gscratch) path_hit(d, sample ? PATH_RESP_SCRATCH_SAMPLED : PATH_RESP_SCRATCH_FULL);
         }
         poff += cap; q++;
         __syncthreads();

@@ -473,6 +473,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   d.capj = (BUFSZ - 20 - Lid - 1) / (18 + Lid);       // 20 + L + k(18+L) <  10240
   d.paybound = C < d.capk ? C : d.capk;
   if (const char* ab = getenv("KB_ABLATE")) d.ablate = (uint32_t)atoi(ab);
+  d.dbg = cfg->debug_flags;
   s->debug_waves = getenv("KB_DEBUG_WAVES") != nullptr;
   s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid); s->h_ever.assign(C, 0);
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &s->h_ident[(size_t)j * MAXID]);
@@ -485,7 +486,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   AR(d.last_bcast, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
   AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
   A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
-  A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1);
+  A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
   s->msg_cap = std::max<uint32_t>(8u * R + (uint32_t)TICK_MAX * R, 1u << 16);
   s->pay_cap = std::max<uint32_t>((d.capk + 1) * R, 1u << 24);
@@ -722,7 +723,8 @@ static int step_round(kb_sim* s) {
     k_churn_join<<<1, 1024, 0, st>>>(d, r);
   }
   k_alive_bits<<<(d.NWR + tb - 1) / tb, tb, 0, st>>>(d);
-  k_truefp<<<1, 1024, 0, st>>>(d);
+  k_truefp_part<<<TRUEFP_G, 256, 0, st>>>(d, d.tfpart);
+  k_truefp_fin<<<1, 64, 0, st>>>(d, d.tfpart);
   k_log_mark<<<gnode, tb, 0, st>>>(d, r);
   // 2. broadcasts of round r-1
   OutBuf& o0 = s->ob[0];
@@ -744,15 +746,16 @@ static int step_round(kb_sim* s) {
   pb.newmask = s->newmask; pb.respmask = s->respmask;
   pb.gid = s->bf_gid; pb.dep = s->bf_dep;
   const bool have_b = s->nf + s->nj > 0;
-  if (s->nf > 2048) k_bfail_prep<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep);
+  const bool pb_hbm = (d.dbg & KB_DBG_PHASEB_HBM) != 0;
+  if (s->nf > 2048 || (pb_hbm && s->nf)) k_bfail_prep<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep, d.ctr + C_PATHS);
   else if (s->nf) k_bfail_prep_lds<<<1, 1024, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep);
   if (have_b) {
     // persistent waves; broadcast lists staged in LDS once per workgroup when they fit
     const uint32_t budget = 65536 / 4;                 // dynamic LDS words per workgroup
     uint32_t lf = s->nf <= PB_FMAX, lj = s->nj <= PB_JMAX;
     uint32_t listw = (lf ? 2 * s->nf : 0) + (lj ? s->nj : 0);
-    if (listw > budget / 2) { lf = lj = 0; listw = 0; }
-    const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR;
+    if (listw > budget / 2 || pb_hbm) { lf = lj = 0; listw = 0; }
+    const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR && !pb_hbm;
     const uint32_t wpb = ldsb ? std::min<uint32_t>(4, (budget - listw) / d.NWR) : 4;
     const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)(s->lds_per_cu / std::max<size_t>(lds + 512, 1))));
@@ -786,7 +789,8 @@ static int step_round(kb_sim* s) {
       const size_t words = resp_words(d.NWR, s->W / 256);
       uint32_t* scratch = nullptr;
       size_t lds = 4 * words;
-      if (s->W > RESP_LDS_W) {
+      const bool resp_hbm = s->W > RESP_LDS_W || (d.dbg & KB_DBG_RESP_HBM);
+      if (resp_hbm) {
         if (s->resp_scratch_words < words * grid) {
           if (s->resp_scratch) (void)hipFree(s->resp_scratch);
           HIPCHK(hipMalloc(&s->resp_scratch, 4 * words * grid));
@@ -797,7 +801,7 @@ static int step_round(kb_sim* s) {
       }
       // a wave per responder where its LDS slice fits (4 responders per 64 KB workgroup), else a workgroup
       const size_t wlds = 16ull * rwave_words(d.NWR, s->W / 256);
-      const bool wave_on = wlds <= 65536;
+      const bool wave_on = wlds <= 65536 && !(d.dbg & KB_DBG_RESP_HBM);
       if (wave_on)
         k_resp_wave<<<std::min<uint32_t>((resp_nodes + 3) / 4, 4096), 256, wlds, st>>>(d, pb, s->resp_nodes,
                                                                                      s->scan_tot + 4, o0, r);
@@ -868,7 +872,7 @@ static int step_round(kb_sim* s) {
     else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
     k_kp_small<<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r, nb);   // also sets up nb.cap / nb.cnt
     {  // BIG groups in LDS: KP_COLS workgroups per destination group, one per column quarter
-      const uint32_t ks = d.NWR <= KP_LDS_WORDS ? KP_COLS : 1u;
+      const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
       const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
       k_kp_group<true><<<ks * groups, 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
     }
@@ -1076,7 +1080,8 @@ extern "C" int kb_sim_true_fingerprint(kb_sim* s, uint32_t* fp) {
   if (!s || !fp) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_true_fingerprint(s->shards[0], fp);
   k_alive_bits<<<(s->d.NWR + 255) / 256, 256, 0, s->st>>>(s->d);
-  k_truefp<<<1, 1024, 0, s->st>>>(s->d);
+  k_truefp_part<<<TRUEFP_G, 256, 0, s->st>>>(s->d, s->d.tfpart);
+  k_truefp_fin<<<1, 64, 0, s->st>>>(s->d, s->d.tfpart);
   HIPCHK(hipMemsetAsync(s->d.ctr + C_ALIVE, 0, 4, s->st));
   HIPCHK(hipMemcpyAsync(fp, s->d.truefp, 4, hipMemcpyDeviceToHost, s->st));
   HIPCHK(hipStreamSynchronize(s->st));
@@ -1119,7 +1124,7 @@ extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, 
     if (!rw[j]) continue;
     if (out && c < cap) {
       kb_peer_state& o = out[c];
-      o.peer = j; o.reserved = 0;
+      o.peer = j; o.latency_ms = KB_LATENCY_NONE;
       if (rw[j] == ST_SUSPECT) {
         const Susp* q = nullptr;
         for (auto& x : sl) if (x.kind && x.peer == j) q = &x;
@@ -1316,5 +1321,17 @@ extern "C" int kb_sim_sweep_bytes(kb_sim* s, uint64_t* bytes) {
   if (!s || !bytes) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_sweep_bytes(s->shards[0], bytes);
   *bytes = sweep_counter(s) - s->sweep_bytes;
+  return KB_OK;
+}
+// OR of the PATH_* bits (kb_common.h) of the kernel variants that did work since creation
+extern "C" int kb_sim_debug_paths(kb_sim* s, uint32_t* mask) {
+  if (!s || !mask) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) {
+    uint32_t m = 0;
+    for (kb_sim* t : s->shards) { uint32_t x = 0; const int rc = kb_sim_debug_paths(t, &x); if (rc) return rc; m |= x; }
+    *mask = m;
+    return KB_OK;
+  }
+  HIPCHK(hipMemcpy(mask, s->d.ctr + C_PATHS, 4, hipMemcpyDeviceToHost));
   return KB_OK;
 }

@@ -277,7 +277,8 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
   const uint32_t t = threadIdx.x, T = blockDim.x;
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
-  const bool lds = BIG && d.NWR <= KP_LDS_WORDS;
+  const bool lds = BIG && d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM);
+  const uint32_t kpb = (d.dbg & KB_DBG_KP_BIG_SMALL) ? 0u : KP_BIG;
   const uint32_t KS = lds ? KP_COLS : 1u, part = blockIdx.x % KS, G = gridDim.x / KS, g = blockIdx.x / KS;
   const uint32_t w0 = part * (d.NWR / KS), w1 = w0 + d.NWR / KS;   // this workgroup's bitset words
   // the active list T entries per workgroup group at a time, interleaved over the groups (consecutive
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
   __syncthreads();
   if (it < nact) {
     const uint32_t x = wc.active[it];
-    if (wc.kcnt[x] && (wc.kpay[x] >= KP_BIG) == BIG) s_list[atomicAdd(&s_nl, 1u)] = x;
+    if (wc.kcnt[x] && (wc.kpay[x] >= kpb) == BIG) s_list[atomicAdd(&s_nl, 1u)] = x;
   }
   __syncthreads();
   const uint32_t nl = s_nl;
@@ -386,6 +387,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
       if (KS > 1) atomicAdd(&d.n[i], s_add); else d.n[i] += s_add;
       mark(d, i, sg);
     }
+    if (BIG && t == 0 && li == 0) path_hit(d, lds ? PATH_KP_BIG_LDS : PATH_KP_BIG_HBM);
     __syncthreads();                                   // LDS reused by the next destination
   }
   }
@@ -402,13 +404,14 @@ __global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, 
   }
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
+  const uint32_t kpb = (d.dbg & KB_DBG_KP_BIG_SMALL) ? 0u : KP_BIG;
   for (uint32_t c0 = 0; c0 < nact; c0 += gridDim.x * 256) {
     const uint32_t it = c0 + t * gridDim.x + blockIdx.x;   // interleaved over the workgroups
     if (t == 0) s_nl = 0;
     __syncthreads();
     if (it < nact) {
       const uint32_t x = wc.active[it];
-      if (wc.kcnt[x] && wc.kpay[x] < KP_BIG) s_list[atomicAdd(&s_nl, 1u)] = x;
+      if (wc.kcnt[x] && wc.kpay[x] < kpb) s_list[atomicAdd(&s_nl, 1u)] = x;
     }
     __syncthreads();
     const uint32_t nl = s_nl;
@@ -467,6 +470,7 @@ __global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, 
 // index, one workgroup per node, bitonic in LDS (up to SORT_MAX entries; longer ones keep the
 // selection path of k_proc)
 constexpr uint32_t SORT_MAX = 8192;
+__device__ inline uint32_t sort_max(const Dev& d) { return (d.dbg & KB_DBG_PROC_UNSORTED) ? 64u : SORT_MAX; }
 __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc) {
   __shared__ uint32_t v[SORT_MAX];
   __shared__ uint32_t s_list[1024], s_nl;
@@ -480,7 +484,7 @@ __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc) {
   if (it < nact) {
     const uint32_t x = wc.active[it];
     const uint32_t c = wc.cnt1[x];
-    if (c > 64 && c <= SORT_MAX) s_list[atomicAdd(&s_nl, 1u)] = x;
+    if (c > 64 && c <= sort_max(d)) s_list[atomicAdd(&s_nl, 1u)] = x;
   }
   __syncthreads();
   const uint32_t nl = s_nl;
@@ -644,7 +648,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     // canonical order = ascending outbox index = (sender, seq): one wave sorts <= 64 entries in
     // registers; k_sort_inbox has sorted longer inboxes up to SORT_MAX in place
     uint32_t mine = l < icnt ? wc.inbox[ibase + l] : 0xFFFFFFFFu;
-    const bool small = icnt <= 64, sorted = icnt <= SORT_MAX;
+    const bool small = icnt <= 64, sorted = icnt <= sort_max(d);
     if (small) {
 #pragma unroll
       for (int k = 2; k <= 64; k <<= 1) {
@@ -788,6 +792,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
         }
         g = bcast(mine, (int)(t & 63));
       } else {      // beyond SORT_MAX: next smallest index above the previous one
+        if (t == 0 && l == 0) path_hit(d, PATH_PROC_UNSORTED);
         uint32_t best = 0xFFFFFFFFu;
         for (uint32_t q = l; q < icnt; q += 64) {
           const uint32_t v = wc.inbox[ibase + q];

@@ -100,7 +100,6 @@ struct kbo_sim {
   oevent* ev; size_t nev, capev;
   ovec* out;                  /* per-node outbox of the wave being produced */
   uint32_t* oseq;             /* per-node emission counter for the wave being produced */
-  int32_t* a3fp;              /* unused */
   kb_stats st;
   /* event observers (kbo_sim_watch): watched node, its membership at the last drain, last reported fp */
   uint32_t* wnode; uint8_t** wsnap; uint32_t* wfp; size_t nwatch;
@@ -352,7 +351,8 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   }
   s->uniform = 1; s->ulen = ADDR_LEN + cfg->id_len; build_mulz(s);
   s->round = 0; s->next_free = cfg->initial_nodes;
-  for (uint32_t i = 0; i < cfg->initial_nodes; ++i) {
+#pragma omp parallel for schedule(static)
+  for (uint32_t i = 0; i < cfg->initial_nodes; ++i) {   /* touches row i and per-id slots of i only */
     node_start(s, i, 0);
     if (cfg->init_mode == KB_INIT_CONVERGED) {
       uint8_t* rw = row(s, i);
@@ -915,12 +915,14 @@ int kbo_sim_peer_states(kbo_sim* s, uint32_t node, kb_peer_state* out, size_t ca
   if (check(s, node) || !n) return KB_INVALID_ARGUMENT;
   const uint8_t* rw = row(s, node);
   size_t c = 0;
-  int32_t E = epoch_base(s->round);
+  /* the stamps hold the encoding of the last simulated round (the window is rebased at the START of
+   * a round, step_round above), so their base is epoch_base(round - 1), not epoch_base(round) */
+  int32_t E = epoch_base(s->round > 0 ? s->round - 1 : 0);
   for (uint32_t j = 0; j < s->C; ++j) {
     if (!rw[j]) continue;
     if (out && c < cap) {
       kb_peer_state* o = &out[c];
-      o->peer = j; o->reserved = 0;
+      o->peer = j; o->latency_ms = KB_LATENCY_NONE;
       if (rw[j] == ST_SUSPECT) {
         osusp* q = susp_find(s, node, j);
         o->state = q && q->kind == SK_WFIP ? KB_STATE_WAITING_FOR_INDIRECT_PING : KB_STATE_WAITING_FOR_PING;

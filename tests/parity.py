@@ -75,11 +75,32 @@ def setup(sim: Sim, case: dict) -> None:
         sim.start_node(i)
 
 
+def diff_peer_states(o: Sim, g: Sim, nodes) -> list[str]:
+    """Kaboodle::peer_states (src/lib.rs:348-354) of `nodes` on both implementations: (peer, state,
+    since round, latency) for every entry; it must also list exactly the ids peers() reports."""
+    out = []
+    for i in nodes:
+        a, b = o.peer_states(int(i)), g.peer_states(int(i))
+        if a != b:
+            bad = [(x, y) for x, y in zip(a, b) if x != y][:2]
+            out.append(f"peer_states[{i}]: {len(a)} vs {len(b)} entries, first differing {bad}")
+            break
+        if [p for p, *_ in b] != g.peers(int(i)):
+            out.append(f"peer_states[{i}] ids != peers()")
+            break
+    return out
+
+
+def with_cfg(case: dict, **kw) -> dict:
+    """The case with config fields replaced (e.g. debug_flags=KB_DBG_ALL)."""
+    return {**case, "cfg": replace(case["cfg"], **kw)}
+
+
 def run_case(case: dict, rounds: int, check_every: int = 1, full_rows: bool = True, verbose: bool = False,
-             shards: int = 0, gpu: Sim | None = None):
+             shards: int = 0, gpu: Sim | None = None, peer_states: bool = False):
     """Run `case` on both implementations; returns (ok, message, final gpu stats).  shards=k runs the
     GPU mesh as k row shards exchanging every wave (kb_sim_create_local); `gpu` = an already created
-    GPU handle for the case (e.g. an RCCL rank)."""
+    GPU handle for the case (e.g. an RCCL rank); peer_states: also compare peer_states() of every node."""
     cfg = case["cfg"]
     o = Sim(oracle_lib(), cfg)
     g = gpu if gpu is not None else Sim(gpu_lib(), cfg, shards=shards)
@@ -91,12 +112,37 @@ def run_case(case: dict, rounds: int, check_every: int = 1, full_rows: bool = Tr
         g.step(1)
         if (r + 1) % check_every == 0 or r == rounds - 1:
             d = diff_states(state_of(o, full_rows), state_of(g, full_rows))
+            if not d and peer_states:
+                d = diff_peer_states(o, g, range(cfg.capacity))
             if d:
                 return False, f"round {r}: " + "; ".join(d[:6]), g.stats()
             if verbose:
                 st = g.stats()
                 print(f"  round {r}: agree {st['agree']}/{st['alive']} ok", flush=True)
     return True, "ok", g.stats()
+
+
+def compare_sampled(o: Sim, g: Sim, rng, nrows: int = 24) -> list[str]:
+    """Full-size comparison after a round: counters, every fingerprint and per-node scalar, and for a
+    random sample of nodes the whole stamp row, suspect/curious tables and peer_states."""
+    out = []
+    so, sg = o.stats(), g.stats()
+    out += [f"stats.{k}: {v} != {sg[k]}" for k, v in so.items() if sg[k] != v]
+    fo, fg = o.fingerprints(), g.fingerprints()
+    if not np.array_equal(fo, fg):
+        out.append(f"fingerprints: {int((fo != fg).sum())} differ, first {np.argwhere(fo != fg)[:3].ravel().tolist()}")
+    if not np.array_equal(o.scalars(), g.scalars()):
+        out.append("scalars differ")
+    for i in rng.choice(o.capacity, nrows, replace=False):
+        i = int(i)
+        if not np.array_equal(o.row(i), g.row(i)):
+            out.append(f"row {i} differs")
+        if o.suspects(i) != g.suspects(i) or o.curious(i) != g.curious(i):
+            out.append(f"suspect/curious table {i} differs")
+        out += diff_peer_states(o, g, [i])
+        if out:
+            break
+    return out
 
 
 def apply_events(sims, case: dict, r: int) -> None:
@@ -177,6 +223,10 @@ def standard_cases() -> list[tuple[str, dict, int]]:
     cases.append(("rebase_window", {"cfg": SimConfig(capacity=192, initial_nodes=192, init_mode=KB_INIT_CONVERGED,
                                                      loss=0.01, churn=0.002, seed=4)}, 140))
     cases.append(("waves_2", {"cfg": SimConfig(capacity=256, initial_nodes=256, loss=0.03, max_waves=2, seed=13)}, 15))
+    # 200 peers ping_addrs the same peer before their first tick: one in-order inbox of 200 Pings in
+    # wave 0 (k_sort_inbox + k_proc's sorted path; with KB_DBG_PROC_UNSORTED the selection path)
+    cases.append(("hot_inbox", {"cfg": SimConfig(capacity=256, initial_nodes=256, loss=0.02, seed=17),
+                                "events": {0: [("ping", i, [0]) for i in range(1, 201)]}}, 8))
     return cases
 
 

@@ -7,7 +7,7 @@ identities computed by zlib (src/kaboodle.rs:71-83), and instants are exact roun
 stamp-byte window of DESIGN.md §2.2 appears only where the semantics define it (the ordering key of
 ping_random_peer).  Pure-Python loops: for small meshes only.
 
-It pins the C oracle (tests/test_pyref_pin.py) and generates the committed round-trace fixtures
+It pins the C oracle (tests/test_oracle_traces.py replays its committed traces) and generates the committed round-trace fixtures
 (tests/golden/make_golden.py).
 """
 from __future__ import annotations
@@ -422,6 +422,19 @@ class PyMesh:
         out = [0] * self.C
         for q, (st, t) in self.peers[i].known.items():
             out[q] = 1 if st != KNOWN else stamp_key(t, max(self.round - 1, 0))
+        return out
+
+    def peer_states(self, i):
+        """Kaboodle::peer_states (src/lib.rs:348-354) as the ABI reports it: (peer, state, since,
+        latency); since = the exact instant, or INT32_MIN once the stamp window has saturated it
+        (DESIGN.md §2.2); latency not modelled here (none)."""
+        rl = max(self.round - 1, 0)
+        out = []
+        for q, (st, t) in sorted(self.peers[i].known.items()):
+            if st == KNOWN:
+                out.append((q, 0, t if stamp_key(t, rl) > 2 else -2 ** 31, 0xFFFFFFFF))
+            else:
+                out.append((q, 1 if st == WFP else 2, t, 0xFFFFFFFF))
         return out
 
     def suspects(self, i):

@@ -1,0 +1,119 @@
+"""Full-size parity on an MI355X: the HIP library against the OpenMP oracle at the sizes the bench and the
+wide-row configs run, through the C ABI.
+
+- configs[2] exactly as bench.py runs it (65,536 peers, capacity 69,632, 1 % loss, 0.1 %/round churn,
+  faults until round 25) over the whole benched horizon (25 faulty rounds) plus a 10-round quiet tail,
+  every round: counters, every fingerprint and per-node scalar, and sampled whole rows, suspect and
+  curious tables and peer_states (src/kaboodle.rs:746-779 per round).
+- a 140K-id mesh: rows wider than RESP_LDS_W = 131,072 ids, so Join responses take the HBM-scratch
+  path a >= 1M-id mesh takes (kb_sim.hip, the W > RESP_LDS_W branch), unsharded and as 8 row shards.
+- configs[4] scaled to one GPU: 65,536 peers, 5 % loss, a two-way partition, then the heal by injected
+  ping_addrs across the halves.
+
+Each scenario is split into chunks of rounds (one test each, sharing the handles) so no single test
+runs for minutes without output."""
+import numpy as np
+import pytest
+
+import parity
+from kaboodle_amd._ffi import KB_INIT_CONVERGED, Sim, SimConfig
+
+pytestmark = pytest.mark.gpu
+
+BENCH_CFG = SimConfig(capacity=65536 + 4096, initial_nodes=65536, init_mode=KB_INIT_CONVERGED, loss=0.01,
+                      churn=0.001, fault_end_round=25, seed=1)     # bench.rank_config at --steps 20 --warmup 5
+
+
+class Pair:
+    """An oracle handle and a GPU handle advanced in lock step."""
+
+    def __init__(self, cfg, shards=0, events=None, omp=True):
+        import kaboodle_amd
+        kaboodle_amd.require_gpu()
+        self.o = Sim(parity.oracle_lib(omp=omp), cfg)
+        self.g = Sim(parity.gpu_lib(), cfg, shards=shards)
+        self.events = events or {}
+        self.round = 0
+        self.rng = np.random.default_rng(cfg.seed)
+
+    def advance(self, upto, nrows=24):
+        while self.round < upto:
+            parity.apply_events((self.o, self.g), {"events": self.events}, self.round)
+            self.o.step(1)
+            self.g.step(1)
+            d = parity.compare_sampled(self.o, self.g, self.rng, nrows)
+            assert not d, f"round {self.round}: " + "; ".join(d[:4])
+            self.round += 1
+
+    def close(self):
+        self.o.close()
+        self.g.close()
+
+
+@pytest.fixture(scope="module")
+def horizon():
+    p = Pair(BENCH_CFG)
+    yield p
+    p.close()
+
+
+@pytest.mark.parametrize("upto", [7, 14, 21, 28, 35])
+def test_bench_horizon_64k(horizon, upto):
+    """The bench's workload, rounds [upto - 7, upto): 25 faulty rounds, then the quiet tail."""
+    horizon.advance(upto)
+    if upto == 35:
+        st = horizon.g.stats()
+        assert st["churn_joins"] > 0 and st["removed_failed"] > 0 and st["join_responses"] > 0
+
+
+@pytest.fixture(scope="module")
+def wide():
+    cfg = SimConfig(capacity=140000, initial_nodes=136000, init_mode=KB_INIT_CONVERGED, loss=0.01, churn=0.001,
+                    seed=5)
+    p = Pair(cfg)
+    yield p
+    p.close()
+
+
+@pytest.mark.parametrize("upto", [2, 4])
+def test_wide_rows_140k(wide, upto):
+    """W = 147,456 > RESP_LDS_W: Join responses of non-wave responders from HBM scratch."""
+    wide.advance(upto, nrows=12)
+    if upto == 4:
+        assert wide.g.stats()["join_responses"] > 0
+
+
+def test_wide_rows_140k_sharded(wide):
+    """The same mesh as 8 row shards (kb_sim_create_local, all-to-all-v of every wave) equals the
+    unsharded GPU mesh after 4 rounds."""
+    cfg = wide.g.cfg
+    with Sim(parity.gpu_lib(), cfg, shards=8) as s:
+        s.step(wide.round)
+        a, b = wide.g, s
+        assert a.stats() == b.stats()
+        assert np.array_equal(a.fingerprints(), b.fingerprints())
+        assert np.array_equal(a.scalars(), b.scalars())
+        for i in np.random.default_rng(3).choice(cfg.capacity, 16, replace=False):
+            assert np.array_equal(a.row(int(i)), b.row(int(i))), f"node {i}"
+    assert wide.g.debug_paths() & (2 | 4), "no Join response took the scratch path"
+
+
+@pytest.fixture(scope="module")
+def split():
+    n = 65536
+    cfg = SimConfig(capacity=n, initial_nodes=n, init_mode=KB_INIT_CONVERGED, loss=0.05, partition_groups=2,
+                    partition_start=3, partition_end=12, seed=9)
+    # heal: every 256th peer of each half is told an address in the other half (Kaboodle::ping_addrs)
+    heal = {12: [("ping", i, [(i + n // 2) % n]) for i in range(0, n, 256)]}
+    p = Pair(cfg, events=heal)
+    yield p
+    p.close()
+
+
+@pytest.mark.parametrize("upto", [6, 12, 18, 24])
+def test_partition_heal_64k(split, upto):
+    """configs[4] on one GPU: 5 % loss, the halves cut off for rounds 3-11, healed at round 12."""
+    split.advance(upto, nrows=16)
+    if upto == 24:
+        st = split.g.stats()
+        assert st["drop_partition"] > 0

@@ -10,7 +10,7 @@ import pytest
 
 import parity
 import scenarios
-from kaboodle_amd._ffi import KB_INIT_CONVERGED, Sim, SimConfig
+from kaboodle_amd._ffi import KB_DBG_ALL, KB_INIT_CONVERGED, Sim, SimConfig
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -25,8 +25,49 @@ def gpu():
 
 @pytest.mark.parametrize("name,case,rounds", parity.standard_cases(), ids=[c[0] for c in parity.standard_cases()])
 def test_parity_every_round(gpu, name, case, rounds):
-    ok, msg, _ = parity.run_case(case, rounds)
+    """Complete state every round, plus peer_states() of every node (the rebase_window case crosses two
+    64-round stamp-window rebases)."""
+    ok, msg, _ = parity.run_case(case, rounds, peer_states=True)
     assert ok, f"{name}: {msg}"
+
+
+@pytest.mark.parametrize("name,case,rounds", parity.standard_cases(), ids=[c[0] for c in parity.standard_cases()])
+def test_parity_wide_row_paths(gpu, name, case, rounds):
+    """The standard matrix on the kernel variants a >= 1M-id mesh takes (configs[3]/[4]: broadcast phase
+    and KnownPeers groups on the HBM bitset, Join responses from HBM scratch, BIG KnownPeers groups,
+    k_proc's unsorted selection path), forced by kb_config.debug_flags at these sizes."""
+    ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_ALL), rounds)
+    assert ok, f"{name} (debug_flags={KB_DBG_ALL}): {msg}"
+
+
+def test_wide_row_paths_are_hit(gpu):
+    """The forced variants really run: every wide-row kernel path reports work (kb_sim_debug_paths)."""
+    from kaboodle_amd._ffi import KB_DBG_ALL
+    by = {n: (c, r) for n, c, r in parity.standard_cases()}
+    mask = 0
+    for name in ("config2_join_1k", "churn_loss_512", "hot_inbox"):
+        case, rounds = by[name]
+        with Sim(gpu, parity.with_cfg(case, debug_flags=KB_DBG_ALL)["cfg"]) as g:
+            parity.setup(g, case)
+            for r in range(rounds):
+                parity.apply_events((g,), case, r)
+                g.step(1)
+            mask |= g.debug_paths()
+    want = {"phaseB on HBM": 1, "responses from scratch, sampled": 2, "responses from scratch, complete": 4,
+            "KnownPeers BIG on HBM": 8, "k_proc unsorted": 16, "Failed prep from HBM": 32}
+    missing = [k for k, b in want.items() if not mask & b]
+    assert not missing, f"paths not exercised: {missing} (mask {mask:#x})"
+    # and without the flags the same cases take the LDS variants
+    with Sim(gpu, by["config2_join_1k"][0]["cfg"]) as g:
+        g.step(by["config2_join_1k"][1])
+        assert g.debug_paths() & (128 | 64) and not g.debug_paths() & (1 | 8)
+
+
+@pytest.mark.parametrize("name", ["churn_loss_512", "config2_join_1k", "partition_heal"])
+def test_parity_wide_row_paths_sharded(gpu, name):
+    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}[name]
+    ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_ALL), rounds, shards=3)
+    assert ok, f"{name} x3 (debug_flags={KB_DBG_ALL}): {msg}"
 
 
 def _shard_cases():

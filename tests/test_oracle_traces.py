@@ -35,9 +35,10 @@ def test_oracle_matches_trace(name):
         assert o.stats()["first_converged_round"] == TRACES[name]["first_converged"]
 
 
-@pytest.mark.parametrize("name", ["config1", "churn40", "partition", "stop_start"])
+@pytest.mark.parametrize("name", ["config1", "churn40", "partition", "stop_start", "rebase"])
 def test_oracle_live_pin(name):
-    """Full-state comparison with pyref, every round: rows, suspects, curious, fingerprints, counters."""
+    """Full-state comparison with pyref, every round: rows, suspects, curious, peer_states (across the
+    64-round stamp-window rebases in "rebase"), fingerprints, counters."""
     sc = scenarios.BY_NAME[name]
     pm = scenarios.pymesh_of(sc)
     with Sim(oracle_lib(), sc["cfg"]) as o:
@@ -52,6 +53,7 @@ def test_oracle_live_pin(name):
                 assert np.array_equal(o.row(i), np.array(pm.row(i), np.uint8)), f"round {r} node {i} row"
                 assert o.suspects(i) == pm.suspects(i), f"round {r} node {i} suspects"
                 assert o.curious(i) == pm.curious_view(i), f"round {r} node {i} curious"
+                assert o.peer_states(i) == pm.peer_states(i), f"round {r} node {i} peer_states"
                 want = pyref.fingerprint(pm.peers[i].known, pm.identity) if pm.peers[i].running else 0
                 assert o.fingerprint(i) == want if pm.peers[i].running else True
             st = o.stats()
