@@ -614,7 +614,40 @@ static int check_err(kb_sim* s) {
   }
   return KB_OK;
 }
-constexpr uint32_t HERR_WAVE0 = 9;   // raised by the host into C_ERR (kept symmetric across shards)
+
+// replace a tracked device allocation by a larger one (contents are not kept)
+template <class T> static hipError_t regrow(kb_sim* s, T** p, size_t n) {
+  for (auto& q : s->allocs) if (q == (void*)*p) { (void)hipFree(q); q = nullptr; }
+  s->allocs.erase(std::remove(s->allocs.begin(), s->allocs.end(), nullptr), s->allocs.end());
+  *p = nullptr;
+  return talloc(s, p, n);
+}
+// The wave-0 outbox holds the round's Join responses (src/kaboodle.rs:356-392), whose volume follows the
+// mesh's dynamics (≈1 % of the members answer each joiner with up to 567 ids): when the scanned totals
+// exceed it, it grows, with the buffers indexed by its slots (record status, inbox lists, send side).
+static int grow_wave0(kb_sim* s, size_t need_msg, size_t need_pay) {
+  OutBuf& o0 = s->ob[0];
+  const size_t lim = 0xF0000000ull;
+  if (need_pay > o0.pay_cap) {
+    const size_t cap = std::min(lim, need_pay + need_pay / 4);
+    if (cap < need_pay) { seterr("Join-response payload beyond 2^32 ids"); return KB_CAPACITY; }
+    HIPCHK(regrow(s, &o0.pay, cap));
+    o0.pay_cap = (uint32_t)cap;
+    if (s->xf && cap > s->pay_cap) { HIPCHK(regrow(s, &s->xs.spay, cap)); s->pay_cap = (uint32_t)cap; }
+  }
+  if (need_msg > o0.msg_cap) {
+    const size_t cap = std::min(lim, need_msg + need_msg / 4);
+    if (cap < need_msg) { seterr("wave-0 records beyond 2^32"); return KB_CAPACITY; }
+    HIPCHK(regrow(s, &o0.msgs, cap));
+    o0.msg_cap = (uint32_t)cap;
+    if (cap > s->msg_cap) {                  // slot-indexed buffers cover the larger outbox
+      if (!s->xf) { HIPCHK(regrow(s, &s->wc.status, cap)); HIPCHK(regrow(s, &s->wc.inbox, cap)); HIPCHK(regrow(s, &s->wc.kin, cap)); }
+      else { HIPCHK(regrow(s, &s->xs.ostatus, cap)); HIPCHK(regrow(s, &s->xs.smsg, cap)); }
+      s->msg_cap = (uint32_t)cap;
+    }
+  }
+  return KB_OK;
+}
 
 // grow the receive side of the sharded waves to hold nm records and np payload ids
 static int ensure_recv(kb_sim* s, size_t nm, size_t np) {
@@ -779,12 +812,11 @@ static int step_round(kb_sim* s) {
     HIPCHK(hipMemcpyAsync(tot, s->scan_tot, 20, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t pay_tot = tot[1], msg_tot = tot[2], resp_nodes = tot[4];
-    if (msg_tot > s->msg_cap || pay_tot > s->pay_cap) {
-      // no responses are written; the error surfaces on every shard at the round's end
-      const uint32_t he = HERR_WAVE0;
-      HIPCHK(hipMemcpyAsync(d.ctr + C_ERR, &he, 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemsetAsync(L(s, o0.cnt), 0, 4ull * R, st));
-    } else if (resp_nodes) {
+    if (msg_tot > o0.msg_cap || pay_tot > o0.pay_cap) {
+      const int rc = grow_wave0(s, msg_tot, pay_tot);
+      if (rc) return rc;
+    }
+    if (resp_nodes) {
       const uint32_t grid = std::min<uint32_t>(resp_nodes, 4096);
       const size_t words = resp_words(d.NWR, s->W / 256);
       uint32_t* scratch = nullptr;

@@ -1,13 +1,14 @@
 #!/bin/bash
-# round-2 check: the whole GPU suite (with durations), then per-wave kernel traces of the 64K workload in
-# both failed modes (sim_sender = honoured Failed, sock = socket_faithful)
+# usage: tools/gpu_r02a.sh <tag> [pytest targets...] — the GPU suite (with durations)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/${1:-r02a}
+OUT=gpurun_out/${1:-r02a}; shift
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 1100 python -u -m pytest tests -m gpu -x -v --timeout 280 --timeout-method thread --durations=40 \
+T=${@:-tests}
+timeout -k 10 1100 python -u -m pytest $T -m gpu -x -v --timeout 280 --timeout-method thread --durations=40 \
   > $OUT/pytest.log 2>&1
 rc=$?
-tail -60 $OUT/pytest.log
+grep -E "PASSED|FAILED|ERROR|SKIPPED" $OUT/pytest.log | tail -70
+tail -3 $OUT/pytest.log
 exit $rc
