@@ -17,10 +17,12 @@ tracks every peer, so per-GPU work grows with N.  --replicas runs N independent 
 (distinct seeds, no collective on the data path).
 
 Also reported, on the same JSON line:
-  roofline      the dominant kernel (k_sweep, the per-round row sweep of ping_random_peer + fingerprint):
-                algorithmic bytes per launch / its HIP-event duration on the simulator's stream, against
-                8 TB/s; `traffic` = measured HBM bytes per launch from the rocprofv3 PMC summary
-                committed under profiles/ (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), else null;
+  roofline      the dominant kernel (the longer of k_rowpass — broadcast phase + ping_random_peer's
+                candidate scan — and k_fold — the fingerprint checkpoints): algorithmic bytes per launch
+                (counted in-kernel) / its HIP-event duration on the simulator's stream, against 8 TB/s;
+                `traffic` = measured HBM bytes per launch from the rocprofv3 PMC summary committed under
+                profiles/ (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), else null; the other
+                kernel's figures ride along under `kernels`;
   cpu_baseline  the CPU oracle (oracle/, OpenMP build, same semantics and seeds) on a bounded sample of
                 the same workload, on rank 0 only;
   convergence   after the timed rounds faults stop (fault_end_round); untimed rounds continue until every
@@ -39,7 +41,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM [CDNA4]")
-KT_SWEEP, KT_ROUND = 0, 1      # kb_sim_kernel_time kinds
+KT_ROWPASS, KT_ROUND, KT_FOLD = 0, 1, 2   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
+KERNEL_NAMES = {KT_ROWPASS: "k_rowpass", KT_FOLD: "k_fold"}
 
 
 def parse():
@@ -59,20 +62,72 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-conv", action="store_true")
+    ap.add_argument("--no-modes", action="store_true", help="skip the socket_faithful line (N = 1)")
+    ap.add_argument("--failed-mode", choices=("sim_sender", "socket_faithful"), default="sim_sender",
+                    help="Q1: Failed(p) honoured (sim_sender, the headline) or never (socket_faithful)")
     return ap.parse_args()
 
 
-def pmc_traffic(cfg_key: str):
-    """Latest committed PMC summary for this workload (profiles/*pmc*.json), bytes per k_sweep launch."""
+def pmc_traffic(cfg_key: str, kernel: str, capacity: int):
+    """Latest committed PMC summary for this kernel on this exact workload and capacity
+    (profiles/*pmc*.json): HBM bytes per launch."""
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if d.get("workload") == cfg_key and d.get("kernel") == "k_sweep":
+        if d.get("workload") == cfg_key and d.get("kernel") == kernel and d.get("capacity") == capacity:
             best = d
     return None if best is None else int(best["hbm_bytes_per_launch"])
+
+
+def committed_tail(cfg_key: str, mode: str):
+    """The full quiescent tail of this workload (tools/converge.py, run to agreement or 2N rounds on an
+    MI355X; profiles/*converge*.json): too long for the bench's minutes, so read from the record."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*converge*.json"))):
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload", "").startswith(cfg_key) and d.get("failed_mode") == mode:
+            best = {k: d[k] for k in ("converged_round", "tail_rounds_to_converge", "tail_rounds_run", "cap_rounds",
+                                      "stopped_by") if k in d}
+            best["source"] = os.path.relpath(p, ROOT)
+            if d.get("trajectory"):
+                last = d["trajectory"][-1]
+                best["final_agree_frac"] = last.get("agree_frac")
+                best["final_view_gap_mean"] = last.get("view_gap_mean")
+    return best
+
+
+def timed_rounds(mesh, steps: int, world: int):
+    """Steps `steps` rounds between barriers; returns (wall s, sum of live peers over the rounds, stats
+    before, stats after)."""
+    import torch
+    import torch.distributed as dist
+    s0 = mesh.stats()
+    alive_sum = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        mesh.step(1)                                 # synchronous: returns after the round's kernels
+        alive_sum += mesh.stats()["alive"]           # sharded: the whole mesh (collective)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0, alive_sum, s0, mesh.stats()
+
+
+def round_model_bytes(s0: dict, s1: dict, alive_mean: float, steps: int) -> float:
+    """SURVEY.md §8(d)'s dense per-round model: every live peer reads its row of the stamp table
+    (N bytes), plus 32 B per message record and 4 B per KnownPeers entry moved."""
+    msgs = sum(s1[k] - s0[k] for k in ("sent_ping", "sent_ping_req", "sent_ack", "sent_known_peers", "sent_kpr"))
+    ids = s1["sent_kp_ids"] - s0["sent_kp_ids"]
+    return (alive_mean * alive_mean * steps + 32.0 * msgs + 4.0 * ids) / steps
 
 
 def cpu_baseline(cfg, budget_s: float, nodes: int) -> dict:
@@ -110,14 +165,15 @@ def sharded(a, world: int) -> bool:
 def rank_config(a, rank: int, world: int, local: int):
     """This rank's mesh: one mesh of nodes x world peers shared by every rank (sharded), or a replica of
     the nodes-peer workload with a rank-distinct seed (world 1, --replicas)."""
-    from kaboodle_amd._ffi import KB_INIT_CONVERGED, SimConfig
+    from kaboodle_amd._ffi import KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL, KB_INIT_CONVERGED, SimConfig
     total = a.warmup + a.steps
     shard = sharded(a, world)
     peers = a.nodes * world if (shard and getattr(a, "weak", False)) else a.nodes
     reserve = max(4096, int(peers * a.churn * (total + 8) * 1.5))
+    mode = KB_FAILED_SOCKET_FAITHFUL if getattr(a, "failed_mode", "sim_sender") == "socket_faithful" else KB_FAILED_SIM_SENDER
     return SimConfig(capacity=peers + reserve, initial_nodes=peers, init_mode=KB_INIT_CONVERGED, loss=a.loss,
                      churn=a.churn, fault_end_round=total, seed=a.seed + (0 if shard else 1000 * rank),
-                     device=local if world > 1 else -1)
+                     device=local if world > 1 else -1, failed_mode=mode)
 
 
 def share_uid(rank: int, make) -> bytes:
@@ -176,23 +232,13 @@ def main() -> int:
     mesh.step(a.warmup)
     torch.cuda.synchronize()
     mesh.reset_kernel_time()
-    bytes0 = mesh.sweep_bytes()
-    alive_sum = 0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        mesh.step(1)                                 # synchronous: returns after the round's kernels
-        alive_sum += mesh.stats()["alive"]           # sharded: the whole mesh (collective)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    sweep_ms, sweep_n = mesh.kernel_time(KT_SWEEP)
-    round_ms, _ = mesh.kernel_time(KT_ROUND)
-    sweep_bytes = mesh.sweep_bytes() - bytes0
-    st = mesh.stats()
+    dt, alive_sum, st0, st = timed_rounds(mesh, a.steps, world)
+    kern = {}
+    for kind, name in KERNEL_NAMES.items():
+        ms, n = mesh.kernel_time(kind)
+        kern[name] = {"ms": ms, "n": n, "bytes": mesh.kernel_bytes(kind)}
+    round_ms, round_n = mesh.kernel_time(KT_ROUND)
+    model_bytes = round_model_bytes(st0, st, alive_sum / max(a.steps, 1), a.steps)
 
     # sharded: every rank saw the whole mesh's count, so it enters the sum once
     dt, alive_total = aggregate(dt, float(alive_sum if (rank == 0 or not shard) else 0), world, device="cuda")
@@ -225,7 +271,8 @@ def main() -> int:
                 "workload_converged_round": r_conv if r_conv >= 0 else None,
                 "workload_tail_rounds_run": extra,
                 "workload_agree_frac_at_fault_end": round(st["agree"] / max(st["alive"], 1), 4),
-                "workload_agree_frac_final": round(s3["agree"] / max(s3["alive"], 1), 4)}
+                "workload_agree_frac_final": round(s3["agree"] / max(s3["alive"], 1), 4),
+                "workload_full_tail": committed_tail(f"configs[2]: {a.nodes} peers", a.failed_mode)}
         if not shard:
             # how far the views are from agreement: |known_i| against the running count (0 = right size)
             import numpy as np
@@ -237,10 +284,16 @@ def main() -> int:
 
     out = None
     if rank == 0:
-        per_launch_bytes = sweep_bytes / max(sweep_n, 1)
-        sweep_avg_ms = sweep_ms / max(sweep_n, 1)
-        achieved = per_launch_bytes / (sweep_avg_ms * 1e-3) / 1e9 if sweep_n else 0.0
-        traffic = pmc_traffic(workload)
+        rl = {}
+        for name, k in kern.items():
+            per_launch = k["bytes"] / max(k["n"], 1)
+            avg_ms = k["ms"] / max(k["n"], 1)
+            ach = per_launch / (avg_ms * 1e-3) / 1e9 if k["n"] and avg_ms > 0 else 0.0
+            rl[name] = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload, name, capacity),
+                        "algorithmic_bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_ms, 4),
+                        "launches": k["n"]}
+        dominant = max(rl, key=lambda n: rl[n]["avg_launch_ms"])
         out = {
             "metric": "simulated peer-rounds/sec (whole node) + rounds to fingerprint convergence",
             "value": alive_total / dt, "unit": "peer-rounds/s", "n_gpus": world, "steps": a.steps,
@@ -248,16 +301,19 @@ def main() -> int:
             "scaling": "weak" if (getattr(a, "weak", False) or (world > 1 and not shard)) else "strong",
             "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (Philox-keyed loss/churn/targets, seed-determined)",
-            "config": {"workload": workload, "peers": peers, "peers_per_gpu": (peers + world - 1) // world if shard else peers,
+            "config": {"workload": workload, "failed_mode": a.failed_mode, "peers": peers, "peers_per_gpu": (peers + world - 1) // world if shard else peers,
                        "capacity": capacity,
                        "loss": a.loss, "churn": a.churn,
                        "parallelism": (f"rowshard{world}" if shard else f"replicas{world}") if world > 1 else "single",
                        "max_waves": cfg.max_waves},
-            "roofline": {"bound": "hbm", "kernel": "k_sweep", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic, "algorithmic_bytes_per_launch": int(per_launch_bytes),
-                         "avg_launch_ms": round(sweep_avg_ms, 4), "launches": sweep_n},
-            "round_gpu_ms": round(round_ms / max(sweep_n, 1), 4),
+            "roofline": rl[dominant],
+            "kernels": {n: v for n, v in rl.items() if n != dominant},
+            "round_gpu_ms": round(round_ms / max(round_n, 1), 4),
+            # the whole round against SURVEY.md §8(d)'s dense model (every live peer reads its N-byte
+            # row, plus the message bytes), per wall-clock round
+            "round_roofline": {"bytes_model_per_round": int(model_bytes),
+                               "achieved": round(model_bytes / (dt / a.steps) / 1e9, 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(model_bytes / (dt / a.steps) / 1e9 / HBM_PEAK_GBS, 4)},
             "convergence": conv,
         }
         if world == 1 and not a.no_cpu:
@@ -265,8 +321,27 @@ def main() -> int:
             out["cpu_baseline"] = cpu_baseline(ccfg, a.cpu_seconds, a.nodes)
         else:
             out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
     mesh.close()
+    modes = None
+    if world == 1 and not a.no_modes and a.failed_mode == "sim_sender":
+        # Q1's deployment-faithful reading (Failed never honoured, src/networking.rs:44-55): same
+        # workload, seeds, K and W, its own mesh; timed the same way
+        import copy
+        b = copy.copy(a)
+        b.failed_mode = "socket_faithful"
+        with kaboodle_amd.Mesh(rank_config(b, rank, world, local)) as m2:
+            m2.step(a.warmup)
+            torch.cuda.synchronize()
+            dt2, alive2, s20, s21 = timed_rounds(m2, a.steps, world)
+            rb2 = round_model_bytes(s20, s21, alive2 / max(a.steps, 1), a.steps)
+            modes = {"socket_faithful": {
+                "value": alive2 / dt2, "ms_per_step": dt2 / a.steps * 1e3,
+                "round_model_frac": round(rb2 / (dt2 / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
+                "agree_frac_at_fault_end": round(s21["agree"] / max(s21["alive"], 1), 4),
+                "workload_full_tail": committed_tail(f"configs[2]: {a.nodes} peers", "socket_faithful")}}
+    if out is not None:
+        out["modes"] = modes
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0

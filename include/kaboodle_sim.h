@@ -114,7 +114,8 @@ typedef struct kb_stats {
   uint64_t bcast_join, bcast_failed;
   uint64_t drop_dead, drop_loss, drop_window, drop_oversize, drop_partition, drop_bcast;
   uint64_t removed_timeout, removed_failed, join_responses, curious_overflow, churn_leaves, churn_joins;
-  uint64_t reserved[8];
+  uint64_t sent_kp_ids;           /* peer entries carried by the KnownPeers messages sent               */
+  uint64_t reserved[7];
 } kb_stats;
 
 typedef struct kb_sim kb_sim;
@@ -204,12 +205,16 @@ uint32_t kb_fingerprint_of_set(const uint32_t* ids, size_t n, const uint8_t* ide
 const char* kb_last_error(void);
 
 /* ---- timing surface for bench.py ---------------------------------------------------------------- */
-/* HIP-event durations (ms, summed since last reset) of the round's kernels, recorded on the stream
-   they run on.  kind: 0 = ping-step row sweep (the dominant kernel), 1 = whole round.              */
+/* HIP-event durations (ms, summed since last reset) of the round's kernels, recorded by the kernels'
+   own dispatch packets on the stream they run on.  kind: KB_KT_*.                                   */
+enum { KB_KT_ROWPASS = 0,   /* the row pass: broadcast phase + ping_random_peer candidates */
+       KB_KT_ROUND = 1,     /* the whole round                                                           */
+       KB_KT_FOLD = 2 };    /* the fingerprint fold                                                      */
 int  kb_sim_kernel_time(kb_sim* sim, int kind, double* ms, uint64_t* launches);
 int  kb_sim_reset_kernel_time(kb_sim* sim);
-/* Algorithmic HBM bytes moved by the row-sweep kernel since the last reset.         */
-int  kb_sim_sweep_bytes(kb_sim* sim, uint64_t* bytes);
+/* Algorithmic HBM bytes moved by a kernel (KB_KT_ROWPASS or KB_KT_FOLD) since the last reset,
+   counted in-kernel.                                                                  */
+int  kb_sim_kernel_bytes(kb_sim* sim, int kind, uint64_t* bytes);
 
 #ifdef __cplusplus
 }

@@ -17,6 +17,7 @@ KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL = 0, 1
 KB_DBG_PHASEB_HBM, KB_DBG_RESP_HBM, KB_DBG_KP_HBM, KB_DBG_KP_BIG_SMALL, KB_DBG_PROC_UNSORTED = 1, 2, 4, 8, 16
 KB_DBG_ALL = 31
 KB_LATENCY_NONE = 0xFFFFFFFF
+KT_ROWPASS, KT_ROUND, KT_FOLD = 0, 1, 2          # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
 STATE_NAMES = {0: "Known", 1: "WaitingForPing", 2: "WaitingForIndirectPing"}
 
 
@@ -46,7 +47,7 @@ class KbStats(C.Structure):
         ("drop_oversize", C.c_uint64), ("drop_partition", C.c_uint64), ("drop_bcast", C.c_uint64),
         ("removed_timeout", C.c_uint64), ("removed_failed", C.c_uint64), ("join_responses", C.c_uint64),
         ("curious_overflow", C.c_uint64), ("churn_leaves", C.c_uint64), ("churn_joins", C.c_uint64),
-        ("reserved", C.c_uint64 * 8),
+        ("sent_kp_ids", C.c_uint64), ("reserved", C.c_uint64 * 7),
     ]
 
     def as_dict(self) -> dict:
@@ -134,7 +135,7 @@ _OPTIONAL = {
                                  C.POINTER(C.c_uint32)]),
     "sim_kernel_time": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     "sim_reset_kernel_time": (C.c_int, [C.c_void_p]),
-    "sim_sweep_bytes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "sim_kernel_bytes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
     "sim_debug_paths": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
 }
 
@@ -348,7 +349,8 @@ class Sim:
         self.lib.call("sim_debug_paths", self.h, C.byref(v))
         return v.value
 
-    def sweep_bytes(self) -> int:
+    def kernel_bytes(self, kind: int = 0) -> int:
+        """Algorithmic bytes the kernel `kind` (KT_ROWPASS / KT_FOLD) moved since reset_kernel_time."""
         v = C.c_uint64()
-        self.lib.call("sim_sweep_bytes", self.h, C.byref(v))
+        self.lib.call("sim_kernel_bytes", self.h, kind, C.byref(v))
         return v.value

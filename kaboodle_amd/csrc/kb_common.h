@@ -17,7 +17,9 @@ namespace kb {
 enum StatIdx {
   S_PING, S_PINGREQ, S_ACK, S_KP, S_KPR, S_BJOIN, S_BFAIL, S_DEAD, S_LOSS, S_WINDOW, S_OVERSIZE, S_PART, S_BDROP,
   S_RMTIMEOUT, S_RMFAILED, S_JRESP, S_CUROVF, S_CLEAVE, S_CJOIN,
-  S_SWEEPB,                       // bytes the row sweep had to read (bench roofline; not a kb_stats field)
+  S_KPIDS,                        // peer entries of the KnownPeers messages sent (kb_stats.sent_kp_ids)
+  S_ROWB,                         // bytes the row pass moved (bench roofline; not a kb_stats field)
+  S_FOLDB,                        // member-bit bytes the fold read (bench roofline; not a kb_stats field)
   NSTAT
 };
 enum CtrIdx {
@@ -49,7 +51,6 @@ struct Dev {
   uint32_t uniform, L;            // uniform segment length (20 + id_len) when uniform != 0
   uint32_t capk, capj;            // KnownPeers caps: KPR reply (size <= 10240), Join response (size < 10240)
   uint32_t paybound;              // payload entries reserved per KPR reply
-  uint32_t ablate;                // timing experiments only (env KB_ABLATE): 1 = no fold in sweep, 2 = no A3
   uint32_t dbg;                   // kb_config.debug_flags (KB_DBG_*): force the wide-row kernel variants
   uint8_t* stamp;
   uint32_t* bits;
@@ -302,6 +303,15 @@ __device__ inline uint32_t nzmask4(uint32_t x) {
   const uint32_t y = (((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
   return ((y >> 7) | (y >> 14) | (y >> 21) | (y >> 28)) & 0xFu;
 }
+
+// ---- ping_random_peer's candidate lists: keys (stamp << 24 | address rotated to start after self) ----
+__device__ inline void top5_insert(uint32_t (&k)[5], uint32_t nk) {
+#pragma unroll
+  for (int s = 0; s < 5; ++s) { if (nk < k[s]) { const uint32_t t = k[s]; k[s] = nk; nk = t; } }
+}
+__device__ inline uint32_t thr5(const uint32_t (&k)[5]) { return k[4] == 0xFFFFFFFFu ? 256u : (k[4] >> 24); }
+// 4-bit "byte == v" mask of a little-endian dword (SWAR)
+__device__ inline uint32_t eqmask4(uint32_t x, uint32_t v) { return ~nzmask4(x ^ (v * 0x01010101u)) & 0xFu; }
 
 // ---- node-local state, single thread ----------------------------------------------------------
 __device__ inline void susp_clear(const Dev& d, uint32_t i, uint32_t p) {

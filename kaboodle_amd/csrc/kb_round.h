@@ -180,18 +180,77 @@ __global__ __launch_bounds__(1024) void k_bfail_prep_lds(const BCast* bf, uint32
   }
 }
 
-// Persistent waves, one node at a time.  Each workgroup first stages the broadcast lists in LDS
-// (shared by all its nodes: Failed as {sender | bseq << 23 | dep << 31, peer}, Join as
-// {sender | bseq << 23}); then every wave loops over nodes with the node's member bitset staged in
-// LDS (coalesced read, LDS atomics, write-back of the changed segments).  Lists longer than the LDS
-// budget, or rows wider than PB_LDS_W, are read from HBM instead.
+// ================================================================================================
+// THE ROW PASS: one wave per node, the node's member bitset staged in LDS once for the whole pass.
+//  (1) broadcast phase — Failed then Join deliveries of round r-1's broadcasts (src/kaboodle.rs:256-311);
+//  (2) ping_random_peer's candidate scan (A3, :655-703): the five oldest Known peers by (stamp, address
+//      rotated to start right after self), read in address order from self+1 with coalesced 16-byte
+//      stamp loads, 1024 ids per wave step, stopping as soon as five "ancient" (minimum) stamps have
+//      been seen in that order — later ids can then never rank among the five;
+//  (3) write-back of the changed bitset segments.
+// Persistent waves: each workgroup first stages the broadcast lists in LDS (shared by all its nodes:
+// Failed as {sender | bseq << 23 | dep << 31, peer}, Join as {sender | bseq << 23}).  Lists longer than
+// the LDS budget, or rows wider than PB_LDS_W, are read from HBM instead (LDSB = false).
+// ================================================================================================
 constexpr uint32_t PB_LDS_W = 524288;
 constexpr uint32_t PB_FMAX = 2048, PB_JMAX = 1024;
+constexpr uint32_t RP_WAVES = 8;                 // waves per row-pass workgroup (they share the lists)
+constexpr uint32_t RP_LDS_BYTES = 81920;         // dynamic LDS per row-pass workgroup: two fit a CU
+struct RowOut { uint32_t* part; };   // [C][10]: the five smallest keys ascending, then 0xFFFFFFFF x 5
+
+// A3 over the row of node i (members from B: LDS or HBM): the five smallest keys (stamp << 24 | rot),
+// ascending, in every lane.  Returns the stamp bytes read.
+template <bool LDSB>
+__device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, uint32_t i, const uint8_t* rw,
+                                                                  const uint32_t* B, uint32_t (&out)[5]) {
+  const uint32_t l = lane(), C = d.C, W = d.W;
+  const uint32_t p = (i + 1 == C) ? 0 : i + 1;
+  const uint32_t a0 = p & ~15u;
+  uint32_t K[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  uint32_t anc = 0, nbytes = 0;                   // ancient candidates in the scanned address-order prefix
+  bool wrapped = false;
+  for (uint32_t j0 = a0;;) {
+    const uint32_t j = j0 + 16 * l;
+    const bool inr = wrapped ? j < a0 : j < W;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    uint32_t mb = 0;
+    if (inr) {
+      v = *reinterpret_cast<const uint4*>(rw + j);
+      const uint32_t w = LDSB ? B[j >> 5] : __hip_atomic_load(&B[j >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      mb = (w >> (j & 16)) & 0xFFFFu;
+    }
+    nbytes += inr ? 16 : 0;
+    uint32_t cm = (nzmask4(v.x & 0xFEFEFEFEu) | (nzmask4(v.y & 0xFEFEFEFEu) << 4) | (nzmask4(v.z & 0xFEFEFEFEu) << 8) |
+                   (nzmask4(v.w & 0xFEFEFEFEu) << 12)) & mb;                 // Known && member
+    if (i >= j && i < j + 16) cm &= ~(1u << (i - j));                        // != self (:571-577)
+    uint32_t am = cm & (eqmask4(v.x, ST_ANCIENT) | (eqmask4(v.y, ST_ANCIENT) << 4) | (eqmask4(v.z, ST_ANCIENT) << 8) |
+                        (eqmask4(v.w, ST_ANCIENT) << 12));
+    if (!wrapped && j < p) am &= p - j >= 16 ? 0u : ~((1u << (p - j)) - 1u);   // [a0, p) comes last in order
+    anc += wave_sum(__popc(am));
+    for (uint32_t m = cm; m; m &= m - 1) {
+      const uint32_t t = __ffs(m) - 1, jj = j + t;
+      const uint32_t word = (t & 8) ? ((t & 4) ? v.w : v.z) : ((t & 4) ? v.y : v.x);
+      const uint32_t key = (((word >> (8 * (t & 3))) & 0xFFu) << 24) | (jj >= p ? jj - p : jj + C - p);
+      if (key < K[4]) top5_insert(K, key);
+    }
+    if (anc >= (uint32_t)NUM_CANDIDATES) break;   // nothing later in address order can rank
+    j0 += 1024;
+    if (!wrapped && j0 >= W) { wrapped = true; j0 = 0; }
+    if (wrapped && j0 >= a0) break;                 // the whole row
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {                     // merge the lanes' lists (keys are distinct)
+    const uint32_t mn = wave_min(K[0]);
+    out[q] = mn;
+    if (K[0] == mn && mn != 0xFFFFFFFFu) { K[0] = K[1]; K[1] = K[2]; K[2] = K[3]; K[3] = K[4]; K[4] = 0xFFFFFFFFu; }
+  }
+  return wave_sum(nbytes);
+}
 
 template <bool LDSB>
-__global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uint32_t lf, uint32_t lj) {
+__global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, int32_t r, uint32_t lf, uint32_t lj) {
   extern __shared__ uint32_t pb_dyn[];
-  __shared__ uint32_t s_sp[4][SLOTS];
+  __shared__ uint32_t s_sp[RP_WAVES][SLOTS];
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t l = lane();
@@ -221,129 +280,144 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
   const uint8_t now = enc(r, r);
   // counters stay in registers for the whole persistent loop: one atomic per wave at the end (same-
   // address atomics from every node would serialise in L2 and stall the waves that wait on them)
-  unsigned long long w_lost = 0, w_removed = 0, w_resp = 0, w_nodes = 0;
+  unsigned long long w_lost = 0, w_removed = 0, w_resp = 0, w_nodes = 0, w_bytes = 0;
   for (uint32_t i = d.lo + blockIdx.x * wpb + wv; i < d.hi; i += gridDim.x * wpb) {
-    if (!d.alive[i] || d.start_round[i] >= r) {
+    if (!d.alive[i]) {
       if (l == 0) { pb.nresp[i] = 0; pb.paysum[i] = 0; }
       continue;
     }
     uint8_t* rw = row_of(d, i);
     uint32_t* gB = bits_of(d, i);
     uint32_t* B = LDSB ? pb_dyn + (size_t)wv * d.NWR : gB;
-    if (LDSB) stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB), d.NWR / 4, l, 64);
-    if (l < SLOTS) { const Susp sl = d.susp[(size_t)i * SLOTS + l]; s_sp[wv][l] = sl.kind ? sl.peer : 0xFFFFFFFFu; }
-    wait_lds();
-    __builtin_amdgcn_wave_barrier();
-    auto mem = [&](uint32_t x) __attribute__((always_inline)) -> bool {
-      const uint32_t w = LDSB ? B[x >> 5] : __hip_atomic_load(&B[x >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return (w >> (x & 31)) & 1u;
-    };
-    auto is_susp = [&](uint32_t x) __attribute__((always_inline)) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
-    uint32_t n = d.n[i];
-    const uint32_t n0 = n;
-    uint32_t fn = d.flog_n[i];
-    uint32_t lost_cnt = 0, removed_cnt = 0;
+    if (LDSB) { stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB), d.NWR / 4, l, 64); w_bytes += 4ull * d.NWR; }
     unsigned long long segs = 0;
-    // ---- Failed(p) group (src/kaboodle.rs:268-283) ----
-    // In-order semantics, 64 entries at a time.  An entry acts iff it is delivered, names neither the
-    // receiver nor comes from it, and its sender is still a member when it is reached.  Membership at
-    // the chunk start is in B (earlier chunks applied); inside the chunk only an entry whose sender is
-    // named by an earlier entry (dep) can change its mind: those are resolved in lane order with one
-    // ballot each (killed iff an earlier acting lane of the chunk names its sender).  The acting
-    // entries are then applied together: the atomic's return says whether the peer was still present.
-    for (uint32_t c = 0; c < pb.nf; c += 64) {
-      const uint32_t e = c + l;
-      const bool valid = e < pb.nf;
-      uint32_t dep = 0;
-      const BCast b = valid ? fail_at(e, dep) : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
-      const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
-      const bool base = valid && b.sender != i && !lost && b.peer != i && honour && mem(b.sender);
-      unsigned long long actm = __ballot(base);
-      unsigned long long depm = __ballot(base && dep);
-      while (depm) {
-        const uint32_t q = (uint32_t)(__ffsll((long long)depm) - 1);
-        depm &= depm - 1;
-        const uint32_t s_q = bcast(b.sender, q);
-        const unsigned long long killers = __ballot(((actm >> l) & 1ull) && b.peer == s_q) & ((1ull << q) - 1ull);
-        if (killers) actm &= ~(1ull << q);
-      }
-      lost_cnt += __popcll(__ballot(lost));
-      if ((actm >> l) & 1ull) {
-        const uint32_t m = 1u << (b.peer & 31);
-        if (atomicAnd(&B[b.peer >> 5], ~m) & m) {
-          removed_cnt++;
-          if (is_susp(b.peer)) susp_clear(d, i, b.peer);
-          segs |= seg_bit(d, b.peer);
+    uint32_t nresp = 0;
+    if (d.start_round[i] < r) {                       // ---- (1) broadcast phase ----
+      if (l < SLOTS) { const Susp sl = d.susp[(size_t)i * SLOTS + l]; s_sp[wv][l] = sl.kind ? sl.peer : 0xFFFFFFFFu; }
+      wait_lds();
+      __builtin_amdgcn_wave_barrier();
+      auto mem = [&](uint32_t x) __attribute__((always_inline)) -> bool {
+        const uint32_t w = LDSB ? B[x >> 5] : __hip_atomic_load(&B[x >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return (w >> (x & 31)) & 1u;
+      };
+      auto is_susp = [&](uint32_t x) __attribute__((always_inline)) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
+      uint32_t n = d.n[i];
+      const uint32_t n0 = n;
+      uint32_t fn = d.flog_n[i];
+      uint32_t lost_cnt = 0, removed_cnt = 0;
+      // ---- Failed(p) group (src/kaboodle.rs:268-283) ----
+      // In-order semantics, 64 entries at a time.  An entry acts iff it is delivered, names neither the
+      // receiver nor comes from it, and its sender is still a member when it is reached.  Membership at
+      // the chunk start is in B (earlier chunks applied); inside the chunk only an entry whose sender is
+      // named by an earlier entry (dep) can change its mind: those are resolved in lane order with one
+      // ballot each (killed iff an earlier acting lane of the chunk names its sender).  The acting
+      // entries are then applied together: the atomic's return says whether the peer was still present.
+      for (uint32_t c = 0; c < pb.nf; c += 64) {
+        const uint32_t e = c + l;
+        const bool valid = e < pb.nf;
+        uint32_t dep = 0;
+        const BCast b = valid ? fail_at(e, dep) : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+        const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
+        const bool base = valid && b.sender != i && !lost && b.peer != i && honour && mem(b.sender);
+        unsigned long long actm = __ballot(base);
+        unsigned long long depm = __ballot(base && dep);
+        while (depm) {
+          const uint32_t q = (uint32_t)(__ffsll((long long)depm) - 1);
+          depm &= depm - 1;
+          const uint32_t s_q = bcast(b.sender, q);
+          const unsigned long long killers = __ballot(((actm >> l) & 1ull) && b.peer == s_q) & ((1ull << q) - 1ull);
+          if (killers) actm &= ~(1ull << q);
         }
+        lost_cnt += __popcll(__ballot(lost));
+        if ((actm >> l) & 1ull) {
+          const uint32_t m = 1u << (b.peer & 31);
+          if (atomicAnd(&B[b.peer >> 5], ~m) & m) {
+            removed_cnt++;
+            if (is_susp(b.peer)) susp_clear(d, i, b.peer);
+            segs |= seg_bit(d, b.peer);
+          }
+        }
+        if (!LDSB) { __builtin_amdgcn_s_waitcnt(0); }
+        __builtin_amdgcn_wave_barrier();
       }
+      removed_cnt = wave_sum(removed_cnt);
+      n -= removed_cnt;
       if (!LDSB) { __builtin_amdgcn_s_waitcnt(0); }
       __builtin_amdgcn_wave_barrier();
-    }
-    removed_cnt = wave_sum(removed_cnt);
-    n -= removed_cnt;
-    if (!LDSB) { __builtin_amdgcn_s_waitcnt(0); }
-    __builtin_amdgcn_wave_barrier();
-    const uint32_t nbase = n;
-    // ---- Join{addr} group (src/kaboodle.rs:284-304) ----
-    uint32_t nresp = 0, paysum = 0;
-    for (uint32_t c = 0; c < pb.nj; c += 64) {
-      const uint32_t e = c + l;
-      const bool valid = e < pb.nj;
-      const BCast b = valid ? join_at(e) : BCast{0xFFFFFFFFu, 0, 0, 0};
-      const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
-      const bool deliver = valid && b.sender != i && !lost;
-      const bool known = deliver && mem(b.sender);
-      const unsigned long long newm = __ballot(deliver && !known);
-      const bool isnew = (newm >> l) & 1ull;
-      // n right after inserting this joiner = n before the chunk + new joiners up to and including it
-      const uint32_t nq = n + __popcll(newm & ((2ull << l) - 1ull));
-      bool resp = false;
-      if (isnew) {                                   // should_respond_to_broadcast :333-354
-        const int64_t o = (int64_t)nq - 2;
-        if (o <= 0) resp = true;
-        else {
-          int64_t pct = 100 - o * o; if (pct < 1) pct = 1;
-          const uint32_t u = philox(i, (uint32_t)r, (uint32_t)P_RESPOND << 24, b.sender, d.k0, d.k1).x;
-          resp = (int64_t)mulhi(u, 100) < pct;
+      const uint32_t nbase = n;
+      // ---- Join{addr} group (src/kaboodle.rs:284-304) ----
+      uint32_t paysum = 0;
+      for (uint32_t c = 0; c < pb.nj; c += 64) {
+        const uint32_t e = c + l;
+        const bool valid = e < pb.nj;
+        const BCast b = valid ? join_at(e) : BCast{0xFFFFFFFFu, 0, 0, 0};
+        const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
+        const bool deliver = valid && b.sender != i && !lost;
+        const bool known = deliver && mem(b.sender);
+        const unsigned long long newm = __ballot(deliver && !known);
+        const bool isnew = (newm >> l) & 1ull;
+        // n right after inserting this joiner = n before the chunk + new joiners up to and including it
+        const uint32_t nq = n + __popcll(newm & ((2ull << l) - 1ull));
+        bool resp = false;
+        if (isnew) {                                   // should_respond_to_broadcast :333-354
+          const int64_t o = (int64_t)nq - 2;
+          if (o <= 0) resp = true;
+          else {
+            int64_t pct = 100 - o * o; if (pct < 1) pct = 1;
+            const uint32_t u = philox(i, (uint32_t)r, (uint32_t)P_RESPOND << 24, b.sender, d.k0, d.k1).x;
+            resp = (int64_t)mulhi(u, 100) < pct;
+          }
+        }
+        const unsigned long long respm = __ballot(resp);
+        const bool logit = deliver && (!known || rw[b.sender] != now);
+        const unsigned long long lgm = __ballot(logit);
+        if (logit) d.flog[(size_t)i * LOGCAP + ((fn + __popcll(lgm & ((1ull << l) - 1ull))) & (LOGCAP - 1))] = log_entry(b.sender, r);
+        fn += __popcll(lgm);
+        if (deliver) {
+          if (known && is_susp(b.sender)) susp_clear(d, i, b.sender);
+          rw[b.sender] = now;
+          if (isnew) { atomicOr(&B[b.sender >> 5], 1u << (b.sender & 31)); segs |= seg_bit(d, b.sender); }
+        }
+        const uint32_t sz = resp ? (d.uniform ? (nq < d.capj ? nq : d.capj) : nq) : 0;
+        paysum += wave_sum(sz);
+        nresp += __popcll(respm);
+        n += __popcll(newm);
+        lost_cnt += __popcll(__ballot(lost));
+        if (l == 0) {
+          pb.newmask[(size_t)i * pb.JW + c / 64] = newm;
+          pb.respmask[(size_t)i * pb.JW + c / 64] = respm;
         }
       }
-      const unsigned long long respm = __ballot(resp);
-      const bool logit = deliver && (!known || rw[b.sender] != now);
-      const unsigned long long lgm = __ballot(logit);
-      if (logit) d.flog[(size_t)i * LOGCAP + ((fn + __popcll(lgm & ((1ull << l) - 1ull))) & (LOGCAP - 1))] = log_entry(b.sender, r);
-      fn += __popcll(lgm);
-      if (deliver) {
-        if (known && is_susp(b.sender)) susp_clear(d, i, b.sender);
-        rw[b.sender] = now;
-        if (isnew) { atomicOr(&B[b.sender >> 5], 1u << (b.sender & 31)); segs |= seg_bit(d, b.sender); }
-      }
-      const uint32_t sz = resp ? (d.uniform ? (nq < d.capj ? nq : d.capj) : nq) : 0;
-      paysum += wave_sum(sz);
-      nresp += __popcll(respm);
-      n += __popcll(newm);
-      lost_cnt += __popcll(__ballot(lost));
+      segs = (unsigned long long)wave_or((uint32_t)segs) | ((unsigned long long)wave_or((uint32_t)(segs >> 32)) << 32);
       if (l == 0) {
-        pb.newmask[(size_t)i * pb.JW + c / 64] = newm;
-        pb.respmask[(size_t)i * pb.JW + c / 64] = respm;
+        d.n[i] = n;
+        d.flog_n[i] = fn;
+        mark(d, i, segs);
+        if (n != n0) d.dirty[i] = 1;
+        pb.nresp[i] = nresp; pb.paysum[i] = paysum; pb.nbase[i] = nbase;
       }
+      w_lost += lost_cnt; w_removed += removed_cnt;
+      // the Join stamps written above are read back by this wave's A3 loads
+      wave_mem_sync();
+      __builtin_amdgcn_s_waitcnt(0);
+    } else if (l == 0) {                              // started this round: no deliveries yet
+      pb.nresp[i] = 0; pb.paysum[i] = 0;
     }
-    segs = (unsigned long long)wave_or((uint32_t)segs) | ((unsigned long long)wave_or((uint32_t)(segs >> 32)) << 32);
     wait_lds();
     __builtin_amdgcn_wave_barrier();
-    if (LDSB && segs) {                                 // write back the changed segments of the bitset
+    // ---- (2) A3 candidates ----
+    uint32_t top[5];
+    w_bytes += a3_scan<LDSB>(d, i, rw, B, top);
+    if (l < 10) ro.part[(size_t)i * 10 + l] = l < 5 ? (l == 0 ? top[0] : l == 1 ? top[1] : l == 2 ? top[2] : l == 3 ? top[3] : top[4]) : 0xFFFFFFFFu;
+    // ---- (3) write back the changed segments of the bitset ----
+    if (LDSB && segs) {
       const uint32_t wps4 = d.SEGW / 128;             // 16-byte words per segment
       const uint4* B4 = reinterpret_cast<const uint4*>(B);
       uint4* g4 = reinterpret_cast<uint4*>(gB);
       for (uint32_t w = l; w < d.NWR / 4; w += 64) if ((segs >> (w / wps4)) & 1ull) g4[w] = B4[w];
+      w_bytes += (unsigned long long)__popcll(segs) * (d.SEGW / 8);
     }
-    if (l == 0) {
-      d.n[i] = n;
-      d.flog_n[i] = fn;
-      mark(d, i, segs);
-      if (n != n0) d.dirty[i] = 1;
-      pb.nresp[i] = nresp; pb.paysum[i] = paysum; pb.nbase[i] = nbase;
-    }
-    w_lost += lost_cnt; w_removed += removed_cnt; w_resp += nresp; w_nodes++;
+    w_resp += nresp; w_nodes++;
     wait_lds();                                       // LDS bitset is reused by the next node
     __builtin_amdgcn_wave_barrier();
   }
@@ -351,6 +425,7 @@ __global__ __launch_bounds__(256) void k_phaseB(Dev d, PhaseB pb, int32_t r, uin
     if (w_lost) atomicAdd(&d.stats[S_BDROP], w_lost);
     if (w_removed) atomicAdd(&d.stats[S_RMFAILED], w_removed);
     if (w_resp) atomicAdd(&d.stats[S_JRESP], w_resp);
+    if (w_bytes) atomicAdd(&d.stats[S_ROWB], w_bytes);
     if (!LDSB && w_nodes) path_hit(d, PATH_PHASEB_HBM);
   }
 }
@@ -367,18 +442,28 @@ __device__ inline uint32_t mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
-__device__ __attribute__((always_inline)) inline uint32_t prp_walk(uint32_t x, uint32_t n, const U4& key) {
-  uint32_t b = 2;
-  while ((1ull << b) < n) b += 2;
-  const uint32_t h = b / 2, mask = (1u << h) - 1u;
-  const uint32_t kk[4] = {key.x, key.y, key.z, key.w};
+// The keyed permutation of [0, n): a 4-round Feistel network on the smallest even
+// bit width b >= 2 with 2^b >= n, cycle-walked into [0, n).  Prp holds what depends on (n, key) only.
+struct Prp { uint32_t n, h, mask, k[4]; };
+__device__ inline Prp prp_make(uint32_t n, const U4& key) {
+  const uint32_t lg = n <= 1 ? 0u : 32u - __clz(n - 1u);        // ceil(log2 n)
+  const uint32_t b = lg < 2 ? 2u : (lg + 1u) & ~1u;
+  Prp p;
+  p.n = n; p.h = b / 2; p.mask = (1u << p.h) - 1u;
+  p.k[0] = key.x; p.k[1] = key.y; p.k[2] = key.z; p.k[3] = key.w;
+  return p;
+}
+__device__ __attribute__((always_inline)) inline uint32_t prp_eval(uint32_t x, const Prp& p) {
   do {
-    uint32_t L = x >> h, R = x & mask;
+    uint32_t L = x >> p.h, R = x & p.mask;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { const uint32_t t = R; R = L ^ (mix32(R ^ kk[k]) & mask); L = t; }
-    x = (L << h) | R;
-  } while (x >= n);
+    for (int k = 0; k < 4; ++k) { const uint32_t t = R; R = L ^ (mix32(R ^ p.k[k]) & p.mask); L = t; }
+    x = (L << p.h) | R;
+  } while (x >= p.n);
   return x;
+}
+__device__ __attribute__((always_inline)) inline uint32_t prp_walk(uint32_t x, uint32_t n, const U4& key) {
+  return prp_eval(x, prp_make(n, key));
 }
 __device__ inline uint32_t bm_rank(const uint32_t* S, const uint32_t* SP, uint32_t id) {   // members < id
   const uint32_t blk = id >> 8, w = id >> 5;
@@ -390,17 +475,24 @@ __device__ inline uint32_t bm_rank(const uint32_t* S, const uint32_t* SP, uint32
 // The block is bracketed around the density guess b * nbu / total (nbu = blocks up to the last
 // non-empty one; rows are dense below it), falling back to the whole range when the guess misses;
 // the word and bit come from one 32-byte read of the block.  Any nbu gives the same answer.
-__device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint32_t nblk, uint32_t nbu, uint32_t b) {
+// The block (256 ids) holding member b: bracketed around the density guess b * ratio (ratio = nbu /
+// total, nbu = blocks up to the last non-empty one; rows are dense below it), falling back to the whole
+// range when the guess misses.  Any ratio gives the same answer.
+__device__ __attribute__((always_inline)) inline uint32_t bm_block(const uint32_t* SP, uint32_t nblk, float ratio,
+                                                                   uint32_t b) {
   uint32_t lo = 0, hi = nblk;
   {
-    uint32_t g = (uint32_t)(((uint64_t)b * nbu) / SP[nblk]);
+    uint32_t g = (uint32_t)((float)b * ratio);
     g = g < nblk ? g : nblk - 1;
     const uint32_t l2 = g >= 2 ? g - 2 : 0, h2 = g + 3 < nblk ? g + 3 : nblk;
     if (SP[l2] <= b && b < SP[h2]) { lo = l2; hi = h2; }
   }
   while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (SP[mid] <= b) lo = mid; else hi = mid; }
-  uint32_t rem = b - SP[lo];
-  const uint4 q0 = *reinterpret_cast<const uint4*>(S + lo * 8), q1 = *reinterpret_cast<const uint4*>(S + lo * 8 + 4);
+  return lo;
+}
+// rem-th member of the 256-id block whose eight words are q0, q1
+__device__ __attribute__((always_inline)) inline uint32_t block_pick(const uint4& q0, const uint4& q1, uint32_t blk,
+                                                                     uint32_t rem) {
   const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
   uint32_t wi = 7, x = w[7];
   bool found = false;
@@ -412,7 +504,57 @@ __device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint
       else rem -= c;
     }
   }
-  return (lo * 8 + wi) * 32 + select_in_word(x, rem);
+  return (blk * 8 + wi) * 32 + select_in_word(x, rem);
+}
+// b-th member (0-based) of bitset S with 256-id block prefix SP[0..nblk] (SP[nblk] = total > b); the
+// word and bit come from one 32-byte read of the block.
+__device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint32_t nblk, float ratio, uint32_t b) {
+  const uint32_t lo = bm_block(SP, nblk, ratio, b);
+  const uint4 q0 = *reinterpret_cast<const uint4*>(S + lo * 8), q1 = *reinterpret_cast<const uint4*>(S + lo * 8 + 4);
+  return block_pick(q0, q1, lo, b - SP[lo]);
+}
+// The sampled Join response (src/kaboodle.rs:373-383 restated): pay[k] for k in
+// [k_first, cap) step `stride` = the select of rank prp(k) in the member set B minus the joiners
+// inserted after the response (J[upto..nnew), suffix minima JM), stepping over them (least fixed point
+// of e = #later joiners <= select(y + e)).  RESP_U keys per batch: their permutations, block searches and
+// 32-byte block reads are independent, so the loads of a batch are in flight together.
+constexpr int RESP_U = 4;
+__device__ __attribute__((always_inline)) inline void sampled_fill(uint32_t* pay, uint32_t k_first, uint32_t stride,
+                                                                   uint32_t cap, const Prp& P, const uint32_t* B,
+                                                                   const uint32_t* BP, uint32_t NB, float ratio,
+                                                                   const uint32_t* J, const uint32_t* JM, uint32_t upto,
+                                                                   uint32_t nnew) {
+  const uint32_t jmin = JM[upto];
+  for (uint32_t k0 = k_first; k0 < cap; k0 += stride * RESP_U) {
+    uint32_t y[RESP_U], blk[RESP_U];
+    uint4 q0[RESP_U], q1[RESP_U];
+#pragma unroll
+    for (int u = 0; u < RESP_U; ++u) { const uint32_t k = k0 + stride * u; y[u] = k < cap ? prp_eval(k, P) : 0u; }
+#pragma unroll
+    for (int u = 0; u < RESP_U; ++u) blk[u] = bm_block(BP, NB, ratio, y[u]);
+#pragma unroll
+    for (int u = 0; u < RESP_U; ++u) {
+      q0[u] = *reinterpret_cast<const uint4*>(B + blk[u] * 8);
+      q1[u] = *reinterpret_cast<const uint4*>(B + blk[u] * 8 + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < RESP_U; ++u) {
+      const uint32_t k = k0 + stride * u;
+      if (k >= cap) break;
+      uint32_t x = block_pick(q0[u], q1[u], blk[u], y[u] - BP[blk[u]]);
+      if (x >= jmin) {                                // rare: a later joiner may sit at or below x
+        uint32_t e = 0;
+        while (true) {
+          uint32_t c = 0;
+          for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= x;
+          if (c == e) break;
+          e = c;
+          x = bm_select(B, BP, NB, ratio, y[u] + e);
+        }
+      }
+      pay[k] = x;
+    }
+  }
 }
 constexpr uint32_t RESP_LDS_W = 131072;   // rows up to this many ids keep their bitsets in LDS
 constexpr uint32_t RESP_JCAP = 1024;      // new joiners of one receiver kept in LDS (more: read from HBM)
@@ -489,6 +631,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     uint32_t ex = wave_excl(bc);
     const uint32_t nB = wave_sum(bc);
     const uint32_t nbu = wave_max(last);
+    const float ratio = nB ? (float)nbu / (float)nB : 0.0f;
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) { const uint32_t c = BP[k]; BP[k] = ex; ex += c; }
     if (l == 0) BP[NB] = nB;
     for (uint32_t e = l; e < pb.nj; e += 64) {              // new joiners in list order
@@ -527,19 +670,8 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
         const uint32_t a = pb.bjoin[K].sender;
         const uint32_t nk = nB - (nnew - upto), cap = d.capj;
         uint32_t* pay = ob.pay + poff;
-        const U4 key = philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1);
-        for (uint32_t k = l; k < cap; k += 64) {
-          const uint32_t y = prp_walk(k, nk, key);
-          uint32_t e = 0, x;
-          while (true) {                                  // step over the joiners inserted after K
-            x = bm_select(B, BP, NB, nbu, y + e);
-            uint32_t c = 0;
-            if (x >= JM[upto]) for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= x;
-            if (c == e) break;
-            e = c;
-          }
-          pay[k] = x;
-        }
+        const Prp P = prp_make(nk, philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1));
+        sampled_fill(pay, l, 64, cap, P, B, BP, NB, ratio, J, JM, upto, nnew);
         if (l == 0) {
           Msg m; m.dest = a; m.sender = i; m.seq = q; m.kind = K_KP; m.a = cap; m.fp = 0; m.n = 0; m.off = poff;
           ob.msgs[ob.off[i] + q] = m;
@@ -626,23 +758,24 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
         if (sample) {
           // kept ranks = first cap images of the keyed permutation; rank -> id by select on B,
           // stepping over later joiners (least fixed point of e = #later joiners <= select(y + e))
-          const U4 key = philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1);
-          for (uint32_t k = t; k < cap; k += T) {
-            const uint32_t y = prp_walk(k, nk, key);
-            uint32_t e = 0, x;
-            while (true) {
-              x = bm_select(B, BP, NB, NB, y + e);
-              uint32_t c = 0;
-              if (jl) {                                  // later joiners = J[upto..nnew)
-                if (x >= JM[upto]) for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= x;
-              } else {
+          const Prp P = prp_make(nk, philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1));
+          const float ratio = nB ? (float)NB / (float)nB : 0.0f;
+          if (jl) {                                      // later joiners = J[upto..nnew)
+            sampled_fill(pay, t, T, cap, P, B, BP, NB, ratio, J, JM, upto, nnew);
+          } else {
+            for (uint32_t k = t; k < cap; k += T) {
+              const uint32_t y = prp_eval(k, P);
+              uint32_t e = 0, x;
+              while (true) {
+                x = bm_select(B, BP, NB, ratio, y + e);
+                uint32_t c = 0;
                 for (uint32_t f = K + 1; f < pb.nj; ++f)
                   if (newbit(nm, f)) c += pb.bjoin[f].sender <= x;
+                if (c == e) break;
+                e = c;
               }
-              if (c == e) break;
-              e = c;
+              pay[k] = x;
             }
-            pay[k] = x;
           }
         } else {
           for (uint32_t k = t; k < NW; k += T) S[k] = B[k];

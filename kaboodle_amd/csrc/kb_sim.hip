@@ -294,7 +294,7 @@ struct kb_sim {
   uint32_t* resp_nodes; uint32_t* bf_gid; uint8_t* bf_dep;
   uint32_t* slow;                      // the nodes of a wave k_proc_fast leaves to k_proc
   uint32_t* resp_scratch; size_t resp_scratch_words;
-  SweepOut so;
+  RowOut ro;
   Event* d_events; uint32_t events_cap;
   // sharded waves: send side (xs), all-gathered counts, receive buffers (grown on demand)
   XState xs;
@@ -302,9 +302,9 @@ struct kb_sim {
   std::vector<uint32_t> h_xall;
   Msg* rmsg; uint32_t* rpay; uint8_t* rstatus; uint32_t* rinbox; uint32_t* rkp;
   size_t rmsg_cap, rpay_cap;
-  hipEvent_t ev0, ev1, er0, er1;
-  double sweep_ms, round_ms;
-  uint64_t sweep_launches, round_launches, sweep_bytes, bj_total, bf_total;
+  hipEvent_t ev0, ev1, er0, er1, ef0, ef1;   // row pass, whole round, fold
+  double rowpass_ms, round_ms, fold_ms;
+  uint64_t rowpass_launches, round_launches, fold_launches, row_bytes0, fold_bytes0, bj_total, bf_total;
   uint32_t ncu = 256;
   bool debug_waves = false;
   size_t lds_per_cu = 65536;
@@ -417,7 +417,7 @@ static void destroy_shard(kb_sim* s) {
   (void)hipSetDevice(s->device);
   if (s->st) (void)hipStreamSynchronize(s->st);
   free_all(s);
-  if (s->ev0) { (void)hipEventDestroy(s->ev0); (void)hipEventDestroy(s->ev1); (void)hipEventDestroy(s->er0); (void)hipEventDestroy(s->er1); }
+  for (hipEvent_t e : {s->ev0, s->ev1, s->er0, s->er1, s->ef0, s->ef1}) if (e) (void)hipEventDestroy(e);
   if (s->st) (void)hipStreamDestroy(s->st);
   delete s->xf;
   delete s;
@@ -472,7 +472,6 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   d.capk = (BUFSZ - 20 - Lid) / (18 + Lid);           // 20 + L + k(18+L) <= 10240
   d.capj = (BUFSZ - 20 - Lid - 1) / (18 + Lid);       // 20 + L + k(18+L) <  10240
   d.paybound = C < d.capk ? C : d.capk;
-  if (const char* ab = getenv("KB_ABLATE")) d.ablate = (uint32_t)atoi(ab);
   d.dbg = cfg->debug_flags;
   s->debug_waves = getenv("KB_DEBUG_WAVES") != nullptr;
   s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid); s->h_ever.assign(C, 0);
@@ -504,7 +503,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   A(s->scan_tot, 32); A(s->scan_tiles, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
   AR(s->nresp, 1); AR(s->paysum, 1); AR(s->nbase, 1); AR(s->resp_off, 1);
   A(s->resp_nodes, R); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS); A(s->slow, R);
-  AR(s->so.part, (size_t)S * 10);
+  AR(s->ro.part, 10);
   if (xf) {
     XState& x = s->xs;
     x.world = (uint32_t)world; x.R = R; x.S = rows_per;
@@ -518,11 +517,10 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
 #undef A
 #undef AR
   if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); destroy_shard(s); return KB_CAPACITY; }
-  s->so.S = S;
   (void)hipMemset(L(s, d.kpr_big), 0xFF, 4ull * R);          // no round yet
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
-  (void)hipEventCreate(&s->ev0); (void)hipEventCreate(&s->ev1); (void)hipEventCreate(&s->er0); (void)hipEventCreate(&s->er1);
+  for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->er0, &s->er1, &s->ef0, &s->ef1}) (void)hipEventCreate(e);
   int rc = upload_segments(s);
   if (rc) { destroy_shard(s); return rc; }
   uint32_t ctr0[NCTR] = {0};
@@ -782,21 +780,22 @@ static int step_round(kb_sim* s) {
   const bool pb_hbm = (d.dbg & KB_DBG_PHASEB_HBM) != 0;
   if (s->nf > 2048 || (pb_hbm && s->nf)) k_bfail_prep<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep, d.ctr + C_PATHS);
   else if (s->nf) k_bfail_prep_lds<<<1, 1024, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep);
-  if (have_b) {
-    // persistent waves; broadcast lists staged in LDS once per workgroup when they fit
-    const uint32_t budget = 65536 / 4;                 // dynamic LDS words per workgroup
+  {
+    // the row pass (broadcast phase + A3 candidates), persistent waves; broadcast lists staged in LDS
+    // once per workgroup when they fit.  Its events are taken by its own dispatch packet
+    // (hipExtLaunchKernel), so they time the kernel itself.
+    const uint32_t budget = RP_LDS_BYTES / 4;          // dynamic LDS words per workgroup
     uint32_t lf = s->nf <= PB_FMAX, lj = s->nj <= PB_JMAX;
     uint32_t listw = (lf ? 2 * s->nf : 0) + (lj ? s->nj : 0);
     if (listw > budget / 2 || pb_hbm) { lf = lj = 0; listw = 0; }
     const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR && !pb_hbm;
-    const uint32_t wpb = ldsb ? std::min<uint32_t>(4, (budget - listw) / d.NWR) : 4;
+    const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / d.NWR) : RP_WAVES;
     const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
-    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)(s->lds_per_cu / std::max<size_t>(lds + 512, 1))));
+    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)(s->lds_per_cu / std::max<size_t>(lds + 1024, 1))));
     const uint32_t blocks = std::min<uint32_t>((R + wpb - 1) / wpb, s->ncu * per_cu);
-    if (ldsb) k_phaseB<true><<<blocks, 64 * wpb, lds, st>>>(d, pb, r, lf, lj);
-    else k_phaseB<false><<<blocks, 64 * wpb, lds, st>>>(d, pb, r, lf, lj);
+    if (ldsb) hipExtLaunchKernelGGL(k_rowpass<true>, dim3(blocks), dim3(64 * wpb), lds, st, s->ev0, s->ev1, 0, d, pb, s->ro, r, lf, lj);
+    else hipExtLaunchKernelGGL(k_rowpass<false>, dim3(blocks), dim3(64 * wpb), lds, st, s->ev0, s->ev1, 0, d, pb, s->ro, r, lf, lj);
   }
-  else { HIPCHK(hipMemsetAsync(L(s, s->nresp), 0, 4ull * R, st)); HIPCHK(hipMemsetAsync(L(s, s->paysum), 0, 4ull * R, st)); }
   {  // wave-0 outbox regions: responses first, then the tick's messages
     ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 3;
@@ -843,11 +842,12 @@ static int step_round(kb_sim* s) {
   // 3. tick
   k_tick_scan<<<gnode, tb, 0, st>>>(d, s->bs, r, s->slow);                       // A1; list the A2 nodes
   k_tick_pre<<<std::min<uint32_t>(gwave, 1024), 256, 0, st>>>(d, o0, s->bs, r, s->slow);   // A2 per listed node
-  // the sweep's events are taken by its own dispatch packet (hipExtLaunchKernel), so they time the
-  // kernel itself: a marker recorded before the launch can run while k_tick_pre is still executing
-  // and read ~12 % above rocprof's duration
-  hipExtLaunchKernelGGL(k_sweep, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, st, s->ev0, s->ev1, 0, d, s->so);
-  k_tick_post<<<gnode, tb, 0, st>>>(d, s->so, o0, r);
+  // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded; timed by
+  // events on its own dispatch packet (a marker recorded before the launch can run while k_tick_pre
+  // is still executing)
+  if (d.uniform)
+    hipExtLaunchKernelGGL(k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, st, s->ef0, s->ef1, 0, d, FoldArgs{s->S});
+  k_tick_post<<<gnode, tb, 0, st>>>(d, s->ro, o0, r);
   {
     ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 2;
@@ -938,7 +938,8 @@ static int step_round(kb_sim* s) {
   }
   s->bj_total += s->nj; s->bf_total += s->nf;
   float ms = 0;
-  (void)hipEventElapsedTime(&ms, s->ev0, s->ev1); s->sweep_ms += ms; s->sweep_launches++;
+  (void)hipEventElapsedTime(&ms, s->ev0, s->ev1); s->rowpass_ms += ms; s->rowpass_launches++;
+  if (d.uniform) { (void)hipEventElapsedTime(&ms, s->ef0, s->ef1); s->fold_ms += ms; s->fold_launches++; }
   (void)hipEventElapsedTime(&ms, s->er0, s->er1); s->round_ms += ms; s->round_launches++;
   s->round = r + 1;
   return check_err(s);
@@ -1255,6 +1256,7 @@ extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
   out->drop_oversize = st[S_OVERSIZE]; out->drop_partition = st[S_PART]; out->drop_bcast = st[S_BDROP];
   out->removed_timeout = st[S_RMTIMEOUT]; out->removed_failed = st[S_RMFAILED]; out->join_responses = st[S_JRESP];
   out->curious_overflow = st[S_CUROVF]; out->churn_leaves = st[S_CLEAVE]; out->churn_joins = st[S_CJOIN];
+  out->sent_kp_ids = st[S_KPIDS];
   return KB_OK;
 }
 // per id: alive, n, last_bcast, start_round; n and last_bcast only for the rows this handle holds
@@ -1331,28 +1333,33 @@ extern "C" uint32_t kb_fingerprint_of_set(const uint32_t* ids, size_t n, const u
 extern "C" int kb_sim_kernel_time(kb_sim* s, int kind, double* ms, uint64_t* launches) {
   if (!s || !ms || !launches) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_kernel_time(s->shards[0], kind, ms, launches);
-  if (kind == 0) { *ms = s->sweep_ms; *launches = s->sweep_launches; }
-  else { *ms = s->round_ms; *launches = s->round_launches; }
+  if (kind == KB_KT_ROWPASS) { *ms = s->rowpass_ms; *launches = s->rowpass_launches; }
+  else if (kind == KB_KT_ROUND) { *ms = s->round_ms; *launches = s->round_launches; }
+  else if (kind == KB_KT_FOLD) { *ms = s->fold_ms; *launches = s->fold_launches; }
+  else return KB_INVALID_ARGUMENT;
   return KB_OK;
 }
-static uint64_t sweep_counter(kb_sim* s) {
+static uint64_t stat_counter(kb_sim* s, int idx) {
   unsigned long long v = 0;
-  if (hipMemcpy(&v, s->d.stats + S_SWEEPB, 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+  if (hipMemcpy(&v, s->d.stats + idx, 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
   return v;
 }
 extern "C" int kb_sim_reset_kernel_time(kb_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
   GROUP_ALL(kb_sim_reset_kernel_time);
-  s->sweep_ms = s->round_ms = 0; s->sweep_launches = s->round_launches = 0;
-  s->sweep_bytes = sweep_counter(s);            // baseline of the device-side byte counter
+  s->rowpass_ms = s->round_ms = s->fold_ms = 0; s->rowpass_launches = s->round_launches = s->fold_launches = 0;
+  s->row_bytes0 = stat_counter(s, S_ROWB);        // baselines of the device-side byte counters
+  s->fold_bytes0 = stat_counter(s, S_FOLDB);
   return KB_OK;
 }
-// bytes of member bits and stamp lines the row sweep read since the last reset (counted in-kernel;
-// this handle's rows: shard 0's for a group, like kb_sim_kernel_time)
-extern "C" int kb_sim_sweep_bytes(kb_sim* s, uint64_t* bytes) {
+// algorithmic bytes a kernel moved since the last reset, counted in-kernel; this handle's
+// rows: shard 0's for a group, like kb_sim_kernel_time
+extern "C" int kb_sim_kernel_bytes(kb_sim* s, int kind, uint64_t* bytes) {
   if (!s || !bytes) return KB_INVALID_ARGUMENT;
-  if (is_group(s)) return kb_sim_sweep_bytes(s->shards[0], bytes);
-  *bytes = sweep_counter(s) - s->sweep_bytes;
+  if (is_group(s)) return kb_sim_kernel_bytes(s->shards[0], kind, bytes);
+  if (kind == KB_KT_ROWPASS) *bytes = stat_counter(s, S_ROWB) - s->row_bytes0;
+  else if (kind == KB_KT_FOLD) *bytes = stat_counter(s, S_FOLDB) - s->fold_bytes0;
+  else return KB_INVALID_ARGUMENT;
   return KB_OK;
 }
 // OR of the PATH_* bits (kb_common.h) of the kernel variants that did work since creation

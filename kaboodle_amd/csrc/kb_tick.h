@@ -144,210 +144,70 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
 
 
 // ================================================================================================
-// THE ROW SWEEP (dominant kernel).  ping_random_peer (:655-703) keeps the 5 oldest Known peers by
-// (stamp, address rotated to start right after self); generate_fingerprint (:71-83) is refreshed for
-// the segments whose membership changed.  Lane = node: a wave sweeps 64 rows over one column split,
-// every lane streaming whole 128-byte lines of its own row, all lanes sharing the same half-block
-// CRC tables.  Per (node, split) it leaves two partial top-5 lists: ids below the rotation point
-// (part A, rot = j - p + C) and from it on (part B, rot = j - p); in id order each part is monotone
-// in rot, so an equal stamp seen later never displaces an earlier one (strict < test).
+// THE FOLD: generate_fingerprint's checkpoints (:71-83).  Every segment whose membership changed since
+// its checkpoint (sdirty) is refolded from the member bits: per 8-id block, raw = raw·Z^popc ⊕
+// htab[block][mask], the multiply through four LDS byte tables.  Lane = node: a wave folds 64 rows over
+// one column split; workgroups take split blockIdx % S, so each XCD (workgroups are dealt round-robin to
+// the 8 XCDs) stays on 1/min(S, 8) of the columns and its slice of htab stays in that XCD's 4 MB L2.
+// Runs after A2 (the last membership change of the tick), so the tick ends with every checkpoint fresh.
 // ================================================================================================
-struct SweepOut { uint32_t* part; uint32_t S; };   // part: [C][S][10] keys (b << 24 | rot)
+struct FoldArgs { uint32_t S; };
 
-__device__ inline void top5_insert(uint32_t (&k)[5], uint32_t nk) {
-#pragma unroll
-  for (int s = 0; s < 5; ++s) { if (nk < k[s]) { const uint32_t t = k[s]; k[s] = nk; nk = t; } }
-}
-__device__ inline uint32_t thr5(const uint32_t (&k)[5]) { return k[4] == 0xFFFFFFFFu ? 256u : (k[4] >> 24); }
-
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-// smallest (byte - 2) over the 16 bytes of x, computed on 16-bit lanes with packed ops (bytes 0 and 1
-// wrap to >= 0xFFFE): a byte b can enter a top-5 list with threshold T only if this is < T - 2
-__device__ inline uint32_t min_stamp16(const uint4& x) {
-  const u16x2 two = {2, 2};
-  u16x2 mn = {0xFFFF, 0xFFFF};
-  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    mn = __builtin_elementwise_min(mn, __builtin_bit_cast(u16x2, w[k] & 0x00FF00FFu) - two);
-    mn = __builtin_elementwise_min(mn, __builtin_bit_cast(u16x2, (w[k] >> 8) & 0x00FF00FFu) - two);
-  }
-  return mn.x < mn.y ? mn.x : mn.y;
-}
-
-// One 128-id step of one lane's row, software-pipelined: the loads of step k+1 are issued before
-// step k is processed.  Stamp bytes (128 B, plus the 16 B of member bits) are loaded while either
-// part's list can still change: a part is final once it holds five ancient (minimum) stamps, since
-// later ids of the part have larger rot.  Member bits are loaded alone to refold a stale checkpoint.
-struct StepIn { uint4 v[8]; uint4 mb; };
-
-__device__ inline bool step_need(const Dev& d, const uint32_t (&A)[5], const uint32_t (&B)[5], uint32_t p, uint32_t col) {
-  return !(d.ablate & 2) && ((thr5(A) > ST_ANCIENT && col < p) || (thr5(B) > ST_ANCIENT && col + 128 > p));
-}
-
-template <bool FOLD>
-__device__ __attribute__((always_inline)) inline void step_load(const uint8_t* rw, const uint32_t* bw, uint32_t col,
-                                                                bool need, StepIn& s, uint32_t& nbytes) {
-  if (need) {
-#pragma unroll
-    for (int q = 0; q < 8; ++q) s.v[q] = *reinterpret_cast<const uint4*>(rw + col + 16 * q);
-    nbytes += 128;
-  }
-  if (FOLD || need) { s.mb = *reinterpret_cast<const uint4*>(bw + (col >> 5)); nbytes += 16; }
-}
-
-// A packed-u16 filter rejects 16-byte groups with no stamp below the current threshold; surviving
-// groups are examined byte by byte against the member bits (strict <: within a part ids arrive in
-// increasing rot, so an equal stamp seen later never displaces an earlier one).
-// The fold's 16 table reads are issued before the next step's prefetch: vmcnt retires in order,
-// so waiting for them must not also wait for the prefetch.
-template <bool FOLD>
-__device__ __attribute__((always_inline)) inline void fold_fetch(const Dev& d, const StepIn& s, uint32_t col,
-                                                                 uint32_t (&hv)[16]) {
-  if (!FOLD) return;
-  const uint32_t mw[4] = {s.mb.x, s.mb.y, s.mb.z, s.mb.w};
-  const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
-#pragma unroll
-  for (int h = 0; h < 16; ++h) hv[h] = ht[h * 256 + ((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu)];   // entry 0 is 0
-}
-
-// A packed-u16 filter rejects 16-byte groups with no stamp below the current threshold; surviving
-// groups are examined byte by byte against the member bits (strict <: within a part ids arrive in
-// increasing rot, so an equal stamp seen later never displaces an earlier one).
-template <bool FOLD>
-__device__ __attribute__((always_inline)) inline void step_proc(const Dev& d, const uint32_t* zb, const StepIn& s,
-                                                                const uint32_t (&hv)[16], bool loaded, uint32_t i,
-                                                                uint32_t p, uint32_t col, uint32_t (&A)[5],
-                                                                uint32_t (&B)[5], uint32_t& raw, uint32_t& cnt) {
-  if (FOLD) {
-    const uint32_t mw[4] = {s.mb.x, s.mb.y, s.mb.z, s.mb.w};
-#pragma unroll
-    for (int h = 0; h < 16; ++h) {
-      const uint32_t c = __popc((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu);   // Z^0 table is the identity
-      raw = mulzb(zb, raw, c) ^ hv[h];
-      cnt += c;
-    }
-  }
-  if (!loaded) return;
-  const uint32_t C = d.C;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    // thresholds are re-read per 16-id group: once a part holds five ancient stamps (typically
-    // within the first group of a step) the rest of the step is rejected by the packed filter
-    const uint32_t TA = thr5(A), TB = thr5(B);
-    const bool needA = TA > ST_ANCIENT && col < p, needB = TB > ST_ANCIENT && col + 128 > p;
-    if (!(needA || needB)) break;
-    const uint32_t T = (needA && TA > (needB ? TB : 0u)) ? TA : TB;   // the larger relevant threshold
-    if (min_stamp16(s.v[q]) >= T - 2) continue;
-    const uint32_t mwq = (q >> 1) == 0 ? s.mb.x : ((q >> 1) == 1 ? s.mb.y : ((q >> 1) == 2 ? s.mb.z : s.mb.w));
-    uint32_t cm = (nzmask4(s.v[q].x & 0xFEFEFEFEu) | (nzmask4(s.v[q].y & 0xFEFEFEFEu) << 4) |
-                   (nzmask4(s.v[q].z & 0xFEFEFEFEu) << 8) | (nzmask4(s.v[q].w & 0xFEFEFEFEu) << 12)) &
-                  ((mwq >> (16 * (q & 1))) & 0xFFFFu);
-    while (cm) {
-      const uint32_t t = __ffs(cm) - 1;
-      cm &= cm - 1;
-      const uint32_t word = (t & 8) ? ((t & 4) ? s.v[q].w : s.v[q].z) : ((t & 4) ? s.v[q].y : s.v[q].x);
-      const uint32_t b = (word >> (8 * (t & 3))) & 0xFFu;
-      const uint32_t j = col + 16 * q + t;
-      if (j == i) continue;
-      if (j >= p) { if (b < thr5(B)) top5_insert(B, (b << 24) | (j - p)); }
-      else if (b < thr5(A)) top5_insert(A, (b << 24) | (j + C - p));
-    }
-  }
-}
-
-template <bool FOLD>
-__device__ __attribute__((always_inline)) inline void sweep_segment(const Dev& d, const uint32_t* zb, const uint8_t* rw,
-                                                                    const uint32_t* bw, uint32_t i, uint32_t p,
-                                                                    uint32_t c0, uint32_t c1, uint32_t (&A)[5],
-                                                                    uint32_t (&B)[5], uint32_t& raw, uint32_t& cnt,
-                                                                    uint32_t& nbytes) {
-  if (c0 >= c1) return;
-  // Measured: prefetching only the bits (stamps loaded in-step) fits 4 waves/SIMD and is 3 % faster,
-  // but the extra waves evict each row's bit line between its 8 steps: HBM traffic 1.71x the
-  // algorithmic bytes instead of 1.14x.  The full prefetch is kept.
-  StepIn cur;
-  bool need_cur = step_need(d, A, B, p, c0);
-  step_load<FOLD>(rw, bw, c0, need_cur, cur, nbytes);
-  for (uint32_t col = c0; col < c1; col += 128) {
-    uint32_t hv[16];
-    fold_fetch<FOLD>(d, cur, col, hv);
-    StepIn nxt;
-    // thresholds only fall, so the need computed before processing this step is a superset
-    const bool need_nxt = col + 128 < c1 && step_need(d, A, B, p, col + 128);
-    if (col + 128 < c1) step_load<FOLD>(rw, bw, col + 128, need_nxt, nxt, nbytes);
-    step_proc<FOLD>(d, zb, cur, hv, need_cur, i, p, col, A, B, raw, cnt);
-    cur = nxt;
-    need_cur = need_nxt;
-  }
-}
-
-__global__ __launch_bounds__(256) void k_sweep(Dev d, SweepOut so) {
+__global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
   __shared__ uint32_t zb[ZB];
   load_zbtab(d, zb);
-  // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so split s = blockIdx % S keeps each
-  // XCD on 1/min(S,8) of the columns and its slice of the half-block CRC tables resident in its L2.
-  const uint32_t S = so.S;
+  const uint32_t S = fa.S;
   const uint32_t s = blockIdx.x % S;
   const uint32_t g = (blockIdx.x / S) * 4 + (threadIdx.x >> 6);
   const uint32_t i0 = d.lo + g * 64 + lane();
-  const bool act = i0 < d.hi && d.alive[i0];
-  // the ballot is taken once with the full wave active: inside the select below it would run
-  // under the idle lanes' exec mask only and see no live lane
+  const bool act = i0 < d.hi && d.alive[i0] && d.uniform;
   const unsigned long long actm = __ballot(act);
   if (!actm) return;
-  const uint32_t shadow = d.lo + g * 64 + (uint32_t)(__ffsll((long long)actm) - 1);
-  const uint32_t i = act ? i0 : shadow;                 // idle lanes shadow a live one
-  const uint8_t* rw = row_of(d, i);
+  const uint32_t i = act ? i0 : d.lo + g * 64 + (uint32_t)(__ffsll((long long)actm) - 1);   // idle lanes shadow a live one
   const uint32_t* bw = bits_of(d, i);
-  const uint32_t C = d.C;
-  const uint32_t p = (i + 1 == C) ? 0 : i + 1;
-  const unsigned long long sd = (d.uniform && act) ? d.sdirty[i] : 0ull;
-  uint32_t A[5], B[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) { A[k] = 0xFFFFFFFFu; B[k] = 0xFFFFFFFFu; }
-  uint32_t nbytes = 0;
   const uint32_t spp = NSEG / S;
+  const unsigned long long sd = act ? d.sdirty[i] : 0ull;
   unsigned long long folded = 0;
+  uint32_t nbytes = 0;
   for (uint32_t k = s * spp; k < (s + 1) * spp; ++k) {
-    const uint32_t c0 = k * d.SEGW, c1 = c0 + d.SEGW < C ? c0 + d.SEGW : ((C + 127) & ~127u);
+    const bool mine = (sd >> k) & 1ull;
+    if (!__ballot(mine)) continue;                  // wave-uniform: no row of this wave changed here
+    const uint32_t c0 = k * d.SEGW, c1 = c0 + d.SEGW;
     uint32_t raw = 0, cnt = 0;
-    const bool mine = ((sd >> k) & 1ull) && !(d.ablate & 1);
-    if (__ballot(mine)) {                 // wave-uniform: one pass for the whole wave
-      sweep_segment<true>(d, zb, rw, bw, i, p, c0, c1, A, B, raw, cnt, nbytes);
-      if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; }
-    } else {
-      const bool need = (thr5(A) > ST_ANCIENT && c0 < p) || (thr5(B) > ST_ANCIENT && c1 > p);
-      if (!__ballot(act && need)) continue;   // no list of this wave can change in this segment
-      sweep_segment<false>(d, zb, rw, bw, i, p, c0, c1, A, B, raw, cnt, nbytes);
+    uint4 mb = *reinterpret_cast<const uint4*>(bw + (c0 >> 5));
+    for (uint32_t col = c0; col < c1; col += 128) {
+      const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
+      uint32_t hv[16];
+      const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
+#pragma unroll
+      for (int h = 0; h < 16; ++h) hv[h] = ht[h * 256 + ((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu)];   // entry 0 is 0
+      if (col + 128 < c1) mb = *reinterpret_cast<const uint4*>(bw + ((col + 128) >> 5));   // next step's bits
+#pragma unroll
+      for (int h = 0; h < 16; ++h) {
+        const uint32_t c = __popc((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu);   // Z^0 table is the identity
+        raw = mulzb(zb, raw, c) ^ hv[h];
+        cnt += c;
+      }
     }
+    nbytes += d.SEGW / 8;
+    if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; }
   }
   const uint32_t wb = wave_sum(act ? nbytes : 0u);
-  if (lane() == 0 && wb) atomicAdd(&d.stats[S_SWEEPB], (unsigned long long)wb);
-  if (!act) return;
+  if (lane() == 0 && wb) atomicAdd(&d.stats[S_FOLDB], (unsigned long long)wb);
   if (folded) atomicAnd(&d.sdirty[i], ~folded);
-  uint32_t* out = so.part + ((size_t)i * S + s) * 10;
-#pragma unroll
-  for (int k = 0; k < 5; ++k) { out[k] = A[k]; out[5 + k] = B[k]; }
 }
 
 // ---- pick the ping target (one of the oldest 5), WaitingForPing(now), Ping; ping_addrs (:550-556);
 // ---- refresh the fingerprint from the checkpoints; agreement with the running set.  Thread per node.
-__global__ void k_tick_post(Dev d, SweepOut so, OutBuf ob, int32_t r) {
+__global__ void k_tick_post(Dev d, RowOut ro, OutBuf ob, int32_t r) {
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long agree = 0;
   if (i < d.hi && d.alive[i]) {
-    const uint32_t C = d.C, S = so.S;
+    const uint32_t C = d.C;
     const uint32_t p = (i + 1 == C) ? 0 : i + 1;
-    uint32_t k5[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    const uint2* part = reinterpret_cast<const uint2*>(so.part + (size_t)i * S * 10);   // S * 10 is even
-#pragma unroll 8
-    for (uint32_t q = 0; q < S * 5; ++q) {
-      const uint2 x = part[q];
-      if (x.x < k5[4]) top5_insert(k5, x.x);
-      if (x.y < k5[4]) top5_insert(k5, x.y);
-    }
+    uint32_t k5[5];                                 // the row pass's five smallest keys, ascending
+    const uint4 a = *reinterpret_cast<const uint4*>(ro.part + (size_t)i * 10);
+    k5[0] = a.x; k5[1] = a.y; k5[2] = a.z; k5[3] = a.w; k5[4] = ro.part[(size_t)i * 10 + 4];
     uint32_t nc = 0;
     while (nc < 5 && k5[nc] != 0xFFFFFFFFu) nc++;
     uint32_t oseq = ob.cnt[i];

@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
   const uint32_t wv = threadIdx.x >> 6, l = lane();
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0;
+  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0, kpids = 0;
   const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
   s_ex[wv][l] = wave_excl(cnt);
   s_base[wv][l] = i < d.hi ? ob.off[i] : 0;
@@ -61,6 +61,7 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
     const uint32_t g = s_base[wv][j] + q;
     const Msg m = ob.msgs[g];
     ks[m.kind < 5 ? m.kind : 0]++;
+    if (m.kind == K_KP) kpids += m.a;
     uint8_t st = 0;
     if (last) win++;
     else if (!d.alive[m.dest]) dead++;
@@ -81,6 +82,7 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
   }
   for (int k = 0; k < 5; ++k) stat_add(d, S_PING + k, ks[k]);
   stat_add(d, S_DEAD, dead); stat_add(d, S_PART, part); stat_add(d, S_LOSS, loss); stat_add(d, S_WINDOW, win);
+  stat_add(d, S_KPIDS, kpids);
 }
 
 __global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
   const uint32_t wv = threadIdx.x >> 6, l = lane();
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0;
+  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0, kpids = 0;
   const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
   s_ex[wv][l] = wave_excl(cnt);
   s_base[wv][l] = i < d.hi ? ob.off[i] : 0;
@@ -142,6 +144,7 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
     const uint32_t g = s_base[wv][j] + q;
     const Msg m = ob.msgs[g];
     ks[m.kind < 5 ? m.kind : 0]++;
+    if (m.kind == K_KP) kpids += m.a;
     uint8_t st = 0;
     if (last) win++;
     else if (!d.alive[m.dest]) dead++;
@@ -158,6 +161,7 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
   }
   for (int k = 0; k < 5; ++k) stat_add(d, S_PING + k, ks[k]);
   stat_add(d, S_DEAD, dead); stat_add(d, S_PART, part); stat_add(d, S_LOSS, loss); stat_add(d, S_WINDOW, win);
+  stat_add(d, S_KPIDS, kpids);
 }
 
 // records / payload ids this shard sends to each shard (from the scans' block starts and totals)

@@ -650,7 +650,7 @@ static omsg* gather_out(kbo_sim* s, size_t* total) {
         case K_PING: s->st.sent_ping++; break;
         case K_PINGREQ: s->st.sent_ping_req++; break;
         case K_ACK: s->st.sent_ack++; break;
-        case K_KP: s->st.sent_known_peers++; break;
+        case K_KP: s->st.sent_known_peers++; s->st.sent_kp_ids += s->out[i].v[q].pay_len; break;
         case K_KPR: s->st.sent_kpr++; break;
       }
     }
@@ -698,7 +698,7 @@ static int run_waves(kbo_sim* s, int32_t r) {
         case K_PING: s->st.sent_ping++; break;
         case K_PINGREQ: s->st.sent_ping_req++; break;
         case K_ACK: s->st.sent_ack++; break;
-        case K_KP: s->st.sent_known_peers++; break;
+        case K_KP: s->st.sent_known_peers++; s->st.sent_kp_ids += s->out[i].v[q].pay_len; break;
         case K_KPR: s->st.sent_kpr++; break;
       }
       free(s->out[i].v[q].pay);

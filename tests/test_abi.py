@@ -39,7 +39,7 @@ def test_hip_library_exports_every_symbol():
 
 def test_oracle_exports_every_symbol():
     lib = C.CDLL(ORACLE_SO)
-    skip = {"kb_sim_kernel_time", "kb_sim_reset_kernel_time", "kb_sim_sweep_bytes",    # GPU timing surface
+    skip = {"kb_sim_kernel_time", "kb_sim_reset_kernel_time", "kb_sim_kernel_bytes",   # GPU timing surface
             "kb_sim_debug_paths",                                                      # GPU kernel variants
             "kb_rccl_unique_id", "kb_sim_create_rank", "kb_sim_create_local", "kb_sim_shard_info"}  # sharding
     missing = [n for n in declared() if n not in skip and not hasattr(lib, "kbo_" + n[3:])]
@@ -47,9 +47,9 @@ def test_oracle_exports_every_symbol():
 
 
 def test_struct_layouts_match_header():
-    # kb_config: 17 scalar fields (seed is u64) + reserved[4]; kb_stats: 6 x 4-byte + 19 x u64 + reserved[8]
+    # kb_config: 17 scalar fields (seed is u64) + reserved[4]; kb_stats: 6 x 4-byte + 20 x u64 + reserved[7]
     assert C.sizeof(KbConfig) == 4 * 4 + 8 + 4 * 12 + 4 * 4
-    assert C.sizeof(KbStats) == 6 * 4 + 19 * 8 + 8 * 8
+    assert C.sizeof(KbStats) == 6 * 4 + 20 * 8 + 7 * 8
 
 
 def test_config_default_matches_mirror():

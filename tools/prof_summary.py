@@ -3,8 +3,9 @@
   prof_summary.py stats <dir> [K]        kernel_stats.csv -> compact table (name, calls, avg us, total %), and
                                          k_sweep's average over its last K launches of the kernel trace
                                          (bench's timed steps; the table's average includes the warmup)
-  prof_summary.py pmc <dir> [bench args] counter_collection.csv of the FETCH_SIZE / WRITE_SIZE passes ->
-                                         JSON with HBM bytes per k_sweep launch (FETCH_SIZE x2, gfx950)
+  prof_summary.py pmc <dir> <kernel> [bench args]
+                                         counter_collection.csv of the FETCH_SIZE / WRITE_SIZE passes ->
+                                         JSON with HBM bytes per launch of <kernel> (FETCH_SIZE x2, gfx950)
 """
 import csv
 import glob
@@ -35,29 +36,35 @@ def stats(d, k_last=0):
     for r in rs:
         print(f"{short(r['Name'])[:40]:40s} {r['Calls']:>7s} {float(r['AverageNs'])/1e3:10.2f} {float(r['Percentage']):6.2f}")
     if k_last:
-        tr = [r for r in rows(os.path.join(d, "**", "*kernel_trace.csv")) if short(r["Kernel_Name"]) == "k_sweep"]
-        tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-        dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in tr][-k_last:]
-        if dur:
-            print(f"k_sweep over its last {len(dur)} launches (the timed steps): avg {sum(dur) / len(dur):.2f} us")
+        for kn in ("k_rowpass<true>", "k_rowpass<false>", "k_fold"):
+            tr = [r for r in rows(os.path.join(d, "**", "*kernel_trace.csv")) if short(r["Kernel_Name"]) == kn]
+            tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+            dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in tr][-k_last:]
+            if dur:
+                print(f"{kn} over its last {len(dur)} launches (the timed steps): avg {sum(dur) / len(dur):.2f} us")
 
 
-def pmc(d, args):
+def pmc(d, kernel, args):
     res = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
         vals = [float(r["Counter_Value"]) for r in rows(os.path.join(d, c, "**", "*counter_collection.csv"))
-                if "k_sweep" in r.get("Kernel_Name", "") and r.get("Counter_Name") == c]
+                if kernel in r.get("Kernel_Name", "") and r.get("Counter_Name") == c]
         res[c] = sum(vals) / len(vals) if vals else None
         res[c + "_dispatches"] = len(vals)
     # rocprofv3 reports both in KB; gfx950 FETCH_SIZE counts half of a wide streaming read (guide, HBM section)
     fetch = res["FETCH_SIZE"] * 1024 * 2 if res["FETCH_SIZE"] is not None else None
     write = res["WRITE_SIZE"] * 1024 if res["WRITE_SIZE"] is not None else None
-    nodes, loss, churn = 65536, 0.01, 0.001
+    nodes, loss, churn, steps, warmup = 65536, 0.01, 0.001, 50, 5
     for k, v in zip(args[::2], args[1::2]):
         if k == "--nodes":
             nodes = int(v)
+        elif k == "--steps":
+            steps = int(v)
+        elif k == "--warmup":
+            warmup = int(v)
     workload = f"configs[2]: {nodes} peers, converged start, {loss:.0%} loss, {churn:.1%}/round churn"
-    out = {"kernel": "k_sweep", "workload": workload, "raw_kb": res,
+    capacity = nodes + max(4096, int(nodes * churn * (steps + warmup + 8) * 1.5))      # bench.rank_config
+    out = {"kernel": kernel.split("<")[0], "workload": workload, "capacity": capacity, "raw_kb": res,
            "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
            "hbm_bytes_per_launch": (fetch or 0) + (write or 0) if fetch is not None else None,
            "correction": "FETCH_SIZE(KB)*1024*2 (gfx950 half-count of 16B/lane streaming reads) + WRITE_SIZE(KB)*1024"}
@@ -84,4 +91,4 @@ if __name__ == "__main__":
     elif sys.argv[1] == "sq":
         sq(sys.argv[2])
     else:
-        pmc(sys.argv[2], sys.argv[3:])
+        pmc(sys.argv[2], sys.argv[3], sys.argv[4:])

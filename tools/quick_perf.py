@@ -13,8 +13,9 @@ t = time.time(); m = kaboodle_amd.Mesh(cfg); print("create", round(time.time() -
 m.step(2)
 m.reset_kernel_time()
 t = time.time(); m.step(R); dt = time.time() - t
-sw, n = m.kernel_time(0); rd, _ = m.kernel_time(1)
+sw, n = m.kernel_time(0); rd, _ = m.kernel_time(1); fo, nf = m.kernel_time(2)
 st = m.stats()
-print(f"N={N} R={R} wall {dt/R*1e3:.2f} ms/round  sweep {sw/n:.3f} ms  round(ev) {rd/n:.3f} ms  "
-      f"node-rounds/s {st['alive']*R/dt:.3e}  sweep GB/s {m.sweep_bytes()/ (sw*1e-3)/1e9:.1f}", flush=True)
+print(f"N={N} R={R} wall {dt/R*1e3:.2f} ms/round  rowpass {sw/n:.3f} ms ({m.kernel_bytes(0)/(sw*1e-3)/1e9:.1f} GB/s)  "
+      f"fold {fo/max(nf,1):.3f} ms ({m.kernel_bytes(2)/max(fo*1e-3,1e-9)/1e9:.1f} GB/s)  round(ev) {rd/n:.3f} ms  "
+      f"node-rounds/s {st['alive']*R/dt:.3e}", flush=True)
 print(st)
