@@ -42,6 +42,7 @@ constexpr int ZB = 9 * 1024;      // byte tables for Z^0..Z^8 (4 lookups per mul
 struct Dev {
   uint32_t lo, hi;                // local rows (unsharded: 0, C)
   uint32_t C, W, SEGW, NWR;       // capacity, row stride, ids per segment (W/64), bitset words per row (W/32)
+  uint32_t segq, segm;            // SEGW = 128 * segq; segm = ceil(2^32 / segq) (segment of id j without a divide)
   uint32_t k0, k1;
   uint32_t loss_thr, churn_thr;
   int32_t fault_end;
@@ -96,16 +97,13 @@ __device__ inline uint32_t log_window_start(const Dev& d, uint32_t i, int32_t r)
 // copy n 16-byte words global -> LDS with `lanes` cooperating threads (index t), 8 loads in flight each
 __device__ __attribute__((always_inline)) inline void stage16(uint4* dst, const uint4* src, uint32_t n, uint32_t t,
                                                              uint32_t lanes) {
-  for (uint32_t w0 = t; w0 < n; w0 += lanes * 4) {     // four independent loads in flight, then the stores
-    const uint32_t w1 = w0 + lanes, w2 = w1 + lanes, w3 = w2 + lanes;
-    const uint4 v0 = src[w0];
-    const uint4 v1 = src[w1 < n ? w1 : w0];
-    const uint4 v2 = src[w2 < n ? w2 : w0];
-    const uint4 v3 = src[w3 < n ? w3 : w0];
-    dst[w0] = v0;
-    if (w1 < n) dst[w1] = v1;
-    if (w2 < n) dst[w2] = v2;
-    if (w3 < n) dst[w3] = v3;
+  constexpr int U = 8;                                  // independent loads in flight per lane, then the stores
+  for (uint32_t w0 = t; w0 < n; w0 += lanes * U) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) { const uint32_t w = w0 + lanes * u; v[u] = src[w < n ? w : w0]; }
+#pragma unroll
+    for (int u = 0; u < U; ++u) { const uint32_t w = w0 + lanes * u; if (w < n) dst[w] = v[u]; }
   }
 }
 __device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }
@@ -119,7 +117,9 @@ __device__ inline bool part_blocks(const Dev& d, int32_t r, uint32_t a, uint32_t
 __device__ inline uint8_t* row_of(const Dev& d, uint32_t i) { return d.stamp + (size_t)i * d.W; }
 __device__ inline uint32_t* bits_of(const Dev& d, uint32_t i) { return d.bits + (size_t)i * d.NWR; }
 __device__ inline bool is_mem(const Dev& d, uint32_t i, uint32_t j) { return (bits_of(d, i)[j >> 5] >> (j & 31)) & 1u; }
-__device__ inline unsigned long long seg_bit(const Dev& d, uint32_t j) { return 1ull << (j / d.SEGW); }
+// j / SEGW = (j >> 7) / segq by a multiply-high (exact: j >> 7 < 2^16 and segq < 2^16)
+__device__ inline uint32_t seg_of(const Dev& d, uint32_t j) { return d.segq == 1 ? (j >> 7) : __umulhi(j >> 7, d.segm); }
+__device__ inline unsigned long long seg_bit(const Dev& d, uint32_t j) { return 1ull << seg_of(d, j); }
 // membership changes: bit + stale-checkpoint mark (callers that batch marks pass mark=false)
 __device__ inline bool mem_set(const Dev& d, uint32_t i, uint32_t j) {   // returns true if newly set
   const uint32_t m = 1u << (j & 31);

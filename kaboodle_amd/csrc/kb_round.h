@@ -208,35 +208,63 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
   const uint32_t a0 = p & ~15u;
   uint32_t K[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
   uint32_t anc = 0, nbytes = 0;                   // ancient candidates in the scanned address-order prefix
-  bool wrapped = false;
-  for (uint32_t j0 = a0;;) {
-    const uint32_t j = j0 + 16 * l;
-    const bool inr = wrapped ? j < a0 : j < W;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    uint32_t mb = 0;
-    if (inr) {
-      v = *reinterpret_cast<const uint4*>(rw + j);
-      const uint32_t w = LDSB ? B[j >> 5] : __hip_atomic_load(&B[j >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      mb = (w >> (j & 16)) & 0xFFFFu;
+  // chunk order: ids [a0, W) then [0, a0), 1024 ids per chunk; the first step loads one chunk (it
+  // usually decides), later steps A3_U chunks at once (rows with few ancient stamps: recent joiners)
+  constexpr int A3_U = 4;
+  uint32_t next = a0;
+  bool wrapped = false, more = true;
+  for (int step = 0; more; ++step) {
+    const int nu = step == 0 ? 1 : A3_U;
+    uint32_t base[A3_U];
+    bool wr[A3_U], ok[A3_U];
+#pragma unroll
+    for (int u = 0; u < A3_U; ++u) {
+      ok[u] = u < nu && more;
+      base[u] = next; wr[u] = wrapped;
+      if (ok[u]) {
+        next += 1024;
+        if (!wrapped && next >= W) { wrapped = true; next = 0; }
+        if (wrapped && next >= a0) more = false;
+      }
     }
-    nbytes += inr ? 16 : 0;
-    uint32_t cm = (nzmask4(v.x & 0xFEFEFEFEu) | (nzmask4(v.y & 0xFEFEFEFEu) << 4) | (nzmask4(v.z & 0xFEFEFEFEu) << 8) |
-                   (nzmask4(v.w & 0xFEFEFEFEu) << 12)) & mb;                 // Known && member
-    if (i >= j && i < j + 16) cm &= ~(1u << (i - j));                        // != self (:571-577)
-    uint32_t am = cm & (eqmask4(v.x, ST_ANCIENT) | (eqmask4(v.y, ST_ANCIENT) << 4) | (eqmask4(v.z, ST_ANCIENT) << 8) |
-                        (eqmask4(v.w, ST_ANCIENT) << 12));
-    if (!wrapped && j < p) am &= p - j >= 16 ? 0u : ~((1u << (p - j)) - 1u);   // [a0, p) comes last in order
-    anc += wave_sum(__popc(am));
-    for (uint32_t m = cm; m; m &= m - 1) {
-      const uint32_t t = __ffs(m) - 1, jj = j + t;
-      const uint32_t word = (t & 8) ? ((t & 4) ? v.w : v.z) : ((t & 4) ? v.y : v.x);
-      const uint32_t key = (((word >> (8 * (t & 3))) & 0xFFu) << 24) | (jj >= p ? jj - p : jj + C - p);
-      if (key < K[4]) top5_insert(K, key);
+    uint4 v[A3_U];
+    uint32_t mbw[A3_U];
+#pragma unroll
+    for (int u = 0; u < A3_U; ++u) {                // every load of the step in flight together
+      const uint32_t j = base[u] + 16 * l;
+      const bool inr = ok[u] && (wr[u] ? j < a0 : j < W);
+      v[u] = make_uint4(0, 0, 0, 0);
+      mbw[u] = 0;
+      if (inr) {
+        v[u] = *reinterpret_cast<const uint4*>(rw + j);
+        mbw[u] = LDSB ? B[j >> 5] : __hip_atomic_load(&B[j >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        nbytes += 16;
+      }
     }
-    if (anc >= (uint32_t)NUM_CANDIDATES) break;   // nothing later in address order can rank
-    j0 += 1024;
-    if (!wrapped && j0 >= W) { wrapped = true; j0 = 0; }
-    if (wrapped && j0 >= a0) break;                 // the whole row
+    bool done = false;
+#pragma unroll
+    for (int u = 0; u < A3_U; ++u) {
+      if (!ok[u] || done) continue;                 // wave-uniform
+      const uint32_t j = base[u] + 16 * l;
+      const bool inr = wr[u] ? j < a0 : j < W;
+      const uint32_t mb = inr ? (mbw[u] >> (j & 16)) & 0xFFFFu : 0u;
+      const uint4 x = v[u];
+      uint32_t cm = (nzmask4(x.x & 0xFEFEFEFEu) | (nzmask4(x.y & 0xFEFEFEFEu) << 4) | (nzmask4(x.z & 0xFEFEFEFEu) << 8) |
+                     (nzmask4(x.w & 0xFEFEFEFEu) << 12)) & mb;               // Known && member
+      if (i >= j && i < j + 16) cm &= ~(1u << (i - j));                      // != self (:571-577)
+      uint32_t am = cm & (eqmask4(x.x, ST_ANCIENT) | (eqmask4(x.y, ST_ANCIENT) << 4) | (eqmask4(x.z, ST_ANCIENT) << 8) |
+                          (eqmask4(x.w, ST_ANCIENT) << 12));
+      if (!wr[u] && j < p) am &= p - j >= 16 ? 0u : ~((1u << (p - j)) - 1u);   // [a0, p) comes last in order
+      anc += wave_sum(__popc(am));
+      for (uint32_t m = cm; m; m &= m - 1) {
+        const uint32_t t = __ffs(m) - 1, jj = j + t;
+        const uint32_t word = (t & 8) ? ((t & 4) ? x.w : x.z) : ((t & 4) ? x.y : x.x);
+        const uint32_t key = (((word >> (8 * (t & 3))) & 0xFFu) << 24) | (jj >= p ? jj - p : jj + C - p);
+        if (key < K[4]) top5_insert(K, key);
+      }
+      if (anc >= (uint32_t)NUM_CANDIDATES) done = true;   // nothing later in address order can rank
+    }
+    if (done) break;
   }
 #pragma unroll
   for (int q = 0; q < 5; ++q) {                     // merge the lanes' lists (keys are distinct)
@@ -282,7 +310,13 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
   // address atomics from every node would serialise in L2 and stall the waves that wait on them)
   unsigned long long w_lost = 0, w_removed = 0, w_resp = 0, w_nodes = 0, w_bytes = 0;
   for (uint32_t i = d.lo + blockIdx.x * wpb + wv; i < d.hi; i += gridDim.x * wpb) {
-    if (!d.alive[i]) {
+    // the node's header loads are issued together, ahead of the bitset staging (one memory round trip
+    // for all of them instead of one per dependent use)
+    const uint8_t alive = d.alive[i];
+    const int32_t sr = d.start_round[i];
+    const uint32_t n_in = d.n[i], fn_in = d.flog_n[i];
+    const Susp sl_in = l < SLOTS ? d.susp[(size_t)i * SLOTS + l] : Susp{0, 0, 0, 0};
+    if (!alive) {
       if (l == 0) { pb.nresp[i] = 0; pb.paysum[i] = 0; }
       continue;
     }
@@ -292,8 +326,8 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
     if (LDSB) { stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB), d.NWR / 4, l, 64); w_bytes += 4ull * d.NWR; }
     unsigned long long segs = 0;
     uint32_t nresp = 0;
-    if (d.start_round[i] < r) {                       // ---- (1) broadcast phase ----
-      if (l < SLOTS) { const Susp sl = d.susp[(size_t)i * SLOTS + l]; s_sp[wv][l] = sl.kind ? sl.peer : 0xFFFFFFFFu; }
+    if (sr < r) {                                     // ---- (1) broadcast phase ----
+      if (l < SLOTS) s_sp[wv][l] = sl_in.kind ? sl_in.peer : 0xFFFFFFFFu;
       wait_lds();
       __builtin_amdgcn_wave_barrier();
       auto mem = [&](uint32_t x) __attribute__((always_inline)) -> bool {
@@ -301,9 +335,9 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
         return (w >> (x & 31)) & 1u;
       };
       auto is_susp = [&](uint32_t x) __attribute__((always_inline)) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
-      uint32_t n = d.n[i];
+      uint32_t n = n_in;
       const uint32_t n0 = n;
-      uint32_t fn = d.flog_n[i];
+      uint32_t fn = fn_in;
       uint32_t lost_cnt = 0, removed_cnt = 0;
       // ---- Failed(p) group (src/kaboodle.rs:268-283) ----
       // In-order semantics, 64 entries at a time.  An entry acts iff it is delivered, names neither the
@@ -519,40 +553,65 @@ __device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint
 // of e = #later joiners <= select(y + e)).  RESP_U keys per batch: their permutations, block searches and
 // 32-byte block reads are independent, so the loads of a batch are in flight together.
 constexpr int RESP_U = 4;
+constexpr int RESP_KMAX = 9;          // keys per lane at stride >= 64: cap <= 567 (src/kaboodle.rs:43, :373-383)
 __device__ __attribute__((always_inline)) inline void sampled_fill(uint32_t* pay, uint32_t k_first, uint32_t stride,
                                                                    uint32_t cap, const Prp& P, const uint32_t* B,
                                                                    const uint32_t* BP, uint32_t NB, float ratio,
                                                                    const uint32_t* J, const uint32_t* JM, uint32_t upto,
                                                                    uint32_t nnew) {
   const uint32_t jmin = JM[upto];
-  for (uint32_t k0 = k_first; k0 < cap; k0 += stride * RESP_U) {
-    uint32_t y[RESP_U], blk[RESP_U];
-    uint4 q0[RESP_U], q1[RESP_U];
+  // (1) the permutation images of this lane's keys, cycle-walked as one stream: each step is one
+  // Feistel pass of the lane's current key, so the wave waits for the slowest lane's total passes,
+  // not for the slowest lane of every key
+  const uint32_t mcount = k_first < cap ? (cap - k_first + stride - 1) / stride : 0u;
+  uint32_t y[RESP_KMAX];
 #pragma unroll
-    for (int u = 0; u < RESP_U; ++u) { const uint32_t k = k0 + stride * u; y[u] = k < cap ? prp_eval(k, P) : 0u; }
+  for (int q = 0; q < RESP_KMAX; ++q) y[q] = 0;
+  uint32_t m = 0, x = k_first;
+  while (__ballot(m < mcount)) {
+    if (m < mcount) {
+      uint32_t L = x >> P.h, R = x & P.mask;
 #pragma unroll
-    for (int u = 0; u < RESP_U; ++u) blk[u] = bm_block(BP, NB, ratio, y[u]);
+      for (int k = 0; k < 4; ++k) { const uint32_t t = R; R = L ^ (mix32(R ^ P.k[k]) & P.mask); L = t; }
+      x = (L << P.h) | R;
+      if (x < P.n) {
+#pragma unroll
+        for (int q = 0; q < RESP_KMAX; ++q) if ((uint32_t)q == m) y[q] = x;
+        ++m;
+        x = k_first + stride * m;
+      }
+    }
+  }
+  // (2) rank -> id, RESP_U keys at a time with their block searches and 32-byte block reads in flight
+#pragma unroll
+  for (int q0 = 0; q0 < RESP_KMAX; q0 += RESP_U) {
+    if ((uint32_t)q0 >= mcount) break;
+    uint32_t blk[RESP_U];
+    uint4 b0[RESP_U], b1[RESP_U];
+#pragma unroll
+    for (int u = 0; u < RESP_U; ++u) blk[u] = q0 + u < RESP_KMAX ? bm_block(BP, NB, ratio, y[q0 + u < RESP_KMAX ? q0 + u : 0]) : 0u;
 #pragma unroll
     for (int u = 0; u < RESP_U; ++u) {
-      q0[u] = *reinterpret_cast<const uint4*>(B + blk[u] * 8);
-      q1[u] = *reinterpret_cast<const uint4*>(B + blk[u] * 8 + 4);
+      b0[u] = *reinterpret_cast<const uint4*>(B + blk[u] * 8);
+      b1[u] = *reinterpret_cast<const uint4*>(B + blk[u] * 8 + 4);
     }
 #pragma unroll
     for (int u = 0; u < RESP_U; ++u) {
-      const uint32_t k = k0 + stride * u;
-      if (k >= cap) break;
-      uint32_t x = block_pick(q0[u], q1[u], blk[u], y[u] - BP[blk[u]]);
-      if (x >= jmin) {                                // rare: a later joiner may sit at or below x
+      const uint32_t q = q0 + u;
+      if (q >= RESP_KMAX || q >= mcount) break;
+      const uint32_t yq = y[q];
+      uint32_t xq = block_pick(b0[u], b1[u], blk[u], yq - BP[blk[u]]);
+      if (xq >= jmin) {                               // rare: a later joiner may sit at or below xq
         uint32_t e = 0;
         while (true) {
           uint32_t c = 0;
-          for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= x;
+          for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= xq;
           if (c == e) break;
           e = c;
-          x = bm_select(B, BP, NB, ratio, y[u] + e);
+          xq = bm_select(B, BP, NB, ratio, yq + e);
         }
       }
-      pay[k] = x;
+      pay[k_first + stride * q] = xq;
     }
   }
 }

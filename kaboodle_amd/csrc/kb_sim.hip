@@ -464,6 +464,8 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   Dev& d = s->d;
   d.lo = s->lo; d.hi = s->hi;
   d.C = C; d.W = W; d.SEGW = W / NSEG; d.NWR = W / 32;
+  d.segq = d.SEGW / 128;
+  d.segm = d.segq > 1 ? (uint32_t)(((1ull << 32) + d.segq - 1) / d.segq) : 0u;
   d.k0 = (uint32_t)cfg->seed; d.k1 = (uint32_t)(cfg->seed >> 32);
   d.loss_thr = cfg->loss_threshold; d.churn_thr = cfg->churn_threshold; d.fault_end = cfg->fault_end_round;
   d.failed_mode = cfg->failed_mode; d.pgroups = cfg->partition_groups; d.pstart = cfg->partition_start;

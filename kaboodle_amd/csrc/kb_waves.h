@@ -756,7 +756,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
             const uint8_t* hb = reinterpret_cast<const uint8_t*>(bw);
             if (__popcll(insm) >= 8) {              // many: one insertion per lane
               if (ins) {
-                const uint32_t x = lm.sender, k = x / d.SEGW, hend = (k + 1) * (d.SEGW / 8);
+                const uint32_t x = lm.sender, k = seg_of(d, x), hend = (k + 1) * (d.SEGW / 8);
                 uint32_t praw = 0, pcnt = 0;
                 fold_half(d, ztab, x >> 3, hb[x >> 3] & ~((2u << (x & 7)) - 1u) & 0xFFu, praw, pcnt);
                 for (uint32_t h0 = (x >> 3) + 1; h0 < hend; h0 += 16) {   // 16 blocks of loads in flight
@@ -776,7 +776,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
             } else {                                  // few: the whole wave on each insertion
               for (unsigned long long mm = insm; mm; mm &= mm - 1) {
                 const int q = __ffsll((long long)mm) - 1;
-                const uint32_t x = bcast(lm.sender, q), k = x / d.SEGW;
+                const uint32_t x = bcast(lm.sender, q), k = seg_of(d, x);
                 const uint32_t hs = x >> 3, nh = (k + 1) * (d.SEGW / 8) - hs;
                 uint32_t praw = 0, pcnt = 0;
                 for (uint32_t h = hs + (l * nh) / 64; h < hs + ((l + 1) * nh) / 64; ++h) {
