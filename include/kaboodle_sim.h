@@ -191,6 +191,9 @@ int  kb_sim_dump_suspects(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, 
    8 KnownPeers BIG group on the HBM bitset, 16 k_proc unsorted selection path, 32 Failed-list prep
    from HBM, 64 Join responses by wave, 128 KnownPeers BIG group in LDS).  Test surface.           */
 int  kb_sim_debug_paths(kb_sim* sim, uint32_t* mask);
+/* Development counters since creation: [A3 rows scanned, rows scanned past their first 1024 ids,
+   1024-id stamp chunks read].  Test surface.                                                        */
+int  kb_sim_debug_counters(kb_sim* sim, uint64_t* out, size_t cap);
 /* Canonical curious table: for each entry sorted by peer: peer, nobs, obs[0..3] (6 x int32).       */
 int  kb_sim_dump_curious(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, size_t* n);
 

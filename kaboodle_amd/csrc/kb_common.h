@@ -20,6 +20,7 @@ enum StatIdx {
   S_KPIDS,                        // peer entries of the KnownPeers messages sent (kb_stats.sent_kp_ids)
   S_ROWB,                         // bytes the row pass moved (bench roofline; not a kb_stats field)
   S_FOLDB,                        // member-bit bytes the fold read (bench roofline; not a kb_stats field)
+  S_A3ROWS, S_A3DEEP, S_A3CHUNKS,  // A3 scans: rows, rows past their first chunk, chunks read (kb_sim_debug_counters)
   NSTAT
 };
 enum CtrIdx {
@@ -53,6 +54,7 @@ struct Dev {
   uint32_t capk, capj;            // KnownPeers caps: KPR reply (size <= 10240), Join response (size < 10240)
   uint32_t paybound;              // payload entries reserved per KPR reply
   uint32_t dbg;                   // kb_config.debug_flags (KB_DBG_*): force the wide-row kernel variants
+  uint32_t dev;                   // env KB_DEV: timing experiments only (skip parts; results are wrong)
   uint8_t* stamp;
   uint32_t* bits;
   uint2* segp;

@@ -130,10 +130,27 @@ struct PhaseB {
   uint32_t* nresp; uint32_t* paysum; uint32_t* nbase;           // per node
 };
 
-__device__ inline bool bcast_lost(const Dev& d, uint32_t recv, const BCast& b, int32_t r) {
-  if (part_blocks(d, r, b.sender, recv)) return true;
-  if (!faults(d, r) || d.loss_thr == 0) return false;
-  return philox(recv, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | b.bseq, b.sender, d.k0, d.k1).x < d.loss_thr;
+// Broadcast loss: entry e of the round's Failed (lst 0) / Join (lst 1) list reaches
+// receiver i unless word e % 4 of philox(i, r, P_BLOSS << 24 | lst << 23 | e / 4, 0) < loss_thr.  A wave
+// handling entries [c, c + 64) in lane order takes its draws from one Philox call per lane per 256
+// entries (BLossQuad: lane l holds the words of group c256 / 4 + l) and a cross-lane read.
+struct BLossQuad { U4 w; };
+__device__ inline BLossQuad bloss_quad(const Dev& d, uint32_t recv, int32_t r, uint32_t lst, uint32_t c256) {
+  BLossQuad q;
+  q.w = (faults(d, r) && d.loss_thr)
+            ? philox(recv, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | (lst << 23) | ((c256 >> 2) + lane()), 0, d.k0, d.k1)
+            : U4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  return q;
+}
+// lost? for entry c + lane() (c a multiple of 64, q taken at c & ~255), sent by `sender`
+__device__ __attribute__((always_inline)) inline bool bcast_lost(const Dev& d, uint32_t recv, uint32_t sender, int32_t r,
+                                                                 const BLossQuad& q, uint32_t c) {
+  const int src = (int)(((c & 255u) >> 2) + (lane() >> 2));
+  const uint32_t wx = bcast(q.w.x, src), wy = bcast(q.w.y, src), wz = bcast(q.w.z, src), ww = bcast(q.w.w, src);
+  const uint32_t k = lane() & 3u;
+  const uint32_t u = k == 0 ? wx : (k == 1 ? wy : (k == 2 ? wz : ww));
+  if (part_blocks(d, r, sender, recv)) return true;
+  return faults(d, r) && d.loss_thr && u < d.loss_thr;
 }
 
 // Per-list facts about the Failed broadcasts (identical for every receiver).
@@ -202,7 +219,7 @@ struct RowOut { uint32_t* part; };   // [C][10]: the five smallest keys ascendin
 // ascending, in every lane.  Returns the stamp bytes read.
 template <bool LDSB>
 __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, uint32_t i, const uint8_t* rw,
-                                                                  const uint32_t* B, uint32_t (&out)[5]) {
+                                                                  const uint32_t* B, uint32_t (&out)[5], uint3& a3c) {
   const uint32_t l = lane(), C = d.C, W = d.W;
   const uint32_t p = (i + 1 == C) ? 0 : i + 1;
   const uint32_t a0 = p & ~15u;
@@ -235,6 +252,7 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
       const bool inr = ok[u] && (wr[u] ? j < a0 : j < W);
       v[u] = make_uint4(0, 0, 0, 0);
       mbw[u] = 0;
+      a3c.z += ok[u] ? 1u : 0u;
       if (inr) {
         v[u] = *reinterpret_cast<const uint4*>(rw + j);
         mbw[u] = LDSB ? B[j >> 5] : __hip_atomic_load(&B[j >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -264,8 +282,9 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
       }
       if (anc >= (uint32_t)NUM_CANDIDATES) done = true;   // nothing later in address order can rank
     }
-    if (done) break;
+    if (done || (d.dev & 1)) break;               // dev 1: first chunk only (timing experiments)
   }
+  a3c.x += 1; a3c.y += (next != a0 + 1024 || wrapped) ? 1u : 0u;   // scan depth (kb_sim_debug_counters)
 #pragma unroll
   for (int q = 0; q < 5; ++q) {                     // merge the lanes' lists (keys are distinct)
     const uint32_t mn = wave_min(K[0]);
@@ -309,6 +328,7 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
   // counters stay in registers for the whole persistent loop: one atomic per wave at the end (same-
   // address atomics from every node would serialise in L2 and stall the waves that wait on them)
   unsigned long long w_lost = 0, w_removed = 0, w_resp = 0, w_nodes = 0, w_bytes = 0;
+  uint3 a3c = make_uint3(0, 0, 0);
   for (uint32_t i = d.lo + blockIdx.x * wpb + wv; i < d.hi; i += gridDim.x * wpb) {
     // the node's header loads are issued together, ahead of the bitset staging (one memory round trip
     // for all of them instead of one per dependent use)
@@ -346,12 +366,14 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
       // named by an earlier entry (dep) can change its mind: those are resolved in lane order with one
       // ballot each (killed iff an earlier acting lane of the chunk names its sender).  The acting
       // entries are then applied together: the atomic's return says whether the peer was still present.
-      for (uint32_t c = 0; c < pb.nf; c += 64) {
+      BLossQuad lq;
+      for (uint32_t c = 0; c < ((d.dev & 2) ? 0u : pb.nf); c += 64) {   // dev 2: skip (timing experiments)
         const uint32_t e = c + l;
         const bool valid = e < pb.nf;
         uint32_t dep = 0;
         const BCast b = valid ? fail_at(e, dep) : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
-        const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
+        if ((c & 255u) == 0) lq = bloss_quad(d, i, r, 0, c);
+        const bool lost = bcast_lost(d, i, b.sender, r, lq, c) && valid && b.sender != i;
         const bool base = valid && b.sender != i && !lost && b.peer != i && honour && mem(b.sender);
         unsigned long long actm = __ballot(base);
         unsigned long long depm = __ballot(base && dep);
@@ -381,11 +403,13 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
       const uint32_t nbase = n;
       // ---- Join{addr} group (src/kaboodle.rs:284-304) ----
       uint32_t paysum = 0;
-      for (uint32_t c = 0; c < pb.nj; c += 64) {
+      BLossQuad jq;
+      for (uint32_t c = 0; c < ((d.dev & 4) ? 0u : pb.nj); c += 64) {   // dev 4: skip (timing experiments)
         const uint32_t e = c + l;
         const bool valid = e < pb.nj;
         const BCast b = valid ? join_at(e) : BCast{0xFFFFFFFFu, 0, 0, 0};
-        const bool lost = valid && b.sender != i && bcast_lost(d, i, b, r);
+        if ((c & 255u) == 0) jq = bloss_quad(d, i, r, 1, c);
+        const bool lost = bcast_lost(d, i, b.sender, r, jq, c) && valid && b.sender != i;
         const bool deliver = valid && b.sender != i && !lost;
         const bool known = deliver && mem(b.sender);
         const unsigned long long newm = __ballot(deliver && !known);
@@ -432,8 +456,10 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
       }
       w_lost += lost_cnt; w_removed += removed_cnt;
       // the Join stamps written above are read back by this wave's A3 loads
-      wave_mem_sync();
-      __builtin_amdgcn_s_waitcnt(0);
+      if (!(d.dev & 8)) {                           // dev 8: skip (timing experiments)
+        wave_mem_sync();
+        __builtin_amdgcn_s_waitcnt(0);
+      }
     } else if (l == 0) {                              // started this round: no deliveries yet
       pb.nresp[i] = 0; pb.paysum[i] = 0;
     }
@@ -441,7 +467,7 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
     __builtin_amdgcn_wave_barrier();
     // ---- (2) A3 candidates ----
     uint32_t top[5];
-    w_bytes += a3_scan<LDSB>(d, i, rw, B, top);
+    w_bytes += a3_scan<LDSB>(d, i, rw, B, top, a3c);
     if (l < 10) ro.part[(size_t)i * 10 + l] = l < 5 ? (l == 0 ? top[0] : l == 1 ? top[1] : l == 2 ? top[2] : l == 3 ? top[3] : top[4]) : 0xFFFFFFFFu;
     // ---- (3) write back the changed segments of the bitset ----
     if (LDSB && segs) {
@@ -460,6 +486,8 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
     if (w_removed) atomicAdd(&d.stats[S_RMFAILED], w_removed);
     if (w_resp) atomicAdd(&d.stats[S_JRESP], w_resp);
     if (w_bytes) atomicAdd(&d.stats[S_ROWB], w_bytes);
+    atomicAdd(&d.stats[S_A3ROWS], (unsigned long long)a3c.x); atomicAdd(&d.stats[S_A3DEEP], (unsigned long long)a3c.y);
+    atomicAdd(&d.stats[S_A3CHUNKS], (unsigned long long)a3c.z);
     if (!LDSB && w_nodes) path_hit(d, PATH_PHASEB_HBM);
   }
 }

@@ -475,6 +475,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   d.capj = (BUFSZ - 20 - Lid - 1) / (18 + Lid);       // 20 + L + k(18+L) <  10240
   d.paybound = C < d.capk ? C : d.capk;
   d.dbg = cfg->debug_flags;
+  if (const char* dv = getenv("KB_DEV")) d.dev = (uint32_t)atoi(dv);
   s->debug_waves = getenv("KB_DEBUG_WAVES") != nullptr;
   s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid); s->h_ever.assign(C, 0);
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &s->h_ident[(size_t)j * MAXID]);
@@ -1374,5 +1375,14 @@ extern "C" int kb_sim_debug_paths(kb_sim* s, uint32_t* mask) {
     return KB_OK;
   }
   HIPCHK(hipMemcpy(mask, s->d.ctr + C_PATHS, 4, hipMemcpyDeviceToHost));
+  return KB_OK;
+}
+// development counters (test surface): [A3 rows scanned, rows scanned past their first chunk, chunks read]
+extern "C" int kb_sim_debug_counters(kb_sim* s, uint64_t* out, size_t cap) {
+  if (!s || !out || cap < 3) return KB_INVALID_ARGUMENT;
+  kb_sim* h = is_group(s) ? s->shards[0] : s;
+  unsigned long long v[3];
+  HIPCHK(hipMemcpy(v, h->d.stats + S_A3ROWS, sizeof v, hipMemcpyDeviceToHost));
+  for (int k = 0; k < 3; ++k) out[k] = v[k];
   return KB_OK;
 }

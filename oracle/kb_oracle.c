@@ -384,10 +384,13 @@ static void bpush(obcast** v, size_t* n, size_t* cap, uint32_t sender, uint32_t 
   (*v)[*n].sender = sender; (*v)[*n].peer = peer; (*v)[*n].bseq = bseq; (*n)++;
 }
 
-static int bcast_lost(kbo_sim* s, uint32_t recv, const obcast* b, int32_t r) {
+/* delivery of entry e of the round's Failed (lst 0) / Join (lst 1) broadcast list to recv: word e % 4
+ * of philox(recv, r, P_BLOSS << 24 | lst << 23 | e / 4, 0) */
+static int bcast_lost(kbo_sim* s, uint32_t recv, const obcast* b, int32_t r, uint32_t lst, size_t e) {
   if (partition_blocks(s, r, b->sender, recv)) return 2;
   if (!active_faults(s, r) || s->cfg.loss_threshold == 0) return 0;
-  return ph(s, recv, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | b->bseq, b->sender).v[0] < s->cfg.loss_threshold;
+  return ph(s, recv, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | (lst << 23) | (uint32_t)(e >> 2), 0).v[e & 3] <
+         s->cfg.loss_threshold;
 }
 
 /* should_respond_to_broadcast (src/kaboodle.rs:333-354), integer restatement of gen_bool */
@@ -454,7 +457,7 @@ static void phase_broadcasts(kbo_sim* s, uint32_t i, int32_t r) {
   for (size_t k = 0; k < s->nbfail; ++k) {
     const obcast* b = &s->bfail[k];
     if (b->sender == i) continue;                     /* own broadcasts are not delivered to self */
-    if (bcast_lost(s, i, b, r)) { lost++; continue; }
+    if (bcast_lost(s, i, b, r, 0, k)) { lost++; continue; }
     if (b->peer == i) continue;                       /* Failed(self) ignored            :269-273 */
     if (s->cfg.failed_mode == KB_FAILED_SIM_SENDER && row(s, i)[b->sender] != ST_UNKNOWN)
       removed += (uint64_t)map_remove(s, i, b->peer); /* sender is a mesh member         :275-279 */
@@ -463,7 +466,7 @@ static void phase_broadcasts(kbo_sim* s, uint32_t i, int32_t r) {
   for (size_t k = 0; k < s->nbjoin; ++k) {
     const obcast* b = &s->bjoin[k];
     if (b->sender == i) continue;                     /* addr == self_addr               :285-287 */
-    if (bcast_lost(s, i, b, r)) { lost++; continue; }
+    if (bcast_lost(s, i, b, r, 1, k)) { lost++; continue; }
     int is_new = map_insert_known(s, i, b->sender, r, r);
     if (is_new && should_respond(s, i, b->sender, r)) join_response(s, i, b->sender, r);
   }

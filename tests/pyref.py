@@ -231,29 +231,32 @@ class PyMesh:
 
     # handle_incoming_broadcasts (src/kaboodle.rs:256-311)
     def broadcasts(self, p, r):
-        for (s, peer, bseq) in self.bfail:
+        for e, (s, peer, bseq) in enumerate(self.bfail):
             if s == p.id:
                 continue
-            if self.lost_b(p.id, s, bseq, r):
+            if self.lost_b(p.id, s, 0, e, r):
                 continue
             if peer == p.id:
                 continue
             if self.failed_honoured and s in p.known and peer in p.known:
                 del p.known[peer]
                 self.stats["removed_failed"] += 1
-        for (a, _, bseq) in self.bjoin:
-            if a == p.id or self.lost_b(p.id, a, bseq, r):
+        for e, (a, _, bseq) in enumerate(self.bjoin):
+            if a == p.id or self.lost_b(p.id, a, 1, e, r):
                 continue
             is_new = a not in p.known
             p.known[a] = [KNOWN, r]
             if is_new and self.should_respond(p, a, r):
                 self.send_known_peers_to(p, a, r)
 
-    def lost_b(self, recv, sender, bseq, r):
+    def lost_b(self, recv, sender, lst, e, r):
+        """delivery of entry e of the round's Failed (lst 0) / Join (lst 1) list to recv: word e % 4 of
+        philox(recv, r, P_BLOSS << 24 | lst << 23 | e // 4, 0)"""
         if self.blocked(r, sender, recv):
             self.stats["drop_bcast"] += 1
             return True
-        if self.faults(r) and self.loss_thr and self.ph(recv, r, (P_BLOSS << 24) | bseq, sender)[0] < self.loss_thr:
+        if self.faults(r) and self.loss_thr and \
+                self.ph(recv, r, (P_BLOSS << 24) | (lst << 23) | (e >> 2), 0)[e & 3] < self.loss_thr:
             self.stats["drop_bcast"] += 1
             return True
         return False

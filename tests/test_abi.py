@@ -40,7 +40,7 @@ def test_hip_library_exports_every_symbol():
 def test_oracle_exports_every_symbol():
     lib = C.CDLL(ORACLE_SO)
     skip = {"kb_sim_kernel_time", "kb_sim_reset_kernel_time", "kb_sim_kernel_bytes",   # GPU timing surface
-            "kb_sim_debug_paths",                                                      # GPU kernel variants
+            "kb_sim_debug_paths", "kb_sim_debug_counters",                             # GPU kernel variants
             "kb_rccl_unique_id", "kb_sim_create_rank", "kb_sim_create_local", "kb_sim_shard_info"}  # sharding
     missing = [n for n in declared() if n not in skip and not hasattr(lib, "kbo_" + n[3:])]
     assert not missing

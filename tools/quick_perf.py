@@ -19,3 +19,8 @@ print(f"N={N} R={R} wall {dt/R*1e3:.2f} ms/round  rowpass {sw/n:.3f} ms ({m.kern
       f"fold {fo/max(nf,1):.3f} ms ({m.kernel_bytes(2)/max(fo*1e-3,1e-9)/1e9:.1f} GB/s)  round(ev) {rd/n:.3f} ms  "
       f"node-rounds/s {st['alive']*R/dt:.3e}", flush=True)
 print(st)
+import ctypes as C
+lib = kaboodle_amd.lib().lib
+buf = (C.c_uint64 * 3)()
+if lib.kb_sim_debug_counters(m.h, buf, 3) == 0:
+    print(f"A3 rows {buf[0]}  deep {buf[1]} ({buf[1] / max(buf[0], 1):.3f})  chunks/row {buf[2] / max(buf[0], 1):.2f}", flush=True)
