@@ -86,6 +86,8 @@ struct Dev {
   uint32_t* flog_n;
   uint32_t* fstart;
   int32_t* kpr_big;               // round in which the node's KPR reply was proven oversize for the round
+  uint16_t* lat;                  // [C][W] PeerInfo.latency in ms (LAT_NONE = None); null unless track_latency
+  int32_t wave;                   // delivery wave of the launch (latency clock)
 };
 
 // freshness log (the KnownPeersRequest reply set, :503-508, without scanning the row): an entry is
@@ -320,6 +322,26 @@ __device__ inline void susp_clear(const Dev& d, uint32_t i, uint32_t p) {
   Susp* s = d.susp + (size_t)i * SLOTS;
   for (int k = 0; k < SLOTS; ++k) if (s[k].kind && s[k].peer == p) s[k].kind = 0;
 }
+// ---- PeerInfo.latency (src/kaboodle.rs:789-817), DESIGN.md §2.7 ---------------------------------
+// Simulated clock: the tick of round r at 1000·r ms, wave w of its receive window at 1000·r + w + 1.
+// Invariant: LAT_NONE wherever the member bit is clear (removals write it), so an insertion needs no
+// write: a new entry's latency is None (:412 on an absent sender, :294-296, :467).
+constexpr uint16_t LAT_NONE = 0xFFFFu;
+__device__ inline void lat_none(const Dev& d, uint32_t i, uint32_t p) {
+  if (d.lat) d.lat[(size_t)i * d.W + p] = LAT_NONE;
+}
+// the envelope prologue of a unicast from p while p is WaitingFor*(since): calculate_peer_latency
+__device__ inline void lat_sample(const Dev& d, uint32_t i, uint32_t p, int32_t since, int32_t r) {
+  if (!d.lat) return;
+  uint16_t* q = d.lat + (size_t)i * d.W + p;
+  const uint32_t smp = 1000u * (uint32_t)(r - since) + (uint32_t)d.wave + 1u;
+  const uint32_t prev = *q;
+  uint32_t v = smp;
+  if (prev != LAT_NONE)                                 // f64 as the reference, no fma contraction
+    v = (uint32_t)__dadd_rn(__dmul_rn((double)smp, 0.8), __dmul_rn((double)prev, 1.0 - 0.8));
+  *q = (uint16_t)(v < LAT_NONE ? v : LAT_NONE - 1u);
+}
+
 // lifecycle: the per-id part on every shard, the row part on the shard holding the row
 __device__ __attribute__((always_inline)) inline void node_start(const Dev& d, uint32_t i, int32_t r) {      // src/lib.rs:136-156
   if (local(d, i)) {

@@ -389,6 +389,7 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
           const uint32_t m = 1u << (b.peer & 31);
           if (atomicAnd(&B[b.peer >> 5], ~m) & m) {
             removed_cnt++;
+            lat_none(d, i, b.peer);
             if (is_susp(b.peer)) susp_clear(d, i, b.peer);
             segs |= seg_bit(d, b.peer);
           }

@@ -490,6 +490,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
+  if (cfg->track_latency) AR(d.lat, W);
   s->msg_cap = std::max<uint32_t>(8u * R + (uint32_t)TICK_MAX * R, 1u << 16);
   s->pay_cap = std::max<uint32_t>((d.capk + 1) * R, 1u << 24);
   for (int b = 0; b < 2; ++b) {
@@ -521,6 +522,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
 #undef AR
   if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); destroy_shard(s); return KB_CAPACITY; }
   (void)hipMemset(L(s, d.kpr_big), 0xFF, 4ull * R);          // no round yet
+  if (d.lat) (void)hipMemset(d.lat + (size_t)s->lo * W, 0xFF, 2ull * R * W);   // every latency None
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
   for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->er0, &s->er1, &s->ef0, &s->ef1}) (void)hipEventCreate(e);
@@ -866,6 +868,7 @@ static int step_round(kb_sim* s) {
     OutBuf& ob = s->ob[cur];
     OutBuf& nb = s->ob[cur ^ 1];
     const int last = w == s->cfg.max_waves;
+    d.wave = (int32_t)w;                               // latency clock of the wave's prologues
     k_wave_clear<<<gnode, tb, 0, st>>>(d, s->wc);
     OutBuf ib = ob;                                    // the wave's delivered records
     uint32_t nrecv = 0;
@@ -1154,13 +1157,19 @@ extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, 
   if (rc) return rc;
   std::vector<Susp> sl(SLOTS);
   HIPCHK(hipMemcpy(sl.data(), s->d.susp + (size_t)node * SLOTS, sizeof(Susp) * SLOTS, hipMemcpyDeviceToHost));
+  std::vector<uint16_t> lat;
+  if (s->d.lat) {
+    lat.resize(s->C);
+    HIPCHK(hipMemcpy(lat.data(), s->d.lat + (size_t)node * s->W, 2ull * s->C, hipMemcpyDeviceToHost));
+  }
   const int32_t E = epoch_base(s->round > 0 ? s->round - 1 : 0);
   size_t c = 0;
   for (uint32_t j = 0; j < s->C; ++j) {
     if (!rw[j]) continue;
     if (out && c < cap) {
       kb_peer_state& o = out[c];
-      o.peer = j; o.latency_ms = KB_LATENCY_NONE;
+      o.peer = j;
+      o.latency_ms = !lat.empty() && lat[j] != LAT_NONE ? lat[j] : KB_LATENCY_NONE;
       if (rw[j] == ST_SUSPECT) {
         const Susp* q = nullptr;
         for (auto& x : sl) if (x.kind && x.peer == j) q = &x;

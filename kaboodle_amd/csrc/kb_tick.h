@@ -101,6 +101,7 @@ __device__ __attribute__((always_inline)) inline void tick_a2(const Dev& d, cons
       const uint32_t p = removed[q];
       susp_clear(d, i, p);
       mem_clr(d, i, p);
+      lat_none(d, i, p);
       segs |= seg_bit(d, p);
       n--;
       for (int c = 0; c < CSLOTS; ++c) if (cu[c].used && cu[c].peer == p) cu[c].used = 0;

@@ -384,7 +384,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
       if (sl->kind && (sl->peer >> 5) >= w0 && (sl->peer >> 5) < w1) {
         const uint32_t pw = __hip_atomic_load(reinterpret_cast<uint32_t*>(rw + (sl->peer & ~3u)), __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
-        if (((pw >> (8 * (sl->peer & 3u))) & 0xFFu) != ST_SUSPECT) sl->kind = 0;
+        if (((pw >> (8 * (sl->peer & 3u))) & 0xFFu) != ST_SUSPECT) { lat_sample(d, i, sl->peer, sl->since, r); sl->kind = 0; }
       }
     }
     if (t == 0 && (s_add || sg)) {
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, 
         if (sl->kind) {
           const uint32_t pw = __hip_atomic_load(reinterpret_cast<uint32_t*>(rw + (sl->peer & ~3u)), __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
-          if (((pw >> (8 * (sl->peer & 3u))) & 0xFFu) != ST_SUSPECT) sl->kind = 0;
+          if (((pw >> (8 * (sl->peer & 3u))) & 0xFFu) != ST_SUSPECT) { lat_sample(d, i, sl->peer, sl->since, r); sl->kind = 0; }
         }
       }
       if (l == 0 && (added || segs)) { d.n[i] += added; mark(d, i, segs); }
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
         if (s != last_sender) {                        // prologue: insert(sender, Known(now))
           const uint8_t b = rw[s];
           if (b == ST_SUSPECT)
-            for (int j = 0; j < SLOTS; ++j) if (sl[j].kind && sl[j].peer == s) sl[j].kind = 0;
+            for (int j = 0; j < SLOTS; ++j) if (sl[j].kind && sl[j].peer == s) { lat_sample(d, i, s, sl[j].since, r); sl[j].kind = 0; }
           if (b != now) { rw[s] = now; d.flog[(size_t)i * LOGCAP + (fn & (LOGCAP - 1))] = log_entry(s, r); fn++; }
           last_sender = s;
         }
@@ -820,7 +820,10 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
         uint8_t b;
         if (sorted) { was = bcast(pre_was, (int)(t & 63)) != 0; b = (uint8_t)bcast(pre_b, (int)(t & 63)); }
         else { was = (bw[s >> 5] >> (s & 31)) & 1u; b = was ? rw[s] : ST_UNKNOWN; }
-        if (b == ST_SUSPECT && l < SLOTS && s_susp[wv][l].kind && s_susp[wv][l].peer == s) s_susp[wv][l].kind = 0;
+        if (b == ST_SUSPECT && l < SLOTS && s_susp[wv][l].kind && s_susp[wv][l].peer == s) {
+          lat_sample(d, i, s, s_susp[wv][l].since, r);
+          s_susp[wv][l].kind = 0;
+        }
         if (!was) {
           dbg_ins++;
           n++; segs |= seg_bit(d, s);

@@ -79,6 +79,7 @@ struct kbo_sim {
   uint32_t C;
   uint32_t k0, k1;
   uint8_t* stamp;             /* C x C */
+  uint16_t* lat;              /* C x C PeerInfo.latency in ms, LAT_NONE = None (track_latency only) */
   uint8_t* alive;
   uint8_t* ever;
   int32_t* start_round;
@@ -211,13 +212,31 @@ static int susp_count(kbo_sim* s, uint32_t i) {
   for (int k = 0; k < SLOTS; ++k) c += sl[k].kind != 0;
   return c;
 }
-/* insert(p, Known(t)): overwrite; clears WaitingFor* state. returns 1 if p was new */
-static int map_insert_known(kbo_sim* s, uint32_t i, uint32_t p, int32_t t, int32_t r) {
+/* PeerInfo.latency (src/kaboodle.rs:789-817).  Simulated clock: round r's tick is at
+ * 1000·r ms (PROTOCOL_PERIOD, :38) and wave w of its receive window delivers at 1000·r + w + 1 ms.  A
+ * WaitingFor*(since) entry was set by a tick, at 1000·since. */
+#define LAT_NONE 0xFFFFu
+static inline uint16_t lat_ewma(uint32_t sample, uint32_t prev) {   /* :808-816, f64 as the reference */
+  if (prev == LAT_NONE) return (uint16_t)(sample < LAT_NONE ? sample : LAT_NONE - 1);
+  volatile double a = (double)sample * 0.8;          /* no contraction into an fma */
+  volatile double b = (double)prev * (1.0 - 0.8);
+  uint64_t v = (uint64_t)(a + b);
+  return (uint16_t)(v < LAT_NONE ? v : LAT_NONE - 1);
+}
+/* insert(p, Known(t)): overwrite; clears WaitingFor* state. returns 1 if p was new.  lat_w >= 0: the
+ * envelope prologue of a unicast delivered in wave lat_w (calculate_peer_latency, :412); -1: a Join
+ * broadcast or a KnownPeers arm (latency kept, :294-296, or None for a new entry, :467) */
+static int map_insert_known(kbo_sim* s, uint32_t i, uint32_t p, int32_t t, int32_t r, int lat_w) {
   uint8_t* b = row(s, i) + p;
   int was = *b;
-  if (was == ST_SUSPECT) { osusp* q = susp_find(s, i, p); if (q) q->kind = 0; }
+  uint16_t* lt = s->lat ? s->lat + (size_t)i * s->C + p : NULL;
+  if (was == ST_SUSPECT) {
+    osusp* q = susp_find(s, i, p);
+    if (lt && lat_w >= 0 && q) *lt = lat_ewma(1000u * (uint32_t)(r - q->since) + (uint32_t)lat_w + 1u, *lt);
+    if (q) q->kind = 0;
+  }
   *b = enc(t, r);
-  if (was == ST_UNKNOWN) { s->n[i]++; s->dirty[i] = 1; return 1; }
+  if (was == ST_UNKNOWN) { if (lt) *lt = LAT_NONE; s->n[i]++; s->dirty[i] = 1; return 1; }
   return 0;
 }
 static int map_remove(kbo_sim* s, uint32_t i, uint32_t p) {
@@ -301,7 +320,7 @@ static uint32_t kp_cap_uniform(kbo_sim* s) {   /* largest k with 20 + L + k(18+L
 /* ---- lifecycle (src/lib.rs:136-183, src/kaboodle.rs:114-185) ------------------------------------ */
 static void node_start(kbo_sim* s, uint32_t i, int32_t r) {
   s->alive[i] = 1; s->ever[i] = 1; s->start_round[i] = r;
-  map_insert_known(s, i, i, r, r);          /* known_peers.insert(self_addr, Known(now)) :145-152 */
+  map_insert_known(s, i, i, r, r, -1);          /* known_peers.insert(self_addr, Known(now)) :145-152 */
   s->dirty[i] = 1;
   s->last_bcast[i] = INT32_MIN;             /* last_broadcast_time: None                    :170 */
   memset(s->cur + (size_t)i * CSLOTS, 0, sizeof(ocur) * CSLOTS);   /* fresh KaboodleInner     */
@@ -341,7 +360,11 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   s->ident = (uint8_t*)calloc(C * MAXID, 1); s->id_len = (uint8_t*)calloc(C, 1);
   s->cseg = (uint32_t*)calloc(C, 4); s->segmul = (uint32_t*)calloc(C, 4); s->seglen = (uint32_t*)calloc(C, 4);
   s->out = (ovec*)calloc(C, sizeof(ovec)); s->oseq = (uint32_t*)calloc(C, 4);
-  if (!s->stamp || !s->susp || !s->cur) { seterr("out of host memory"); free(s); return KB_CAPACITY; }
+  if (cfg->track_latency) {
+    s->lat = (uint16_t*)malloc(C * C * sizeof(uint16_t));
+    if (s->lat) memset(s->lat, 0xFF, C * C * sizeof(uint16_t));
+  }
+  if (!s->stamp || !s->susp || !s->cur || (cfg->track_latency && !s->lat)) { seterr("out of host memory"); free(s); return KB_CAPACITY; }
   for (uint32_t i = 0; i < s->C; ++i) {
     s->id_len[i] = (uint8_t)cfg->id_len;
     default_identity(i, cfg->id_len, s->ident + (size_t)i * MAXID);
@@ -369,7 +392,7 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
 int kbo_sim_destroy(kbo_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
   for (uint32_t i = 0; i < s->C; ++i) free(s->out[i].v);
-  free(s->stamp); free(s->alive); free(s->ever); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
+  free(s->stamp); free(s->lat); free(s->alive); free(s->ever); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
   free(s->last_bcast); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
   for (size_t k = 0; k < s->nwatch; ++k) free(s->wsnap[k]);
@@ -467,7 +490,7 @@ static void phase_broadcasts(kbo_sim* s, uint32_t i, int32_t r) {
     const obcast* b = &s->bjoin[k];
     if (b->sender == i) continue;                     /* addr == self_addr               :285-287 */
     if (bcast_lost(s, i, b, r, 1, k)) { lost++; continue; }
-    int is_new = map_insert_known(s, i, b->sender, r, r);
+    int is_new = map_insert_known(s, i, b->sender, r, r, -1);
     if (is_new && should_respond(s, i, b->sender, r)) join_response(s, i, b->sender, r);
   }
 #pragma omp atomic
@@ -579,9 +602,9 @@ static void maybe_sync(kbo_sim* s, uint32_t i, uint32_t peer, uint32_t their_fp,
   emit(s, i, peer, K_KPR, 0, f, s->n[i], NULL, 0);
 }
 
-static void handle_message(kbo_sim* s, uint32_t i, const omsg* m, int32_t r) {
+static void handle_message(kbo_sim* s, uint32_t i, const omsg* m, int32_t r, uint32_t w) {
   uint32_t from = m->sender;
-  map_insert_known(s, i, from, r, r);            /* prologue :406-415 */
+  map_insert_known(s, i, from, r, r, (int)w);    /* prologue :406-415 */
   switch (m->kind) {
     case K_ACK: {                                  /* :418-447 */
       ocur* e = cur_find(s, i, m->a);
@@ -598,7 +621,7 @@ static void handle_message(kbo_sim* s, uint32_t i, const omsg* m, int32_t r) {
       uint8_t* rw = row(s, i);
       for (uint32_t k = 0; k < m->pay_len; ++k) {
         uint32_t p = m->pay[k];
-        if (rw[p] == ST_UNKNOWN) map_insert_known(s, i, p, r - SHARE_AGE, r);
+        if (rw[p] == ST_UNKNOWN) map_insert_known(s, i, p, r - SHARE_AGE, r, -1);
       }
       break;
     }
@@ -687,8 +710,8 @@ static int run_waves(kbo_sim* s, int32_t r) {
     for (uint32_t i = 0; i < C; ++i) {
       /* KnownPeers first (arrival order is free; this group commutes), then the rest,
          each in (sender, seq) order */
-      for (size_t q = 0; q < inb0[i].n; ++q) handle_message(s, i, &all[inb0[i].idx[q]], r);
-      for (size_t q = 0; q < inb1[i].n; ++q) handle_message(s, i, &all[inb1[i].idx[q]], r);
+      for (size_t q = 0; q < inb0[i].n; ++q) handle_message(s, i, &all[inb0[i].idx[q]], r, w);
+      for (size_t q = 0; q < inb1[i].n; ++q) handle_message(s, i, &all[inb1[i].idx[q]], r, w);
     }
     for (size_t k = 0; k < M; ++k) free(all[k].pay);
     free(all);
@@ -925,7 +948,8 @@ int kbo_sim_peer_states(kbo_sim* s, uint32_t node, kb_peer_state* out, size_t ca
     if (!rw[j]) continue;
     if (out && c < cap) {
       kb_peer_state* o = &out[c];
-      o->peer = j; o->latency_ms = KB_LATENCY_NONE;
+      o->peer = j;
+      o->latency_ms = s->lat && s->lat[(size_t)node * s->C + j] != LAT_NONE ? s->lat[(size_t)node * s->C + j] : KB_LATENCY_NONE;
       if (rw[j] == ST_SUSPECT) {
         osusp* q = susp_find(s, node, j);
         o->state = q && q->kind == SK_WFIP ? KB_STATE_WAITING_FOR_INDIRECT_PING : KB_STATE_WAITING_FOR_PING;

@@ -94,6 +94,7 @@ class Peer:
         self.ever = False
         self.start_round = None
         self.known = {}          # peer -> [state, instant]
+        self.latency = {}        # peer -> PeerInfo.latency in ms (absent = None)
         self.curious = {}        # peer -> [observers]
         self.last_bcast = None
         self.paq = []
@@ -148,6 +149,8 @@ class PyMesh:
     def _start(self, i, r):
         p = self.peers[i]
         p.running, p.ever, p.start_round = True, True, r
+        if i not in p.known:
+            p.latency.pop(i, None)
         p.known[i] = [KNOWN, r]
         p.last_bcast = None
         p.curious = {}
@@ -245,6 +248,8 @@ class PyMesh:
             if a == p.id or self.lost_b(p.id, a, 1, e, r):
                 continue
             is_new = a not in p.known
+            if is_new:
+                p.latency.pop(a, None)                    # :294-296 keeps an existing entry's latency
             p.known[a] = [KNOWN, r]
             if is_new and self.should_respond(p, a, r):
                 self.send_known_peers_to(p, a, r)
@@ -366,15 +371,16 @@ class PyMesh:
             for d in sorted(inbox):
                 box = inbox[d]
                 for m in [m for m in box if m["kind"] == "KnownPeers"] + [m for m in box if m["kind"] != "KnownPeers"]:
-                    self.handle(self.peers[d], m, r)
+                    self.handle(self.peers[d], m, r, w)
         left = [m for s in sorted(self.out) for m in self.out[s]]
         self.count_sent(left)
         self.stats["drop_window"] += len(left)
         self.out = {}
 
     # handle_incoming_messages (src/kaboodle.rs:394-548)
-    def handle(self, p, m, r):
+    def handle(self, p, m, r, w=0):
         s = m["sender"]
+        self.observe_latency(p, s, r, w)
         p.known[s] = [KNOWN, r]                                   # :406-415
         kind = m["kind"]
         if kind == "Ack":                                         # :418-447
@@ -387,6 +393,7 @@ class PyMesh:
         elif kind == "KnownPeers":                                # :448-472
             for q in m["peers"]:
                 if q not in p.known:
+                    p.latency.pop(q, None)                        # latency: None (:467)
                     p.known[q] = [KNOWN, r - SHARE_AGE]
         elif kind == "KnownPeersRequest":                         # :473-512
             lst = sorted(q for q, (st, t) in p.known.items()
@@ -413,6 +420,21 @@ class PyMesh:
                 p.curious[peer] = [s]
             self.emit(p.id, peer, "Ping")
 
+    @staticmethod
+    def observe_latency(p, s, r, w):
+        """calculate_peer_latency (src/kaboodle.rs:789-817) on the envelope prologue (:408-413), simulated
+        clock: the tick of round t is at 1000·t ms, wave w delivers at 1000·r + w + 1."""
+        old = p.known.get(s)
+        if old is None:
+            p.latency.pop(s, None)
+            return
+        st, t = old
+        if st == KNOWN:
+            return
+        sample = 1000 * (r - t) + w + 1
+        prev = p.latency.get(s)
+        p.latency[s] = sample if prev is None else int((sample * 0.8) + (prev * (1.0 - 0.8)))
+
     def maybe_sync(self, p, peer, their_fp, their_n):           # :707-740
         f = fingerprint(p.known, self.identity)
         if f == their_fp or len(p.known) > their_n:
@@ -430,14 +452,16 @@ class PyMesh:
     def peer_states(self, i):
         """Kaboodle::peer_states (src/lib.rs:348-354) as the ABI reports it: (peer, state, since,
         latency); since = the exact instant, or INT32_MIN once the stamp window has saturated it
-        (DESIGN.md §2.2); latency not modelled here (none)."""
+        (DESIGN.md §2.2); latency in ms, 0xFFFFFFFF = None."""
         rl = max(self.round - 1, 0)
         out = []
-        for q, (st, t) in sorted(self.peers[i].known.items()):
+        p = self.peers[i]
+        for q, (st, t) in sorted(p.known.items()):
+            lat = p.latency.get(q, 0xFFFFFFFF)
             if st == KNOWN:
-                out.append((q, 0, t if stamp_key(t, rl) > 2 else -2 ** 31, 0xFFFFFFFF))
+                out.append((q, 0, t if stamp_key(t, rl) > 2 else -2 ** 31, lat))
             else:
-                out.append((q, 1 if st == WFP else 2, t, 0xFFFFFFFF))
+                out.append((q, 1 if st == WFP else 2, t, lat))
         return out
 
     def suspects(self, i):

@@ -25,9 +25,9 @@ def gpu():
 
 @pytest.mark.parametrize("name,case,rounds", parity.standard_cases(), ids=[c[0] for c in parity.standard_cases()])
 def test_parity_every_round(gpu, name, case, rounds):
-    """Complete state every round, plus peer_states() of every node (the rebase_window case crosses two
-    64-round stamp-window rebases)."""
-    ok, msg, _ = parity.run_case(case, rounds, peer_states=True)
+    """Complete state every round, plus peer_states() of every node with the latency EWMA on (the
+    rebase_window case crosses two 64-round stamp-window rebases)."""
+    ok, msg, _ = parity.run_case(parity.with_cfg(case, track_latency=1), rounds, peer_states=True)
     assert ok, f"{name}: {msg}"
 
 
@@ -66,8 +66,27 @@ def test_wide_row_paths_are_hit(gpu):
 @pytest.mark.parametrize("name", ["churn_loss_512", "config2_join_1k", "partition_heal"])
 def test_parity_wide_row_paths_sharded(gpu, name):
     case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}[name]
-    ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_ALL), rounds, shards=3)
+    ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_ALL, track_latency=1), rounds, shards=3,
+                                 peer_states=True)
     assert ok, f"{name} x3 (debug_flags={KB_DBG_ALL}): {msg}"
+
+
+def test_latency_ewma_measured(gpu):
+    """PeerInfo.latency (src/kaboodle.rs:789-817) is really measured on the GPU: after a lossy run with
+    churn, many entries carry a latency, of several values (direct Ack 2 ms, indirect 4 ms, EWMA mixes),
+    and every node's peer_states equals the oracle's."""
+    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}["churn_loss_512"]
+    cfg = parity.with_cfg(case, track_latency=1)["cfg"]
+    with Sim(parity.oracle_lib(), cfg) as o, Sim(gpu, cfg) as g:
+        o.step(rounds)
+        g.step(rounds)
+        vals = []
+        for i in range(cfg.capacity):
+            a = g.peer_states(i)
+            assert a == o.peer_states(i), f"node {i}"
+            vals += [e[3] for e in a if e[3] != 0xFFFFFFFF]
+    assert len(vals) > cfg.capacity, len(vals)
+    assert len(set(vals)) >= 3, sorted(set(vals))
 
 
 def _shard_cases():

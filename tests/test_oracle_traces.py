@@ -10,6 +10,7 @@ import os
 
 import numpy as np
 import pytest
+from dataclasses import replace
 
 import pyref
 import scenarios
@@ -41,7 +42,8 @@ def test_oracle_live_pin(name):
     64-round stamp-window rebases in "rebase"), fingerprints, counters."""
     sc = scenarios.BY_NAME[name]
     pm = scenarios.pymesh_of(sc)
-    with Sim(oracle_lib(), sc["cfg"]) as o:
+    measured = 0
+    with Sim(oracle_lib(), replace(sc["cfg"], track_latency=1)) as o:
         scenarios.setup(o, sc)
         scenarios.setup(pm, sc)
         for r in range(sc["rounds"]):
@@ -53,9 +55,12 @@ def test_oracle_live_pin(name):
                 assert np.array_equal(o.row(i), np.array(pm.row(i), np.uint8)), f"round {r} node {i} row"
                 assert o.suspects(i) == pm.suspects(i), f"round {r} node {i} suspects"
                 assert o.curious(i) == pm.curious_view(i), f"round {r} node {i} curious"
-                assert o.peer_states(i) == pm.peer_states(i), f"round {r} node {i} peer_states"
+                ps = o.peer_states(i)
+                assert ps == pm.peer_states(i), f"round {r} node {i} peer_states"
+                measured += sum(1 for e in ps if e[3] != 0xFFFFFFFF)
                 want = pyref.fingerprint(pm.peers[i].known, pm.identity) if pm.peers[i].running else 0
                 assert o.fingerprint(i) == want if pm.peers[i].running else True
             st = o.stats()
             assert {k: st[k] for k in scenarios.STAT_KEYS} == {k: pm.stats[k] for k in scenarios.STAT_KEYS}
             assert st["agree"] == pm.agree
+    assert measured > 0, "no latency was ever measured: the EWMA is untested"
