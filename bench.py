@@ -41,6 +41,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM [CDNA4]")
+LAT_TABLE_MAX = 64 << 30        # bytes of latency table per GPU beyond which --latency is dropped
 KT_ROWPASS, KT_ROUND, KT_FOLD = 0, 1, 2   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
 KERNEL_NAMES = {KT_ROWPASS: "k_rowpass", KT_FOLD: "k_fold"}
 
@@ -61,6 +62,7 @@ def parse():
     ap.add_argument("--conv-cap", type=int, default=100, help="max untimed quiescent rounds for convergence")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-latency", action="store_true", help="do not keep PeerInfo.latency (track_latency 0)")
     ap.add_argument("--no-conv", action="store_true")
     ap.add_argument("--no-modes", action="store_true", help="skip the socket_faithful line (N = 1)")
     ap.add_argument("--failed-mode", choices=("sim_sender", "socket_faithful"), default="sim_sender",
@@ -173,7 +175,17 @@ def rank_config(a, rank: int, world: int, local: int):
     mode = KB_FAILED_SOCKET_FAITHFUL if getattr(a, "failed_mode", "sim_sender") == "socket_faithful" else KB_FAILED_SIM_SENDER
     return SimConfig(capacity=peers + reserve, initial_nodes=peers, init_mode=KB_INIT_CONVERGED, loss=a.loss,
                      churn=a.churn, fault_end_round=total, seed=a.seed + (0 if shard else 1000 * rank),
-                     device=local if world > 1 else -1, failed_mode=mode)
+                     device=local if world > 1 else -1, failed_mode=mode,
+                     track_latency=int(latency_on(a, peers + reserve, world if shard else 1)))
+
+
+def latency_on(a, capacity: int, shards: int) -> bool:
+    """PeerInfo.latency is kept (as the reference always does, src/kaboodle.rs:789-817) unless --no-latency,
+    or unless its table (2 B per row x id) would take more than LAT_TABLE_MAX of one GPU's HBM (configs[3]:
+    131K rows x 1M ids = 275 GB on top of the stamps)."""
+    rows = -(-capacity // shards)
+    width = -(-capacity // 8192) * 8192
+    return not getattr(a, "no_latency", False) and 2 * rows * width <= LAT_TABLE_MAX
 
 
 def share_uid(rank: int, make) -> bytes:
@@ -305,7 +317,7 @@ def main() -> int:
                        "capacity": capacity,
                        "loss": a.loss, "churn": a.churn,
                        "parallelism": (f"rowshard{world}" if shard else f"replicas{world}") if world > 1 else "single",
-                       "max_waves": cfg.max_waves},
+                       "max_waves": cfg.max_waves, "latency_ewma": bool(cfg.track_latency)},
             "roofline": rl[dominant],
             "kernels": {n: v for n, v in rl.items() if n != dominant},
             "round_gpu_ms": round(round_ms / max(round_n, 1), 4),

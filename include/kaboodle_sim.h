@@ -96,7 +96,7 @@ typedef struct kb_peer_state {
   uint32_t peer;             /* peer id                                                             */
   uint32_t state;            /* KB_STATE_*                                                          */
   int32_t  since;            /* round of the state's Instant; INT32_MIN = older than the stamp window */
-  uint32_t latency_ms;       /* PeerInfo.latency in simulated ms; KB_LATENCY_NONE =
+  uint32_t latency_ms;       /* PeerInfo.latency in simulated ms ; KB_LATENCY_NONE =
                                 None (never measured, or track_latency off)                          */
 } kb_peer_state;
 #define KB_LATENCY_NONE 0xFFFFFFFFu

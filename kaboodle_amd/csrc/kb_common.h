@@ -86,7 +86,8 @@ struct Dev {
   uint32_t* flog_n;
   uint32_t* fstart;
   int32_t* kpr_big;               // round in which the node's KPR reply was proven oversize for the round
-  uint16_t* lat;                  // [C][W] PeerInfo.latency in ms (LAT_NONE = None); null unless track_latency
+  uint16_t* lat;                  // [W][local rows] PeerInfo.latency in ms, PEER-major (LAT_NONE = None); null
+                                  // unless track_latency
   int32_t wave;                   // delivery wave of the launch (latency clock)
 };
 
@@ -326,14 +327,20 @@ __device__ inline void susp_clear(const Dev& d, uint32_t i, uint32_t p) {
 // Simulated clock: the tick of round r at 1000·r ms, wave w of its receive window at 1000·r + w + 1.
 // Invariant: LAT_NONE wherever the member bit is clear (removals write it), so an insertion needs no
 // write: a new entry's latency is None (:412 on an absent sender, :294-296, :467).
+// The table is peer-major: a round's Failed broadcasts remove the same few hundred peers from every
+// row, so those writes land in a few contiguous columns (lines shared by adjacent rows) instead of
+// one scattered line per (row, peer).
 constexpr uint16_t LAT_NONE = 0xFFFFu;
+__device__ inline uint16_t* lat_at(const Dev& d, uint32_t i, uint32_t p) {
+  return d.lat + (size_t)p * (d.hi - d.lo) + (i - d.lo);
+}
 __device__ inline void lat_none(const Dev& d, uint32_t i, uint32_t p) {
-  if (d.lat) d.lat[(size_t)i * d.W + p] = LAT_NONE;
+  if (d.lat) *lat_at(d, i, p) = LAT_NONE;
 }
 // the envelope prologue of a unicast from p while p is WaitingFor*(since): calculate_peer_latency
 __device__ inline void lat_sample(const Dev& d, uint32_t i, uint32_t p, int32_t since, int32_t r) {
   if (!d.lat) return;
-  uint16_t* q = d.lat + (size_t)i * d.W + p;
+  uint16_t* q = lat_at(d, i, p);
   const uint32_t smp = 1000u * (uint32_t)(r - since) + (uint32_t)d.wave + 1u;
   const uint32_t prev = *q;
   uint32_t v = smp;

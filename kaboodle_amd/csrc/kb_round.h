@@ -128,7 +128,34 @@ struct PhaseB {
   const BCast* bjoin; uint32_t nj; uint32_t JW;
   unsigned long long* newmask; unsigned long long* respmask;   // [C * JW]
   uint32_t* nresp; uint32_t* paysum; uint32_t* nbase;           // per node
+  const uint32_t* fnamed;  // track_latency: bitset of the peers the Failed list names (k_lat_mark)
 };
+
+// ---- PeerInfo.latency upkeep for the Failed removals ---------------------------
+// The row pass does not write the (peer-major) latency table when Failed removes a peer: a round
+// removes tens of millions of (row, peer) entries in the sim_sender workload, nearly all of them
+// never measured.  k_lat_sweep instead reads each named peer's column once, right after the row pass
+// and before anything can re-insert and measure, and resets the entries whose member bit is now
+// clear.  The one re-insertion inside the row pass itself (a Join of a peer the same round's Failed
+// list names) resets its entry there, using the fnamed bitset.
+__global__ void k_lat_mark(const BCast* bf, uint32_t nf, uint32_t* fnamed) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f < nf) atomicOr(&fnamed[bf[f].peer >> 5], 1u << (bf[f].peer & 31));
+}
+__global__ __launch_bounds__(256) void k_lat_sweep(Dev d, const BCast* bf, const uint32_t* gid, uint32_t nf,
+                                                   uint32_t* fnamed) {
+  const uint32_t R = d.hi - d.lo;
+  for (uint32_t f = blockIdx.y; f < nf; f += gridDim.y) {
+    if (gid[f] != f) continue;                        // first entry naming the peer only
+    const uint32_t p = bf[f].peer;
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAnd(&fnamed[p >> 5], ~(1u << (p & 31)));
+    uint16_t* col = d.lat + (size_t)p * R;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < R; k += gridDim.x * blockDim.x) {
+      const uint16_t v = col[k];
+      if (v != LAT_NONE && !is_mem(d, d.lo + k, p)) col[k] = LAT_NONE;
+    }
+  }
+}
 
 // Broadcast loss: entry e of the round's Failed (lst 0) / Join (lst 1) list reaches
 // receiver i unless word e % 4 of philox(i, r, P_BLOSS << 24 | lst << 23 | e / 4, 0) < loss_thr.  A wave
@@ -389,7 +416,6 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
           const uint32_t m = 1u << (b.peer & 31);
           if (atomicAnd(&B[b.peer >> 5], ~m) & m) {
             removed_cnt++;
-            lat_none(d, i, b.peer);
             if (is_susp(b.peer)) susp_clear(d, i, b.peer);
             segs |= seg_bit(d, b.peer);
           }
@@ -435,7 +461,10 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
         if (deliver) {
           if (known && is_susp(b.sender)) susp_clear(d, i, b.sender);
           rw[b.sender] = now;
-          if (isnew) { atomicOr(&B[b.sender >> 5], 1u << (b.sender & 31)); segs |= seg_bit(d, b.sender); }
+          if (isnew) {
+            atomicOr(&B[b.sender >> 5], 1u << (b.sender & 31)); segs |= seg_bit(d, b.sender);
+            if (pb.fnamed && ((pb.fnamed[b.sender >> 5] >> (b.sender & 31)) & 1u)) lat_none(d, i, b.sender);
+          }
         }
         const uint32_t sz = resp ? (d.uniform ? (nq < d.capj ? nq : d.capj) : nq) : 0;
         paysum += wave_sum(sz);

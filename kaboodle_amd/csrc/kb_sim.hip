@@ -263,6 +263,11 @@ __global__ __launch_bounds__(256) void k_events_commit(const uint32_t* __restric
   const uint32_t w = blockIdx.x * 256 + threadIdx.x;
   if (w < nw) snap[w] = row[w];
 }
+// one node's latencies out of the peer-major table (peer_states)
+__global__ __launch_bounds__(256) void k_lat_column(Dev d, uint32_t node, uint16_t* out) {
+  const uint32_t j = blockIdx.x * 256 + threadIdx.x;
+  if (j < d.C) out[j] = *lat_at(d, node, j);
+}
 
 struct kb_sim {
   kb_config cfg;
@@ -293,6 +298,8 @@ struct kb_sim {
   uint32_t* nresp; uint32_t* paysum; uint32_t* nbase; uint32_t* resp_off;
   uint32_t* resp_nodes; uint32_t* bf_gid; uint8_t* bf_dep;
   uint32_t* slow;                      // the nodes of a wave k_proc_fast leaves to k_proc
+  uint16_t* lat_col;                   // [C] one node's latencies (peer_states), track_latency only
+  uint32_t* fnamed;                    // [NWR] peers named by the round's Failed list (track_latency only)
   uint32_t* resp_scratch; size_t resp_scratch_words;
   RowOut ro;
   Event* d_events; uint32_t events_cap;
@@ -490,7 +497,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
-  if (cfg->track_latency) AR(d.lat, W);
+  if (cfg->track_latency) { A(d.lat, (size_t)W * R); A(s->lat_col, C); A(s->fnamed, d.NWR); }   // peer-major [W][R]
   s->msg_cap = std::max<uint32_t>(8u * R + (uint32_t)TICK_MAX * R, 1u << 16);
   s->pay_cap = std::max<uint32_t>((d.capk + 1) * R, 1u << 24);
   for (int b = 0; b < 2; ++b) {
@@ -522,7 +529,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
 #undef AR
   if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); destroy_shard(s); return KB_CAPACITY; }
   (void)hipMemset(L(s, d.kpr_big), 0xFF, 4ull * R);          // no round yet
-  if (d.lat) (void)hipMemset(d.lat + (size_t)s->lo * W, 0xFF, 2ull * R * W);   // every latency None
+  if (d.lat) { (void)hipMemset(d.lat, 0xFF, 2ull * R * W); (void)hipMemset(s->fnamed, 0, 4ull * d.NWR); }   // every latency None
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
   for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->er0, &s->er1, &s->ef0, &s->ef1}) (void)hipEventCreate(e);
@@ -781,6 +788,10 @@ static int step_round(kb_sim* s) {
   }
   pb.newmask = s->newmask; pb.respmask = s->respmask;
   pb.gid = s->bf_gid; pb.dep = s->bf_dep;
+  // latency upkeep for Failed removals; socket_faithful never honours Failed, so nothing to do there
+  const bool lat_fail = d.lat && s->nf && d.failed_mode == KB_FAILED_SIM_SENDER;
+  pb.fnamed = lat_fail ? s->fnamed : nullptr;
+  if (lat_fail) k_lat_mark<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->fnamed);
   const bool have_b = s->nf + s->nj > 0;
   const bool pb_hbm = (d.dbg & KB_DBG_PHASEB_HBM) != 0;
   if (s->nf > 2048 || (pb_hbm && s->nf)) k_bfail_prep<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep, d.ctr + C_PATHS);
@@ -801,6 +812,8 @@ static int step_round(kb_sim* s) {
     if (ldsb) hipExtLaunchKernelGGL(k_rowpass<true>, dim3(blocks), dim3(64 * wpb), lds, st, s->ev0, s->ev1, 0, d, pb, s->ro, r, lf, lj);
     else hipExtLaunchKernelGGL(k_rowpass<false>, dim3(blocks), dim3(64 * wpb), lds, st, s->ev0, s->ev1, 0, d, pb, s->ro, r, lf, lj);
   }
+  if (lat_fail)
+    k_lat_sweep<<<dim3((R + 1023) / 1024, std::min<uint32_t>(s->nf, 8192)), 256, 0, st>>>(d, s->bfail, s->bf_gid, s->nf, s->fnamed);
   {  // wave-0 outbox regions: responses first, then the tick's messages
     ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 3;
@@ -1160,7 +1173,9 @@ extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, 
   std::vector<uint16_t> lat;
   if (s->d.lat) {
     lat.resize(s->C);
-    HIPCHK(hipMemcpy(lat.data(), s->d.lat + (size_t)node * s->W, 2ull * s->C, hipMemcpyDeviceToHost));
+    k_lat_column<<<(s->C + 255) / 256, 256, 0, s->st>>>(s->d, node, s->lat_col);
+    HIPCHK(hipMemcpyAsync(lat.data(), s->lat_col, 2ull * s->C, hipMemcpyDeviceToHost, s->st));
+    HIPCHK(hipStreamSynchronize(s->st));
   }
   const int32_t E = epoch_base(s->round > 0 ? s->round - 1 : 0);
   size_t c = 0;
