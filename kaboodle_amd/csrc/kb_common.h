@@ -25,7 +25,9 @@ enum StatIdx {
 };
 enum CtrIdx {
   C_KP, C_SLOW, C_ACTIVE, C_AGREE, C_ALIVE, C_LEAVES, C_NEXTFREE, C_ERR, C_FIRSTCONV, C_LASTCONV, C_LASTAGREE,
-  C_LASTALIVE, C_DBG_INS, C_DBG_FP, C_DBG_MAXFP, C_TICK,
+  C_LASTALIVE, C_DBG_INS, C_DBG_FP, C_DBG_MAXFP,
+  C_DBG_KPR, C_DBG_KPRLOG, C_DBG_BASE,   // KB_DEBUG_WAVES: full KPR reply scans, log entries read, take_base
+  C_TICK,
   C_PATHS,                        // OR of the PATH_* bits of the kernel variants that did work (test surface)
   NCTR
 };
@@ -331,8 +333,9 @@ __device__ inline void susp_clear(const Dev& d, uint32_t i, uint32_t p) {
 // row, so those writes land in a few contiguous columns (lines shared by adjacent rows) instead of
 // one scattered line per (row, peer).
 constexpr uint16_t LAT_NONE = 0xFFFFu;
+__host__ __device__ inline uint32_t lat_stride(uint32_t rows) { return (rows + 7u) & ~7u; }   // 16-byte columns
 __device__ inline uint16_t* lat_at(const Dev& d, uint32_t i, uint32_t p) {
-  return d.lat + (size_t)p * (d.hi - d.lo) + (i - d.lo);
+  return d.lat + (size_t)p * lat_stride(d.hi - d.lo) + (i - d.lo);
 }
 __device__ inline void lat_none(const Dev& d, uint32_t i, uint32_t p) {
   if (d.lat) *lat_at(d, i, p) = LAT_NONE;

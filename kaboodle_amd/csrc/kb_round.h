@@ -144,15 +144,20 @@ __global__ void k_lat_mark(const BCast* bf, uint32_t nf, uint32_t* fnamed) {
 }
 __global__ __launch_bounds__(256) void k_lat_sweep(Dev d, const BCast* bf, const uint32_t* gid, uint32_t nf,
                                                    uint32_t* fnamed) {
-  const uint32_t R = d.hi - d.lo;
+  const uint32_t R = d.hi - d.lo, RS = lat_stride(R);
   for (uint32_t f = blockIdx.y; f < nf; f += gridDim.y) {
     if (gid[f] != f) continue;                        // first entry naming the peer only
     const uint32_t p = bf[f].peer;
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAnd(&fnamed[p >> 5], ~(1u << (p & 31)));
-    uint16_t* col = d.lat + (size_t)p * R;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < R; k += gridDim.x * blockDim.x) {
-      const uint16_t v = col[k];
-      if (v != LAT_NONE && !is_mem(d, d.lo + k, p)) col[k] = LAT_NONE;
+    uint4* col = reinterpret_cast<uint4*>(d.lat + (size_t)p * RS);      // 8 rows per 16-byte load
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < RS / 8; k += gridDim.x * blockDim.x) {
+      const uint4 v = col[k];
+      if ((v.x & v.y & v.z & v.w) == 0xFFFFFFFFu) continue;            // all eight None (the common case)
+      uint16_t* e = reinterpret_cast<uint16_t*>(col + k);
+      for (uint32_t q = 0; q < 8; ++q) {
+        const uint32_t row = 8 * k + q;
+        if (row < R && e[q] != LAT_NONE && !is_mem(d, d.lo + row, p)) e[q] = LAT_NONE;
+      }
     }
   }
 }
@@ -454,7 +459,10 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
           }
         }
         const unsigned long long respm = __ballot(resp);
-        const bool logit = deliver && (!known || rw[b.sender] != now);
+        // every delivered Join stamps its sender Known(now) afresh: before the row pass no stamp of the
+        // round's own instant exists except self's (a node broadcasts one Join per round), so each
+        // delivery is a transition to Known(now) and is logged — no read of the old byte needed
+        const bool logit = deliver;
         const unsigned long long lgm = __ballot(logit);
         if (logit) d.flog[(size_t)i * LOGCAP + ((fn + __popcll(lgm & ((1ull << l) - 1ull))) & (LOGCAP - 1))] = log_entry(b.sender, r);
         fn += __popcll(lgm);

@@ -1,18 +1,22 @@
 // kb_sim.hip — MI355X (gfx950) implementation of the Kaboodle SWIM round as a bulk-synchronous
 // simulator over HBM-resident structure-of-arrays tables.  Exposes the C ABI of include/kaboodle_sim.h.
 //
-// Round pipeline, one HIP stream, one 8-byte host read per round (+1 when broadcasts
-// produced Join responses):
+// Round pipeline, one HIP stream; the host reads 8 bytes per round (+20 when the
+// broadcasts produced Join responses, to size the wave-0 outbox):
 //   k_rebase (every 64 rounds)      stamp window shift                             
 //   k_events / k_churn_*            Kaboodle::start/stop, churn                    src/lib.rs:136-183
-//   k_alive_bits, k_truefp          running set and its fingerprint
-//   k_bfail_prep, k_phaseB          handle_incoming_broadcasts (Failed, Join)      src/kaboodle.rs:256-311
-//   k_resp_node                     maybe_send_known_peers_to_peer                 src/kaboodle.rs:356-392
-//   k_tick_pre                      maybe_broadcast_join + handle_suspected_peers  :228-251, :558-653
-//   k_sweep    <- dominant kernel   ping_random_peer row sweep + fingerprint checkpoints :655-703, :71-83
+//   k_alive_bits, k_truefp_*        running set and its fingerprint
+//   k_bfail_prep(_lds), k_lat_mark  per-list facts of the Failed broadcasts
+//   k_rowpass  <- dominant kernel   handle_incoming_broadcasts (Failed, Join) + ping_random_peer's
+//                                   oldest-5 candidates, one pass per row        :256-311, :655-703
+//   k_lat_sweep                     latency entries of Failed removals (track_latency)  :789-817
+//   k_resp_wave / k_resp_node       maybe_send_known_peers_to_peer                 :356-392
+//   k_tick_scan, k_tick_pre         maybe_broadcast_join + handle_suspected_peers  :228-251, :558-653
+//   k_fold                          stale fingerprint checkpoints refolded         :71-83
 //   k_tick_post                     ping target, handle_incoming_ping_requests     :655-703, :550-556
-//   waves: k_wave_clear, k_route (k_route_x, k_pack, exchange, k_route_recv when sharded), k_scan_*,
-//          k_scatter, k_kp_group, k_sort_inbox, k_proc
+//   k_bcast_write                   the round's Join/Failed lists
+//   waves: k_route (k_route_x, k_pack, exchange, k_route_recv when sharded), k_scan_*, k_scatter,
+//          k_kp_small, k_kp_group, k_sort_inbox (+ KPR oversize probe), k_proc_fast, k_proc
 //                                   handle_incoming_messages                       src/kaboodle.rs:394-548
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
@@ -497,7 +501,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
-  if (cfg->track_latency) { A(d.lat, (size_t)W * R); A(s->lat_col, C); A(s->fnamed, d.NWR); }   // peer-major [W][R]
+  if (cfg->track_latency) { A(d.lat, (size_t)W * lat_stride(R)); A(s->lat_col, C); A(s->fnamed, d.NWR); }   // peer-major
   s->msg_cap = std::max<uint32_t>(8u * R + (uint32_t)TICK_MAX * R, 1u << 16);
   s->pay_cap = std::max<uint32_t>((d.capk + 1) * R, 1u << 24);
   for (int b = 0; b < 2; ++b) {
@@ -529,7 +533,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
 #undef AR
   if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); destroy_shard(s); return KB_CAPACITY; }
   (void)hipMemset(L(s, d.kpr_big), 0xFF, 4ull * R);          // no round yet
-  if (d.lat) { (void)hipMemset(d.lat, 0xFF, 2ull * R * W); (void)hipMemset(s->fnamed, 0, 4ull * d.NWR); }   // every latency None
+  if (d.lat) { (void)hipMemset(d.lat, 0xFF, 2ull * lat_stride(R) * W); (void)hipMemset(s->fnamed, 0, 4ull * d.NWR); }   // all None
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
   for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->er0, &s->er1, &s->ef0, &s->ef1}) (void)hipEventCreate(e);
@@ -813,7 +817,7 @@ static int step_round(kb_sim* s) {
     else hipExtLaunchKernelGGL(k_rowpass<false>, dim3(blocks), dim3(64 * wpb), lds, st, s->ev0, s->ev1, 0, d, pb, s->ro, r, lf, lj);
   }
   if (lat_fail)
-    k_lat_sweep<<<dim3((R + 1023) / 1024, std::min<uint32_t>(s->nf, 8192)), 256, 0, st>>>(d, s->bfail, s->bf_gid, s->nf, s->fnamed);
+    k_lat_sweep<<<dim3((lat_stride(R) / 8 + 255) / 256, std::min<uint32_t>(s->nf, 16384)), 256, 0, st>>>(d, s->bfail, s->bf_gid, s->nf, s->fnamed);
   {  // wave-0 outbox regions: responses first, then the tick's messages
     ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 3;
@@ -882,7 +886,6 @@ static int step_round(kb_sim* s) {
     OutBuf& nb = s->ob[cur ^ 1];
     const int last = w == s->cfg.max_waves;
     d.wave = (int32_t)w;                               // latency clock of the wave's prologues
-    k_wave_clear<<<gnode, tb, 0, st>>>(d, s->wc);
     OutBuf ib = ob;                                    // the wave's delivered records
     uint32_t nrecv = 0;
     if (!s->xf) {
@@ -927,19 +930,21 @@ static int step_round(kb_sim* s) {
       const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
       k_kp_group<true><<<ks * groups, 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
     }
-    k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc);
-    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 12, st));
+    k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc, r);   // + the KPR oversize probe
+    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 24, st));
     k_proc_fast<<<gnode, tb, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
     // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
     // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
     // on the late waves with few nodes.
     k_proc<<<std::min<uint32_t>(4096, 2 * s->ncu), 256, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
     if (s->debug_waves) {
-      uint32_t dbg[3];
-      HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 12, hipMemcpyDeviceToHost, st));
+      uint32_t dbg[6], slow = 0;
+      HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 24, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&slow, d.ctr + C_SLOW, 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
-      fprintf(stderr, "[kb] round %d wave %u: prologue inserts %u, fingerprint refreshes %u (max per node %u)\n", r, w,
-              dbg[0], dbg[1], dbg[2]);
+      fprintf(stderr, "[kb] round %d wave %u: k_proc nodes %u, prologue inserts %u, fingerprint refreshes %u (max per "
+              "node %u), KPR scans %u (log entries %u), incremental bases %u\n", r, w, slow, dbg[0], dbg[1], dbg[2], dbg[3],
+              dbg[4], dbg[5]);
     }
     cur ^= 1;
   }

@@ -14,14 +14,12 @@ struct WaveCtl {
   uint32_t msg_cap; uint32_t pay_cap;
 };
 
-// per-wave counters of the local rows back to zero (one launch instead of a memset per array)
-__global__ void k_wave_clear(Dev d, WaveCtl wc) {
-  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < d.hi) {
-    wc.cnt1[i] = 0; wc.bnd[i] = 0; wc.bpay[i] = 0; wc.cursor[i] = 0;
-    wc.kcnt[i] = 0; wc.kpay[i] = 0; wc.kcur[i] = 0;
-  }
-  if (blockIdx.x == 0 && threadIdx.x < 3) d.ctr[C_KP + threadIdx.x] = 0;     // C_KP, C_SLOW, C_ACTIVE
+// The per-destination counters of a wave are zero outside the wave's active nodes.  Whoever handles
+// an active node last in the wave puts them back to zero: k_proc_fast for the nodes it finishes (or
+// that have no in-order delivery), k_proc for the rest.  No clearing launch per wave.
+__device__ inline void wave_ctr_clear(const WaveCtl& wc, uint32_t i) {
+  wc.cnt1[i] = 0; wc.bnd[i] = 0; wc.bpay[i] = 0; wc.cursor[i] = 0;
+  wc.kcnt[i] = 0; wc.kpay[i] = 0; wc.kcur[i] = 0;
 }
 
 // messages a handler may emit per delivered message (next-wave outbox reservation)
@@ -405,6 +403,7 @@ __global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, 
   {  // the next outbox of every local row: capacity = the wave's reservation, empty (was a copy + memset)
     const uint32_t i = d.lo + blockIdx.x * blockDim.x + t;
     if (i < d.hi) { nb.cap[i] = wc.bnd[i]; nb.cnt[i] = 0; }
+    if (blockIdx.x == 0 && t == 0) d.ctr[C_SLOW] = 0;   // k_proc_fast lists this wave's slow nodes afresh
   }
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
@@ -470,12 +469,59 @@ __global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, 
   }
 }
 
+// ---- KnownPeersRequest oversize probe (:473-512, Q3) -----------------------------------------------
+// A KPR reply lists every fresh entry (Known, stamped within SHARE_AGE, not self, not the requester);
+// above capk entries it is lost at the receiver, so only its size matters.  The fresh set only grows
+// while a round's waves run (stamps rise to now; removals happen before the waves), so counting it
+// once, as it stands when the wave starts, proves every reply of the rest of the round oversize as
+// soon as the count exceeds capk + 1 (one requester excluded): kpr_big = r, and k_proc's KPR handler
+// takes its constant-time path.  A wave per node with a KPR delivery this wave, all of its log window
+// in flight at once (up to 8 x 64 entries per step); run by the small, high-occupancy k_sort_inbox
+// after its sorts, in front of the register-heavy k_proc.
+__device__ __attribute__((always_inline)) inline void kpr_probe(const Dev& d, const WaveCtl& wc, int32_t r) {
+  const uint32_t nact = d.ctr[C_ACTIVE];
+  const uint32_t nwv = blockDim.x >> 6, wv = threadIdx.x >> 6, l = lane();
+  for (uint32_t it = blockIdx.x * nwv + wv; it < nact; it += gridDim.x * nwv) {
+    const uint32_t i = wc.active[it];
+    if (!wc.bpay[i] || d.kpr_big[i] == r) continue;  // wave-uniform: no KPR, or already proven
+    const uint8_t* rw = row_of(d, i);
+    const uint32_t* bw = bits_of(d, i);
+    const uint32_t fn = d.flog_n[i], ws = log_window_start(d, i, r);
+    const uint32_t k_lo = fn - ws <= LOGCAP ? ws : fn - LOGCAP;
+    uint32_t total = 0;
+    constexpr int PB = 8;
+    for (uint32_t k0 = k_lo; k0 < fn && total <= d.capk + 1; k0 += 64 * PB) {
+      uint32_t ev[PB], wv4[PB], bv[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const uint32_t k = k0 + 64u * u + l;
+        ev[u] = k < fn ? d.flog[(size_t)i * LOGCAP + (k & (LOGCAP - 1))] : LOG_INVALID;
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const uint32_t j = ev[u] == LOG_INVALID ? i : ev[u] >> 8;
+        wv4[u] = bw[j >> 5];
+        bv[u] = rw[j];
+      }
+      uint32_t c = 0;
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const uint32_t e = ev[u], j = e >> 8;
+        c += e != LOG_INVALID && j != i && r - log_round(e, r) < SHARE_AGE && ((wv4[u] >> (j & 31)) & 1u) &&
+             bv[u] == enc(log_round(e, r), r);
+      }
+      total += wave_sum(c);
+    }
+    if (total > d.capk + 1 && l == 0) d.kpr_big[i] = r;
+  }
+}
+
 // ---- inboxes longer than one wave: sorted into canonical (sender, seq) order = ascending outbox
 // index, one workgroup per node, bitonic in LDS (up to SORT_MAX entries; longer ones keep the
 // selection path of k_proc)
 constexpr uint32_t SORT_MAX = 8192;
 __device__ inline uint32_t sort_max(const Dev& d) { return (d.dbg & KB_DBG_PROC_UNSORTED) ? 64u : SORT_MAX; }
-__global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc) {
+__global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc, int32_t r) {
   __shared__ uint32_t v[SORT_MAX];
   __shared__ uint32_t s_list[1024], s_nl;
   const uint32_t nact = d.ctr[C_ACTIVE];
@@ -515,13 +561,15 @@ __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc) {
     __syncthreads();
   }
   }
+  if (d.uniform) kpr_probe(d, wc, r);               // then the KPR oversize probe, wave per node
 }
 
 // ---- the per-node in-order program for Ping / PingRequest / Ack / KnownPeersRequest ---------------
 // ---- fast lane of the in-order handlers: a THREAD per node --------------------------------------
-// The common inbox — at most FAST_MAX Ping / PingRequest / Ack envelopes, every sender already a
-// member, the node's fingerprint current — changes no membership, so no fingerprint work: the
-// handlers reduce to stamp/log/slot updates and emissions.  Such nodes are handled here, one per
+// The common inbox — at most FAST_MAX Ping / PingRequest / Ack envelopes (and KnownPeersRequests
+// once kpr_probe (in k_sort_inbox) has proven this round's replies oversize), every sender already a member, the
+// node's fingerprint current — changes no membership, so no fingerprint work: the handlers reduce
+// to stamp/log/slot updates and emissions.  Such nodes are handled here, one per
 // thread, in canonical (sender, seq) order; every other node with in-order deliveries goes to the
 // `slow` list for k_proc (same semantics: prologue :406-415, Ping :513-532, PingRequest :533-545,
 // Ack :418-447, maybe_sync :707-740).
@@ -537,7 +585,7 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint32_t it = blockIdx.x * blockDim.x + threadIdx.x;
   const uint8_t now = enc(r, r);
-  unsigned long long curovf = 0;
+  unsigned long long curovf = 0, over = 0;
   bool to_slow = false;
   uint32_t i = 0;
   if (it < nact) {
@@ -555,11 +603,12 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
         for (uint32_t b = a; b > 0; --b)
           if (g[b - 1] > g[b]) { const uint32_t x = g[b]; g[b] = g[b - 1]; g[b - 1] = x; }
       const uint32_t* bw = bits_of(d, i);
+      const bool kpr_over = d.uniform && d.kpr_big[i] == r;      // every KPR reply of the round oversize
 #pragma unroll
       for (uint32_t k = 0; k < FAST_MAX; ++k) {
         if (k >= icnt) break;
         const Msg m = ib.msgs[g[k]];
-        if (m.kind == K_KPR || !((bw[m.sender >> 5] >> (m.sender & 31)) & 1u)) fast = false;
+        if ((m.kind == K_KPR && !kpr_over) || !((bw[m.sender >> 5] >> (m.sender & 31)) & 1u)) fast = false;
       }
     }
     to_slow = icnt && !fast;
@@ -607,11 +656,15 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
             cu[e].used = 0;
           }
           if (fp != m.fp && !(n > m.n)) emit_t(ob, d, i, oseq, m.a, K_KPR, 0, fp, n);
+        } else if (m.kind == K_KPR) {                  // :473-512, reply lost as oversize (Q3), then :507
+          over++;
+          if (fp != m.fp && !(n > m.n)) emit_t(ob, d, i, oseq, s, K_KPR, 0, fp, n);
         }
       }
       ob.cnt[i] = oseq;
       d.flog_n[i] = fn;
     }
+    if (!to_slow) wave_ctr_clear(wc, i);              // done with this node for the wave
   }
   const unsigned long long sm = __ballot(to_slow);  // the rest goes to k_proc
   if (sm) {
@@ -621,6 +674,7 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
     if (to_slow) slow[base + __popcll(sm & ((1ull << lane()) - 1ull))] = i;
   }
   stat_add(d, S_CUROVF, curovf);
+  stat_add(d, S_OVERSIZE, over);
 }
 
 __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r, const uint32_t* list) {
@@ -665,7 +719,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
         }
       }
     }
-    uint32_t dbg_fp = 0, dbg_ins = 0;
+    uint32_t dbg_fp = 0, dbg_ins = 0, dbg_kpr = 0, dbg_log = 0, dbg_base = 0;
     // Incremental fingerprint (uniform identities, sorted inbox).  Prologue insertions arrive in
     // ascending id order, so for an inserted x every member above x is still the base set's:
     //   raw(S + x) = raw(S)·Z ⊕ B·(Z ⊕ 1) ⊕ c_x·Z^{n>x},  B = fold of the members above x, n>x their count
@@ -676,6 +730,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     uint32_t R = 0;
     auto take_base = [&]() __attribute__((always_inline)) {
       if (need_sync) { wave_mem_sync(); need_sync = false; }
+      dbg_base++;
       const unsigned long long sd = d.sdirty[i] | segs;
       uint2 sp;
       if ((sd >> l) & 1ull) { sp = fold_segment(d, ztab, i, l); d.segp[(size_t)i * NSEG + l] = sp; }
@@ -910,6 +965,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           // those entries are still exact members of the reply, enough to prove it oversize
           const uint32_t ws = log_window_start(d, i, r);
           const bool complete = fn - ws <= LOGCAP;
+          dbg_kpr++;
           // KPR_BATCH x 64 entries per step: all their log, member-bit and stamp loads in flight at once,
           // then taken in log order (the early exit stays between steps)
           constexpr int KPR_BATCH = 4;
@@ -926,6 +982,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
               wv4[u] = bw[j >> 5];
               bv[u] = rw[j];
             }
+            dbg_log += 64 * KPR_BATCH;
 #pragma unroll
             for (int u = 0; u < KPR_BATCH; ++u) {
               if (over) break;                          // wave-uniform
@@ -969,8 +1026,11 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       if (segs) atomicOr(&d.sdirty[i], segs);
       d.n[i] = n; d.fp[i] = fp; d.dirty[i] = dirty ? 1 : 0; d.flog_n[i] = fn; d.kpr_big[i] = kbig;
       ob.cnt[i] = oseq;
+      wave_ctr_clear(wc, i);
       if (dbg_fp) { atomicAdd(&d.ctr[C_DBG_FP], dbg_fp); atomicMax(&d.ctr[C_DBG_MAXFP], dbg_fp); }
       if (dbg_ins) atomicAdd(&d.ctr[C_DBG_INS], dbg_ins);
+      if (dbg_kpr) { atomicAdd(&d.ctr[C_DBG_KPR], dbg_kpr); atomicAdd(&d.ctr[C_DBG_KPRLOG], dbg_log); }
+      if (dbg_base) atomicAdd(&d.ctr[C_DBG_BASE], dbg_base);
     }
     wait_lds();                                       // the LDS slot caches are reused by the next node
     __builtin_amdgcn_wave_barrier();
