@@ -27,6 +27,7 @@ enum CtrIdx {
   C_KP, C_SLOW, C_ACTIVE, C_AGREE, C_ALIVE, C_LEAVES, C_NEXTFREE, C_ERR, C_FIRSTCONV, C_LASTCONV, C_LASTAGREE,
   C_LASTALIVE, C_DBG_INS, C_DBG_FP, C_DBG_MAXFP,
   C_DBG_KPR, C_DBG_KPRLOG, C_DBG_BASE,   // KB_DEBUG_WAVES: full KPR reply scans, log entries read, take_base
+  C_DBG_TNODE, C_DBG_TMAX, C_DBG_TBASE, C_DBG_TINS,   // KB_DEV & 64: k_proc wall time (10 ns ticks) per part
   C_TICK,
   C_PATHS,                        // OR of the PATH_* bits of the kernel variants that did work (test surface)
   NCTR
@@ -68,6 +69,7 @@ struct Dev {
   uint32_t* n;
   uint32_t* fp;
   int32_t* last_bcast;
+  uint32_t* a3cur;                // A3's rotation base: the node's last ping target
   Susp* susp;
   Cur* cur;
   uint32_t* paq;
@@ -359,7 +361,7 @@ __device__ __attribute__((always_inline)) inline void node_start(const Dev& d, u
     else susp_clear(d, i, i);
     row_of(d, i)[i] = enc(r, r);
     mark(d, i, seg_bit(d, i));
-    d.last_bcast[i] = NONE_ROUND; d.paq_n[i] = 0;
+    d.last_bcast[i] = NONE_ROUND; d.paq_n[i] = 0; d.a3cur[i] = i;
     for (int k = 0; k < CSLOTS; ++k) d.cur[(size_t)i * CSLOTS + k].used = 0;
   }
   d.alive[i] = 1; d.start_round[i] = r;

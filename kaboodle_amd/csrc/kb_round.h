@@ -248,12 +248,13 @@ constexpr uint32_t RP_LDS_BYTES = 81920;         // dynamic LDS per row-pass wor
 struct RowOut { uint32_t* part; };   // [C][10]: the five smallest keys ascending, then 0xFFFFFFFF x 5
 
 // A3 over the row of node i (members from B: LDS or HBM): the five smallest keys (stamp << 24 | rot),
-// ascending, in every lane.  Returns the stamp bytes read.
+// ascending, in every lane; rot = address rotated to start right after `cur`, the node's last ping
+// target.  Returns the stamp bytes read.
 template <bool LDSB>
-__device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, uint32_t i, const uint8_t* rw,
+__device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, uint32_t i, uint32_t cur, const uint8_t* rw,
                                                                   const uint32_t* B, uint32_t (&out)[5], uint3& a3c) {
   const uint32_t l = lane(), C = d.C, W = d.W;
-  const uint32_t p = (i + 1 == C) ? 0 : i + 1;
+  const uint32_t p = (cur + 1 == C) ? 0 : cur + 1;
   const uint32_t a0 = p & ~15u;
   uint32_t K[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
   uint32_t anc = 0, nbytes = 0;                   // ancient candidates in the scanned address-order prefix
@@ -366,7 +367,7 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
     // for all of them instead of one per dependent use)
     const uint8_t alive = d.alive[i];
     const int32_t sr = d.start_round[i];
-    const uint32_t n_in = d.n[i], fn_in = d.flog_n[i];
+    const uint32_t n_in = d.n[i], fn_in = d.flog_n[i], cur = d.a3cur[i];
     const Susp sl_in = l < SLOTS ? d.susp[(size_t)i * SLOTS + l] : Susp{0, 0, 0, 0};
     if (!alive) {
       if (l == 0) { pb.nresp[i] = 0; pb.paysum[i] = 0; }
@@ -505,7 +506,7 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
     __builtin_amdgcn_wave_barrier();
     // ---- (2) A3 candidates ----
     uint32_t top[5];
-    w_bytes += a3_scan<LDSB>(d, i, rw, B, top, a3c);
+    w_bytes += a3_scan<LDSB>(d, i, cur, rw, B, top, a3c);
     if (l < 10) ro.part[(size_t)i * 10 + l] = l < 5 ? (l == 0 ? top[0] : l == 1 ? top[1] : l == 2 ? top[2] : l == 3 ? top[3] : top[4]) : 0xFFFFFFFFu;
     // ---- (3) write back the changed segments of the bitset ----
     if (LDSB && segs) {
@@ -542,24 +543,28 @@ __device__ inline uint32_t mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
-// The keyed permutation of [0, n): a 4-round Feistel network on the smallest even
-// bit width b >= 2 with 2^b >= n, cycle-walked into [0, n).  Prp holds what depends on (n, key) only.
-struct Prp { uint32_t n, h, mask, k[4]; };
+// The keyed permutation of [0, n): a 4-round Feistel network on b = max(2, ceil(log2 n))
+// bits, halves of ceil(b/2) (high, mask ma) and floor(b/2) (low, mask mc) bits whose widths swap every
+// round, cycle-walked into [0, n): at least half of every walk step lands in range.  Prp holds what
+// depends on (n, key) only.
+struct Prp { uint32_t n, c, ma, mc, k[4]; };
 __device__ inline Prp prp_make(uint32_t n, const U4& key) {
   const uint32_t lg = n <= 1 ? 0u : 32u - __clz(n - 1u);        // ceil(log2 n)
-  const uint32_t b = lg < 2 ? 2u : (lg + 1u) & ~1u;
+  const uint32_t b = lg < 2 ? 2u : lg;
   Prp p;
-  p.n = n; p.h = b / 2; p.mask = (1u << p.h) - 1u;
+  p.n = n; p.c = b / 2; p.mc = (1u << p.c) - 1u; p.ma = (1u << (b - p.c)) - 1u;
   p.k[0] = key.x; p.k[1] = key.y; p.k[2] = key.z; p.k[3] = key.w;
   return p;
 }
-__device__ __attribute__((always_inline)) inline uint32_t prp_eval(uint32_t x, const Prp& p) {
-  do {
-    uint32_t L = x >> p.h, R = x & p.mask;
+// one Feistel pass over x (4 rounds; the XORed half is a bits wide in rounds 0 and 2, c bits in 1 and 3)
+__device__ __attribute__((always_inline)) inline uint32_t prp_pass(uint32_t x, const Prp& p) {
+  uint32_t L = x >> p.c, R = x & p.mc;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { const uint32_t t = R; R = L ^ (mix32(R ^ p.k[k]) & p.mask); L = t; }
-    x = (L << p.h) | R;
-  } while (x >= p.n);
+  for (int k = 0; k < 4; ++k) { const uint32_t t = R; R = L ^ (mix32(R ^ p.k[k]) & ((k & 1) ? p.mc : p.ma)); L = t; }
+  return (L << p.c) | R;
+}
+__device__ __attribute__((always_inline)) inline uint32_t prp_eval(uint32_t x, const Prp& p) {
+  do { x = prp_pass(x, p); } while (x >= p.n);
   return x;
 }
 __device__ __attribute__((always_inline)) inline uint32_t prp_walk(uint32_t x, uint32_t n, const U4& key) {
@@ -636,10 +641,7 @@ __device__ __attribute__((always_inline)) inline void sampled_fill(uint32_t* pay
   uint32_t m = 0, x = k_first;
   while (__ballot(m < mcount)) {
     if (m < mcount) {
-      uint32_t L = x >> P.h, R = x & P.mask;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) { const uint32_t t = R; R = L ^ (mix32(R ^ P.k[k]) & P.mask); L = t; }
-      x = (L << P.h) | R;
+      x = prp_pass(x, P);
       if (x < P.n) {
 #pragma unroll
         for (int q = 0; q < RESP_KMAX; ++q) if ((uint32_t)q == m) y[q] = x;

@@ -126,7 +126,7 @@ __global__ void k_set_cap(Dev d, const uint32_t* nresp, uint32_t* cap, uint32_t*
 __global__ void k_init_nodes(Dev d, uint32_t n0) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.C) return;
-  if (local(d, i)) d.last_bcast[i] = NONE_ROUND;
+  if (local(d, i)) { d.last_bcast[i] = NONE_ROUND; d.a3cur[i] = i; }
   d.start_round[i] = NONE_ROUND;
   if (i < n0) node_start(d, i, 0);
 }
@@ -164,7 +164,7 @@ __global__ void k_init_converged_nodes(Dev d, uint32_t n0) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.C) return;
   const bool loc = local(d, i);
-  if (loc) d.last_bcast[i] = NONE_ROUND;
+  if (loc) { d.last_bcast[i] = NONE_ROUND; d.a3cur[i] = i; }
   d.start_round[i] = NONE_ROUND;
   if (i >= n0) return;
   d.alive[i] = 1; d.start_round[i] = 0;
@@ -496,7 +496,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
 #define AR(ptr, n) if (e == hipSuccess) e = ralloc(s, &(ptr), (n))   // row tables: n entries per local row
   AR(d.stamp, W); AR(d.bits, d.NWR); AR(d.segp, NSEG); AR(d.sdirty, 1);
   AR(d.dirty, 1); A(d.alive, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
-  AR(d.last_bcast, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
+  AR(d.last_bcast, 1); AR(d.a3cur, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
   AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
   A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
@@ -931,20 +931,23 @@ static int step_round(kb_sim* s) {
       k_kp_group<true><<<ks * groups, 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
     }
     k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc, r);   // + the KPR oversize probe
-    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 24, st));
+    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 40, st));
     k_proc_fast<<<gnode, tb, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
     // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
     // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
     // on the late waves with few nodes.
     k_proc<<<std::min<uint32_t>(4096, 2 * s->ncu), 256, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
     if (s->debug_waves) {
-      uint32_t dbg[6], slow = 0;
-      HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 24, hipMemcpyDeviceToHost, st));
+      uint32_t dbg[10], slow = 0;
+      HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 40, hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(&slow, d.ctr + C_SLOW, 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       fprintf(stderr, "[kb] round %d wave %u: k_proc nodes %u, prologue inserts %u, fingerprint refreshes %u (max per "
               "node %u), KPR scans %u (log entries %u), incremental bases %u\n", r, w, slow, dbg[0], dbg[1], dbg[2], dbg[3],
               dbg[4], dbg[5]);
+      if (d.dev & 64)
+        fprintf(stderr, "[kb] round %d wave %u: k_proc node time sum %.1f us (max %.1f), take_base %.1f, insertions %.1f\n",
+                r, w, dbg[6] * 0.01, dbg[7] * 0.01, dbg[8] * 0.01, dbg[9] * 0.01);
     }
     cur ^= 1;
   }

@@ -692,6 +692,9 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
   unsigned long long w_over = 0, w_curovf = 0;      // flushed once per wave (see k_phaseB)
   for (uint32_t it = blockIdx.x * 4 + wv; it < nact; it += gridDim.x * 4) {
     const uint32_t i = list[it];
+    const bool tdbg = (d.dev & 64) != 0;                // timing breakdown (KB_DEV=64, KB_DEBUG_WAVES)
+    const uint64_t t_node = tdbg ? wall_clock64() : 0;
+    uint64_t t_base = 0, t_ins = 0;
     uint8_t* rw = row_of(d, i);
     const uint32_t* bw = bits_of(d, i);
     uint32_t n = d.n[i], fp = d.fp[i], oseq = 0, pay_used = 0, fn = d.flog_n[i];
@@ -807,7 +810,10 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           const bool ins = gl != 0xFFFFFFFFu && !pre_was && lm.sender != (l == 0 ? last_sender : prev);
           const unsigned long long insm = __ballot(ins);
           if (d.uniform && insm) {
+            const uint64_t ta = tdbg ? wall_clock64() : 0;
             if (!inc) take_base();
+            const uint64_t tb = tdbg ? wall_clock64() : 0;
+            t_base += tb - ta;
             const uint8_t* hb = reinterpret_cast<const uint8_t*>(bw);
             if (__popcll(insm) >= 8) {              // many: one insertion per lane
               if (ins) {
@@ -847,6 +853,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
                 if (l == (uint32_t)q) Kx = K;
               }
             }
+            if (tdbg) t_ins += wall_clock64() - tb;
           }
         }
         g = bcast(mine, (int)(t & 63));
@@ -1027,6 +1034,11 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       d.n[i] = n; d.fp[i] = fp; d.dirty[i] = dirty ? 1 : 0; d.flog_n[i] = fn; d.kpr_big[i] = kbig;
       ob.cnt[i] = oseq;
       wave_ctr_clear(wc, i);
+      if (tdbg) {
+        const uint32_t tn = (uint32_t)(wall_clock64() - t_node);
+        atomicAdd(&d.ctr[C_DBG_TNODE], tn); atomicMax(&d.ctr[C_DBG_TMAX], tn);
+        atomicAdd(&d.ctr[C_DBG_TBASE], (uint32_t)t_base); atomicAdd(&d.ctr[C_DBG_TINS], (uint32_t)t_ins);
+      }
       if (dbg_fp) { atomicAdd(&d.ctr[C_DBG_FP], dbg_fp); atomicMax(&d.ctr[C_DBG_MAXFP], dbg_fp); }
       if (dbg_ins) atomicAdd(&d.ctr[C_DBG_INS], dbg_ins);
       if (dbg_kpr) { atomicAdd(&d.ctr[C_DBG_KPR], dbg_kpr); atomicAdd(&d.ctr[C_DBG_KPRLOG], dbg_log); }

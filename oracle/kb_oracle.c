@@ -87,6 +87,7 @@ struct kbo_sim {
   uint32_t* fp;
   uint8_t* dirty;
   int32_t* last_bcast;
+  uint32_t* a3cur;            /* A3's rotation base: the node's last ping target */
   osusp* susp;                /* C x SLOTS */
   ocur* cur;                  /* C x CSLOTS */
   uint32_t* paq; uint32_t* paq_n;
@@ -325,6 +326,7 @@ static void node_start(kbo_sim* s, uint32_t i, int32_t r) {
   s->last_bcast[i] = INT32_MIN;             /* last_broadcast_time: None                    :170 */
   memset(s->cur + (size_t)i * CSLOTS, 0, sizeof(ocur) * CSLOTS);   /* fresh KaboodleInner     */
   s->paq_n[i] = 0;
+  s->a3cur[i] = i;                          /* A3 rotation starts right after self */
 }
 static void node_stop(kbo_sim* s, uint32_t i) {
   map_remove(s, i, i);                      /* known_peers.remove(&self_addr)   src/lib.rs:167-170 */
@@ -354,7 +356,7 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   s->stamp = (uint8_t*)calloc(C * C, 1);
   s->alive = (uint8_t*)calloc(C, 1); s->ever = (uint8_t*)calloc(C, 1);
   s->start_round = (int32_t*)calloc(C, 4); s->n = (uint32_t*)calloc(C, 4); s->fp = (uint32_t*)calloc(C, 4);
-  s->dirty = (uint8_t*)calloc(C, 1); s->last_bcast = (int32_t*)calloc(C, 4);
+  s->dirty = (uint8_t*)calloc(C, 1); s->last_bcast = (int32_t*)calloc(C, 4); s->a3cur = (uint32_t*)calloc(C, 4);
   s->susp = (osusp*)calloc(C * SLOTS, sizeof(osusp)); s->cur = (ocur*)calloc(C * CSLOTS, sizeof(ocur));
   s->paq = (uint32_t*)calloc(C * PAQ, 4); s->paq_n = (uint32_t*)calloc(C, 4);
   s->ident = (uint8_t*)calloc(C * MAXID, 1); s->id_len = (uint8_t*)calloc(C, 1);
@@ -393,7 +395,7 @@ int kbo_sim_destroy(kbo_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
   for (uint32_t i = 0; i < s->C; ++i) free(s->out[i].v);
   free(s->stamp); free(s->lat); free(s->alive); free(s->ever); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
-  free(s->last_bcast); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len);
+  free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
   for (size_t k = 0; k < s->nwatch; ++k) free(s->wsnap[k]);
   free(s->wnode); free(s->wsnap); free(s->wfp);
@@ -426,20 +428,22 @@ static int should_respond(kbo_sim* s, uint32_t i, uint32_t joiner, int32_t r) {
   return (int64_t)o_mulhi(u, 100) < pct;
 }
 
-/* Keyed permutation of [0, n): 4-round Feistel network on the smallest even bit width b with 2^b >= n,
- * round function lowbias32(R ^ key[k]) masked to b/2 bits, cycle-walked into [0, n). */
+/* Keyed permutation of [0, n): 4-round Feistel network on b = max(2, ceil(log2 n))
+ * bits, halves of ceil(b/2) (high) and floor(b/2) (low) bits whose widths swap every round, round
+ * function lowbias32(R ^ key[k]) masked to the width of the half it is XORed into, cycle-walked into
+ * [0, n). */
 static inline uint32_t o_mix32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
 static uint32_t prp_walk(uint32_t x, uint32_t n, const uint32_t key[4]) {
   uint32_t b = 2;
-  while ((1ull << b) < n) b += 2;
-  const uint32_t h = b / 2, mask = (1u << h) - 1u;
+  while ((1ull << b) < n) b += 1;
+  const uint32_t c = b / 2, a = b - c;
   do {
-    uint32_t L = x >> h, R = x & mask;
-    for (int k = 0; k < 4; ++k) { uint32_t t = R; R = L ^ (o_mix32(R ^ key[k]) & mask); L = t; }
-    x = (L << h) | R;
+    uint32_t L = x >> c, R = x & ((1u << c) - 1u), wl = a;
+    for (int k = 0; k < 4; ++k) { uint32_t t = R; R = L ^ (o_mix32(R ^ key[k]) & ((1u << wl) - 1u)); L = t; wl = b - wl; }
+    x = (L << c) | R;
   } while (x >= n);
   return x;
 }
@@ -502,8 +506,8 @@ static void phase_broadcasts(kbo_sim* s, uint32_t i, int32_t r) {
 /* ---- tick (src/kaboodle.rs:746-779) -------------------------------------------------------------- */
 typedef struct { uint32_t fail_peers[SLOTS]; int nfail; int join; } otick_bc;
 
-static inline uint32_t rot_key(uint32_t j, uint32_t i, uint32_t C) {  /* rotated address order from self+1 */
-  return (j + C - i - 1) % C;
+static inline uint32_t rot_key(uint32_t j, uint32_t base, uint32_t C) {  /* rotated address order from base+1 */
+  return (j + C - base - 1) % C;
 }
 
 static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
@@ -566,13 +570,14 @@ static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
       s->st.removed_timeout += (uint64_t)nrem;
     }
   }
-  /* A3 ping_random_peer (:655-703): oldest 5 by (stamp, rotated id), one uniformly */
+  /* A3 ping_random_peer (:655-703): oldest 5 by (stamp, id rotated to start after the node's last
+     target), one uniformly; the target becomes the next rotation base */
   {
     uint32_t best[NUM_CANDIDATES]; uint32_t bkey_hi[NUM_CANDIDATES], bkey_lo[NUM_CANDIDATES]; int nb = 0;
     for (uint32_t j = 0; j < s->C; ++j) {
       uint8_t b = rw[j];
       if (b < ST_ANCIENT || j == i) continue;
-      uint32_t kh = b, kl = rot_key(j, i, s->C);
+      uint32_t kh = b, kl = rot_key(j, s->a3cur[i], s->C);
       if (nb == NUM_CANDIDATES && (kh > bkey_hi[nb - 1] || (kh == bkey_hi[nb - 1] && kl > bkey_lo[nb - 1]))) continue;
       int pos = nb < NUM_CANDIDATES ? nb : NUM_CANDIDATES - 1;
       while (pos > 0 && (bkey_hi[pos - 1] > kh || (bkey_hi[pos - 1] == kh && bkey_lo[pos - 1] > kl))) {
@@ -584,6 +589,7 @@ static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
     if (nb > 0) {
       uint32_t u = ph(s, i, (uint32_t)r, (uint32_t)P_PING << 24, 0).v[0];
       uint32_t t = best[o_mulhi(u, (uint32_t)nb)];
+      s->a3cur[i] = t;
       if (set_suspect(s, i, t, SK_WFP, r) != KB_OK) return KB_CAPACITY;
       emit(s, i, t, K_PING, 0, 0, 0, NULL, 0);
     }

@@ -46,17 +46,20 @@ def mix32(x):
 
 
 def prp_walk(x, n, key):
-    """x-th image of the keyed permutation of [0, n) (4-round Feistel, cycle walking)"""
+    """x-th image of the keyed permutation of [0, n): a 4-round Feistel network on b = max(2, ceil(log2 n))
+    bits, halves of ceil(b/2) (high) and floor(b/2) (low) bits whose widths swap every round, round
+    function lowbias32(R ^ key[k]) masked to the width of the half it is XORed into, cycle walking."""
     b = 2
     while (1 << b) < n:
-        b += 2
-    h = b // 2
-    mask = (1 << h) - 1
+        b += 1
+    c = b // 2
+    a = b - c
     while True:
-        L, R = x >> h, x & mask
+        L, R, wl = x >> c, x & ((1 << c) - 1), a
         for k in range(4):
-            L, R = R, L ^ (mix32(R ^ key[k]) & mask)
-        x = (L << h) | R
+            L, R = R, L ^ (mix32(R ^ key[k]) & ((1 << wl) - 1))
+            wl = b - wl
+        x = (L << c) | R
         if x < n:
             return x
 
@@ -95,6 +98,7 @@ class Peer:
         self.start_round = None
         self.known = {}          # peer -> [state, instant]
         self.latency = {}        # peer -> PeerInfo.latency in ms (absent = None)
+        self.a3cur = i           # A3's rotation base: the last ping target
         self.curious = {}        # peer -> [observers]
         self.last_bcast = None
         self.paq = []
@@ -152,6 +156,7 @@ class PyMesh:
         if i not in p.known:
             p.latency.pop(i, None)
         p.known[i] = [KNOWN, r]
+        p.a3cur = i
         p.last_bcast = None
         p.curious = {}
         p.paq = []
@@ -330,10 +335,11 @@ class PyMesh:
             self.stats["removed_timeout"] += 1
         # ping_random_peer :655-703
         c = [q for q, (st, _) in p.known.items() if st == KNOWN and q != p.id]
-        c.sort(key=lambda q: (stamp_key(p.known[q][1], r), (q - p.id - 1) % self.C))
+        c.sort(key=lambda q: (stamp_key(p.known[q][1], r), (q - p.a3cur - 1) % self.C))
         c = c[:NUM_CANDIDATES]
         if c:
             t = c[mulhi(self.ph(p.id, r, P_PING << 24, 0)[0], len(c))]
+            p.a3cur = t
             p.known[t] = [WFP, r]
             self.emit(p.id, t, "Ping")
         for a in p.paq:                                   # :550-556

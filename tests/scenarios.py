@@ -39,6 +39,8 @@ SCENARIOS = [
                             churn=0.01), 140),
     _sc("waves2", SimConfig(capacity=40, initial_nodes=40, seed=13, loss=0.03, max_waves=2), 15),
     _sc("trunc_join", SimConfig(capacity=700, initial_nodes=700, seed=21), 3),
+    # Join responses truncated from views of ~1200 ids: an odd permutation width (11 bits)
+    _sc("trunc_odd", SimConfig(capacity=1300, initial_nodes=1200, init_mode=KB_INIT_CONVERGED, churn=0.01, seed=23), 3),
 ]
 
 BY_NAME = {s["name"]: s for s in SCENARIOS}

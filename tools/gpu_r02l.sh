@@ -1,0 +1,14 @@
+#!/bin/bash
+# full GPU suite, quick perf in both modes, k_proc timing breakdown
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+OUT=gpurun_out/${1:-r02l}; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 280 --timeout-method thread --durations=15 \
+  > $OUT/pytest.log 2>&1
+rc=$?; grep -E "passed|failed" $OUT/pytest.log | tail -2; [ $rc -eq 0 ] || { grep -E "FAILED|Error|assert" $OUT/pytest.log | head -20; exit $rc; }
+timeout -k 10 120 python3 tools/quick_perf.py 65536 20 sim lat > $OUT/quick_sim.log 2>&1 || { tail -20 $OUT/quick_sim.log; exit 1; }
+timeout -k 10 120 python3 tools/quick_perf.py 65536 20 sock lat > $OUT/quick_sock.log 2>&1 || { tail -20 $OUT/quick_sock.log; exit 1; }
+grep N= $OUT/quick_*.log
+KB_DEV=64 KB_DEBUG_WAVES=1 timeout -k 10 120 python3 tools/quick_perf.py 65536 12 sim lat > $OUT/dbgwaves_sim.log 2>&1 || { tail -20 $OUT/dbgwaves_sim.log; exit 1; }
+grep "round 12 " $OUT/dbgwaves_sim.log
