@@ -28,6 +28,7 @@ enum CtrIdx {
   C_LASTALIVE, C_DBG_INS, C_DBG_FP, C_DBG_MAXFP,
   C_DBG_KPR, C_DBG_KPRLOG, C_DBG_BASE,   // KB_DEBUG_WAVES: full KPR reply scans, log entries read, take_base
   C_DBG_TNODE, C_DBG_TMAX, C_DBG_TBASE, C_DBG_TINS,   // KB_DEV & 64: k_proc wall time (10 ns ticks) per part
+  C_DBG_TSTART, C_DBG_TEND, C_DBG_MSGS,
   C_TICK,
   C_PATHS,                        // OR of the PATH_* bits of the kernel variants that did work (test surface)
   NCTR

@@ -19,7 +19,7 @@ __global__ void k_rebase(Dev d) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         uint32_t b = (x >> (8 * t)) & 0xFF;
-        if (b > ST_ANCIENT) { b = b - EPOCH > ST_ANCIENT ? b - EPOCH : ST_ANCIENT; any = true; }
+        if (b > ST_ANCIENT) { b = b > ST_ANCIENT + EPOCH ? b - EPOCH : ST_ANCIENT; any = true; }   // unsigned: no b - EPOCH < 0
         y |= b << (8 * t);
       }
       w[q] = y;

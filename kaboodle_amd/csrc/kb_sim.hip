@@ -931,23 +931,24 @@ static int step_round(kb_sim* s) {
       k_kp_group<true><<<ks * groups, 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
     }
     k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc, r);   // + the KPR oversize probe
-    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 40, st));
+    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
     k_proc_fast<<<gnode, tb, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
     // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
     // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
     // on the late waves with few nodes.
     k_proc<<<std::min<uint32_t>(4096, 2 * s->ncu), 256, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
     if (s->debug_waves) {
-      uint32_t dbg[10], slow = 0;
-      HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 40, hipMemcpyDeviceToHost, st));
+      uint32_t dbg[13], slow = 0;
+      HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(&slow, d.ctr + C_SLOW, 4, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
       fprintf(stderr, "[kb] round %d wave %u: k_proc nodes %u, prologue inserts %u, fingerprint refreshes %u (max per "
               "node %u), KPR scans %u (log entries %u), incremental bases %u\n", r, w, slow, dbg[0], dbg[1], dbg[2], dbg[3],
               dbg[4], dbg[5]);
       if (d.dev & 64)
-        fprintf(stderr, "[kb] round %d wave %u: k_proc node time sum %.1f us (max %.1f), take_base %.1f, insertions %.1f\n",
-                r, w, dbg[6] * 0.01, dbg[7] * 0.01, dbg[8] * 0.01, dbg[9] * 0.01);
+        fprintf(stderr, "[kb] round %d wave %u: k_proc node time sum %.1f us (max %.1f), take_base %.1f, insertions %.1f, "
+                "start %.1f, end %.1f, messages %u\n", r, w, dbg[6] * 0.01, dbg[7] * 0.01, dbg[8] * 0.01, dbg[9] * 0.01,
+                dbg[10] * 0.01, dbg[11] * 0.01, dbg[12]);
     }
     cur ^= 1;
   }

@@ -276,8 +276,10 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
   __shared__ unsigned long long s_segs;
   __shared__ uint32_t s_add, s_nl;
   __shared__ uint32_t s_list[BIG ? 1024 : 256];
+  __shared__ uint32_t ztab[BIG ? ZT * 128 : 1];
   const uint32_t t = threadIdx.x, T = blockDim.x;
   const uint32_t nact = d.ctr[C_ACTIVE];
+  if (BIG) load_ztab(d, ztab);
   const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
   const bool lds = BIG && d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM);
   const uint32_t kpb = (d.dbg & KB_DBG_KP_BIG_SMALL) ? 0u : KP_BIG;
@@ -371,11 +373,30 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     if (added) atomicAdd(&s_add, added);
     __syncthreads();
     const unsigned long long sg = s_segs;
+    unsigned long long refolded = 0;
     if (lds && sg) {                                   // write back the changed segments of the bitset
       const uint32_t wps4 = d.SEGW / 128;
       const uint4* B4 = reinterpret_cast<const uint4*>(B);
       uint4* g4 = reinterpret_cast<uint4*>(gB);
       for (uint32_t w = w0 / 4 + t; w < w1 / 4; w += T) if ((sg >> (w / wps4)) & 1ull) g4[w] = B4[w - w0 / 4];
+      if (d.uniform) {
+        // and refold their checkpoints from the staged bitset, a wave per segment (a joiner's group
+        // changes every segment of its row: its fingerprint is then a combine, not a 64-segment refold
+        // on k_proc's critical path)
+        const uint8_t* hb = reinterpret_cast<const uint8_t*>(B);   // byte of 8-id block h at h - 4 w0
+        const uint32_t nh = d.SEGW / 8, nwv = T >> 6, wv = t >> 6, l = lane();
+        uint32_t q = 0;
+        for (unsigned long long m = sg; m; m &= m - 1, ++q) {
+          if (q % nwv != wv) continue;
+          const uint32_t k = (uint32_t)(__ffsll((long long)m) - 1);
+          uint32_t raw = 0, cnt = 0;
+          const uint32_t h0 = k * nh + (l * nh) / 64, h1 = k * nh + ((l + 1) * nh) / 64;
+          for (uint32_t h = h0; h < h1; ++h) fold_half(d, ztab, h, hb[h - 4 * w0], raw, cnt);
+          wave_combine(d, raw, cnt);
+          if (l == 0) d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt);
+        }
+        refolded = sg;
+      }
     }
     if (t < SLOTS) {                                   // a prologue overwrote a WaitingFor* entry to Known
       Susp* sl = d.susp + (size_t)i * SLOTS + t;
@@ -387,7 +408,8 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     }
     if (t == 0 && (s_add || sg)) {
       if (KS > 1) atomicAdd(&d.n[i], s_add); else d.n[i] += s_add;
-      mark(d, i, sg);
+      if (refolded) { atomicAnd(&d.sdirty[i], ~refolded); d.dirty[i] = 1; }   // checkpoints fresh, fp stale
+      else mark(d, i, sg);
     }
     if (BIG && t == 0 && li == 0) path_hit(d, lds ? PATH_KP_BIG_LDS : PATH_KP_BIG_HBM);
     __syncthreads();                                   // LDS reused by the next destination
@@ -730,7 +752,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     // node, s_suf).  Each batch precomputes K = B·(Z ⊕ 1) ⊕ c_x·Z^{n>x} lane-parallel; the in-order
     // update is then one multiply by Z per insertion.
     bool inc = false, fpstale = false;
-    uint32_t R = 0;
+    uint32_t R = 0, zf = 0, zf_n = 0;   // zf: lane k holds zfin[zf_n + k] (the node's next counts)
     auto take_base = [&]() __attribute__((always_inline)) {
       if (need_sync) { wave_mem_sync(); need_sync = false; }
       dbg_base++;
@@ -765,10 +787,16 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       if (l == 0 && sd) atomicAnd(&d.sdirty[i], ~sd);
       segs = 0;
       inc = true; dirty = false; fpstale = true;
+      zf_n = n;
+      zf = d.zfin[n + l <= d.C + 1 ? n + l : d.C + 1];
     };
     auto fp_now = [&]() __attribute__((always_inline)) -> uint32_t {
       if (inc) {
-        if (fpstale) { fp = R ^ d.zfin[n] ^ 0xFFFFFFFFu; fpstale = false; }
+        if (fpstale) {
+          const uint32_t dz = n - zf_n;                 // insertions since the base: prefetched Z^n term
+          fp = R ^ (dz < 64 ? __builtin_amdgcn_readlane(zf, (int)dz) : d.zfin[n]) ^ 0xFFFFFFFFu;
+          fpstale = false;
+        }
         return fp;
       }
       if (dirty) {
@@ -793,6 +821,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     // the prefetched state of a later message of the batch is still current when it is reached.
     Msg lm;
     uint32_t pre_was = 0, pre_b = 0, Kx = 0;
+    const uint64_t t_loop = tdbg ? wall_clock64() : 0;
     for (uint32_t t = 0; t < icnt; ++t) {
       uint32_t g;
       if (sorted) {
@@ -802,7 +831,8 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           if (gl != 0xFFFFFFFFu) {
             lm = ib.msgs[gl];
             pre_was = (bw[lm.sender >> 5] >> (lm.sender & 31)) & 1u;
-            pre_b = pre_was ? rw[lm.sender] : ST_UNKNOWN;
+            const uint32_t sb = rw[lm.sender];         // issued with the bit load, not after it
+            pre_b = pre_was ? sb : ST_UNKNOWN;
           }
           if (!small) mine = gl;
           // insertions of this batch: first message of a sender run whose sender is not a member
@@ -1026,6 +1056,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
         default: break;
       }
     }
+    const uint64_t t_after = tdbg ? wall_clock64() : 0;
     if (l < SLOTS) d.susp[(size_t)i * SLOTS + l] = s_susp[wv][l];
     if (l < CSLOTS) d.cur[(size_t)i * CSLOTS + l] = s_cur[wv][l];
     if (inc) fp_now();                              // exact: the touched checkpoints stay marked stale
@@ -1038,6 +1069,8 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
         const uint32_t tn = (uint32_t)(wall_clock64() - t_node);
         atomicAdd(&d.ctr[C_DBG_TNODE], tn); atomicMax(&d.ctr[C_DBG_TMAX], tn);
         atomicAdd(&d.ctr[C_DBG_TBASE], (uint32_t)t_base); atomicAdd(&d.ctr[C_DBG_TINS], (uint32_t)t_ins);
+        atomicAdd(&d.ctr[C_DBG_TSTART], (uint32_t)(t_loop - t_node)); atomicAdd(&d.ctr[C_DBG_TEND], (uint32_t)(wall_clock64() - t_after));
+        atomicAdd(&d.ctr[C_DBG_MSGS], icnt);
       }
       if (dbg_fp) { atomicAdd(&d.ctr[C_DBG_FP], dbg_fp); atomicMax(&d.ctr[C_DBG_MAXFP], dbg_fp); }
       if (dbg_ins) atomicAdd(&d.ctr[C_DBG_INS], dbg_ins);

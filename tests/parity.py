@@ -227,6 +227,9 @@ def standard_cases() -> list[tuple[str, dict, int]]:
     # wave 0 (k_sort_inbox + k_proc's sorted path; with KB_DBG_PROC_UNSORTED the selection path)
     cases.append(("hot_inbox", {"cfg": SimConfig(capacity=256, initial_nodes=256, loss=0.02, seed=17),
                                 "events": {0: [("ping", i, [0]) for i in range(1, 201)]}}, 8))
+    # stamps from before round 0 (early joiners' KnownPeers inserts) crossing three window rebases
+    cases.append(("old_stamps", {"cfg": SimConfig(capacity=160, initial_nodes=128, init_mode=KB_INIT_CONVERGED, loss=0.02,
+                                                  churn=0.03, fault_end_round=12, seed=31)}, 200))
     return cases
 
 

@@ -41,6 +41,10 @@ SCENARIOS = [
     _sc("trunc_join", SimConfig(capacity=700, initial_nodes=700, seed=21), 3),
     # Join responses truncated from views of ~1200 ids: an odd permutation width (11 bits)
     _sc("trunc_odd", SimConfig(capacity=1300, initial_nodes=1200, init_mode=KB_INIT_CONVERGED, churn=0.01, seed=23), 3),
+    # early joiners' KnownPeers inserts are stamped before round 0 (Known(r - 10), r < 10); three stamp-window
+    # rebases later (rounds 64, 128, 192) they sit at the bottom of the window: the saturation edge of k_rebase
+    _sc("old_stamps", SimConfig(capacity=160, initial_nodes=128, init_mode=KB_INIT_CONVERGED, loss=0.02, churn=0.03,
+                                fault_end_round=12, seed=31), 200),
 ]
 
 BY_NAME = {s["name"]: s for s in SCENARIOS}

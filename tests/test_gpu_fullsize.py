@@ -117,3 +117,46 @@ def test_partition_heal_64k(split, upto):
     if upto == 24:
         st = split.g.stats()
         assert st["drop_partition"] > 0
+
+
+# ---- a long quiet tail: stamps age through many window rebases (k_rebase's saturation edge, the A3
+# ---- rotation base sweeping the ancient peers, timeouts of dead peers) -----------------------------
+LONG_N = 8192
+
+
+def _long_cfg(mode):
+    from kaboodle_amd._ffi import KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL
+    return SimConfig(capacity=LONG_N + 512, initial_nodes=LONG_N, init_mode=KB_INIT_CONVERGED, loss=0.01, churn=0.001,
+                     fault_end_round=25, seed=1,
+                     failed_mode=KB_FAILED_SOCKET_FAITHFUL if mode == "sock" else KB_FAILED_SIM_SENDER)
+
+
+@pytest.fixture(scope="module", params=["sock", "sim"])
+def long_tail(request):
+    import kaboodle_amd
+    kaboodle_amd.require_gpu()
+    cfg = _long_cfg(request.param)
+    o, g = Sim(parity.oracle_lib(omp=True), cfg), Sim(parity.gpu_lib(), cfg)
+    yield {"o": o, "g": g, "round": 0}
+    o.close()
+    g.close()
+
+
+@pytest.mark.parametrize("upto", [300, 600, 900, 1200])
+def test_long_tail_8k(long_tail, upto):
+    """configs[2]'s shape at 8K peers, both failed modes, 1200 rounds (18 window rebases): every stamp row,
+    fingerprint, scalar and counter equal the oracle's every 100 rounds."""
+    o, g = long_tail["o"], long_tail["g"]
+    while long_tail["round"] < upto:
+        o.step(100)
+        g.step(100)
+        long_tail["round"] += 100
+        r = long_tail["round"]
+        assert o.stats() == g.stats(), f"round {r}: counters"
+        assert np.array_equal(o.fingerprints(), g.fingerprints()), f"round {r}: fingerprints"
+        assert np.array_equal(o.scalars(), g.scalars()), f"round {r}: scalars"
+        ro, rg = o.rows(), g.rows()
+        if not np.array_equal(ro, rg):
+            bad = np.argwhere(ro != rg)
+            i, j = bad[0]
+            pytest.fail(f"round {r}: {len(bad)} stamp bytes differ, first node {i} peer {j}: {ro[i, j]} != {rg[i, j]}")
