@@ -70,7 +70,7 @@ struct Dev {
   uint32_t* n;
   uint32_t* fp;
   int32_t* last_bcast;
-  uint32_t* a3cur;                // A3's rotation base: the node's last ping target
+  uint32_t* a3cur;                // A3's rotation base: just before the last round's oldest candidate (§2.6)
   Susp* susp;
   Cur* cur;
   uint32_t* paq;

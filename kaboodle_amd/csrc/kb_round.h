@@ -248,8 +248,8 @@ constexpr uint32_t RP_LDS_BYTES = 81920;         // dynamic LDS per row-pass wor
 struct RowOut { uint32_t* part; };   // [C][10]: the five smallest keys ascending, then 0xFFFFFFFF x 5
 
 // A3 over the row of node i (members from B: LDS or HBM): the five smallest keys (stamp << 24 | rot),
-// ascending, in every lane; rot = address rotated to start right after `cur`, the node's last ping
-// target.  Returns the stamp bytes read.
+// ascending, in every lane; rot = address rotated to start right after `cur`, the node's sweep front
+// (DESIGN.md §2.6).  Returns the stamp bytes read.
 template <bool LDSB>
 __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, uint32_t i, uint32_t cur, const uint8_t* rw,
                                                                   const uint32_t* B, uint32_t (&out)[5], uint3& a3c) {

@@ -241,7 +241,9 @@ __global__ void k_tick_post(Dev d, RowOut ro, OutBuf ob, int32_t r) {
       const uint32_t u = philox(i, (uint32_t)r, (uint32_t)P_PING << 24, 0, d.k0, d.k1).x;
       const uint32_t rot = k5[mulhi(u, nc)] & 0xFFFFFFu;
       const uint32_t t = rot + p >= C ? rot + p - C : rot + p;
-      d.a3cur[i] = t;                               // the next round's rotation base
+      const uint32_t rot0 = k5[0] & 0xFFFFFFu;      // the sweep front: just before the oldest candidate
+      const uint32_t c1 = rot0 + p >= C ? rot0 + p - C : rot0 + p;
+      d.a3cur[i] = c1 == 0 ? C - 1 : c1 - 1;
       Susp* sl = d.susp + (size_t)i * SLOTS;
       int k = 0;
       while (k < SLOTS && sl[k].kind) ++k;

@@ -87,7 +87,7 @@ struct kbo_sim {
   uint32_t* fp;
   uint8_t* dirty;
   int32_t* last_bcast;
-  uint32_t* a3cur;            /* A3's rotation base: the node's last ping target */
+  uint32_t* a3cur;            /* A3's rotation base: just before the last round's oldest candidate (§2.6) */
   osusp* susp;                /* C x SLOTS */
   ocur* cur;                  /* C x CSLOTS */
   uint32_t* paq; uint32_t* paq_n;
@@ -570,8 +570,8 @@ static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
       s->st.removed_timeout += (uint64_t)nrem;
     }
   }
-  /* A3 ping_random_peer (:655-703): oldest 5 by (stamp, id rotated to start after the node's last
-     target), one uniformly; the target becomes the next rotation base */
+  /* A3 ping_random_peer (:655-703): oldest 5 by (stamp, id rotated to start at the node's sweep front),
+     one uniformly; the front moves to the oldest candidate */
   {
     uint32_t best[NUM_CANDIDATES]; uint32_t bkey_hi[NUM_CANDIDATES], bkey_lo[NUM_CANDIDATES]; int nb = 0;
     for (uint32_t j = 0; j < s->C; ++j) {
@@ -589,7 +589,7 @@ static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
     if (nb > 0) {
       uint32_t u = ph(s, i, (uint32_t)r, (uint32_t)P_PING << 24, 0).v[0];
       uint32_t t = best[o_mulhi(u, (uint32_t)nb)];
-      s->a3cur[i] = t;
+      s->a3cur[i] = (best[0] + s->C - 1) % s->C;
       if (set_suspect(s, i, t, SK_WFP, r) != KB_OK) return KB_CAPACITY;
       emit(s, i, t, K_PING, 0, 0, 0, NULL, 0);
     }

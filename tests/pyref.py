@@ -98,7 +98,7 @@ class Peer:
         self.start_round = None
         self.known = {}          # peer -> [state, instant]
         self.latency = {}        # peer -> PeerInfo.latency in ms (absent = None)
-        self.a3cur = i           # A3's rotation base: the last ping target
+        self.a3cur = i           # A3's rotation base: just before the last round's oldest candidate (§2.6)
         self.curious = {}        # peer -> [observers]
         self.last_bcast = None
         self.paq = []
@@ -339,7 +339,7 @@ class PyMesh:
         c = c[:NUM_CANDIDATES]
         if c:
             t = c[mulhi(self.ph(p.id, r, P_PING << 24, 0)[0], len(c))]
-            p.a3cur = t
+            p.a3cur = (c[0] - 1) % self.C           # the sweep front: just before the oldest candidate
             p.known[t] = [WFP, r]
             self.emit(p.id, t, "Ping")
         for a in p.paq:                                   # :550-556
