@@ -207,6 +207,38 @@ uint32_t kb_fingerprint_of_set(const uint32_t* ids, size_t n, const uint8_t* ide
 
 const char* kb_last_error(void);
 
+/* ---- wire codec: the datagrams of a real Kaboodle instance ----------------
+   bincode 1.3.3 (legacy `bincode::serialize` defaults) of src/structs.rs:65-116, so simulated nodes can be
+   bridged to real ones: SwimEnvelope on the unicast socket (src/kaboodle.rs:188-226, :394-403),
+   SwimBroadcast on the multicast socket (:256-311), ProbeResponse (:312-331, src/discovery.rs:30-89).
+   Addresses are IPv4 (SocketAddr::V4).  Identities are (offset, length) views: into `idents` when
+   encoding, into the datagram when decoding.  A datagram longer than 10240 B is truncated by the
+   receiver (INCOMING_BUFFER_SIZE, src/kaboodle.rs:43) and then fails to decode: the simulator's
+   oversize rule.                                                               */
+enum { KB_WIRE_PING = 0, KB_WIRE_PING_REQUEST = 1, KB_WIRE_ACK = 2, KB_WIRE_KNOWN_PEERS = 3,
+       KB_WIRE_KNOWN_PEERS_REQUEST = 4,              /* SwimMessage variants, in declaration order      */
+       KB_WIRE_JOIN = 16, KB_WIRE_FAILED = 17, KB_WIRE_PROBE = 18,   /* SwimBroadcast variants           */
+       KB_WIRE_PROBE_RESPONSE = 32 };
+enum { KB_WIRE_CHANNEL_UNICAST = 0, KB_WIRE_CHANNEL_BROADCAST = 1, KB_WIRE_CHANNEL_PROBE_RESPONSE = 2 };
+typedef struct kb_wire_addr { uint8_t ip[4]; uint16_t port; uint16_t pad; } kb_wire_addr;
+typedef struct kb_wire_entry { kb_wire_addr addr; uint32_t id_off, id_len; } kb_wire_entry;   /* KnownPeers */
+typedef struct kb_wire_msg {
+  uint32_t kind;                       /* KB_WIRE_*                                                     */
+  uint32_t identity_off, identity_len; /* envelope / Join / ProbeResponse identity                      */
+  kb_wire_addr peer;                   /* PingRequest(peer), Ack.peer, Join.addr, Failed, Probe         */
+  uint32_t fingerprint, num_peers;     /* Ack, KnownPeersRequest                                        */
+  uint32_t n_entries;                  /* KnownPeers                                                    */
+} kb_wire_msg;
+/* *size = the datagram's length; written to buf when cap suffices (buf = NULL: size query).          */
+int kb_wire_encode(const kb_wire_msg* m, const kb_wire_entry* entries, const uint8_t* idents, uint8_t* buf,
+                   size_t cap, size_t* size);
+/* channel: KB_WIRE_CHANNEL_*.  Malformed or truncated -> KB_INVALID_ARGUMENT.  KnownPeers entries are
+   stored up to cap (m->n_entries is always set; KB_CAPACITY when entries != NULL and cap is short).   */
+int kb_wire_decode(const uint8_t* buf, size_t len, int channel, kb_wire_msg* m, kb_wire_entry* entries, size_t cap);
+/* the simulator's canonical address of an id (kb_format_addr) and back (KB_INVALID_ARGUMENT: not one) */
+int kb_wire_addr_of_id(uint32_t id, kb_wire_addr* out);
+int kb_wire_id_of_addr(const kb_wire_addr* addr, uint32_t* id);
+
 /* ---- timing surface for bench.py ---------------------------------------------------------------- */
 /* HIP-event durations (ms, summed since last reset) of the round's kernels, recorded by the kernels'
    own dispatch packets on the stream they run on.  kind: KB_KT_*.                                   */

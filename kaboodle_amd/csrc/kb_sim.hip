@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <thread>
 #include "kb_common.h"
+#include "kb_wire.h"
 #include "kb_round.h"
 #include "kb_tick.h"
 #include "kb_waves.h"

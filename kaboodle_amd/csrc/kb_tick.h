@@ -168,56 +168,31 @@ __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
   const uint32_t* bw = bits_of(d, i);
   const uint32_t spp = NSEG / S;
   const unsigned long long sd = act ? d.sdirty[i] : 0ull;
-  // the segments of the split that any row of the wave needs, two at a time for the whole wave: two
-  // independent Horner chains per lane (their LDS table lookups and htab gathers overlap) while every
-  // lane still reads the same columns of htab (L1/L2 locality); lanes whose row does not need a
-  // segment fold it anyway and drop the result
-  const unsigned long long smask = spp == 64 ? ~0ull : ((1ull << spp) - 1ull);
-  const unsigned long long mine_m = (sd >> (s * spp)) & smask;
-  unsigned long long todo = ((unsigned long long)wave_or((uint32_t)(mine_m >> 32)) << 32) | wave_or((uint32_t)mine_m);
   unsigned long long folded = 0;
-  uint32_t nseg = 0;
-  while (todo) {                                    // wave-uniform
-    uint32_t k[2];
-    bool v[2];
+  uint32_t nbytes = 0;
+  for (uint32_t k = s * spp; k < (s + 1) * spp; ++k) {
+    const bool mine = (sd >> k) & 1ull;
+    if (!__ballot(mine)) continue;                  // wave-uniform: no row of this wave changed here
+    const uint32_t c0 = k * d.SEGW, c1 = c0 + d.SEGW;
+    uint32_t raw = 0, cnt = 0;
+    uint4 mb = *reinterpret_cast<const uint4*>(bw + (c0 >> 5));
+    for (uint32_t col = c0; col < c1; col += 128) {
+      const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
+      uint32_t hv[16];
+      const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const bool any = todo != 0;
-      const uint32_t kk = any ? (uint32_t)(__ffsll((long long)todo) - 1) : 0u;
-      todo &= todo - 1;
-      k[q] = s * spp + kk;
-      v[q] = any && ((mine_m >> kk) & 1ull);
-    }
-    uint32_t raw[2] = {0, 0}, cnt[2] = {0, 0};
-    uint4 mb[2];
-#pragma unroll
-    for (int q = 0; q < 2; ++q) mb[q] = *reinterpret_cast<const uint4*>(bw + ((k[q] * d.SEGW) >> 5));
-    for (uint32_t off = 0; off < d.SEGW; off += 128) {
-      uint32_t hv[2][16], mw[2][4];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const uint32_t col = k[q] * d.SEGW + off;
-        mw[q][0] = mb[q].x; mw[q][1] = mb[q].y; mw[q][2] = mb[q].z; mw[q][3] = mb[q].w;
-        const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
-#pragma unroll
-        for (int h = 0; h < 16; ++h) hv[q][h] = ht[h * 256 + ((mw[q][h >> 2] >> (8 * (h & 3))) & 0xFFu)];   // entry 0 is 0
-        if (off + 128 < d.SEGW) mb[q] = *reinterpret_cast<const uint4*>(bw + ((col + 128) >> 5));   // next step's bits
-      }
+      for (int h = 0; h < 16; ++h) hv[h] = ht[h * 256 + ((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu)];   // entry 0 is 0
+      if (col + 128 < c1) mb = *reinterpret_cast<const uint4*>(bw + ((col + 128) >> 5));   // next step's bits
 #pragma unroll
       for (int h = 0; h < 16; ++h) {
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const uint32_t c = __popc((mw[q][h >> 2] >> (8 * (h & 3))) & 0xFFu);   // Z^0 table is the identity
-          raw[q] = mulzb(zb, raw[q], c) ^ hv[q][h];
-          cnt[q] += c;
-        }
+        const uint32_t c = __popc((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu);   // Z^0 table is the identity
+        raw = mulzb(zb, raw, c) ^ hv[h];
+        cnt += c;
       }
     }
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-      if (v[q]) { d.segp[(size_t)i * NSEG + k[q]] = make_uint2(raw[q], cnt[q]); folded |= 1ull << k[q]; nseg++; }
+    if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; nbytes += d.SEGW / 8; }
   }
-  const uint32_t wb = wave_sum(act ? nseg * (d.SEGW / 8) : 0u);
+  const uint32_t wb = wave_sum(act ? nbytes : 0u);
   if (lane() == 0 && wb) atomicAdd(&d.stats[S_FOLDB], (unsigned long long)wb);
   if (folded) atomicAnd(&d.sdirty[i], ~folded);
 }
