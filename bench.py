@@ -85,8 +85,8 @@ def pmc_traffic(cfg_key: str, kernel: str, capacity: int):
 
 
 def committed_tail(cfg_key: str, mode: str):
-    """The full quiescent tail of this workload (tools/converge.py, run to agreement or 2N rounds on an
-    MI355X; profiles/*converge*.json): too long for the bench's minutes, so read from the record."""
+    """The full quiescent tail of this workload (tools/converge.py, run to agreement or a cap of 2-4 N rounds
+    on an MI355X; profiles/*converge*.json): too long for the bench's minutes, so read from the record."""
     best = None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*converge*.json"))):
         try:
@@ -97,10 +97,10 @@ def committed_tail(cfg_key: str, mode: str):
             best = {k: d[k] for k in ("converged_round", "tail_rounds_to_converge", "tail_rounds_run", "cap_rounds",
                                       "stopped_by") if k in d}
             best["source"] = os.path.relpath(p, ROOT)
-            if d.get("trajectory"):
-                last = d["trajectory"][-1]
-                best["final_agree_frac"] = last.get("agree_frac")
-                best["final_view_gap_mean"] = last.get("view_gap_mean")
+            samples = [t for t in d.get("trajectory", []) if "agree_frac" in t]
+            if samples:
+                best["final_agree_frac"] = samples[-1]["agree_frac"]
+                best["final_view_gap_mean"] = samples[-1]["view_gap_mean"]
     return best
 
 

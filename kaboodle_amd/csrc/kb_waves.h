@@ -596,13 +596,6 @@ __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc, int32_t 
 // `slow` list for k_proc (same semantics: prologue :406-415, Ping :513-532, PingRequest :533-545,
 // Ack :418-447, maybe_sync :707-740).
 constexpr uint32_t FAST_MAX = 8;
-__device__ __attribute__((always_inline)) inline void emit_t(const OutBuf& ob, const Dev& d, uint32_t i, uint32_t& oseq,
-                                                             uint32_t dest, uint32_t kind, uint32_t a, uint32_t fp,
-                                                             uint32_t n) {
-  if (oseq >= ob.cap[i] || ob.off[i] + oseq >= ob.msg_cap) set_err(d, DERR_OUTBOX);
-  else ob.msgs[ob.off[i] + oseq] = Msg{dest, i, oseq, kind, a, fp, n, 0};
-  oseq++;
-}
 __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r, uint32_t* slow) {
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint32_t it = blockIdx.x * blockDim.x + threadIdx.x;
@@ -636,7 +629,13 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
     to_slow = icnt && !fast;
     if (fast) {
       const uint32_t n = d.n[i], fp = d.fp[i];
+      const uint32_t ob_cap = ob.cap[i], ob_off = ob.off[i];   // this node's outbox region, loaded once
       uint32_t fn = d.flog_n[i], oseq = 0, last_sender = 0xFFFFFFFFu;
+      auto emit = [&](uint32_t dest, uint32_t kind, uint32_t a, uint32_t efp, uint32_t en) __attribute__((always_inline)) {
+        if (oseq >= ob_cap || ob_off + oseq >= ob.msg_cap) set_err(d, DERR_OUTBOX);
+        else ob.msgs[ob_off + oseq] = Msg{dest, i, oseq, kind, a, efp, en, 0};
+        oseq++;
+      };
       uint8_t* rw = row_of(d, i);
       Susp* sl = d.susp + (size_t)i * SLOTS;
       Cur* cu = d.cur + (size_t)i * CSLOTS;
@@ -653,7 +652,7 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
           last_sender = s;
         }
         if (m.kind == K_PING) {
-          emit_t(ob, d, i, oseq, s, K_ACK, i, fp, n);
+          emit(s, K_ACK, i, fp, n);
         } else if (m.kind == K_PINGREQ) {
           int e = -1;
           for (int j = 0; j < CSLOTS && e < 0; ++j) if (cu[j].used && cu[j].peer == m.a) e = j;
@@ -668,19 +667,19 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
             for (uint32_t q = 0; q < nobs; ++q) dup |= cu[e].obs[q] == s;
             if (!dup) { if (nobs == NOBS) curovf++; else { cu[e].obs[nobs] = s; cu[e].nobs = nobs + 1; } }
           }
-          emit_t(ob, d, i, oseq, m.a, K_PING, 0, 0, 0);
+          emit(m.a, K_PING, 0, 0, 0);
         } else if (m.kind == K_ACK) {
           int e = -1;
           for (int j = 0; j < CSLOTS && e < 0; ++j) if (cu[j].used && cu[j].peer == m.a) e = j;
           if (e >= 0) {
             const uint32_t nobs = cu[e].nobs;
-            for (uint32_t q = 0; q < nobs; ++q) emit_t(ob, d, i, oseq, cu[e].obs[q], K_ACK, m.a, m.fp, m.n);
+            for (uint32_t q = 0; q < nobs; ++q) emit(cu[e].obs[q], K_ACK, m.a, m.fp, m.n);
             cu[e].used = 0;
           }
-          if (fp != m.fp && !(n > m.n)) emit_t(ob, d, i, oseq, m.a, K_KPR, 0, fp, n);
+          if (fp != m.fp && !(n > m.n)) emit(m.a, K_KPR, 0, fp, n);
         } else if (m.kind == K_KPR) {                  // :473-512, reply lost as oversize (Q3), then :507
           over++;
-          if (fp != m.fp && !(n > m.n)) emit_t(ob, d, i, oseq, s, K_KPR, 0, fp, n);
+          if (fp != m.fp && !(n > m.n)) emit(s, K_KPR, 0, fp, n);
         }
       }
       ob.cnt[i] = oseq;
@@ -720,6 +719,15 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     uint8_t* rw = row_of(d, i);
     const uint32_t* bw = bits_of(d, i);
     uint32_t n = d.n[i], fp = d.fp[i], oseq = 0, pay_used = 0, fn = d.flog_n[i];
+    const uint32_t ob_cap = ob.cap[i], ob_off = ob.off[i];   // this node's outbox region, loaded once
+    auto emit = [&](uint32_t dest, uint32_t kind, uint32_t a, uint32_t efp, uint32_t en, uint32_t off)
+        __attribute__((always_inline)) {
+      if (l == 0) {
+        if (oseq >= ob_cap || ob_off + oseq >= ob.msg_cap) set_err(d, DERR_OUTBOX);
+        else ob.msgs[ob_off + oseq] = Msg{dest, i, oseq, kind, a, efp, en, off};
+      }
+      oseq++;
+    };
     int32_t kbig = d.kpr_big[i];
     bool dirty = d.dirty[i] != 0, need_sync = false;
     unsigned long long segs = 0;
@@ -811,7 +819,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     auto maybe_sync = [&](uint32_t peer, uint32_t their_fp, uint32_t their_n) __attribute__((always_inline)) {   // :707-740
       const uint32_t f = fp_now();
       if (f == their_fp || n > their_n) return;
-      emit_msg(ob, d, i, oseq, peer, K_KPR, 0, f, n, 0);
+      emit(peer, K_KPR, 0, f, n, 0);
     };
     uint32_t last_g = 0xFFFFFFFFu, last_sender = 0xFFFFFFFFu;
     // messages are fetched 64 at a time (lane k holds the record of message base + k) and handed to
@@ -934,7 +942,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       switch (m.kind) {
         case K_PING: {                                               // :513-532
           const uint32_t f = fp_now();
-          emit_msg(ob, d, i, oseq, s, K_ACK, i, f, n, 0);
+          emit(s, K_ACK, i, f, n, 0);
           break;
         }
         case K_PINGREQ: {                                            // :533-545
@@ -956,7 +964,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           }
           wait_lds();
           __builtin_amdgcn_wave_barrier();
-          emit_msg(ob, d, i, oseq, m.a, K_PING, 0, 0, 0, 0);
+          emit(m.a, K_PING, 0, 0, 0, 0);
           break;
         }
         case K_ACK: {                                                // :418-447
@@ -965,7 +973,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
             const int e = __ffsll((long long)hit) - 1;
             const uint32_t nobs = s_cur[wv][e].nobs;
             // the entry's observers stay in LDS until a later PingRequest reuses the slot: read in place
-            for (uint32_t q = 0; q < nobs; ++q) emit_msg(ob, d, i, oseq, s_cur[wv][e].obs[q], K_ACK, m.a, m.fp, m.n, 0);
+            for (uint32_t q = 0; q < nobs; ++q) emit(s_cur[wv][e].obs[q], K_ACK, m.a, m.fp, m.n, 0);
             wait_lds();
             __builtin_amdgcn_wave_barrier();
             if (l == 0) s_cur[wv][e].used = 0;
@@ -1049,7 +1057,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           if (d.uniform && total > d.capk + 1) kbig = r;
           over = d.uniform ? total > d.capk : size > (uint64_t)BUFSZ;
           if (over) w_over++;
-          else { emit_msg(ob, d, i, oseq, s, K_KP, total, 0, 0, poff); pay_used += total; }
+          else { emit(s, K_KP, total, 0, 0, poff); pay_used += total; }
           maybe_sync(s, m.fp, m.n);
           break;
         }

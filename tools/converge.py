@@ -74,6 +74,19 @@ def main() -> int:
                       f"mean view gap {traj[-1]['view_gap_mean']}, {time.time() - t0:.0f} s", flush=True)
         if conv is None:
             sample(m, r - 1)
+            # the few nodes still disagreeing: what their views lack or keep
+            sc = m.scalars()
+            live = np.nonzero(sc[:, 0] != 0)[0]
+            lset = set(int(x) for x in live)
+            tfp = m.true_fingerprint() if hasattr(m, "true_fingerprint") else None
+            fps = m.fingerprints()
+            bad = [int(i) for i in live if tfp is not None and fps[i] != tfp][:8]
+            for i in bad:
+                ids = set(m.peers(i)) if hasattr(m, "peers") else set()
+                extra, missing = sorted(ids - lset)[:10], sorted(lset - ids)[:10]
+                st = [e for e in m.peer_states(i) if e[0] in extra][:10] if hasattr(m, "peer_states") else []
+                print(f"[converge {a.mode}] node {i} disagrees: extra {extra} missing {missing} extra states {st}", flush=True)
+                traj.append({"round": r - 1, "node": i, "extra": extra, "missing": missing})
     out = {"workload": f"configs[2]: {n} peers, converged start, 1% loss, 0.1%/round churn, faults until round {F}",
            "failed_mode": "socket_faithful" if a.mode == "sock" else "sim_sender", "fault_end_round": F,
            "converged_round": conv, "tail_rounds_to_converge": None if conv is None else conv - F + 1,
