@@ -330,7 +330,6 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
 template <bool LDSB>
 __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, int32_t r, uint32_t lf, uint32_t lj) {
   extern __shared__ uint32_t pb_dyn[];
-  __shared__ uint32_t s_sp[RP_WAVES][SLOTS];
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t l = lane();
@@ -380,14 +379,27 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
     unsigned long long segs = 0;
     uint32_t nresp = 0;
     if (sr < r) {                                     // ---- (1) broadcast phase ----
-      if (l < SLOTS) s_sp[wv][l] = sl_in.kind ? sl_in.peer : 0xFFFFFFFFu;
+      // the node's suspects as wave-uniform values (most rows have none): is_susp is a few scalar
+      // compares per lane instead of eight LDS reads
+      const uint32_t spv = l < SLOTS && sl_in.kind ? sl_in.peer : 0xFFFFFFFFu;
+      const unsigned long long spm = __ballot(spv != 0xFFFFFFFFu);
+      uint32_t sp[SLOTS];
+#pragma unroll
+      for (int k = 0; k < SLOTS; ++k) sp[k] = __builtin_amdgcn_readlane(spv, k);
       wait_lds();
       __builtin_amdgcn_wave_barrier();
       auto mem = [&](uint32_t x) __attribute__((always_inline)) -> bool {
         const uint32_t w = LDSB ? B[x >> 5] : __hip_atomic_load(&B[x >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return (w >> (x & 31)) & 1u;
       };
-      auto is_susp = [&](uint32_t x) __attribute__((always_inline)) { bool f = false; for (int k = 0; k < SLOTS; ++k) f |= s_sp[wv][k] == x; return f; };
+      auto is_susp = [&](uint32_t x) __attribute__((always_inline)) {
+        bool f = false;
+        if (spm) {
+#pragma unroll
+          for (int k = 0; k < SLOTS; ++k) f |= sp[k] == x;
+        }
+        return f;
+      };
       uint32_t n = n_in;
       const uint32_t n0 = n;
       uint32_t fn = fn_in;
@@ -718,12 +730,10 @@ __device__ __attribute__((always_inline)) inline uint32_t block_prefix(const uin
 // workgroup at once, each with its own LDS slice (bitset, block prefix, joiners, suffix minima), and
 // only wave-level synchronisation.  Same arithmetic as k_resp_node's sampled path.
 constexpr uint32_t RW_JCAP = 128;
-// The row bitset is read in place (L2/L1-resident while its wave works on it), so the LDS slice holds
-// only the block prefix and the joiner lists: more responder waves fit per CU.
-__host__ __device__ inline uint32_t rwave_words(uint32_t NW, uint32_t NB) {
-  (void)NW;
-  return (NB + 1 + 2 * RW_JCAP + 1 + 3) & ~3u;
-}
+// The slice also holds a copy of the row bitset, taken while the block prefix is counted (the same
+// loads): every sampled select then reads its 32-byte block from LDS instead of L2.
+__host__ __device__ inline uint32_t rwave_head(uint32_t NB) { return (NB + 1 + 2 * RW_JCAP + 1 + 3) & ~3u; }
+__host__ __device__ inline uint32_t rwave_words(uint32_t NW, uint32_t NB) { return rwave_head(NB) + NW; }
 __device__ inline bool resp_by_wave(const Dev& d, uint32_t i, uint32_t nnew, bool on) {
   return on && d.uniform && nnew <= RW_JCAP && d.n[i] - nnew > d.capj;
 }
@@ -735,6 +745,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
   uint32_t* BP = rw_lds + (size_t)wv * rwave_words(NW, NB);  // block prefix of the row's bitset    [NB + 1]
   uint32_t* J = BP + NB + 1;                                    // this receiver's new joiners       [RW_JCAP]
   uint32_t* JM = J + RW_JCAP;                                   // suffix minima of J                [RW_JCAP + 1]
+  uint32_t* S = BP + rwave_head(NB);                            // the row bitset                    [NW]
   const uint32_t nnodes = *nnodes_p;
   for (uint32_t it = blockIdx.x * 4 + wv; it < nnodes; it += gridDim.x * 4) {
     const uint32_t i = nodes[it];
@@ -748,8 +759,10 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     const uint4* B4 = reinterpret_cast<const uint4*>(B);
     const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
     uint32_t bc = 0, last = 0;
+    uint4* S4 = reinterpret_cast<uint4*>(S);
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) {
       const uint4 q0 = B4[2 * k], q1 = B4[2 * k + 1];
+      S4[2 * k] = q0; S4[2 * k + 1] = q1;
       const uint32_t c = __popc(q0.x) + __popc(q0.y) + __popc(q0.z) + __popc(q0.w) + __popc(q1.x) + __popc(q1.y) +
                          __popc(q1.z) + __popc(q1.w);
       BP[k] = c; bc += c;
@@ -798,7 +811,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
         const uint32_t nk = nB - (nnew - upto), cap = d.capj;
         uint32_t* pay = ob.pay + poff;
         const Prp P = prp_make(nk, philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1));
-        sampled_fill(pay, l, 64, cap, P, B, BP, NB, ratio, J, JM, upto, nnew);
+        sampled_fill(pay, l, 64, cap, P, S, BP, NB, ratio, J, JM, upto, nnew);
         if (l == 0) {
           Msg m; m.dest = a; m.sender = i; m.seq = q; m.kind = K_KP; m.a = cap; m.fp = 0; m.n = 0; m.off = poff;
           ob.msgs[ob.off[i] + q] = m;
