@@ -244,7 +244,7 @@ __global__ __launch_bounds__(1024) void k_bfail_prep_lds(const BCast* bf, uint32
 constexpr uint32_t PB_LDS_W = 524288;
 constexpr uint32_t PB_FMAX = 2048, PB_JMAX = 1024;
 constexpr uint32_t RP_WAVES = 8;                 // waves per row-pass workgroup (they share the lists)
-constexpr uint32_t RP_LDS_BYTES = 81920;         // dynamic LDS per row-pass workgroup: two fit a CU
+constexpr uint32_t RP_LDS_BYTES = 81920 - 1024;  // dynamic LDS per row-pass workgroup: two (+ static) fit a CU
 struct RowOut { uint32_t* part; };   // [C][10]: the five smallest keys ascending, then 0xFFFFFFFF x 5
 
 // A3 over the row of node i (members from B: LDS or HBM): the five smallest keys (stamp << 24 | rot),
@@ -412,11 +412,18 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
       // ballot each (killed iff an earlier acting lane of the chunk names its sender).  The acting
       // entries are then applied together: the atomic's return says whether the peer was still present.
       BLossQuad lq;
-      for (uint32_t c = 0; c < ((d.dev & 2) ? 0u : pb.nf); c += 64) {   // dev 2: skip (timing experiments)
+      // the list entries of the next chunk are loaded one iteration ahead: they do not depend on the
+      // removals of this chunk, only the membership tests do
+      const uint32_t nfl = (d.dev & 2) ? 0u : pb.nf;   // dev 2: skip (timing experiments)
+      uint32_t dep_nx = 0;
+      BCast b_nx = l < nfl ? fail_at(l, dep_nx) : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+      for (uint32_t c = 0; c < nfl; c += 64) {
         const uint32_t e = c + l;
         const bool valid = e < pb.nf;
-        uint32_t dep = 0;
-        const BCast b = valid ? fail_at(e, dep) : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
+        const uint32_t dep = dep_nx;
+        const BCast b = b_nx;
+        dep_nx = 0;
+        b_nx = e + 64 < nfl ? fail_at(e + 64, dep_nx) : BCast{0xFFFFFFFFu, 0xFFFFFFFFu, 0, 0};
         if ((c & 255u) == 0) lq = bloss_quad(d, i, r, 0, c);
         const bool lost = bcast_lost(d, i, b.sender, r, lq, c) && valid && b.sender != i;
         const bool base = valid && b.sender != i && !lost && b.peer != i && honour && mem(b.sender);

@@ -812,8 +812,15 @@ static int step_round(kb_sim* s) {
     const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR && !pb_hbm;
     const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / d.NWR) : RP_WAVES;
     const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
-    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)(s->lds_per_cu / std::max<size_t>(lds + 1024, 1))));
+    int occ = 0;                                       // resident workgroups per CU (LDS, registers)
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ldsb ? reinterpret_cast<const void*>(&k_rowpass<true>)
+                                                                   : reinterpret_cast<const void*>(&k_rowpass<false>),
+                                                       (int)(64 * wpb), lds);
+    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)occ));
     const uint32_t blocks = std::min<uint32_t>((R + wpb - 1) / wpb, s->ncu * per_cu);
+    if (s->debug_waves && r == 2)
+      fprintf(stderr, "[kb] row pass: %u waves/workgroup, %zu B LDS, %u workgroups/CU (lds_per_cu %zu), %u workgroups\n", wpb,
+              lds, per_cu, (size_t)s->lds_per_cu, blocks);
     if (ldsb) hipExtLaunchKernelGGL(k_rowpass<true>, dim3(blocks), dim3(64 * wpb), lds, st, s->ev0, s->ev1, 0, d, pb, s->ro, r, lf, lj);
     else hipExtLaunchKernelGGL(k_rowpass<false>, dim3(blocks), dim3(64 * wpb), lds, st, s->ev0, s->ev1, 0, d, pb, s->ro, r, lf, lj);
   }
