@@ -13,7 +13,8 @@ import os
 from ._ffi import (KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL, KB_INIT_CONVERGED, KB_INIT_JOIN,  # noqa: F401
                    KbError, Sim, SimConfig, SimLib, STATE_NAMES)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkaboodle_sim.so")
+LIB_PATH = os.environ.get("KB_LIB_PATH") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkaboodle_sim.so")
+# (KB_LIB_PATH: an alternative build of the same library, for A/B timing experiments only)
 _LIB = None
 
 

@@ -686,8 +686,10 @@ static int ensure_recv(kb_sim* s, size_t nm, size_t np) {
   return KB_OK;
 }
 
-// all-to-all-v of this wave's delivered records; returns the received record count
-static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb) {
+// all-to-all-v of this wave's delivered records; returns the received record count, and
+// in `any` whether any rank delivered a record this wave (the same answer on every rank: when no
+// record moves, no handler runs and every later wave of the round is empty)
+static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb, bool& any) {
   const int W = s->world, me = s->rank;
   XState& x = s->xs;
   hipStream_t st = s->st;
@@ -705,6 +707,10 @@ static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb)
   HIPCHK(hipStreamSynchronize(st));
   size_t sc[XMAX], sd[XMAX], rc[XMAX], rd[XMAX], psc[XMAX], psd[XMAX], prc[XMAX], prd[XMAX];
   size_t so = 0, pso = 0, ro = 0, pro = 0;
+  uint64_t total = 0;
+  for (int k = 0; k < W * W; ++k) total += s->h_xall[(size_t)(k / W) * 2 * W + (k % W)];
+  any = total != 0;
+  if (!any) { nrecv = 0; return KB_OK; }
   for (int k = 0; k < W; ++k) {
     sc[k] = s->h_xall[(size_t)me * 2 * W + k]; psc[k] = s->h_xall[(size_t)me * 2 * W + W + k];
     rc[k] = s->h_xall[(size_t)k * 2 * W + me]; prc[k] = s->h_xall[(size_t)k * 2 * W + W + me];
@@ -906,8 +912,10 @@ static int step_round(kb_sim* s) {
       if (last) break;
       RecvBlocks rb;
       memset(&rb, 0, sizeof rb);
-      int rc = exchange_wave(s, ob, nrecv, rb);
+      bool any = true;
+      int rc = exchange_wave(s, ob, nrecv, rb, any);
       if (rc) return rc;
+      if (!any) break;                                 // no record anywhere: the rest of the round's waves are empty
       ib.msgs = s->rmsg; ib.pay = s->rpay;
       if (nrecv) k_route_recv<<<(nrecv + 255) / 256, 256, 0, st>>>(d, ib, s->wc, rb, nrecv);
     }

@@ -265,7 +265,10 @@ __global__ void k_scatter_flat(OutBuf ib, WaveCtl wc, uint32_t n) {
 constexpr uint32_t KP_BIG = 4096;          // payload ids from which a group takes the BIG kernel
 constexpr uint32_t KP_LDS_WORDS = 16384;   // BIG: rows up to 512K ids keep their bitset in LDS (64 KB)
 constexpr int KP_UNROLL = 10;            // 640 ids per wave step: a whole Join response (<= 567)
-constexpr uint32_t KP_COLS = 4;          // BIG groups in LDS: workgroups per destination, one per column quarter
+#ifndef KB_KP_COLS
+#define KB_KP_COLS 2
+#endif
+constexpr uint32_t KP_COLS = KB_KP_COLS; // BIG groups in LDS: workgroups per destination, one per column part (A/B: 2 beats 4 and 1)
 __host__ __device__ constexpr size_t kp_lds_bytes(uint32_t nwr) {
   return 4ull * (nwr <= KP_LDS_WORDS ? nwr : 4);
 }
