@@ -941,7 +941,7 @@ static int step_round(kb_sim* s) {
     if (!s->xf) k_scatter<<<gnode, tb, 0, st>>>(d, ob, s->wc);
     else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
     k_kp_small<<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r, nb);   // also sets up nb.cap / nb.cnt
-    {  // BIG groups in LDS: KP_COLS workgroups per destination group, one per column quarter
+    {  // BIG groups in LDS: KP_COLS workgroups per destination group, one per column part
       const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
       const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
       k_kp_group<true><<<ks * groups, 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);

@@ -258,10 +258,10 @@ __global__ void k_scatter_flat(OutBuf ib, WaveCtl wc, uint32_t n) {
 // BIG = the groups of at least KP_BIG ids (a joiner's hundreds of Join responses, all on one row):
 // 1024 threads on the row's member bitset staged in LDS, a wave per message with KP_UNROLL
 // independent id loads in flight per lane.  The other groups take 256 threads on the bitset in place.
-// A BIG group whose bitset fits in LDS is served by KP_COLS workgroups, each owning a quarter of the
-// row's ids: every one reads all the group's ids and applies those in its quarter, arms then
+// A BIG group whose bitset fits in LDS is served by KP_COLS workgroups, each owning a 1/KP_COLS part of the
+// row's ids: every one reads all the group's ids and applies those in its part, arms then
 // prologues.  An arm and a prologue conflict only on the same id, which one workgroup owns, so the
-// quarters need no synchronisation with each other.
+// parts need no synchronisation with each other.
 constexpr uint32_t KP_BIG = 4096;          // payload ids from which a group takes the BIG kernel
 constexpr uint32_t KP_LDS_WORDS = 16384;   // BIG: rows up to 512K ids keep their bitset in LDS (64 KB)
 constexpr int KP_UNROLL = 10;            // 640 ids per wave step: a whole Join response (<= 567)
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     uint32_t added = 0;
     auto arm = [&](uint32_t p) __attribute__((always_inline)) {
       const uint32_t wi = p >> 5;
-      if (wi < w0 || wi >= w1) return;                  // another workgroup's quarter
+      if (wi < w0 || wi >= w1) return;                  // another workgroup's part
       const uint32_t bit = 1u << (p & 31);
       const uint32_t w = lds ? B[wi - w0] : __hip_atomic_load(&B[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (w & bit) return;
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     for (uint32_t q = t; q < nk; q += T) {             // prologues
       const Msg m = ib.msgs[wc.kin[k0 + q]];
       const uint32_t s = m.sender;
-      if ((s >> 5) < w0 || (s >> 5) >= w1) continue;     // another workgroup's quarter
+      if ((s >> 5) < w0 || (s >> 5) >= w1) continue;     // another workgroup's part
       // byte update by CAS on its word: exactly one envelope per (dest, sender) sees the transition to
       // Known(now) and appends it to the freshness log
       uint32_t* wp = reinterpret_cast<uint32_t*>(rw + (s & ~3u));
