@@ -719,8 +719,11 @@ static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb,
   }
   int rcode = ensure_recv(s, ro, pro);
   if (rcode) return rcode;
-  if (!s->xf->alltoallv(x.smsg, sc, sd, s->rmsg, rc, rd, sizeof(Msg), st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  if (!s->xf->alltoallv(x.spay, psc, psd, s->rpay, prc, prd, 4, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  if (!s->xf->group_begin() ||                                     // records and payload as one grouped exchange
+      !s->xf->alltoallv(x.smsg, sc, sd, s->rmsg, rc, rd, sizeof(Msg), st) ||
+      !s->xf->alltoallv(x.spay, psc, psd, s->rpay, prc, prd, 4, st) || !s->xf->group_end()) {
+    seterr(s->xf->error()); return KB_IO_ERROR;
+  }
   rb.world = (uint32_t)W;
   for (int k = 0; k <= W && k <= (int)XMAX; ++k) {
     rb.m0[k] = k < W ? (uint32_t)rd[k] : (uint32_t)ro;
@@ -744,8 +747,11 @@ static int gather_broadcasts(kb_sim* s, uint32_t nj_loc, uint32_t nf_loc) {
     rc[k] = s->h_xall[2 * k]; frc[k] = s->h_xall[2 * k + 1];
     rd[k] = oj; oj += rc[k]; frd[k] = of; of += frc[k];
   }
-  if (!s->xf->alltoallv(s->bjoin_loc, sc, sd, s->bjoin, rc, rd, sizeof(BCast), st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  if (!s->xf->alltoallv(s->bfail_loc, fsc, sd, s->bfail, frc, frd, sizeof(BCast), st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  if (!s->xf->group_begin() ||
+      !s->xf->alltoallv(s->bjoin_loc, sc, sd, s->bjoin, rc, rd, sizeof(BCast), st) ||
+      !s->xf->alltoallv(s->bfail_loc, fsc, sd, s->bfail, frc, frd, sizeof(BCast), st) || !s->xf->group_end()) {
+    seterr(s->xf->error()); return KB_IO_ERROR;
+  }
   s->nj = (uint32_t)oj; s->nf = (uint32_t)of;
   return KB_OK;
 }

@@ -39,6 +39,9 @@ struct Xfer {
   virtual bool allreduce_max_u32(uint32_t* buf, size_t count, hipStream_t st) = 0;
   virtual bool allreduce_sum_u64(unsigned long long* buf, size_t count, hipStream_t st) = 0;
   virtual void abort() {}
+  // brackets several exchanges that may be issued as one (RCCL group: one launch for both all-to-alls)
+  virtual bool group_begin() { return true; }
+  virtual bool group_end() { return true; }
   virtual std::string error() const = 0;
 };
 
@@ -46,23 +49,27 @@ struct Xfer {
 struct RcclXfer : Xfer {
   ncclComm_t comm = nullptr;
   ncclResult_t last = ncclSuccess;
-  std::vector<size_t> sc, sd, rc, rd;
+  std::vector<size_t> sc[2], sd[2], rc[2], rd[2];   // two calls can share one group: a set each
+  int cur = 0;
   bool ok(ncclResult_t r) { last = r; return r == ncclSuccess; }
   bool init(int r, int w, const void* uid) {
     rank = r; world = w;
-    sc.resize(w); sd.resize(w); rc.resize(w); rd.resize(w);
+    for (int b = 0; b < 2; ++b) { sc[b].resize(w); sd[b].resize(w); rc[b].resize(w); rd[b].resize(w); }
     ncclUniqueId id;
     memcpy(&id, uid, sizeof id);
     return ok(ncclCommInitRank(&comm, w, id, r));
   }
   ~RcclXfer() override { if (comm) ncclCommDestroy(comm); }
+  bool group_begin() override { return ok(ncclGroupStart()); }
+  bool group_end() override { return ok(ncclGroupEnd()); }
   bool alltoallv(const void* send, const size_t* scounts, const size_t* sdispls, void* recv, const size_t* rcounts,
                  const size_t* rdispls, size_t elem, hipStream_t st) override {
     // moved as bytes: counts and displacements scale by the element size
+    const int b = cur; cur ^= 1;
     for (int k = 0; k < world; ++k) {
-      sc[k] = scounts[k] * elem; sd[k] = sdispls[k] * elem; rc[k] = rcounts[k] * elem; rd[k] = rdispls[k] * elem;
+      sc[b][k] = scounts[k] * elem; sd[b][k] = sdispls[k] * elem; rc[b][k] = rcounts[k] * elem; rd[b][k] = rdispls[k] * elem;
     }
-    return ok(ncclAllToAllv(send, sc.data(), sd.data(), recv, rc.data(), rd.data(), ncclUint8, comm, st));
+    return ok(ncclAllToAllv(send, sc[b].data(), sd[b].data(), recv, rc[b].data(), rd[b].data(), ncclUint8, comm, st));
   }
   bool allgather_u32(const uint32_t* send, uint32_t* recv, size_t count, hipStream_t st) override {
     return ok(ncclAllGather(send, recv, count, ncclUint32, comm, st));
