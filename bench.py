@@ -110,18 +110,19 @@ def timed_rounds(mesh, steps: int, world: int):
     import torch
     import torch.distributed as dist
     s0 = mesh.stats()
-    alive_sum = 0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         mesh.step(1)                                 # synchronous: returns after the round's kernels
-        alive_sum += mesh.stats()["alive"]           # sharded: the whole mesh (collective)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    return time.perf_counter() - t0, alive_sum, s0, mesh.stats()
+    dt = time.perf_counter() - t0
+    s1 = mesh.stats()                                # sharded: the whole mesh (collective)
+    # live peers of every simulated round, counted on the device during the round (kb_stats.alive_rounds)
+    return dt, s1["alive_rounds"] - s0["alive_rounds"], s0, s1
 
 
 def round_model_bytes(s0: dict, s1: dict, alive_mean: float, steps: int) -> float:

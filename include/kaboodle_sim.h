@@ -115,7 +115,8 @@ typedef struct kb_stats {
   uint64_t drop_dead, drop_loss, drop_window, drop_oversize, drop_partition, drop_bcast;
   uint64_t removed_timeout, removed_failed, join_responses, curious_overflow, churn_leaves, churn_joins;
   uint64_t sent_kp_ids;           /* peer entries carried by the KnownPeers messages sent               */
-  uint64_t reserved[7];
+  uint64_t alive_rounds;          /* sum over the simulated rounds of the peers running in that round  */
+  uint64_t reserved[6];
 } kb_stats;
 
 typedef struct kb_sim kb_sim;

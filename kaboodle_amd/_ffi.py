@@ -47,7 +47,7 @@ class KbStats(C.Structure):
         ("drop_oversize", C.c_uint64), ("drop_partition", C.c_uint64), ("drop_bcast", C.c_uint64),
         ("removed_timeout", C.c_uint64), ("removed_failed", C.c_uint64), ("join_responses", C.c_uint64),
         ("curious_overflow", C.c_uint64), ("churn_leaves", C.c_uint64), ("churn_joins", C.c_uint64),
-        ("sent_kp_ids", C.c_uint64), ("reserved", C.c_uint64 * 7),
+        ("sent_kp_ids", C.c_uint64), ("alive_rounds", C.c_uint64), ("reserved", C.c_uint64 * 6),
     ]
 
     def as_dict(self) -> dict:

@@ -328,6 +328,8 @@ struct kb_sim {
   std::vector<uint32_t> watch_node, watch_fp;
   std::vector<uint32_t*> watch_snap;
   uint32_t* ev_out = nullptr;          // [2*C + 4]: discovered ids, departed ids, counters
+  uint32_t* rres = nullptr;            // [4] device: the round's results (k_round_end)
+  uint32_t* h_pin = nullptr;           // [16] pinned host: small per-round copies (no staging)
 };
 
 // allocation of this handle's device memory; row tables hold the local rows only and their pointer
@@ -430,6 +432,7 @@ static void destroy_shard(kb_sim* s) {
   if (s->st) (void)hipStreamSynchronize(s->st);
   free_all(s);
   for (hipEvent_t e : {s->ev0, s->ev1, s->er0, s->er1, s->ef0, s->ef1}) if (e) (void)hipEventDestroy(e);
+  if (s->h_pin) (void)hipHostFree(s->h_pin);
   if (s->st) (void)hipStreamDestroy(s->st);
   delete s->xf;
   delete s;
@@ -519,7 +522,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   A(s->scan_tot, 32); A(s->scan_tiles, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
   AR(s->nresp, 1); AR(s->paysum, 1); AR(s->nbase, 1); AR(s->resp_off, 1);
   A(s->resp_nodes, R); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS); A(s->slow, R);
-  AR(s->ro.part, 10);
+  AR(s->ro.part, 10); A(s->rres, 4);
   if (xf) {
     XState& x = s->xs;
     x.world = (uint32_t)world; x.R = R; x.S = rows_per;
@@ -537,6 +540,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (d.lat) { (void)hipMemset(d.lat, 0xFF, 2ull * lat_stride(R) * W); (void)hipMemset(s->fnamed, 0, 4ull * d.NWR); }   // all None
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
+  if (hipHostMalloc((void**)&s->h_pin, 64, hipHostMallocDefault) != hipSuccess) { s->h_pin = nullptr; destroy_shard(s); seterr("pinned buffer"); return KB_IO_ERROR; }
   for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->er0, &s->er1, &s->ef0, &s->ef1}) (void)hipEventCreate(e);
   int rc = upload_segments(s);
   if (rc) { destroy_shard(s); return rc; }
@@ -615,11 +619,7 @@ extern "C" int kb_sim_shard_info(kb_sim* s, int32_t* rank, int32_t* world, uint3
   return KB_OK;
 }
 
-static int check_err(kb_sim* s) {
-  uint32_t e = 0;
-  if (s->xf && !s->xf->allreduce_max_u32(s->d.ctr + C_ERR, 1, s->st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  HIPCHK(hipMemcpyAsync(&e, s->d.ctr + C_ERR, 4, hipMemcpyDeviceToHost, s->st));
-  HIPCHK(hipStreamSynchronize(s->st));
+static int err_status(uint32_t e) {
   if (e) {
     const char* what[] = {"", "suspect slots exhausted", "outbox region overflow", "payload pool overflow",
                           "truncated Join response too large", "inbox overflow", "Join response member count mismatch",
@@ -628,6 +628,12 @@ static int check_err(kb_sim* s) {
     return KB_CAPACITY;
   }
   return KB_OK;
+}
+static int check_err(kb_sim* s) {
+  if (s->xf && !s->xf->allreduce_max_u32(s->d.ctr + C_ERR, 1, s->st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  HIPCHK(hipMemcpyAsync(s->h_pin, s->d.ctr + C_ERR, 4, hipMemcpyDeviceToHost, s->st));
+  HIPCHK(hipStreamSynchronize(s->st));
+  return err_status(s->h_pin[0]);
 }
 
 // replace a tracked device allocation by a larger one (contents are not kept)
@@ -849,8 +855,8 @@ static int step_round(kb_sim* s) {
   }
   k_set_cap<<<gnode, tb, 0, st>>>(d, s->nresp, o0.cap, o0.cnt);
   if (have_b && s->nj) {
-    uint32_t tot[5];
-    HIPCHK(hipMemcpyAsync(tot, s->scan_tot, 20, hipMemcpyDeviceToHost, st));
+    const uint32_t* tot = s->h_pin;
+    HIPCHK(hipMemcpyAsync(s->h_pin, s->scan_tot, 20, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t pay_tot = tot[1], msg_tot = tot[2], resp_nodes = tot[4];
     if (msg_tot > o0.msg_cap || pay_tot > o0.pay_cap) {
@@ -975,16 +981,17 @@ static int step_round(kb_sim* s) {
     cur ^= 1;
   }
   if (s->xf && !s->xf->allreduce_sum_u32(d.ctr + C_AGREE, 1, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  k_round_end<<<1, 1, 0, st>>>(d, r);
+  k_round_end<<<1, 1, 0, st>>>(d, r, s->scan_tot, s->rres);
   (void)hipEventRecord(s->er1, st);
-  uint32_t tot[2];
-  HIPCHK(hipMemcpyAsync(tot, s->scan_tot, 8, hipMemcpyDeviceToHost, st));
+  // one copy and one synchronisation: the next round's broadcast counts and the error flag
+  HIPCHK(hipMemcpyAsync(s->h_pin, s->rres, 12, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
+  const uint32_t nj_loc = s->h_pin[0], nf_loc = s->h_pin[1], err = s->h_pin[2];
   if (s->xf) {
-    const int rc = gather_broadcasts(s, tot[0], tot[1]);
+    const int rc = gather_broadcasts(s, nj_loc, nf_loc);
     if (rc) return rc;
   } else {
-    s->nj = tot[0]; s->nf = tot[1];
+    s->nj = nj_loc; s->nf = nf_loc;
   }
   s->bj_total += s->nj; s->bf_total += s->nf;
   float ms = 0;
@@ -992,7 +999,7 @@ static int step_round(kb_sim* s) {
   if (d.uniform) { (void)hipEventElapsedTime(&ms, s->ef0, s->ef1); s->fold_ms += ms; s->fold_launches++; }
   (void)hipEventElapsedTime(&ms, s->er0, s->er1); s->round_ms += ms; s->round_launches++;
   s->round = r + 1;
-  return check_err(s);
+  return s->xf ? check_err(s) : err_status(err);   // shards: the flag of any rank
 }
 
 static bool is_group(const kb_sim* s) { return !s->shards.empty(); }
@@ -1315,6 +1322,7 @@ extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
   out->removed_timeout = st[S_RMTIMEOUT]; out->removed_failed = st[S_RMFAILED]; out->join_responses = st[S_JRESP];
   out->curious_overflow = st[S_CUROVF]; out->churn_leaves = st[S_CLEAVE]; out->churn_joins = st[S_CJOIN];
   out->sent_kp_ids = st[S_KPIDS];
+  out->alive_rounds = st[S_ALIVER];
   return KB_OK;
 }
 // per id: alive, n, last_bcast, start_round; n and last_bcast only for the rows this handle holds

@@ -272,10 +272,13 @@ __global__ void k_bcast_write(Dev d, BcastSlots bs, const uint32_t* join_off, co
   for (uint32_t q = 0; q < nfl; ++q) bfail[fail_off[i] + q] = BCast{i, bs.fail[(size_t)i * SLOTS + q], bseq++, 0};
 }
 
-__global__ void k_round_end(Dev d, int32_t r) {
+// round results for the host in one small copy: rres = {Join broadcasts, Failed broadcasts, error}
+__global__ void k_round_end(Dev d, int32_t r, const uint32_t* tot, uint32_t* rres) {
   if (threadIdx.x || blockIdx.x) return;
   const uint32_t a = d.ctr[C_AGREE], al = d.ctr[C_ALIVE];
   d.ctr[C_LASTAGREE] = a; d.ctr[C_LASTALIVE] = al;
+  if (d.lo == 0) d.stats[S_ALIVER] += al;          // the running set is replicated: shard 0 counts it
+  rres[0] = tot[0]; rres[1] = tot[1]; rres[2] = d.ctr[C_ERR];
   if (al && a == al) {
     if ((int32_t)d.ctr[C_FIRSTCONV] < 0) d.ctr[C_FIRSTCONV] = (uint32_t)r;
     d.ctr[C_LASTCONV] = (uint32_t)r;

@@ -806,7 +806,7 @@ static int step_round(kbo_sim* s) {
   /* 4. receive window: unicast waves */
   err = run_waves(s, r);
   if (err) return err;
-  s->st.agree = agree; s->st.alive = alive;
+  s->st.agree = agree; s->st.alive = alive; s->st.alive_rounds += alive;
   if (alive && agree == alive) {
     if (s->st.first_converged_round < 0) s->st.first_converged_round = r;
     s->st.last_converged_round = r;

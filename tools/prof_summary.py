@@ -78,9 +78,8 @@ def sq(d):
         k = short(r["Kernel_Name"])
         a = agg.setdefault(k, {})
         a.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    names = ["SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY",
-             "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"]
-    print(f"{'kernel':28s} " + " ".join(f"{n[3:]:>14s}" for n in names))
+    names = sorted({n for a in agg.values() for n in a})
+    print(f"{'kernel':28s} " + " ".join(f"{n[3:][:14]:>14s}" for n in names))
     for k, a in sorted(agg.items(), key=lambda kv: -sum(kv[1].get("SQ_WAVE_CYCLES", [0]))):
         print(f"{k[:28]:28s} " + " ".join(f"{(sum(a[n]) / len(a[n]) if n in a else 0):14.0f}" for n in names))
 
