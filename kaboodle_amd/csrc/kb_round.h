@@ -762,6 +762,8 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
     if (!resp_by_wave(d, i, nnew, true)) continue;          // wave-uniform: k_resp_node serves it
     if (l == 0) path_hit(d, PATH_RESP_WAVE);
+    const bool tdbg = (d.dev & 512) != 0;                   // phase timing (KB_DEV=512, KB_DEBUG_WAVES)
+    uint64_t tp0 = tdbg ? wall_clock64() : 0, tp1 = 0, tp2 = 0;
     const uint32_t* B = bits_of(d, i);                      // row membership after the Join group
     const uint4* B4 = reinterpret_cast<const uint4*>(B);
     const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
@@ -781,6 +783,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     const float ratio = nB ? (float)nbu / (float)nB : 0.0f;
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) { const uint32_t c = BP[k]; BP[k] = ex; ex += c; }
     if (l == 0) BP[NB] = nB;
+    if (tdbg) { wait_lds(); tp1 = wall_clock64(); }
     for (uint32_t e = l; e < pb.nj; e += 64) {              // new joiners in list order
       if (!newbit(nm, e)) continue;
       uint32_t pos = __popcll(nm[e >> 6] & ((1ull << (e & 63)) - 1ull));
@@ -805,6 +808,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     wait_lds();
     __builtin_amdgcn_wave_barrier();
     uint32_t poff = ob.poff[i], q = 0, ins_before = 0;
+    if (tdbg) tp2 = wall_clock64();
     for (uint32_t wj = 0; wj < pb.JW; ++wj) {
       unsigned long long rmw = rm[wj];
       const unsigned long long nmw = nm[wj];
@@ -827,6 +831,13 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
         poff += cap; q++;
       }
       ins_before += __popcll(nmw);
+    }
+    if (tdbg && l == 0) {
+      __builtin_amdgcn_s_waitcnt(0);
+      const uint64_t tp3 = wall_clock64();
+      atomicAdd(&d.ctr[C_DBG_TNODE], (uint32_t)(tp1 - tp0)); atomicAdd(&d.ctr[C_DBG_TBASE], (uint32_t)(tp2 - tp1));
+      atomicAdd(&d.ctr[C_DBG_TINS], (uint32_t)(tp3 - tp2)); atomicAdd(&d.ctr[C_DBG_TSTART], 1u);
+      atomicAdd(&d.ctr[C_DBG_MSGS], q);
     }
     wait_lds();                                           // the LDS slice is reused by the next responder
     __builtin_amdgcn_wave_barrier();

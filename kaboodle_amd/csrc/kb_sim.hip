@@ -881,10 +881,18 @@ static int step_round(kb_sim* s) {
       // a wave per responder where its LDS slice fits (4 responders per 64 KB workgroup), else a workgroup
       const size_t wlds = 16ull * rwave_words(d.NWR, s->W / 256);
       const bool wave_on = wlds <= 65536 && !(d.dbg & KB_DBG_RESP_HBM);
+      if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
       if (wave_on)
         k_resp_wave<<<std::min<uint32_t>((resp_nodes + 3) / 4, 4096), 256, wlds, st>>>(d, pb, s->resp_nodes,
                                                                                      s->scan_tot + 4, o0, r);
       k_resp_node<<<grid, 256, lds, st>>>(d, pb, s->resp_nodes, s->scan_tot + 4, o0, r, scratch, wave_on);
+      if (s->debug_waves && (d.dev & 512)) {
+        uint32_t dbg[13];
+        HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        fprintf(stderr, "[kb] round %d k_resp_wave: responders %u, responses %u: staging+prefix %.1f us, joiners %.1f, "
+                "fills %.1f (sums over waves)\n", r, dbg[10], dbg[12], dbg[6] * 0.01, dbg[8] * 0.01, dbg[9] * 0.01);
+      }
     }
   }
   // 3. tick
@@ -952,6 +960,7 @@ static int step_round(kb_sim* s) {
     }
     if (!s->xf) k_scatter<<<gnode, tb, 0, st>>>(d, ob, s->wc);
     else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
+    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
     k_kp_small<<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r, nb);   // also sets up nb.cap / nb.cnt
     {  // BIG groups in LDS: KP_COLS workgroups per destination group, one per column part
       const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
@@ -959,7 +968,6 @@ static int step_round(kb_sim* s) {
       k_kp_group<true><<<ks * groups, 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
     }
     k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc, r);   // + the KPR oversize probe
-    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
     k_proc_fast<<<gnode, tb, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
     // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
     // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
@@ -973,6 +981,10 @@ static int step_round(kb_sim* s) {
       fprintf(stderr, "[kb] round %d wave %u: k_proc nodes %u, prologue inserts %u, fingerprint refreshes %u (max per "
               "node %u), KPR scans %u (log entries %u), incremental bases %u\n", r, w, slow, dbg[0], dbg[1], dbg[2], dbg[3],
               dbg[4], dbg[5]);
+      if (d.dev & 128)
+        fprintf(stderr, "[kb] round %d wave %u: k_kp_group BIG workgroup-destinations %u, messages %u: stage+arms %.1f us, "
+                "prologues %.1f, write-back+refold %.1f (sums), max total %.1f\n", r, w, dbg[10], dbg[12], dbg[6] * 0.01,
+                dbg[8] * 0.01, dbg[9] * 0.01, dbg[7] * 0.01);
       if (d.dev & 64)
         fprintf(stderr, "[kb] round %d wave %u: k_proc node time sum %.1f us (max %.1f), take_base %.1f, insertions %.1f, "
                 "start %.1f, end %.1f, messages %u\n", r, w, dbg[6] * 0.01, dbg[7] * 0.01, dbg[8] * 0.01, dbg[9] * 0.01,

@@ -309,6 +309,9 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     uint32_t* B = lds ? kp_lds : gB;
     uint8_t* rw = row_of(d, i);
     if (t == 0) { s_segs = 0; s_add = 0; }
+    const bool tdbg = BIG && (d.dev & 128) && t == 0;     // phase timing (KB_DEV=128, KB_DEBUG_WAVES)
+    uint64_t tp[5];
+    if (tdbg) tp[0] = wall_clock64();
     if (lds) stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB + w0), (w1 - w0) / 4, t, T);
     unsigned long long segs = 0;
     uint32_t added = 0;
@@ -330,20 +333,57 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
         uint32_t moff = 0, mlen = 0;
         if (qm < nk) { const Msg m = ib.msgs[wc.kin[k0 + qm]]; moff = m.off; mlen = m.a; }
         const uint32_t cnt = q0 + 64 * nwv <= nk ? 64u : (nk - q0 + nwv - 1) / nwv;
-        for (uint32_t j = 0; j < cnt; ++j) {
+        // software pipeline over the batch's (message, 640-id chunk) items: the ids of the next item are
+        // loaded while the current item's arms run, so a message costs its arms, not arms + a load trip
+        auto load = [&](uint32_t j, uint32_t e0, uint32_t (&pv)[KP_UNROLL]) __attribute__((always_inline)) {
           const uint32_t off = bcast(moff, (int)j), len = bcast(mlen, (int)j);
-          for (uint32_t e0 = 0; e0 < len; e0 += 64 * KP_UNROLL) {
-            uint32_t pv[KP_UNROLL];
 #pragma unroll
-            for (int u = 0; u < KP_UNROLL; ++u) {
-              const uint32_t e = e0 + 64u * u + l;
-              pv[u] = e < len ? ib.pay[off + e] : 0xFFFFFFFFu;
-            }
-#pragma unroll
-            for (int u = 0; u < KP_UNROLL; ++u) if (pv[u] != 0xFFFFFFFFu) arm(pv[u]);
+          for (int u = 0; u < KP_UNROLL; ++u) {
+            const uint32_t e = e0 + 64u * u + l;
+            pv[u] = e < len ? ib.pay[off + e] : 0xFFFFFFFFu;
           }
+        };
+        auto next = [&](uint32_t& j, uint32_t& e0) __attribute__((always_inline)) {
+          e0 += 64 * KP_UNROLL;
+          if (e0 >= bcast(mlen, (int)j)) { e0 = 0; ++j; }
+        };
+        uint32_t j = 0, e0 = 0;
+        while (j < cnt && bcast(mlen, (int)j) == 0) ++j;
+        uint32_t pv[KP_UNROLL];
+        if (j < cnt) load(j, e0, pv);
+        while (j < cnt) {
+          uint32_t jn = j, en = e0;
+          next(jn, en);
+          while (jn < cnt && bcast(mlen, (int)jn) == 0) ++jn;
+          uint32_t pn[KP_UNROLL];
+          if (jn < cnt) load(jn, en, pn);
+          // the item's arms in three batched phases (all membership reads, then all atomics, then the
+          // stamp writes), so a lane waits for two LDS round trips per item instead of two per id
+          uint32_t wv_[KP_UNROLL], ob_[KP_UNROLL];
+#pragma unroll
+          for (int u = 0; u < KP_UNROLL; ++u) {
+            const uint32_t wi = pv[u] >> 5;
+            const bool inr = pv[u] != 0xFFFFFFFFu && wi >= w0 && wi < w1;
+            wv_[u] = inr ? (lds ? B[wi - w0] : __hip_atomic_load(&B[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                         : 0xFFFFFFFFu;
+          }
+#pragma unroll
+          for (int u = 0; u < KP_UNROLL; ++u) {
+            const uint32_t bit = 1u << (pv[u] & 31);
+            ob_[u] = (wv_[u] & bit) ? bit : atomicOr(&B[(pv[u] >> 5) - w0], bit);
+          }
+#pragma unroll
+          for (int u = 0; u < KP_UNROLL; ++u) {
+            const uint32_t p = pv[u];
+            if (!(ob_[u] & (1u << (p & 31)))) { rw[p] = old; segs |= seg_bit(d, p); added++; }
+          }
+#pragma unroll
+          for (int u = 0; u < KP_UNROLL; ++u) pv[u] = pn[u];
+          j = jn; e0 = en;
         }
       }
+      __syncthreads();
+      if (tdbg) tp[1] = wall_clock64();
     } else {
       __syncthreads();
       for (uint32_t q = 0; q < nk; ++q) {              // message by message
@@ -375,6 +415,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     if (segs) atomicOr(&s_segs, segs);
     if (added) atomicAdd(&s_add, added);
     __syncthreads();
+    if (tdbg) tp[2] = wall_clock64();
     const unsigned long long sg = s_segs;
     unsigned long long refolded = 0;
     if (lds && sg) {                                   // write back the changed segments of the bitset
@@ -416,6 +457,14 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     }
     if (BIG && t == 0 && li == 0) path_hit(d, lds ? PATH_KP_BIG_LDS : PATH_KP_BIG_HBM);
     __syncthreads();                                   // LDS reused by the next destination
+    if (tdbg) {
+      tp[3] = wall_clock64();
+      atomicAdd(&d.ctr[C_DBG_TNODE], (uint32_t)(tp[1] - tp[0]));   // stage + arms
+      atomicAdd(&d.ctr[C_DBG_TBASE], (uint32_t)(tp[2] - tp[1]));   // prologues
+      atomicAdd(&d.ctr[C_DBG_TINS], (uint32_t)(tp[3] - tp[2]));    // write-back + refold
+      atomicAdd(&d.ctr[C_DBG_MSGS], nk); atomicAdd(&d.ctr[C_DBG_TSTART], 1u);
+      atomicMax(&d.ctr[C_DBG_TMAX], (uint32_t)(tp[3] - tp[0]));
+    }
   }
   }
 }
