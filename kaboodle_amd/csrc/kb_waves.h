@@ -39,11 +39,32 @@ struct SenderSpan {
   }
 };
 
+// Per-workgroup aggregation of the KnownPeers counters: wave 0 carries tens of thousands of Join
+// responses addressed to the round's few dozen joiners, and one global atomic per message on those few
+// counters serialises in the memory system.  A workgroup first sums its messages per destination in a
+// small LDS hash table, then adds each sum once; a destination that finds no free slot in KAGG_PROBE
+// probes goes to the global counters directly.
+constexpr uint32_t KAGG = 256, KAGG_PROBE = 8, KAGG_EMPTY = 0xFFFFFFFFu;
+__device__ inline uint32_t kagg_slot(uint32_t x) { return (x * 0x9E3779B1u) >> 24; }   // 8 bits: KAGG slots
+// slot of dest (inserted when `insert`), or KAGG when it is not (cannot be) in the table
+__device__ inline uint32_t kagg_find(uint32_t* kd, uint32_t dest, bool insert) {
+  uint32_t h = kagg_slot(dest);
+  for (uint32_t p = 0; p < KAGG_PROBE; ++p, h = (h + 1) & (KAGG - 1)) {
+    const uint32_t cur = insert ? atomicCAS(&kd[h], KAGG_EMPTY, dest) : kd[h];
+    if (cur == dest || (insert && cur == KAGG_EMPTY)) return h;
+    if (cur == KAGG_EMPTY) return KAGG;
+  }
+  return KAGG;
+}
+
 // delivery decisions for every message of the wave: dead receiver, partition, loss (Philox keyed on
 // the message), else delivered; counts per destination.
 __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int32_t r, uint32_t w, int last) {
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
+  __shared__ uint32_t s_kd[KAGG], s_kc[KAGG], s_kp[KAGG];
   const uint32_t wv = threadIdx.x >> 6, l = lane();
+  s_kd[threadIdx.x] = KAGG_EMPTY; s_kc[threadIdx.x] = 0; s_kp[threadIdx.x] = 0;   // blockDim == KAGG
+  __syncthreads();
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0, kpids = 0;
   const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
@@ -68,8 +89,9 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
              philox(m.sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m.seq, d.k0, d.k1).x < d.loss_thr) loss++;
     else if (m.kind == K_KP) {
       st = 2;
-      atomicAdd(&wc.kcnt[m.dest], 1u);
-      if (m.a) atomicAdd(&wc.kpay[m.dest], m.a);
+      const uint32_t h = kagg_find(s_kd, m.dest, true);
+      if (h < KAGG) { atomicAdd(&s_kc[h], 1u); if (m.a) atomicAdd(&s_kp[h], m.a); }
+      else { atomicAdd(&wc.kcnt[m.dest], 1u); if (m.a) atomicAdd(&wc.kpay[m.dest], m.a); }
     } else {
       st = 1;
       atomicAdd(&wc.cnt1[m.dest], 1u);
@@ -78,22 +100,33 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
     }
     if (!last) wc.status[g] = st;
   }
+  __syncthreads();
+  if (s_kd[threadIdx.x] != KAGG_EMPTY) {
+    const uint32_t x = s_kd[threadIdx.x];
+    atomicAdd(&wc.kcnt[x], s_kc[threadIdx.x]);
+    if (s_kp[threadIdx.x]) atomicAdd(&wc.kpay[x], s_kp[threadIdx.x]);
+  }
   for (int k = 0; k < 5; ++k) stat_add(d, S_PING + k, ks[k]);
   stat_add(d, S_DEAD, dead); stat_add(d, S_PART, part); stat_add(d, S_LOSS, loss); stat_add(d, S_WINDOW, win);
   stat_add(d, S_KPIDS, kpids);
 }
 
+// KnownPeers records are placed in two passes (their order within a destination's group is free: the
+// group commutes): count per destination in LDS, reserve each destination's block once,
+// then place; in-order records take their global cursor directly (in-order inboxes are sorted later).
 __global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
+  __shared__ uint32_t s_kd[KAGG], s_kc[KAGG], s_kb[KAGG];
   const uint32_t wv = threadIdx.x >> 6, l = lane();
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  s_kd[threadIdx.x] = KAGG_EMPTY; s_kc[threadIdx.x] = 0;   // blockDim == KAGG
   const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
   s_ex[wv][l] = wave_excl(cnt);
   s_base[wv][l] = i < d.hi ? ob.off[i] : 0;
   const uint32_t T = wave_sum(cnt);
-  wait_lds();
-  __builtin_amdgcn_wave_barrier();
+  __syncthreads();
   const SenderSpan sp{T};
+  bool anykp = false;
   for (uint32_t k = l; k < T; k += 64) {
     uint32_t j, q;
     sp.owner(s_ex[wv], k, j, q);
@@ -102,7 +135,20 @@ __global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
     if (!st) continue;
     const uint32_t dst = ob.msgs[g].dest;
     if (st == 1) wc.inbox[wc.in_off[dst] + atomicAdd(&wc.cursor[dst], 1u)] = g;
-    else wc.kin[wc.koff[dst] + atomicAdd(&wc.kcur[dst], 1u)] = g;
+    else { const uint32_t h = kagg_find(s_kd, dst, true); if (h < KAGG) atomicAdd(&s_kc[h], 1u); anykp = true; }
+  }
+  if (!__syncthreads_or(anykp)) return;
+  if (s_kd[threadIdx.x] != KAGG_EMPTY) { s_kb[threadIdx.x] = atomicAdd(&wc.kcur[s_kd[threadIdx.x]], s_kc[threadIdx.x]); s_kc[threadIdx.x] = 0; }
+  __syncthreads();
+  for (uint32_t k = l; k < T; k += 64) {
+    uint32_t j, q;
+    sp.owner(s_ex[wv], k, j, q);
+    const uint32_t g = s_base[wv][j] + q;
+    if (wc.status[g] != 2) continue;
+    const uint32_t dst = ob.msgs[g].dest;
+    const uint32_t h = kagg_find(s_kd, dst, false);
+    const uint32_t pos = h < KAGG ? s_kb[h] + atomicAdd(&s_kc[h], 1u) : atomicAdd(&wc.kcur[dst], 1u);
+    wc.kin[wc.koff[dst] + pos] = g;
   }
 }
 
