@@ -85,6 +85,7 @@ struct Dev {
   uint32_t* zbtab;                // [9][4][256] byte tables of multiplication by Z^c
   uint32_t* htab;                 // [(W/8)][256] crc0 of every member pattern of every 8-id half block
   unsigned long long* stats;
+  unsigned long long* sacc;       // [NACC][NSTAT] per-workgroup partial counters, folded into stats on read
   uint32_t* ctr;
   uint32_t* truefp;
   uint2* tfpart;                  // [64] ordered partials of the running set's fingerprint
@@ -391,6 +392,31 @@ __device__ inline unsigned long long block_sum(unsigned long long v) {
 __device__ inline void stat_add(const Dev& d, int idx, unsigned long long v) {
   const unsigned long long t = block_sum(v);
   if (threadIdx.x == 0 && t) atomicAdd(&d.stats[idx], t);
+}
+// Counters of the per-wave kernels: block-wide sums of N counters with one LDS exchange and one
+// barrier, added to the block's own accumulation slot (d.sacc; k_stats_fold folds the slots into
+// d.stats when the host reads them).  Every workgroup of every wave adding to the same few stats
+// words would serialise in the memory system.
+constexpr uint32_t NACC = 1024;
+template <int N>
+__device__ inline void stat_add_n(const Dev& d, const int (&idx)[N], const unsigned long long (&v)[N]) {
+  __shared__ unsigned long long red[16][N];
+  const int w = threadIdx.x >> 6;
+  unsigned long long s[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    s[k] = v[k];
+    for (int o = 32; o > 0; o >>= 1) s[k] += __shfl_xor(s[k], o, 64);
+  }
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < N; ++k) red[w][k] = s[k];
+  __syncthreads();
+  if (threadIdx.x < (unsigned)N) {
+    unsigned long long t = 0;
+    for (int k = 0; k < (int)((blockDim.x + 63) >> 6); ++k) t += red[k][threadIdx.x];
+    if (t) atomicAdd(&d.sacc[(size_t)(blockIdx.x % NACC) * NSTAT + idx[threadIdx.x]], t);
+  }
 }
 
 // ---- message outboxes --------------------------------------------------------------------------

@@ -539,14 +539,20 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
     wait_lds();                                       // LDS bitset is reused by the next node
     __builtin_amdgcn_wave_barrier();
   }
+  // the counters are summed over the workgroup's waves in LDS and added once per workgroup (one atomic
+  // per wave and counter on the same few addresses would serialise in the memory system)
+  __shared__ unsigned long long s_cnt[RP_WAVES][7];
   if (l == 0) {
-    if (w_lost) atomicAdd(&d.stats[S_BDROP], w_lost);
-    if (w_removed) atomicAdd(&d.stats[S_RMFAILED], w_removed);
-    if (w_resp) atomicAdd(&d.stats[S_JRESP], w_resp);
-    if (w_bytes) atomicAdd(&d.stats[S_ROWB], w_bytes);
-    atomicAdd(&d.stats[S_A3ROWS], (unsigned long long)a3c.x); atomicAdd(&d.stats[S_A3DEEP], (unsigned long long)a3c.y);
-    atomicAdd(&d.stats[S_A3CHUNKS], (unsigned long long)a3c.z);
+    s_cnt[wv][0] = w_lost; s_cnt[wv][1] = w_removed; s_cnt[wv][2] = w_resp; s_cnt[wv][3] = w_bytes;
+    s_cnt[wv][4] = a3c.x; s_cnt[wv][5] = a3c.y; s_cnt[wv][6] = a3c.z;
     if (!LDSB && w_nodes) path_hit(d, PATH_PHASEB_HBM);
+  }
+  __syncthreads();
+  if (threadIdx.x < 7) {
+    unsigned long long t = 0;
+    for (uint32_t k = 0; k < wpb; ++k) t += s_cnt[k][threadIdx.x];
+    const int idx[7] = {S_BDROP, S_RMFAILED, S_JRESP, S_ROWB, S_A3ROWS, S_A3DEEP, S_A3CHUNKS};
+    if (t) atomicAdd(&d.stats[idx[threadIdx.x]], t);
   }
 }
 

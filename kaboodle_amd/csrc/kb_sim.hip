@@ -503,7 +503,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   AR(d.last_bcast, 1); AR(d.a3cur, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
   AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
   A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
-  A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
+  A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.sacc, (size_t)NACC * NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
   if (cfg->track_latency) { A(d.lat, (size_t)W * lat_stride(R)); A(s->lat_col, C); A(s->fnamed, d.NWR); }   // peer-major
   s->msg_cap = std::max<uint32_t>(8u * R + (uint32_t)TICK_MAX * R, 1u << 16);
@@ -1294,8 +1294,27 @@ extern "C" int kb_sim_events(kb_sim* s, uint32_t node, uint32_t* discovered, siz
   if (*fp_changed) s->watch_fp[k] = *fp;
   return KB_OK;
 }
+// the per-workgroup partial counters (d.sacc) folded into d.stats; the stream is idle afterwards
+__global__ __launch_bounds__(256) void k_stats_fold(Dev d) {
+  const uint32_t k = blockIdx.x;                   // one counter per workgroup
+  unsigned long long t = 0;
+  for (uint32_t q = threadIdx.x; q < NACC; q += blockDim.x) {
+    unsigned long long& x = d.sacc[(size_t)q * NSTAT + k];
+    t += x; x = 0;
+  }
+  t = block_sum(t);
+  if (threadIdx.x == 0 && t) d.stats[k] += t;
+}
+static int fold_stats(kb_sim* s) {
+  if (is_group(s)) { for (kb_sim* t : s->shards) { const int rc = fold_stats(t); if (rc) return rc; } return KB_OK; }
+  (void)hipSetDevice(s->device);
+  k_stats_fold<<<NSTAT, 256, 0, s->st>>>(s->d);
+  HIPCHK(hipStreamSynchronize(s->st));
+  return KB_OK;
+}
 extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
   if (!s || !out) return KB_INVALID_ARGUMENT;
+  { const int rc = fold_stats(s); if (rc) return rc; }
   unsigned long long st[NSTAT];
   uint32_t ctr[NCTR];
   kb_sim* h = is_group(s) ? s->shards[0] : s;       // replicated facts come from any shard
@@ -1419,6 +1438,7 @@ extern "C" int kb_sim_kernel_time(kb_sim* s, int kind, double* ms, uint64_t* lau
 }
 static uint64_t stat_counter(kb_sim* s, int idx) {
   unsigned long long v = 0;
+  if (fold_stats(s)) return 0;
   if (hipMemcpy(&v, s->d.stats + idx, 8, hipMemcpyDeviceToHost) != hipSuccess) return 0;
   return v;
 }
@@ -1456,6 +1476,7 @@ extern "C" int kb_sim_debug_paths(kb_sim* s, uint32_t* mask) {
 extern "C" int kb_sim_debug_counters(kb_sim* s, uint64_t* out, size_t cap) {
   if (!s || !out || cap < 3) return KB_INVALID_ARGUMENT;
   kb_sim* h = is_group(s) ? s->shards[0] : s;
+  { const int rc = fold_stats(h); if (rc) return rc; }
   unsigned long long v[3];
   HIPCHK(hipMemcpy(v, h->d.stats + S_A3ROWS, sizeof v, hipMemcpyDeviceToHost));
   for (int k = 0; k < 3; ++k) out[k] = v[k];

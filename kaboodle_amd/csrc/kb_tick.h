@@ -163,13 +163,16 @@ __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
   const uint32_t i0 = d.lo + g * 64 + lane();
   const bool act = i0 < d.hi && d.alive[i0] && d.uniform;
   const unsigned long long actm = __ballot(act);
-  if (!actm) return;
+  // the fold's byte counter (bench roofline) is summed over the workgroup and added once: one atomic
+  // per wave on one address serialises thousands of waves in the memory system
+  __shared__ uint32_t s_nb[4];
+  uint32_t nbytes = 0;
+  if (actm) {
   const uint32_t i = act ? i0 : d.lo + g * 64 + (uint32_t)(__ffsll((long long)actm) - 1);   // idle lanes shadow a live one
   const uint32_t* bw = bits_of(d, i);
   const uint32_t spp = NSEG / S;
   const unsigned long long sd = act ? d.sdirty[i] : 0ull;
   unsigned long long folded = 0;
-  uint32_t nbytes = 0;
   for (uint32_t k = s * spp; k < (s + 1) * spp; ++k) {
     const bool mine = (sd >> k) & 1ull;
     if (!__ballot(mine)) continue;                  // wave-uniform: no row of this wave changed here
@@ -192,9 +195,15 @@ __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
     }
     if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; nbytes += d.SEGW / 8; }
   }
-  const uint32_t wb = wave_sum(act ? nbytes : 0u);
-  if (lane() == 0 && wb) atomicAdd(&d.stats[S_FOLDB], (unsigned long long)wb);
   if (folded) atomicAnd(&d.sdirty[i], ~folded);
+  }
+  const uint32_t wb = wave_sum(act ? nbytes : 0u);
+  if (lane() == 0) s_nb[threadIdx.x >> 6] = wb;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = s_nb[0] + s_nb[1] + s_nb[2] + s_nb[3];
+    if (t) atomicAdd(&d.stats[S_FOLDB], (unsigned long long)t);
+  }
 }
 
 // ---- pick the ping target (one of the oldest 5), WaitingForPing(now), Ping; ping_addrs (:550-556);

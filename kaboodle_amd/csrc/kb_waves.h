@@ -106,9 +106,11 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
     atomicAdd(&wc.kcnt[x], s_kc[threadIdx.x]);
     if (s_kp[threadIdx.x]) atomicAdd(&wc.kpay[x], s_kp[threadIdx.x]);
   }
-  for (int k = 0; k < 5; ++k) stat_add(d, S_PING + k, ks[k]);
-  stat_add(d, S_DEAD, dead); stat_add(d, S_PART, part); stat_add(d, S_LOSS, loss); stat_add(d, S_WINDOW, win);
-  stat_add(d, S_KPIDS, kpids);
+  {
+    const int idx[10] = {S_PING, S_PING + 1, S_PING + 2, S_PING + 3, S_PING + 4, S_DEAD, S_PART, S_LOSS, S_WINDOW, S_KPIDS};
+    const unsigned long long v[10] = {ks[0], ks[1], ks[2], ks[3], ks[4], dead, part, loss, win, kpids};
+    stat_add_n(d, idx, v);
+  }
 }
 
 // KnownPeers records are placed in two passes (their order within a destination's group is free: the
@@ -203,9 +205,11 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
     }
     if (!last) x.ostatus[g] = st;
   }
-  for (int k = 0; k < 5; ++k) stat_add(d, S_PING + k, ks[k]);
-  stat_add(d, S_DEAD, dead); stat_add(d, S_PART, part); stat_add(d, S_LOSS, loss); stat_add(d, S_WINDOW, win);
-  stat_add(d, S_KPIDS, kpids);
+  {
+    const int idx[10] = {S_PING, S_PING + 1, S_PING + 2, S_PING + 3, S_PING + 4, S_DEAD, S_PART, S_LOSS, S_WINDOW, S_KPIDS};
+    const unsigned long long v[10] = {ks[0], ks[1], ks[2], ks[3], ks[4], dead, part, loss, win, kpids};
+    stat_add_n(d, idx, v);
+  }
 }
 
 // records / payload ids this shard sends to each shard (from the scans' block starts and totals)
@@ -792,8 +796,11 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
     base = bcast(base, __ffsll((long long)sm) - 1);
     if (to_slow) slow[base + __popcll(sm & ((1ull << lane()) - 1ull))] = i;
   }
-  stat_add(d, S_CUROVF, curovf);
-  stat_add(d, S_OVERSIZE, over);
+  {
+    const int idx[2] = {S_CUROVF, S_OVERSIZE};
+    const unsigned long long v[2] = {curovf, over};
+    stat_add_n(d, idx, v);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r, const uint32_t* list) {
