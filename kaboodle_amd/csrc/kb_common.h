@@ -119,7 +119,10 @@ __device__ __attribute__((always_inline)) inline void stage16(uint4* dst, const 
   }
 }
 __device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }
-__device__ inline void path_hit(const Dev& d, uint32_t bit) { atomicOr(&d.ctr[C_PATHS], bit); }
+// (read first: after the first hit the bit is set and the atomic on that one word is skipped)
+__device__ inline void path_hit(const Dev& d, uint32_t bit) {
+  if (!(__hip_atomic_load(&d.ctr[C_PATHS], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) atomicOr(&d.ctr[C_PATHS], bit);
+}
 __device__ inline bool faults(const Dev& d, int32_t r) { return d.fault_end < 0 || r < d.fault_end; }
 __device__ inline bool local(const Dev& d, uint32_t i) { return i >= d.lo && i < d.hi; }
 __device__ inline bool part_blocks(const Dev& d, int32_t r, uint32_t a, uint32_t b) {
@@ -398,6 +401,9 @@ __device__ inline void stat_add(const Dev& d, int idx, unsigned long long v) {
 // d.stats when the host reads them).  Every workgroup of every wave adding to the same few stats
 // words would serialise in the memory system.
 constexpr uint32_t NACC = 1024;
+__device__ inline void slot_add(const Dev& d, int idx, unsigned long long v) {   // this workgroup's slot
+  atomicAdd(&d.sacc[(size_t)(blockIdx.x % NACC) * NSTAT + idx], v);
+}
 template <int N>
 __device__ inline void stat_add_n(const Dev& d, const int (&idx)[N], const unsigned long long (&v)[N]) {
   __shared__ unsigned long long red[16][N];

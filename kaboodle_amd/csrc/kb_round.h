@@ -552,7 +552,7 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
     unsigned long long t = 0;
     for (uint32_t k = 0; k < wpb; ++k) t += s_cnt[k][threadIdx.x];
     const int idx[7] = {S_BDROP, S_RMFAILED, S_JRESP, S_ROWB, S_A3ROWS, S_A3DEEP, S_A3CHUNKS};
-    if (t) atomicAdd(&d.stats[idx[threadIdx.x]], t);
+    if (t) slot_add(d, idx[threadIdx.x], t);
   }
 }
 

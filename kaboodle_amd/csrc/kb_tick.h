@@ -108,7 +108,7 @@ __device__ __attribute__((always_inline)) inline void tick_a2(const Dev& d, cons
       bs.fail[(size_t)i * SLOTS + q] = p;
     }
     bs.nfail[i] = nrem;
-    if (nrem) { d.n[i] = n; mark(d, i, segs); atomicAdd(&d.stats[S_RMTIMEOUT], nrem); }
+    if (nrem) { d.n[i] = n; mark(d, i, segs); slot_add(d, S_RMTIMEOUT, nrem); }
     ob.cnt[i] = oseq;
   }
 }
@@ -128,7 +128,12 @@ __global__ __launch_bounds__(256) void k_tick_scan(Dev d, BcastSlots bs, int32_t
 #pragma unroll
   for (int k = 0; k < SLOTS; ++k) { const Susp x = sl[k]; tim |= x.kind != 0 && r - x.since >= PING_TIMEOUT; }
   if (!tim) { bs.nfail[i] = 0; return; }
-  list[atomicAdd(&d.ctr[C_TICK], 1u)] = i;
+  // one list reservation per wave (the list counter is one word)
+  const unsigned long long m = __ballot(true);
+  const int first = __ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if (lane() == (uint32_t)first) base = atomicAdd(&d.ctr[C_TICK], (uint32_t)__popcll(m));
+  list[bcast(base, first) + __popcll(m & ((1ull << lane()) - 1ull))] = i;
 }
 
 // ---- A2 handle_suspected_peers (:558-653) for the nodes k_tick_scan listed, one wave per node
@@ -202,7 +207,7 @@ __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t t = s_nb[0] + s_nb[1] + s_nb[2] + s_nb[3];
-    if (t) atomicAdd(&d.stats[S_FOLDB], (unsigned long long)t);
+    if (t) slot_add(d, S_FOLDB, t);
   }
 }
 

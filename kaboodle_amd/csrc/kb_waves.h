@@ -789,13 +789,20 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
     }
     if (!to_slow) wave_ctr_clear(wc, i);              // done with this node for the wave
   }
-  const unsigned long long sm = __ballot(to_slow);  // the rest goes to k_proc
-  if (sm) {
-    uint32_t base = 0;
-    if (lane() == (uint32_t)(__ffsll((long long)sm) - 1)) base = atomicAdd(&d.ctr[C_SLOW], (uint32_t)__popcll(sm));
-    base = bcast(base, __ffsll((long long)sm) - 1);
-    if (to_slow) slow[base + __popcll(sm & ((1ull << lane()) - 1ull))] = i;
+  // the rest goes to k_proc: listed with one atomic per workgroup (the list counter is one word)
+  __shared__ uint32_t s_wn[4], s_wb[4];
+  const unsigned long long sm = __ballot(to_slow);
+  const uint32_t wv = threadIdx.x >> 6;
+  if (lane() == 0) s_wn[wv] = (uint32_t)__popcll(sm);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t a = s_wn[0], b = s_wn[1], c = s_wn[2], e = s_wn[3], tot = a + b + c + e;
+    const uint32_t base = tot ? atomicAdd(&d.ctr[C_SLOW], tot) : 0u;
+    s_wb[0] = base; s_wb[1] = base + a; s_wb[2] = base + a + b; s_wb[3] = base + a + b + c;
+    (void)e;
   }
+  __syncthreads();
+  if (to_slow) slow[s_wb[wv] + __popcll(sm & ((1ull << lane()) - 1ull))] = i;
   {
     const int idx[2] = {S_CUROVF, S_OVERSIZE};
     const unsigned long long v[2] = {curovf, over};
@@ -1194,8 +1201,8 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     __builtin_amdgcn_wave_barrier();
   }
   if (l == 0) {
-    if (w_over) atomicAdd(&d.stats[S_OVERSIZE], w_over);
-    if (w_curovf) atomicAdd(&d.stats[S_CUROVF], w_curovf);
+    if (w_over) slot_add(d, S_OVERSIZE, w_over);
+    if (w_curovf) slot_add(d, S_CUROVF, w_curovf);
   }
 }
 
