@@ -120,9 +120,11 @@ __global__ void k_build_htab(Dev d) {
   }
   d.htab[k] = raw;
 }
-__global__ void k_set_cap(Dev d, const uint32_t* nresp, uint32_t* cap, uint32_t* cnt) {
+// (also hands the wave-0 scan totals to the host: tot[0..4] -> host-mapped hpin[0..4], no copy kernel)
+__global__ void k_set_cap(Dev d, const uint32_t* nresp, uint32_t* cap, uint32_t* cnt, const uint32_t* tot, uint32_t* hpin) {
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (i < d.hi) { cap[i] = nresp[i] + TICK_MAX; cnt[i] = nresp[i]; }
+  if (blockIdx.x == 0 && threadIdx.x < 5) hpin[threadIdx.x] = tot[threadIdx.x];
 }
 __global__ void k_init_nodes(Dev d, uint32_t n0) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -328,8 +330,8 @@ struct kb_sim {
   std::vector<uint32_t> watch_node, watch_fp;
   std::vector<uint32_t*> watch_snap;
   uint32_t* ev_out = nullptr;          // [2*C + 4]: discovered ids, departed ids, counters
-  uint32_t* rres = nullptr;            // [4] device: the round's results (k_round_end)
-  uint32_t* h_pin = nullptr;           // [16] pinned host: small per-round copies (no staging)
+  uint32_t* h_pin = nullptr;           // [16] pinned host memory, mapped: per-round results written by kernels
+  uint32_t* d_pin = nullptr;           //      its device address
 };
 
 // allocation of this handle's device memory; row tables hold the local rows only and their pointer
@@ -522,7 +524,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   A(s->scan_tot, 32); A(s->scan_tiles, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
   AR(s->nresp, 1); AR(s->paysum, 1); AR(s->nbase, 1); AR(s->resp_off, 1);
   A(s->resp_nodes, R); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS); A(s->slow, R);
-  AR(s->ro.part, 10); A(s->rres, 4);
+  AR(s->ro.part, 10);
   if (xf) {
     XState& x = s->xs;
     x.world = (uint32_t)world; x.R = R; x.S = rows_per;
@@ -540,7 +542,10 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (d.lat) { (void)hipMemset(d.lat, 0xFF, 2ull * lat_stride(R) * W); (void)hipMemset(s->fnamed, 0, 4ull * d.NWR); }   // all None
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
-  if (hipHostMalloc((void**)&s->h_pin, 64, hipHostMallocDefault) != hipSuccess) { s->h_pin = nullptr; destroy_shard(s); seterr("pinned buffer"); return KB_IO_ERROR; }
+  if (hipHostMalloc((void**)&s->h_pin, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    s->h_pin = nullptr; destroy_shard(s); seterr("pinned buffer"); return KB_IO_ERROR;
+  }
+  if (hipHostGetDevicePointer((void**)&s->d_pin, s->h_pin, 0) != hipSuccess) { destroy_shard(s); seterr("pinned buffer mapping"); return KB_IO_ERROR; }
   for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->er0, &s->er1, &s->ef0, &s->ef1}) (void)hipEventCreate(e);
   int rc = upload_segments(s);
   if (rc) { destroy_shard(s); return rc; }
@@ -853,10 +858,9 @@ static int step_round(kb_sim* s) {
     a.list = s->resp_nodes; a.list_base = s->lo;
     launch_scan(a, st);
   }
-  k_set_cap<<<gnode, tb, 0, st>>>(d, s->nresp, o0.cap, o0.cnt);
+  k_set_cap<<<gnode, tb, 0, st>>>(d, s->nresp, o0.cap, o0.cnt, s->scan_tot, s->d_pin);
   if (have_b && s->nj) {
-    const uint32_t* tot = s->h_pin;
-    HIPCHK(hipMemcpyAsync(s->h_pin, s->scan_tot, 20, hipMemcpyDeviceToHost, st));
+    const uint32_t* tot = s->h_pin;                 // written by k_set_cap through the host mapping
     HIPCHK(hipStreamSynchronize(st));
     const uint32_t pay_tot = tot[1], msg_tot = tot[2], resp_nodes = tot[4];
     if (msg_tot > o0.msg_cap || pay_tot > o0.pay_cap) {
@@ -993,10 +997,10 @@ static int step_round(kb_sim* s) {
     cur ^= 1;
   }
   if (s->xf && !s->xf->allreduce_sum_u32(d.ctr + C_AGREE, 1, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  k_round_end<<<1, 1, 0, st>>>(d, r, s->scan_tot, s->rres);
+  k_round_end<<<1, 1, 0, st>>>(d, r, s->scan_tot, s->d_pin);
   (void)hipEventRecord(s->er1, st);
-  // one copy and one synchronisation: the next round's broadcast counts and the error flag
-  HIPCHK(hipMemcpyAsync(s->h_pin, s->rres, 12, hipMemcpyDeviceToHost, st));
+  // one synchronisation: k_round_end wrote the next round's broadcast counts and the error flag
+  // straight into the host-mapped pinned buffer
   HIPCHK(hipStreamSynchronize(st));
   const uint32_t nj_loc = s->h_pin[0], nf_loc = s->h_pin[1], err = s->h_pin[2];
   if (s->xf) {

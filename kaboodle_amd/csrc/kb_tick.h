@@ -286,7 +286,8 @@ __global__ void k_bcast_write(Dev d, BcastSlots bs, const uint32_t* join_off, co
   for (uint32_t q = 0; q < nfl; ++q) bfail[fail_off[i] + q] = BCast{i, bs.fail[(size_t)i * SLOTS + q], bseq++, 0};
 }
 
-// round results for the host in one small copy: rres = {Join broadcasts, Failed broadcasts, error}
+// round results for the host, written into its mapped pinned buffer: rres = {Join broadcasts, Failed
+// broadcasts, error}
 __global__ void k_round_end(Dev d, int32_t r, const uint32_t* tot, uint32_t* rres) {
   if (threadIdx.x || blockIdx.x) return;
   const uint32_t a = d.ctr[C_AGREE], al = d.ctr[C_ALIVE];
