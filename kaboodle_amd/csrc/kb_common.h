@@ -118,6 +118,15 @@ __device__ __attribute__((always_inline)) inline void stage16(uint4* dst, const 
     for (int u = 0; u < U; ++u) { const uint32_t w = w0 + lanes * u; if (w < n) dst[w] = v[u]; }
   }
 }
+// hand-off to the host through mapped pinned memory: the values, a system-scope release, then the
+// sequence number the host polls for (one thread)
+constexpr uint32_t PIN_SEQ = 15;
+__device__ inline void pin_publish(uint32_t* h, const uint32_t* v, uint32_t n, uint32_t seq) {
+  for (uint32_t k = 0; k < n; ++k) h[k] = v[k];
+  if (!seq) return;
+  __threadfence_system();
+  __hip_atomic_store(h + PIN_SEQ, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 __device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }
 // (read first: after the first hit the bit is set and the atomic on that one word is skipped)
 __device__ inline void path_hit(const Dev& d, uint32_t bit) {

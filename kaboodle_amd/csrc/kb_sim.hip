@@ -28,6 +28,7 @@
 #include <vector>
 #include <array>
 #include <algorithm>
+#include <atomic>
 #include <thread>
 #include "kb_common.h"
 #include "kb_wire.h"
@@ -120,11 +121,13 @@ __global__ void k_build_htab(Dev d) {
   }
   d.htab[k] = raw;
 }
-// (also hands the wave-0 scan totals to the host: tot[0..4] -> host-mapped hpin[0..4], no copy kernel)
-__global__ void k_set_cap(Dev d, const uint32_t* nresp, uint32_t* cap, uint32_t* cnt, const uint32_t* tot, uint32_t* hpin) {
+// (also hands the wave-0 scan totals to the host: tot[0..4] -> host-mapped hpin[0..4], then the
+// sequence number the host polls for)
+__global__ void k_set_cap(Dev d, const uint32_t* nresp, uint32_t* cap, uint32_t* cnt, const uint32_t* tot, uint32_t* hpin,
+                          uint32_t seq) {
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (i < d.hi) { cap[i] = nresp[i] + TICK_MAX; cnt[i] = nresp[i]; }
-  if (blockIdx.x == 0 && threadIdx.x < 5) hpin[threadIdx.x] = tot[threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 0) pin_publish(hpin, tot, 5, seq);
 }
 __global__ void k_init_nodes(Dev d, uint32_t n0) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -332,6 +335,8 @@ struct kb_sim {
   uint32_t* ev_out = nullptr;          // [2*C + 4]: discovered ids, departed ids, counters
   uint32_t* h_pin = nullptr;           // [16] pinned host memory, mapped: per-round results written by kernels
   uint32_t* d_pin = nullptr;           //      its device address
+  uint32_t pin_seq = 0;                // hand-off sequence number (h_pin[PIN_SEQ])
+  uint64_t occ_key = ~0ull; int occ_val = 0;   // row-pass occupancy query, cached per launch shape
 };
 
 // allocation of this handle's device memory; row tables hold the local rows only and their pointer
@@ -624,6 +629,23 @@ extern "C" int kb_sim_shard_info(kb_sim* s, int32_t* rank, int32_t* world, uint3
   return KB_OK;
 }
 
+// Host side of the pinned hand-offs: spin on the mapped sequence word (a stream synchronisation would
+// pay an interrupt wake-up, tens of microseconds with the GPU idle), with the stream's own status as
+// the way out when it drained without publishing (a fault).
+static int wait_pin(kb_sim* s, uint32_t seq) {
+  volatile uint32_t* p = s->h_pin + PIN_SEQ;
+  for (uint64_t it = 0;; ++it) {
+    if (*p == seq) { std::atomic_thread_fence(std::memory_order_acquire); return KB_OK; }
+    if ((it & 4095) == 4095) {
+      const hipError_t e = hipStreamQuery(s->st);
+      if (e == hipSuccess) {
+        if (*p == seq) { std::atomic_thread_fence(std::memory_order_acquire); return KB_OK; }
+        seterr("stream drained without publishing its results"); return KB_IO_ERROR;
+      }
+      if (e != hipErrorNotReady) { seterr(std::string("stream: ") + hipGetErrorString(e)); return KB_IO_ERROR; }
+    }
+  }
+}
 static int err_status(uint32_t e) {
   if (e) {
     const char* what[] = {"", "suspect slots exhausted", "outbox region overflow", "payload pool overflow",
@@ -836,9 +858,14 @@ static int step_round(kb_sim* s) {
     const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / d.NWR) : RP_WAVES;
     const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
     int occ = 0;                                       // resident workgroups per CU (LDS, registers)
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ldsb ? reinterpret_cast<const void*>(&k_rowpass<true>)
-                                                                   : reinterpret_cast<const void*>(&k_rowpass<false>),
-                                                       (int)(64 * wpb), lds);
+    const uint64_t okey = ((uint64_t)ldsb << 63) | ((uint64_t)wpb << 40) | (uint64_t)lds;   // queried once per shape
+    if (okey == s->occ_key) occ = s->occ_val;
+    else {
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ldsb ? reinterpret_cast<const void*>(&k_rowpass<true>)
+                                                                     : reinterpret_cast<const void*>(&k_rowpass<false>),
+                                                         (int)(64 * wpb), lds);
+      s->occ_key = okey; s->occ_val = occ;
+    }
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)occ));
     const uint32_t blocks = std::min<uint32_t>((R + wpb - 1) / wpb, s->ncu * per_cu);
     if (s->debug_waves && r == 2)
@@ -858,10 +885,11 @@ static int step_round(kb_sim* s) {
     a.list = s->resp_nodes; a.list_base = s->lo;
     launch_scan(a, st);
   }
-  k_set_cap<<<gnode, tb, 0, st>>>(d, s->nresp, o0.cap, o0.cnt, s->scan_tot, s->d_pin);
-  if (have_b && s->nj) {
+  const bool need_tot = have_b && s->nj;
+  k_set_cap<<<gnode, tb, 0, st>>>(d, s->nresp, o0.cap, o0.cnt, s->scan_tot, s->d_pin, need_tot ? ++s->pin_seq : 0u);
+  if (need_tot) {
     const uint32_t* tot = s->h_pin;                 // written by k_set_cap through the host mapping
-    HIPCHK(hipStreamSynchronize(st));
+    { const int rc = wait_pin(s, s->pin_seq); if (rc) return rc; }
     const uint32_t pay_tot = tot[1], msg_tot = tot[2], resp_nodes = tot[4];
     if (msg_tot > o0.msg_cap || pay_tot > o0.pay_cap) {
       const int rc = grow_wave0(s, msg_tot, pay_tot);
@@ -997,10 +1025,11 @@ static int step_round(kb_sim* s) {
     cur ^= 1;
   }
   if (s->xf && !s->xf->allreduce_sum_u32(d.ctr + C_AGREE, 1, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  k_round_end<<<1, 1, 0, st>>>(d, r, s->scan_tot, s->d_pin);
+  k_round_end<<<1, 1, 0, st>>>(d, r, s->scan_tot, s->d_pin, ++s->pin_seq);
   (void)hipEventRecord(s->er1, st);
-  // one synchronisation: k_round_end wrote the next round's broadcast counts and the error flag
-  // straight into the host-mapped pinned buffer
+  // k_round_end wrote the next round's broadcast counts and the error flag straight into the
+  // host-mapped pinned buffer; the host polls for them, then finds the stream drained
+  { const int rc = wait_pin(s, s->pin_seq); if (rc) return rc; }
   HIPCHK(hipStreamSynchronize(st));
   const uint32_t nj_loc = s->h_pin[0], nf_loc = s->h_pin[1], err = s->h_pin[2];
   if (s->xf) {

@@ -288,12 +288,13 @@ __global__ void k_bcast_write(Dev d, BcastSlots bs, const uint32_t* join_off, co
 
 // round results for the host, written into its mapped pinned buffer: rres = {Join broadcasts, Failed
 // broadcasts, error}
-__global__ void k_round_end(Dev d, int32_t r, const uint32_t* tot, uint32_t* rres) {
+__global__ void k_round_end(Dev d, int32_t r, const uint32_t* tot, uint32_t* rres, uint32_t seq) {
   if (threadIdx.x || blockIdx.x) return;
   const uint32_t a = d.ctr[C_AGREE], al = d.ctr[C_ALIVE];
   d.ctr[C_LASTAGREE] = a; d.ctr[C_LASTALIVE] = al;
   if (d.lo == 0) d.stats[S_ALIVER] += al;          // the running set is replicated: shard 0 counts it
-  rres[0] = tot[0]; rres[1] = tot[1]; rres[2] = d.ctr[C_ERR];
+  const uint32_t v[3] = {tot[0], tot[1], d.ctr[C_ERR]};
+  pin_publish(rres, v, 3, seq);
   if (al && a == al) {
     if ((int32_t)d.ctr[C_FIRSTCONV] < 0) d.ctr[C_FIRSTCONV] = (uint32_t)r;
     d.ctr[C_LASTCONV] = (uint32_t)r;
