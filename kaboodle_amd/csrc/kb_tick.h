@@ -8,16 +8,6 @@ namespace kb {
 
 struct BcastSlots { uint32_t* join; uint32_t* nfail; uint32_t* fail; };
 
-// Candidates of handle_suspected_peers (Known && != self, :571-577) in 16-id blocks: member bit set,
-// stamp byte >= 2 (not WaitingFor*), not self.
-__device__ inline uint32_t cand16(const Dev& d, const uint8_t* rw, const uint32_t* bw, uint32_t i, uint32_t j0) {
-  const uint4 v = *reinterpret_cast<const uint4*>(rw + j0);
-  const uint32_t m = nzmask4(v.x & 0xFEFEFEFEu) | (nzmask4(v.y & 0xFEFEFEFEu) << 4) |
-                     (nzmask4(v.z & 0xFEFEFEFEu) << 8) | (nzmask4(v.w & 0xFEFEFEFEu) << 12);
-  uint32_t c = m & ((bw[j0 >> 5] >> (j0 & 16)) & 0xFFFFu);
-  if (i >= j0 && i < j0 + 16) c &= ~(1u << (i - j0));
-  return c;
-}
 __device__ __attribute__((always_inline)) inline void tick_a2(const Dev& d, const OutBuf& ob, const BcastSlots& bs, int32_t r,
                                                               uint32_t i, uint32_t l, uint32_t* pr, uint32_t* pp,
                                                               uint32_t* pid) {
@@ -61,29 +51,53 @@ __device__ __attribute__((always_inline)) inline void tick_a2(const Dev& d, cons
       removed[nrem++] = peer;
     }
   }
-  const uint8_t* rw = row_of(d, i);
   uint32_t oseq = ob.cnt[i];
   if (npick) {                                            // choose_multiple over the candidate list
-    // rank -> id for every pick in coalesced passes over the row: lane l takes ids [j0 + 16 l, +16)
-    // of each 1024-id pass, four passes' loads in flight; a pass resolves the picks whose rank
-    // falls in its candidate range (ranks are in address order, :571-577)
+    // rank -> id for every pick from the membership bitset alone: the candidates (Known, != self,
+    // :571-577) are the members minus self minus the suspect slots (the members whose stamp byte is
+    // WaitingFor*), so no stamp byte is read.  Lane l takes ids [128 w, +128) of 16-byte word
+    // w = w0 + 64 u + l: 8 words per lane in flight (64 K ids per step, the whole 64K-peer row in one
+    // memory round trip); a word resolves the picks whose rank falls in its candidate range (ranks are
+    // in address order)
     wait_lds();
     __builtin_amdgcn_wave_barrier();
-    const uint32_t* bw = bits_of(d, i);
+    const uint4* b4 = reinterpret_cast<const uint4*>(bits_of(d, i));
+    uint32_t ex[SLOTS + 1];                               // excluded members: self, the suspects
+    ex[0] = i;
+#pragma unroll
+    for (int k = 0; k < SLOTS; ++k) ex[k + 1] = ((occm >> k) & 1ull) ? bcast(me.peer, k) : 0xFFFFFFFFu;
     uint32_t maxrank = 0;
     for (uint32_t q = 0; q < npick; ++q) maxrank = pr[q] > maxrank ? pr[q] : maxrank;
+    const uint32_t n4 = d.NWR / 4;
     uint32_t base = 0;
-    for (uint32_t j0 = 0; j0 < d.W && base <= maxrank; j0 += 4096) {
-      uint32_t mk[4];
+    constexpr int PB = 8;
+    for (uint32_t w0 = 0; w0 < n4 && base <= maxrank; w0 += 64 * PB) {
+      uint4 v[PB];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) { const uint32_t j = j0 + 1024 * u + 16 * l; mk[u] = j < d.W ? cand16(d, rw, bw, i, j) : 0u; }
+      for (int u = 0; u < PB; ++u) { const uint32_t w = w0 + 64u * u + l; v[u] = w < n4 ? b4[w] : make_uint4(0, 0, 0, 0); }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t j = j0 + 1024 * u + 16 * l;
-        const uint32_t pc = __popc(mk[u]), ex = wave_excl(pc), tot = wave_sum(pc);
+      for (int u = 0; u < PB; ++u) {
+        if (base > maxrank) break;                        // wave-uniform
+        const uint32_t w = w0 + 64u * u + l, id0 = w * 128;
+        const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+        uint32_t c = __popc(wd[0]) + __popc(wd[1]) + __popc(wd[2]) + __popc(wd[3]);
+#pragma unroll
+        for (int k = 0; k <= SLOTS; ++k) c -= (ex[k] - id0 < 128u) ? 1u : 0u;   // excluded ids are members
+        const uint32_t exl = wave_excl(c), tot = wave_sum(c);
         for (uint32_t q = 0; q < npick; ++q) {
           const uint32_t rk = pr[q];
-          if (rk >= base + ex && rk < base + ex + pc) pid[q] = j + select_in_word(mk[u], rk - base - ex);
+          if (rk >= base + exl && rk < base + exl + c) {
+            uint32_t rem = rk - base - exl, id = 0xFFFFFFFFu;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              uint32_t m = wd[k];
+#pragma unroll
+              for (int e = 0; e <= SLOTS; ++e) if ((ex[e] >> 5) == w * 4 + k) m &= ~(1u << (ex[e] & 31));
+              const uint32_t pc = __popc(m);
+              if (id == 0xFFFFFFFFu) { if (rem < pc) id = id0 + 32 * k + select_in_word(m, rem); else rem -= pc; }
+            }
+            pid[q] = id;
+          }
         }
         base += tot;
       }
