@@ -935,7 +935,7 @@ static int step_round(kb_sim* s) {
   // is still executing)
   if (d.uniform)
     hipExtLaunchKernelGGL(k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, st, s->ef0, s->ef1, 0, d, FoldArgs{s->S});
-  if (d.uniform) k_fp_quad<<<(4 * R + tb - 1) / tb, tb, 0, st>>>(d);
+  if (d.uniform) k_fp_rows<<<(FP_LANES * R + tb - 1) / tb, tb, 0, st>>>(d);
   k_tick_post<<<gnode, tb, 0, st>>>(d, s->ro, o0, r);
   {
     ScanArgs a = scan_args(s, R, s->scan_tot);

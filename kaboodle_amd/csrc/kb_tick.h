@@ -225,38 +225,38 @@ __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
   }
 }
 
-// ---- fingerprints of the rows whose membership changed (:71-83), from their fresh checkpoints: four
-// lanes per row, each combining 16 checkpoints (16 Z^cnt multiplies), then two combine levels across
-// the four.  Spreading the 64-multiply chain over four lanes gives the SIMDs four times the waves to
-// hide its latency with.  Runs after k_fold; k_tick_post then finds the row clean.
-__global__ __launch_bounds__(256) void k_fp_quad(Dev d) {
+// ---- fingerprints of the rows whose membership changed (:71-83), from their fresh checkpoints:
+// FP_LANES lanes per row, each combining NSEG / FP_LANES checkpoints (one Z^cnt multiply each), then
+// log2(FP_LANES) combine levels across them in address order.  Spreading the 64-multiply chain over
+// several lanes gives the SIMDs that many times the waves to hide its latency with.  Runs after
+// k_fold; k_tick_post then finds the row clean.
+constexpr uint32_t FP_LANES = 8;
+__global__ __launch_bounds__(256) void k_fp_rows(Dev d) {
+  constexpr uint32_t PER = NSEG / FP_LANES;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t i = d.lo + (t >> 2), part = t & 3u;
+  const uint32_t i = d.lo + t / FP_LANES, part = t % FP_LANES;
   const bool on = i < d.hi && d.uniform && d.alive[i] && d.dirty[i];
   uint32_t raw = 0, cnt = 0;
   if (on) {
-    const uint4* sp4 = reinterpret_cast<const uint4*>(d.segp + (size_t)i * NSEG + 16 * part);   // two checkpoints per 16 B
-    uint4 q[8];
+    const uint4* sp4 = reinterpret_cast<const uint4*>(d.segp + (size_t)i * NSEG + PER * part);   // two checkpoints per 16 B
+    uint4 q[PER / 2];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) q[k] = sp4[k];
-    uint32_t z[16];
+    for (uint32_t k = 0; k < PER / 2; ++k) q[k] = sp4[k];
+    uint32_t z[PER];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) { const uint32_t c = (k & 1) ? q[k >> 1].w : q[k >> 1].y; z[k] = c ? d.zpow[c] : 0u; }
+    for (uint32_t k = 0; k < PER; ++k) { const uint32_t c = (k & 1) ? q[k >> 1].w : q[k >> 1].y; z[k] = c ? d.zpow[c] : 0u; }
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
+    for (uint32_t k = 0; k < PER; ++k) {
       const uint32_t x = (k & 1) ? q[k >> 1].z : q[k >> 1].x, c = (k & 1) ? q[k >> 1].w : q[k >> 1].y;
       if (c) { raw = multmodp(z[k], raw) ^ x; cnt += c; }
     }
   }
-  // combine (0,1) and (2,3), then the pairs, in address order
-  const uint32_t raw1 = __shfl_down(raw, 1, 64), cnt1 = __shfl_down(cnt, 1, 64);
-  if (on && !(part & 1u)) { raw = multmodp(d.zpow[cnt1], raw) ^ raw1; cnt += cnt1; }
-  const uint32_t raw2 = __shfl_down(raw, 2, 64), cnt2 = __shfl_down(cnt, 2, 64);
-  if (on && part == 0) {
-    raw = multmodp(d.zpow[cnt2], raw) ^ raw2; cnt += cnt2;
-    d.fp[i] = finish_fp(d, raw, cnt);
-    d.dirty[i] = 0;
+#pragma unroll
+  for (uint32_t st = 1; st < FP_LANES; st <<= 1) {    // combine (part, part + st) for part % 2st == 0
+    const uint32_t r2 = __shfl_down(raw, st, 64), c2 = __shfl_down(cnt, st, 64);
+    if (on && (part & (2 * st - 1)) == 0) { raw = multmodp(d.zpow[c2], raw) ^ r2; cnt += c2; }
   }
+  if (on && part == 0) { d.fp[i] = finish_fp(d, raw, cnt); d.dirty[i] = 0; }
 }
 
 // ---- pick the ping target (one of the oldest 5), WaitingForPing(now), Ping; ping_addrs (:550-556);
