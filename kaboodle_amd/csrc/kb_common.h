@@ -31,6 +31,7 @@ enum CtrIdx {
   C_DBG_TNODE, C_DBG_TMAX, C_DBG_TBASE, C_DBG_TINS,   // KB_DEV & 64: k_proc wall time (10 ns ticks) per part
   C_DBG_TSTART, C_DBG_TEND, C_DBG_MSGS,
   C_TICK,
+  C_ROUND,                        // the round being simulated (k_log_mark): graph-replayed kernels read it here
   C_PATHS,                        // OR of the PATH_* bits of the kernel variants that did work (test surface)
   NCTR
 };
@@ -126,6 +127,10 @@ __device__ inline void pin_publish(uint32_t* h, const uint32_t* v, uint32_t n, u
   if (!seq) return;
   __threadfence_system();
   __hip_atomic_store(h + PIN_SEQ, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// a wave kernel's round: its argument, or (argument < 0, the graph-captured receive window) the device copy
+__device__ inline int32_t round_of(const Dev& d, int32_t r_arg) {
+  return r_arg >= 0 ? r_arg : (int32_t)__builtin_amdgcn_readfirstlane(d.ctr[C_ROUND]);
 }
 __device__ inline void set_err(const Dev& d, uint32_t e) { atomicCAS(&d.ctr[C_ERR], 0u, e); }
 // (read first: after the first hit the bit is set and the atomic on that one word is skipped)

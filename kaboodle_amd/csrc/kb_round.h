@@ -115,6 +115,7 @@ static_assert(TRUEFP_G == 64, "k_truefp_fin combines one partial per lane");
 // round start of every node's freshness log window
 __global__ void k_log_mark(Dev d, int32_t r) {
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.ctr[C_ROUND] = (uint32_t)r;   // for the graph-replayed waves
   if (i < d.hi) d.fstart[(size_t)i * 16 + ((uint32_t)r & 15u)] = d.flog_n[i];
 }
 

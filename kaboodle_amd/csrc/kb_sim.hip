@@ -337,6 +337,10 @@ struct kb_sim {
   uint32_t* d_pin = nullptr;           //      its device address
   uint32_t pin_seq = 0;                // hand-off sequence number (h_pin[PIN_SEQ])
   uint64_t occ_key = ~0ull; int occ_val = 0;   // row-pass occupancy query, cached per launch shape
+  // the unsharded receive window as a HIP graph (launch_waves), re-captured when buffers are regrown
+  bool graph_on = true;
+  hipGraph_t wave_graph = nullptr; hipGraphExec_t wave_exec = nullptr;
+  uint64_t buf_gen = 0, wave_gen = ~0ull;
 };
 
 // allocation of this handle's device memory; row tables hold the local rows only and their pointer
@@ -440,6 +444,8 @@ static void destroy_shard(kb_sim* s) {
   free_all(s);
   for (hipEvent_t e : {s->ev0, s->ev1, s->er0, s->er1, s->ef0, s->ef1}) if (e) (void)hipEventDestroy(e);
   if (s->h_pin) (void)hipHostFree(s->h_pin);
+  if (s->wave_exec) (void)hipGraphExecDestroy(s->wave_exec);
+  if (s->wave_graph) (void)hipGraphDestroy(s->wave_graph);
   if (s->st) (void)hipStreamDestroy(s->st);
   delete s->xf;
   delete s;
@@ -499,6 +505,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   d.dbg = cfg->debug_flags;
   if (const char* dv = getenv("KB_DEV")) d.dev = (uint32_t)atoi(dv);
   s->debug_waves = getenv("KB_DEBUG_WAVES") != nullptr;
+  s->graph_on = getenv("KB_NO_GRAPH") == nullptr;
   s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid); s->h_ever.assign(C, 0);
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &s->h_ident[(size_t)j * MAXID]);
   for (uint32_t j = 0; j < cfg->initial_nodes; ++j) s->h_ever[j] = 1;
@@ -675,6 +682,7 @@ template <class T> static hipError_t regrow(kb_sim* s, T** p, size_t n) {
 // exceed it, it grows, with the buffers indexed by its slots (record status, inbox lists, send side).
 static int grow_wave0(kb_sim* s, size_t need_msg, size_t need_pay) {
   OutBuf& o0 = s->ob[0];
+  s->buf_gen++;                                    // the captured receive window holds the old buffers
   const size_t lim = 0xF0000000ull;
   if (need_pay > o0.pay_cap) {
     const size_t cap = std::min(lim, need_pay + need_pay / 4);
@@ -786,6 +794,96 @@ static int gather_broadcasts(kb_sim* s, uint32_t nj_loc, uint32_t nf_loc) {
     seterr(s->xf->error()); return KB_IO_ERROR;
   }
   s->nj = (uint32_t)oj; s->nf = (uint32_t)of;
+  return KB_OK;
+}
+
+// The receive window's delivery waves.  rk is the round the kernels take as
+// argument; rk < 0 makes them read it from the device (d.ctr[C_ROUND], set by k_log_mark), which lets
+// the unsharded window be captured once as a HIP graph and replayed every round.
+static int launch_waves(kb_sim* s, int32_t rk) {
+  Dev& d = s->d;
+  const int32_t r = rk;
+  const uint32_t R = s->R;
+  hipStream_t st = s->st;
+  const uint32_t tb = 256, gnode = (R + tb - 1) / tb;
+  int cur = 0;
+  for (uint32_t w = 0; w <= s->cfg.max_waves; ++w) {
+    OutBuf& ob = s->ob[cur];
+    OutBuf& nb = s->ob[cur ^ 1];
+    const int last = w == s->cfg.max_waves;
+    d.wave = (int32_t)w;                               // latency clock of the wave's prologues
+    OutBuf ib = ob;                                    // the wave's delivered records
+    uint32_t nrecv = 0;
+    if (!s->xf) {
+      k_route<<<gnode, tb, 0, st>>>(d, ob, s->wc, r, w, last);
+      if (last) break;
+    } else {
+      HIPCHK(hipMemsetAsync(s->xs.xcnt, 0, 4ull * s->world * R, st));
+      HIPCHK(hipMemsetAsync(s->xs.xpay, 0, 4ull * s->world * R, st));
+      k_route_x<<<gnode, tb, 0, st>>>(d, ob, s->xs, r, w, last);
+      if (last) break;
+      RecvBlocks rb;
+      memset(&rb, 0, sizeof rb);
+      bool any = true;
+      int rc = exchange_wave(s, ob, nrecv, rb, any);
+      if (rc) return rc;
+      if (!any) break;                                 // no record anywhere: the rest of the round's waves are empty
+      ib.msgs = s->rmsg; ib.pay = s->rpay;
+      if (nrecv) k_route_recv<<<(nrecv + 255) / 256, 256, 0, st>>>(d, ib, s->wc, rb, nrecv);
+    }
+    {
+      ScanArgs a = scan_args(s, R, s->scan_tot + 8);
+      a.narr = 4;
+      a.in[0] = L(s, s->wc.cnt1); a.out[0] = L(s, s->wc.in_off);
+      a.in[1] = L(s, s->wc.bnd); a.out[1] = L(s, nb.off);
+      a.in[2] = L(s, s->wc.bpay); a.out[2] = L(s, nb.poff);
+      a.in[3] = L(s, s->wc.kcnt); a.out[3] = L(s, s->wc.koff);
+      a.list = s->wc.active; a.list_count = d.ctr + C_ACTIVE; a.list_base = s->lo; a.list_or3 = 1;
+      launch_scan(a, st);
+    }
+    if (s->debug_waves) {                               // KB_DEBUG_WAVES: inbox sizes per wave
+      std::vector<uint32_t> c1(R);
+      HIPCHK(hipMemcpyAsync(c1.data(), L(s, s->wc.cnt1), 4ull * R, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      uint64_t sum = 0; uint32_t mx = 0, arg = 0, big = 0;
+      for (uint32_t k = 0; k < R; ++k) { sum += c1[k]; if (c1[k] > mx) { mx = c1[k]; arg = s->lo + k; } big += c1[k] > 64; }
+      fprintf(stderr, "[kb] round %d wave %u: in-order msgs %llu, max inbox %u (node %u), inboxes > 64: %u\n", r, w,
+              (unsigned long long)sum, mx, arg, big);
+    }
+    if (!s->xf) k_scatter<<<gnode, tb, 0, st>>>(d, ob, s->wc);
+    else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
+    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
+    k_kp_small<<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r, nb);   // also sets up nb.cap / nb.cnt
+    {  // BIG groups in LDS: KP_COLS workgroups per destination group, one per column part
+      const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
+      const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
+      k_kp_group<true><<<ks * groups, 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
+    }
+    k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc, r);   // + the KPR oversize probe
+    k_proc_fast<<<gnode, tb, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
+    // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
+    // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
+    // on the late waves with few nodes.
+    k_proc<<<std::min<uint32_t>(4096, 2 * s->ncu), 256, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
+    if (s->debug_waves) {
+      uint32_t dbg[13], slow = 0;
+      HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(&slow, d.ctr + C_SLOW, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      fprintf(stderr, "[kb] round %d wave %u: k_proc nodes %u, prologue inserts %u, fingerprint refreshes %u (max per "
+              "node %u), KPR scans %u (log entries %u), incremental bases %u\n", r, w, slow, dbg[0], dbg[1], dbg[2], dbg[3],
+              dbg[4], dbg[5]);
+      if (d.dev & 128)
+        fprintf(stderr, "[kb] round %d wave %u: k_kp_group BIG workgroup-destinations %u, messages %u: stage+arms %.1f us, "
+                "prologues %.1f, write-back+refold %.1f (sums), max total %.1f\n", r, w, dbg[10], dbg[12], dbg[6] * 0.01,
+                dbg[8] * 0.01, dbg[9] * 0.01, dbg[7] * 0.01);
+      if (d.dev & 64)
+        fprintf(stderr, "[kb] round %d wave %u: k_proc node time sum %.1f us (max %.1f), take_base %.1f, insertions %.1f, "
+                "start %.1f, end %.1f, messages %u\n", r, w, dbg[6] * 0.01, dbg[7] * 0.01, dbg[8] * 0.01, dbg[9] * 0.01,
+                dbg[10] * 0.01, dbg[11] * 0.01, dbg[12]);
+    }
+    cur ^= 1;
+  }
   return KB_OK;
 }
 
@@ -946,84 +1044,27 @@ static int step_round(kb_sim* s) {
   }
   k_bcast_write<<<gnode, tb, 0, st>>>(d, s->bs, s->join_off, s->fail_off, s->xf ? s->bjoin_loc : s->bjoin,
                                       s->xf ? s->bfail_loc : s->bfail);
-  // 4. receive window: unicast waves
-  int cur = 0;
-  for (uint32_t w = 0; w <= s->cfg.max_waves; ++w) {
-    OutBuf& ob = s->ob[cur];
-    OutBuf& nb = s->ob[cur ^ 1];
-    const int last = w == s->cfg.max_waves;
-    d.wave = (int32_t)w;                               // latency clock of the wave's prologues
-    OutBuf ib = ob;                                    // the wave's delivered records
-    uint32_t nrecv = 0;
-    if (!s->xf) {
-      k_route<<<gnode, tb, 0, st>>>(d, ob, s->wc, r, w, last);
-      if (last) break;
-    } else {
-      HIPCHK(hipMemsetAsync(s->xs.xcnt, 0, 4ull * s->world * R, st));
-      HIPCHK(hipMemsetAsync(s->xs.xpay, 0, 4ull * s->world * R, st));
-      k_route_x<<<gnode, tb, 0, st>>>(d, ob, s->xs, r, w, last);
-      if (last) break;
-      RecvBlocks rb;
-      memset(&rb, 0, sizeof rb);
-      bool any = true;
-      int rc = exchange_wave(s, ob, nrecv, rb, any);
-      if (rc) return rc;
-      if (!any) break;                                 // no record anywhere: the rest of the round's waves are empty
-      ib.msgs = s->rmsg; ib.pay = s->rpay;
-      if (nrecv) k_route_recv<<<(nrecv + 255) / 256, 256, 0, st>>>(d, ib, s->wc, rb, nrecv);
+  // 4. receive window: unicast waves.  Unsharded, the window has no host decision inside it: its ≈ 80
+  // launches are one HIP graph, captured once per buffer generation and replayed each round (the host
+  // otherwise pays ≈ 5 µs per launch, which the late, nearly empty waves cannot hide).
+  if (!s->xf && !s->debug_waves && s->graph_on) {
+    if (!s->wave_exec || s->wave_gen != s->buf_gen) {
+      if (s->wave_exec) { (void)hipGraphExecDestroy(s->wave_exec); s->wave_exec = nullptr; }
+      if (s->wave_graph) { (void)hipGraphDestroy(s->wave_graph); s->wave_graph = nullptr; }
+      HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      const int rc = launch_waves(s, -1);
+      hipGraph_t g = nullptr;
+      const hipError_t e = hipStreamEndCapture(st, &g);
+      if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
+      HIPCHK(e);
+      s->wave_graph = g;
+      HIPCHK(hipGraphInstantiate(&s->wave_exec, g, nullptr, nullptr, 0));
+      s->wave_gen = s->buf_gen;
     }
-    {
-      ScanArgs a = scan_args(s, R, s->scan_tot + 8);
-      a.narr = 4;
-      a.in[0] = L(s, s->wc.cnt1); a.out[0] = L(s, s->wc.in_off);
-      a.in[1] = L(s, s->wc.bnd); a.out[1] = L(s, nb.off);
-      a.in[2] = L(s, s->wc.bpay); a.out[2] = L(s, nb.poff);
-      a.in[3] = L(s, s->wc.kcnt); a.out[3] = L(s, s->wc.koff);
-      a.list = s->wc.active; a.list_count = d.ctr + C_ACTIVE; a.list_base = s->lo; a.list_or3 = 1;
-      launch_scan(a, st);
-    }
-    if (s->debug_waves) {                               // KB_DEBUG_WAVES: inbox sizes per wave
-      std::vector<uint32_t> c1(R);
-      HIPCHK(hipMemcpyAsync(c1.data(), L(s, s->wc.cnt1), 4ull * R, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      uint64_t sum = 0; uint32_t mx = 0, arg = 0, big = 0;
-      for (uint32_t k = 0; k < R; ++k) { sum += c1[k]; if (c1[k] > mx) { mx = c1[k]; arg = s->lo + k; } big += c1[k] > 64; }
-      fprintf(stderr, "[kb] round %d wave %u: in-order msgs %llu, max inbox %u (node %u), inboxes > 64: %u\n", r, w,
-              (unsigned long long)sum, mx, arg, big);
-    }
-    if (!s->xf) k_scatter<<<gnode, tb, 0, st>>>(d, ob, s->wc);
-    else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
-    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
-    k_kp_small<<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r, nb);   // also sets up nb.cap / nb.cnt
-    {  // BIG groups in LDS: KP_COLS workgroups per destination group, one per column part
-      const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
-      const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
-      k_kp_group<true><<<ks * groups, 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
-    }
-    k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc, r);   // + the KPR oversize probe
-    k_proc_fast<<<gnode, tb, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
-    // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
-    // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
-    // on the late waves with few nodes.
-    k_proc<<<std::min<uint32_t>(4096, 2 * s->ncu), 256, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
-    if (s->debug_waves) {
-      uint32_t dbg[13], slow = 0;
-      HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipMemcpyAsync(&slow, d.ctr + C_SLOW, 4, hipMemcpyDeviceToHost, st));
-      HIPCHK(hipStreamSynchronize(st));
-      fprintf(stderr, "[kb] round %d wave %u: k_proc nodes %u, prologue inserts %u, fingerprint refreshes %u (max per "
-              "node %u), KPR scans %u (log entries %u), incremental bases %u\n", r, w, slow, dbg[0], dbg[1], dbg[2], dbg[3],
-              dbg[4], dbg[5]);
-      if (d.dev & 128)
-        fprintf(stderr, "[kb] round %d wave %u: k_kp_group BIG workgroup-destinations %u, messages %u: stage+arms %.1f us, "
-                "prologues %.1f, write-back+refold %.1f (sums), max total %.1f\n", r, w, dbg[10], dbg[12], dbg[6] * 0.01,
-                dbg[8] * 0.01, dbg[9] * 0.01, dbg[7] * 0.01);
-      if (d.dev & 64)
-        fprintf(stderr, "[kb] round %d wave %u: k_proc node time sum %.1f us (max %.1f), take_base %.1f, insertions %.1f, "
-                "start %.1f, end %.1f, messages %u\n", r, w, dbg[6] * 0.01, dbg[7] * 0.01, dbg[8] * 0.01, dbg[9] * 0.01,
-                dbg[10] * 0.01, dbg[11] * 0.01, dbg[12]);
-    }
-    cur ^= 1;
+    HIPCHK(hipGraphLaunch(s->wave_exec, st));
+  } else {
+    const int rc = launch_waves(s, r);
+    if (rc) return rc;
   }
   if (s->xf && !s->xf->allreduce_sum_u32(d.ctr + C_AGREE, 1, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
   k_round_end<<<1, 1, 0, st>>>(d, r, s->scan_tot, s->d_pin, ++s->pin_seq);

@@ -59,7 +59,8 @@ __device__ inline uint32_t kagg_find(uint32_t* kd, uint32_t dest, bool insert) {
 
 // delivery decisions for every message of the wave: dead receiver, partition, loss (Philox keyed on
 // the message), else delivered; counts per destination.
-__global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int32_t r, uint32_t w, int last) {
+__global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int32_t r_arg, uint32_t w, int last) {
+  const int32_t r = round_of(d, r_arg);
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
   __shared__ uint32_t s_kd[KAGG], s_kc[KAGG], s_kp[KAGG];
   const uint32_t wv = threadIdx.x >> 6, l = lane();
@@ -324,7 +325,8 @@ __host__ __device__ constexpr size_t kp_lds_bytes(uint32_t nwr) {
 }
 
 template <bool BIG>
-__global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib, WaveCtl wc, int32_t r) {
+__global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib, WaveCtl wc, int32_t r_arg) {
+  const int32_t r = round_of(d, r_arg);
   extern __shared__ __attribute__((aligned(16))) uint32_t kp_lds[];
   __shared__ unsigned long long s_segs;
   __shared__ uint32_t s_add, s_nl;
@@ -521,7 +523,8 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
 
 // The groups under KP_BIG ids (KnownPeersRequest replies, small Join lists): a wave per destination,
 // in place on the row's bitset, the same arms-then-prologues order as k_kp_group.
-__global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, int32_t r, OutBuf nb) {
+__global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, int32_t r_arg, OutBuf nb) {
+  const int32_t r = round_of(d, r_arg);
   __shared__ uint32_t s_list[256], s_nl;
   const uint32_t t = threadIdx.x, wv = t >> 6, l = lane();
   {  // the next outbox of every local row: capacity = the wave's reservation, empty (was a copy + memset)
@@ -645,7 +648,8 @@ __device__ __attribute__((always_inline)) inline void kpr_probe(const Dev& d, co
 // selection path of k_proc)
 constexpr uint32_t SORT_MAX = 8192;
 __device__ inline uint32_t sort_max(const Dev& d) { return (d.dbg & KB_DBG_PROC_UNSORTED) ? 64u : SORT_MAX; }
-__global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc, int32_t r) {
+__global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc, int32_t r_arg) {
+  const int32_t r = round_of(d, r_arg);
   __shared__ uint32_t v[SORT_MAX];
   __shared__ uint32_t s_list[1024], s_nl;
   const uint32_t nact = d.ctr[C_ACTIVE];
@@ -698,7 +702,8 @@ __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc, int32_t 
 // `slow` list for k_proc (same semantics: prologue :406-415, Ping :513-532, PingRequest :533-545,
 // Ack :418-447, maybe_sync :707-740).
 constexpr uint32_t FAST_MAX = 8;
-__global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r, uint32_t* slow) {
+__global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, uint32_t* slow) {
+  const int32_t r = round_of(d, r_arg);
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint32_t it = blockIdx.x * blockDim.x + threadIdx.x;
   const uint8_t now = enc(r, r);
@@ -810,7 +815,8 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
   }
 }
 
-__global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r, const uint32_t* list) {
+__global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32_t* list) {
+  const int32_t r = round_of(d, r_arg);
   __shared__ uint32_t ztab[ZT * 128];
   __shared__ Susp s_susp[4][SLOTS];
   __shared__ Cur s_cur[4][CSLOTS];
