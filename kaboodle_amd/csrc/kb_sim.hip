@@ -338,7 +338,7 @@ struct kb_sim {
   uint32_t pin_seq = 0;                // hand-off sequence number (h_pin[PIN_SEQ])
   uint64_t occ_key = ~0ull; int occ_val = 0;   // row-pass occupancy query, cached per launch shape
   // the unsharded receive window as a HIP graph (launch_waves), re-captured when buffers are regrown
-  bool graph_on = true;
+  bool graph_on = false;               // env KB_WAVE_GRAPH=1
   hipGraph_t wave_graph = nullptr; hipGraphExec_t wave_exec = nullptr;
   uint64_t buf_gen = 0, wave_gen = ~0ull;
 };
@@ -505,7 +505,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   d.dbg = cfg->debug_flags;
   if (const char* dv = getenv("KB_DEV")) d.dev = (uint32_t)atoi(dv);
   s->debug_waves = getenv("KB_DEBUG_WAVES") != nullptr;
-  s->graph_on = getenv("KB_NO_GRAPH") == nullptr;
+  s->graph_on = getenv("KB_WAVE_GRAPH") != nullptr;
   s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid); s->h_ever.assign(C, 0);
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &s->h_ident[(size_t)j * MAXID]);
   for (uint32_t j = 0; j < cfg->initial_nodes; ++j) s->h_ever[j] = 1;
@@ -1044,9 +1044,10 @@ static int step_round(kb_sim* s) {
   }
   k_bcast_write<<<gnode, tb, 0, st>>>(d, s->bs, s->join_off, s->fail_off, s->xf ? s->bjoin_loc : s->bjoin,
                                       s->xf ? s->bfail_loc : s->bfail);
-  // 4. receive window: unicast waves.  Unsharded, the window has no host decision inside it: its ≈ 80
-  // launches are one HIP graph, captured once per buffer generation and replayed each round (the host
-  // otherwise pays ≈ 5 µs per launch, which the late, nearly empty waves cannot hide).
+  // 4. receive window: unicast waves.  Unsharded, the window has no host decision inside it, so with
+  // KB_WAVE_GRAPH=1 its ≈ 80 launches are one HIP graph, captured once per buffer generation and
+  // replayed each round: that removes host launch gaps in multi-round steps, but the benched one-round
+  // steps are GPU-bound and measured no faster, so it is off by default.
   if (!s->xf && !s->debug_waves && s->graph_on) {
     if (!s->wave_exec || s->wave_gen != s->buf_gen) {
       if (s->wave_exec) { (void)hipGraphExecDestroy(s->wave_exec); s->wave_exec = nullptr; }
