@@ -42,8 +42,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM [CDNA4]")
 LAT_TABLE_MAX = 64 << 30        # bytes of latency table per GPU beyond which --latency is dropped
-KT_ROWPASS, KT_ROUND, KT_FOLD = 0, 1, 2   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
-KERNEL_NAMES = {KT_ROWPASS: "k_rowpass", KT_FOLD: "k_fold"}
+KT_ROWPASS, KT_ROUND, KT_FOLD, KT_RESP = 0, 1, 2, 3   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
+KERNEL_NAMES = {KT_ROWPASS: "k_rowpass", KT_FOLD: "k_fold", KT_RESP: "k_resp_wave"}
 
 
 def parse():

@@ -245,10 +245,11 @@ int kb_wire_id_of_addr(const kb_wire_addr* addr, uint32_t* id);
    own dispatch packets on the stream they run on.  kind: KB_KT_*.                                   */
 enum { KB_KT_ROWPASS = 0,   /* the row pass: broadcast phase + ping_random_peer candidates */
        KB_KT_ROUND = 1,     /* the whole round                                                           */
-       KB_KT_FOLD = 2 };    /* the fingerprint fold                                                      */
+       KB_KT_FOLD = 2,      /* the fingerprint fold                                                      */
+       KB_KT_RESP = 3 };    /* the sampled Join responses, a wave per responder (k_resp_wave)            */
 int  kb_sim_kernel_time(kb_sim* sim, int kind, double* ms, uint64_t* launches);
 int  kb_sim_reset_kernel_time(kb_sim* sim);
-/* Algorithmic HBM bytes moved by a kernel (KB_KT_ROWPASS or KB_KT_FOLD) since the last reset,
+/* Algorithmic HBM bytes moved by a kernel (KB_KT_ROWPASS, KB_KT_FOLD or KB_KT_RESP) since the last reset,
    counted in-kernel.                                                                  */
 int  kb_sim_kernel_bytes(kb_sim* sim, int kind, uint64_t* bytes);
 

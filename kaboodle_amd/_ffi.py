@@ -17,7 +17,7 @@ KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL = 0, 1
 KB_DBG_PHASEB_HBM, KB_DBG_RESP_HBM, KB_DBG_KP_HBM, KB_DBG_KP_BIG_SMALL, KB_DBG_PROC_UNSORTED = 1, 2, 4, 8, 16
 KB_DBG_ALL = 31
 KB_LATENCY_NONE = 0xFFFFFFFF
-KT_ROWPASS, KT_ROUND, KT_FOLD = 0, 1, 2          # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
+KT_ROWPASS, KT_ROUND, KT_FOLD, KT_RESP = 0, 1, 2, 3   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
 STATE_NAMES = {0: "Known", 1: "WaitingForPing", 2: "WaitingForIndirectPing"}
 
 
@@ -350,7 +350,7 @@ class Sim:
         return v.value
 
     def kernel_bytes(self, kind: int = 0) -> int:
-        """Algorithmic bytes the kernel `kind` (KT_ROWPASS / KT_FOLD) moved since reset_kernel_time."""
+        """Algorithmic bytes the kernel `kind` (KT_ROWPASS / KT_FOLD / KT_RESP) moved since reset_kernel_time."""
         v = C.c_uint64()
         self.lib.call("sim_kernel_bytes", self.h, kind, C.byref(v))
         return v.value

@@ -839,6 +839,9 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
       }
       ins_before += __popcll(nmw);
     }
+    // algorithmic bytes: the row bitset, its Join masks and joiner ids read; the responses' ids and
+    // records written
+    if (l == 0) slot_add(d, S_RESPB, 4ull * NW + 16ull * pb.JW + 4ull * pb.nj + (4ull * d.capj + 32ull) * q);
     if (tdbg && l == 0) {
       __builtin_amdgcn_s_waitcnt(0);
       const uint64_t tp3 = wall_clock64();

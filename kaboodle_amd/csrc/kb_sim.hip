@@ -319,9 +319,10 @@ struct kb_sim {
   std::vector<uint32_t> h_xall;
   Msg* rmsg; uint32_t* rpay; uint8_t* rstatus; uint32_t* rinbox; uint32_t* rkp;
   size_t rmsg_cap, rpay_cap;
-  hipEvent_t ev0, ev1, er0, er1, ef0, ef1;   // row pass, whole round, fold
-  double rowpass_ms, round_ms, fold_ms;
-  uint64_t rowpass_launches, round_launches, fold_launches, row_bytes0, fold_bytes0, bj_total, bf_total;
+  hipEvent_t ev0, ev1, er0, er1, ef0, ef1, ew0, ew1;   // row pass, whole round, fold, Join responses
+  double rowpass_ms, round_ms, fold_ms, resp_ms;
+  uint64_t rowpass_launches, round_launches, fold_launches, resp_launches, row_bytes0, fold_bytes0, resp_bytes0, bj_total, bf_total;
+  bool resp_timed = false;             // k_resp_wave ran (with its events) this round
   uint32_t ncu = 256;
   bool debug_waves = false;
   size_t lds_per_cu = 65536;
@@ -442,7 +443,7 @@ static void destroy_shard(kb_sim* s) {
   (void)hipSetDevice(s->device);
   if (s->st) (void)hipStreamSynchronize(s->st);
   free_all(s);
-  for (hipEvent_t e : {s->ev0, s->ev1, s->er0, s->er1, s->ef0, s->ef1}) if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {s->ev0, s->ev1, s->er0, s->er1, s->ef0, s->ef1, s->ew0, s->ew1}) if (e) (void)hipEventDestroy(e);
   if (s->h_pin) (void)hipHostFree(s->h_pin);
   if (s->wave_exec) (void)hipGraphExecDestroy(s->wave_exec);
   if (s->wave_graph) (void)hipGraphDestroy(s->wave_graph);
@@ -558,7 +559,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
     s->h_pin = nullptr; destroy_shard(s); seterr("pinned buffer"); return KB_IO_ERROR;
   }
   if (hipHostGetDevicePointer((void**)&s->d_pin, s->h_pin, 0) != hipSuccess) { destroy_shard(s); seterr("pinned buffer mapping"); return KB_IO_ERROR; }
-  for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->er0, &s->er1, &s->ef0, &s->ef1}) (void)hipEventCreate(e);
+  for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->er0, &s->er1, &s->ef0, &s->ef1, &s->ew0, &s->ew1}) (void)hipEventCreate(e);
   int rc = upload_segments(s);
   if (rc) { destroy_shard(s); return rc; }
   uint32_t ctr0[NCTR] = {0};
@@ -1012,9 +1013,11 @@ static int step_round(kb_sim* s) {
       const size_t wlds = 16ull * rwave_words(d.NWR, s->W / 256);
       const bool wave_on = wlds <= 65536 && !(d.dbg & KB_DBG_RESP_HBM);
       if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
-      if (wave_on)
-        k_resp_wave<<<std::min<uint32_t>((resp_nodes + 3) / 4, 4096), 256, wlds, st>>>(d, pb, s->resp_nodes,
-                                                                                     s->scan_tot + 4, o0, r);
+      if (wave_on) {                                   // timed by events on its own dispatch packet
+        hipExtLaunchKernelGGL(k_resp_wave, dim3(std::min<uint32_t>((resp_nodes + 3) / 4, 4096)), dim3(256), wlds, st, s->ew0,
+                              s->ew1, 0, d, pb, (const uint32_t*)s->resp_nodes, (const uint32_t*)(s->scan_tot + 4), o0, r);
+        s->resp_timed = true;
+      }
       k_resp_node<<<grid, 256, lds, st>>>(d, pb, s->resp_nodes, s->scan_tot + 4, o0, r, scratch, wave_on);
       if (s->debug_waves && (d.dev & 512)) {
         uint32_t dbg[13];
@@ -1085,6 +1088,7 @@ static int step_round(kb_sim* s) {
   float ms = 0;
   (void)hipEventElapsedTime(&ms, s->ev0, s->ev1); s->rowpass_ms += ms; s->rowpass_launches++;
   if (d.uniform) { (void)hipEventElapsedTime(&ms, s->ef0, s->ef1); s->fold_ms += ms; s->fold_launches++; }
+  if (s->resp_timed) { (void)hipEventElapsedTime(&ms, s->ew0, s->ew1); s->resp_ms += ms; s->resp_launches++; s->resp_timed = false; }
   (void)hipEventElapsedTime(&ms, s->er0, s->er1); s->round_ms += ms; s->round_launches++;
   s->round = r + 1;
   return s->xf ? check_err(s) : err_status(err);   // shards: the flag of any rank
@@ -1509,6 +1513,7 @@ extern "C" int kb_sim_kernel_time(kb_sim* s, int kind, double* ms, uint64_t* lau
   if (kind == KB_KT_ROWPASS) { *ms = s->rowpass_ms; *launches = s->rowpass_launches; }
   else if (kind == KB_KT_ROUND) { *ms = s->round_ms; *launches = s->round_launches; }
   else if (kind == KB_KT_FOLD) { *ms = s->fold_ms; *launches = s->fold_launches; }
+  else if (kind == KB_KT_RESP) { *ms = s->resp_ms; *launches = s->resp_launches; }
   else return KB_INVALID_ARGUMENT;
   return KB_OK;
 }
@@ -1521,7 +1526,9 @@ static uint64_t stat_counter(kb_sim* s, int idx) {
 extern "C" int kb_sim_reset_kernel_time(kb_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
   GROUP_ALL(kb_sim_reset_kernel_time);
-  s->rowpass_ms = s->round_ms = s->fold_ms = 0; s->rowpass_launches = s->round_launches = s->fold_launches = 0;
+  s->rowpass_ms = s->round_ms = s->fold_ms = s->resp_ms = 0;
+  s->rowpass_launches = s->round_launches = s->fold_launches = s->resp_launches = 0;
+  s->resp_bytes0 = stat_counter(s, S_RESPB);
   s->row_bytes0 = stat_counter(s, S_ROWB);        // baselines of the device-side byte counters
   s->fold_bytes0 = stat_counter(s, S_FOLDB);
   return KB_OK;
@@ -1533,6 +1540,7 @@ extern "C" int kb_sim_kernel_bytes(kb_sim* s, int kind, uint64_t* bytes) {
   if (is_group(s)) return kb_sim_kernel_bytes(s->shards[0], kind, bytes);
   if (kind == KB_KT_ROWPASS) *bytes = stat_counter(s, S_ROWB) - s->row_bytes0;
   else if (kind == KB_KT_FOLD) *bytes = stat_counter(s, S_FOLDB) - s->fold_bytes0;
+  else if (kind == KB_KT_RESP) *bytes = stat_counter(s, S_RESPB) - s->resp_bytes0;
   else return KB_INVALID_ARGUMENT;
   return KB_OK;
 }
