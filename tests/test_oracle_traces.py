@@ -64,3 +64,19 @@ def test_oracle_live_pin(name):
             assert {k: st[k] for k in scenarios.STAT_KEYS} == {k: pm.stats[k] for k in scenarios.STAT_KEYS}
             assert st["agree"] == pm.agree
     assert measured > 0, "no latency was ever measured: the EWMA is untested"
+
+
+@pytest.mark.parametrize("name", ["churn40", "stop_start"])
+def test_alive_rounds_counts_every_round(name):
+    """kb_stats.alive_rounds (what bench.py's `value` divides by wall time) is the running-peer count of
+    every simulated round, summed: the peers running after a round are those its tick counted."""
+    sc = scenarios.BY_NAME[name]
+    with Sim(oracle_lib(), sc["cfg"]) as o:
+        scenarios.setup(o, sc)
+        total = o.stats()["alive_rounds"]
+        assert total == 0
+        for r in range(sc["rounds"]):
+            scenarios.apply_events(o, sc, r)
+            o.step(1)
+            total += o.stats()["alive"]
+            assert o.stats()["alive_rounds"] == total, f"{name} round {r}"
