@@ -72,11 +72,20 @@ __host__ __device__ inline uint32_t mulhi(uint32_t u, uint32_t k) { return (uint
 // ---- GF(2) arithmetic mod the CRC-32 polynomial, reflected (x^0 = 0x80000000) ---------------------
 __host__ __device__ inline uint32_t multmodp(uint32_t a, uint32_t b) {
   uint32_t p = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // device: the bit masks by signed bit-field extracts (0 or all ones), no compare/select per bit
+#pragma unroll 4
+  for (int k = 31; k >= 0; --k) {
+    p ^= b & (uint32_t)__builtin_amdgcn_sbfe((int)a, k, 1);
+    b = (b >> 1) ^ (CRC_POLY & (uint32_t)__builtin_amdgcn_sbfe((int)b, 0, 1));
+  }
+#else
 #pragma unroll 4
   for (int k = 31; k >= 0; --k) {
     if (a & (1u << k)) p ^= b;
     b = (b & 1u) ? (b >> 1) ^ CRC_POLY : b >> 1;
   }
+#endif
   return p;
 }
 
