@@ -187,34 +187,34 @@ __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
   __shared__ uint32_t s_nb[4];
   uint32_t nbytes = 0;
   if (actm) {
-  const uint32_t i = act ? i0 : d.lo + g * 64 + (uint32_t)(__ffsll((long long)actm) - 1);   // idle lanes shadow a live one
-  const uint32_t* bw = bits_of(d, i);
-  const uint32_t spp = NSEG / S;
-  const unsigned long long sd = act ? d.sdirty[i] : 0ull;
-  unsigned long long folded = 0;
-  for (uint32_t k = s * spp; k < (s + 1) * spp; ++k) {
-    const bool mine = (sd >> k) & 1ull;
-    if (!__ballot(mine)) continue;                  // wave-uniform: no row of this wave changed here
-    const uint32_t c0 = k * d.SEGW, c1 = c0 + d.SEGW;
-    uint32_t raw = 0, cnt = 0;
-    uint4 mb = *reinterpret_cast<const uint4*>(bw + (c0 >> 5));
-    for (uint32_t col = c0; col < c1; col += 128) {
-      const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
-      uint32_t hv[16];
-      const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
+    const uint32_t i = act ? i0 : d.lo + g * 64 + (uint32_t)(__ffsll((long long)actm) - 1);   // idle lanes shadow a live one
+    const uint32_t* bw = bits_of(d, i);
+    const uint32_t spp = NSEG / S;
+    const unsigned long long sd = act ? d.sdirty[i] : 0ull;
+    unsigned long long folded = 0;
+    for (uint32_t k = s * spp; k < (s + 1) * spp; ++k) {
+      const bool mine = (sd >> k) & 1ull;
+      if (!__ballot(mine)) continue;                  // wave-uniform: no row of this wave changed here
+      const uint32_t c0 = k * d.SEGW, c1 = c0 + d.SEGW;
+      uint32_t raw = 0, cnt = 0;
+      uint4 mb = *reinterpret_cast<const uint4*>(bw + (c0 >> 5));
+      for (uint32_t col = c0; col < c1; col += 128) {
+        const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
+        uint32_t hv[16];
+        const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
 #pragma unroll
-      for (int h = 0; h < 16; ++h) hv[h] = ht[h * 256 + ((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu)];   // entry 0 is 0
-      if (col + 128 < c1) mb = *reinterpret_cast<const uint4*>(bw + ((col + 128) >> 5));   // next step's bits
+        for (int h = 0; h < 16; ++h) hv[h] = ht[h * 256 + ((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu)];   // entry 0 is 0
+        if (col + 128 < c1) mb = *reinterpret_cast<const uint4*>(bw + ((col + 128) >> 5));   // next step's bits
 #pragma unroll
-      for (int h = 0; h < 16; ++h) {
-        const uint32_t c = __popc((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu);   // Z^0 table is the identity
-        raw = mulzb(zb, raw, c) ^ hv[h];
-        cnt += c;
+        for (int h = 0; h < 16; ++h) {
+          const uint32_t c = __popc((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu);   // Z^0 table is the identity
+          raw = mulzb(zb, raw, c) ^ hv[h];
+          cnt += c;
+        }
       }
+      if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; nbytes += d.SEGW / 8; }
     }
-    if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; nbytes += d.SEGW / 8; }
-  }
-  if (folded) atomicAnd(&d.sdirty[i], ~folded);
+    if (folded) atomicAnd(&d.sdirty[i], ~folded);
   }
   const uint32_t wb = wave_sum(act ? nbytes : 0u);
   if (lane() == 0) s_nb[threadIdx.x >> 6] = wb;
