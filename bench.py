@@ -17,12 +17,15 @@ tracks every peer, so per-GPU work grows with N.  --replicas runs N independent 
 (distinct seeds, no collective on the data path).
 
 Also reported, on the same JSON line:
-  roofline      the dominant kernel (the longer of k_rowpass — broadcast phase + ping_random_peer's
-                candidate scan — and k_fold — the fingerprint checkpoints): algorithmic bytes per launch
-                (counted in-kernel) / its HIP-event duration on the simulator's stream, against 8 TB/s;
-                `traffic` = measured HBM bytes per launch from the rocprofv3 PMC summary committed under
-                profiles/ (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE), else null; the other
-                kernel's figures ride along under `kernels`;
+  kernels       every kernel of the round: HIP-event ms per round (each launch timed by its own dispatch
+                packet on the simulator's stream), launches per round, wave-0 share, and for the kernels
+                with an in-kernel byte counter (k_rowpass, k_fold, k_resp_wave, k_proc) the algorithmic
+                bytes and GB/s; `gaps` = round_gpu_ms minus the kernels (launch gaps, host hand-offs), so
+                the rows sum to round_gpu_ms;
+  roofline      the kernel with the most time per round: algorithmic bytes per launch (counted in-kernel)
+                / its mean HIP-event launch duration, against 8 TB/s; `traffic` = measured HBM bytes per
+                launch from the rocprofv3 PMC summary committed under profiles/ for this exact command
+                (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, timed rounds only), else null;
   cpu_baseline  the CPU oracle (oracle/, OpenMP build, same semantics and seeds) on a bounded sample of
                 the same workload, on rank 0 only;
   convergence   after the timed rounds faults stop (fault_end_round); untimed rounds continue until every
@@ -42,8 +45,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM [CDNA4]")
 LAT_TABLE_MAX = 64 << 30        # bytes of latency table per GPU beyond which --latency is dropped
-KT_ROWPASS, KT_ROUND, KT_FOLD, KT_RESP = 0, 1, 2, 3   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
-KERNEL_NAMES = {KT_ROWPASS: "k_rowpass", KT_FOLD: "k_fold", KT_RESP: "k_resp_wave"}
+KT_ROUND = 1                    # kb_sim_kernel_time kind of the whole round
+CHURN_RESERVE = 8192            # fresh ids kept for churn joins: capacity does not depend on --steps
 
 
 def parse():
@@ -70,18 +73,20 @@ def parse():
     return ap.parse_args()
 
 
-def pmc_traffic(cfg_key: str, kernel: str, capacity: int):
-    """Latest committed PMC summary for this kernel on this exact workload and capacity
-    (profiles/*pmc*.json): HBM bytes per launch."""
-    best = None
+def pmc_summary(cfg_key: str, capacity: int, steps: int, warmup: int, failed_mode: str):
+    """The latest committed PMC summary (tools/gpu_pmc.sh -> profiles/*pmc*.json) taken on exactly this
+    workload, capacity, step and warmup counts: {kernel: {hbm_bytes_per_launch, hbm_bytes_per_round, ...}}
+    over the timed rounds, and the summary's path."""
+    best, src = None, None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if d.get("workload") == cfg_key and d.get("kernel") == kernel and d.get("capacity") == capacity:
-            best = d
-    return None if best is None else int(best["hbm_bytes_per_launch"])
+        if (d.get("workload") == cfg_key and d.get("capacity") == capacity and d.get("steps") == steps and
+                d.get("warmup") == warmup and d.get("failed_mode", "sim_sender") == failed_mode and "kernels" in d):
+            best, src = d["kernels"], os.path.relpath(p, ROOT)
+    return best, src
 
 
 def committed_tail(cfg_key: str, mode: str):
@@ -172,7 +177,7 @@ def rank_config(a, rank: int, world: int, local: int):
     total = a.warmup + a.steps
     shard = sharded(a, world)
     peers = a.nodes * world if (shard and getattr(a, "weak", False)) else a.nodes
-    reserve = max(4096, int(peers * a.churn * (total + 8) * 1.5))
+    reserve = max(CHURN_RESERVE, int(peers * a.churn * (total + 8) * 1.5))   # 8192 up to ~80 churn rounds at 64K
     mode = KB_FAILED_SOCKET_FAITHFUL if getattr(a, "failed_mode", "sim_sender") == "socket_faithful" else KB_FAILED_SIM_SENDER
     return SimConfig(capacity=peers + reserve, initial_nodes=peers, init_mode=KB_INIT_CONVERGED, loss=a.loss,
                      churn=a.churn, fault_end_round=total, seed=a.seed + (0 if shard else 1000 * rank),
@@ -245,11 +250,10 @@ def main() -> int:
     mesh.step(a.warmup)
     torch.cuda.synchronize()
     mesh.reset_kernel_time()
+    syncs0 = mesh.host_syncs()
     dt, alive_sum, st0, st = timed_rounds(mesh, a.steps, world)
-    kern = {}
-    for kind, name in KERNEL_NAMES.items():
-        ms, n = mesh.kernel_time(kind)
-        kern[name] = {"ms": ms, "n": n, "bytes": mesh.kernel_bytes(kind)}
+    syncs = mesh.host_syncs() - syncs0
+    bd = mesh.kernel_breakdown()
     round_ms, round_n = mesh.kernel_time(KT_ROUND)
     model_bytes = round_model_bytes(st0, st, alive_sum / max(a.steps, 1), a.steps)
 
@@ -297,16 +301,33 @@ def main() -> int:
 
     out = None
     if rank == 0:
-        rl = {}
-        for name, k in kern.items():
-            per_launch = k["bytes"] / max(k["n"], 1)
-            avg_ms = k["ms"] / max(k["n"], 1)
-            ach = per_launch / (avg_ms * 1e-3) / 1e9 if k["n"] and avg_ms > 0 else 0.0
-            rl[name] = {"bound": "hbm", "kernel": name, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": pmc_traffic(workload, name, capacity),
-                        "algorithmic_bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_ms, 4),
-                        "launches": k["n"]}
-        dominant = max(rl, key=lambda n: rl[n]["avg_launch_ms"])
+        nr = max(round_n, 1)
+        pmc, pmc_src = pmc_summary(workload, capacity, a.steps, a.warmup, a.failed_mode)
+        table = {}
+        for name, k in sorted(bd.items(), key=lambda kv: -kv[1]["ms"]):
+            e = {"ms_per_round": round(k["ms"] / nr, 4), "launches_per_round": round(k["launches"] / nr, 2),
+                 "wave0_ms_per_round": round(k["wave_ms"][0] / nr, 4)}
+            if k["bytes"] is not None and k["launches"]:
+                per_launch = k["bytes"] / k["launches"]
+                avg_ms = k["ms"] / k["launches"]
+                ach = per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+                e.update({"algorithmic_bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_ms, 4),
+                          "achieved_GBs": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4)})
+            if pmc and name in pmc:
+                e["traffic_per_launch"] = pmc[name].get("hbm_bytes_per_launch")
+            table[name] = e
+        kern_sum = sum(v["ms_per_round"] for v in table.values())
+        gaps = round(round_ms / nr - kern_sum, 4)
+        counted = [n for n, v in table.items() if "achieved_GBs" in v]
+        top = max(table, key=lambda n: table[n]["ms_per_round"])
+        dominant = top if top in counted else max(counted, key=lambda n: table[n]["ms_per_round"])
+        dk, db = table[dominant], bd[dominant]
+        roof = {"bound": "hbm", "kernel": dominant, "achieved": dk["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": dk["frac"], "traffic": dk.get("traffic_per_launch"),
+                "traffic_source": pmc_src if dk.get("traffic_per_launch") is not None else None,
+                "algorithmic_bytes_per_launch": dk["algorithmic_bytes_per_launch"], "avg_launch_ms": dk["avg_launch_ms"],
+                "launches": db["launches"], "ms_per_round": dk["ms_per_round"],
+                "note": None if top == dominant else f"{top} takes more time per round but has no byte counter"}
         out = {
             "metric": "simulated peer-rounds/sec (whole node) + rounds to fingerprint convergence",
             "value": alive_total / dt, "unit": "peer-rounds/s", "n_gpus": world, "steps": a.steps,
@@ -319,9 +340,10 @@ def main() -> int:
                        "loss": a.loss, "churn": a.churn,
                        "parallelism": (f"rowshard{world}" if shard else f"replicas{world}") if world > 1 else "single",
                        "max_waves": cfg.max_waves, "latency_ewma": bool(cfg.track_latency)},
-            "roofline": rl[dominant],
-            "kernels": {n: v for n, v in rl.items() if n != dominant},
-            "round_gpu_ms": round(round_ms / max(round_n, 1), 4),
+            "roofline": roof,
+            "kernels": {**table, "gaps": {"ms_per_round": gaps}},
+            "round_gpu_ms": round(round_ms / nr, 4),
+            "host_syncs_per_round": round(syncs / max(a.steps, 1), 2),
             # the whole round against SURVEY.md §8(d)'s dense model (every live peer reads its N-byte
             # row, plus the message bytes), per wall-clock round
             "round_roofline": {"bytes_model_per_round": int(model_bytes),

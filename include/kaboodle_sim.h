@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 1u
+#define KB_ABI_VERSION 2u   /* 2: kernel breakdown, identities on the inspection surface */
 
 /* ---- status codes (mirror KaboodleError, src/errors.rs:8-24) ------------------------------------ */
 enum {
@@ -87,7 +87,9 @@ enum {
   KB_DBG_RESP_HBM = 2u,      /* Join responses by workgroup with HBM scratch (rows > RESP_LDS_W ids)     */
   KB_DBG_KP_HBM = 4u,        /* KnownPeers groups on the HBM bitset, one workgroup per destination      */
   KB_DBG_KP_BIG_SMALL = 8u,  /* every KnownPeers group takes the BIG (1024-thread) kernel                */
-  KB_DBG_PROC_UNSORTED = 16u /* inboxes > 64 taken by k_proc's selection path (inboxes > SORT_MAX)       */
+  KB_DBG_PROC_UNSORTED = 16u,/* inboxes > 64 taken by k_proc's selection path (inboxes > SORT_MAX)       */
+  KB_DBG_WAVE_GRAPH = 32u    /* the unsharded receive window captured once as a HIP graph and replayed
+                                every round (also env KB_WAVE_GRAPH=1)                  */
 };
 
 /* Per-peer state as reported by peer_states() (PeerState, src/structs.rs:27-41). */
@@ -98,6 +100,8 @@ typedef struct kb_peer_state {
   int32_t  since;            /* round of the state's Instant; INT32_MIN = older than the stamp window */
   uint32_t latency_ms;       /* PeerInfo.latency in simulated ms ; KB_LATENCY_NONE =
                                 None (never measured, or track_latency off)                          */
+  uint32_t identity_len;     /* PeerInfo.identity (src/structs.rs:18-22): the peer's identity bytes  */
+  uint8_t  identity[32];
 } kb_peer_state;
 #define KB_LATENCY_NONE 0xFFFFFFFFu
 
@@ -133,7 +137,13 @@ int  kb_sim_start_node(kb_sim* sim, uint32_t node);                 /* takes eff
 int  kb_sim_stop_node(kb_sim* sim, uint32_t node);                  /* takes effect next round start */
 int  kb_sim_is_running(kb_sim* sim, uint32_t node, int* running);
 int  kb_sim_ping_addrs(kb_sim* sim, uint32_t node, const uint32_t* peers, size_t n);
+/* Kaboodle::set_identity (src/lib.rs:323-336): only while the node is not running, counting the start /
+   stop calls queued since the last step (they take effect at the next round start).  Identity belongs
+   to the id: the new bytes are what every view reports and fingerprints from then on. */
 int  kb_sim_set_identity(kb_sim* sim, uint32_t node, const uint8_t* identity, size_t len);
+/* The identity bytes of id `node` (Kaboodle::peers / peer_states values, src/lib.rs:339-354): *len is
+   the length; copied into buf when cap suffices (buf = NULL: length query).                         */
+int  kb_sim_identity(kb_sim* sim, uint32_t node, uint8_t* buf, size_t cap, size_t* len);
 
 int  kb_sim_fingerprint(kb_sim* sim, uint32_t node, uint32_t* fp);
 int  kb_sim_fingerprints(kb_sim* sim, uint32_t* fps, size_t cap);   /* all ids; 0 for non-running  */
@@ -246,12 +256,30 @@ int kb_wire_id_of_addr(const kb_wire_addr* addr, uint32_t* id);
 enum { KB_KT_ROWPASS = 0,   /* the row pass: broadcast phase + ping_random_peer candidates */
        KB_KT_ROUND = 1,     /* the whole round                                                           */
        KB_KT_FOLD = 2,      /* the fingerprint fold                                                      */
-       KB_KT_RESP = 3 };    /* the sampled Join responses, a wave per responder (k_resp_wave)            */
+       KB_KT_RESP = 3,      /* the sampled Join responses, a wave per responder (k_resp_wave)            */
+       KB_KT_PROC = 4 };    /* the in-order unicast handlers, a wave per node (k_proc, every wave)       */
 int  kb_sim_kernel_time(kb_sim* sim, int kind, double* ms, uint64_t* launches);
 int  kb_sim_reset_kernel_time(kb_sim* sim);
-/* Algorithmic HBM bytes moved by a kernel (KB_KT_ROWPASS, KB_KT_FOLD or KB_KT_RESP) since the last reset,
-   counted in-kernel.                                                                  */
+/* Algorithmic HBM bytes moved by a kernel (KB_KT_ROWPASS, KB_KT_FOLD, KB_KT_RESP or KB_KT_PROC) since the
+   last reset, counted in-kernel.                                                      */
 int  kb_sim_kernel_bytes(kb_sim* sim, int kind, uint64_t* bytes);
+/* Per-kernel profile of every launch of the rounds since the last reset (profiling on: the default;
+   env KB_PROF=0 or kb_sim_set_profiling(sim, 0) turns the per-launch events off).  wave_ms[w] is the
+   part spent in delivery wave w (slot KB_WAVE_SLOTS-1 holds waves >= KB_WAVE_SLOTS-1).  Kernels that
+   did not run are omitted; cap = 0 queries the count.                                               */
+#define KB_WAVE_SLOTS 9
+typedef struct kb_kernel_time {
+  char     name[24];
+  double   ms;
+  uint64_t launches;
+  uint64_t bytes;                 /* algorithmic bytes counted in-kernel (has_bytes), else 0          */
+  uint32_t has_bytes, pad;
+  double   wave_ms[KB_WAVE_SLOTS];
+} kb_kernel_time;
+int  kb_sim_set_profiling(kb_sim* sim, int on);
+int  kb_sim_kernel_breakdown(kb_sim* sim, kb_kernel_time* out, size_t cap, size_t* n);
+/* Host waits on the device since creation (stream synchronisations and pinned hand-offs).          */
+int  kb_sim_host_syncs(kb_sim* sim, uint64_t* n);
 
 #ifdef __cplusplus
 }

@@ -79,7 +79,7 @@ class Mesh(Sim):
             disc, dep, fp, changed = self.events(node)
             for x in disc:
                 for c in subs["peers"]:
-                    c.send((self.format_addr(x), x))
+                    c.send((self.format_addr(x), self.identity(x)))
             for x in dep:
                 for c in subs["departures"]:
                     c.send(self.format_addr(x))
@@ -146,9 +146,12 @@ class Kaboodle:
         return self.mesh.fingerprint(self.id)
 
     def peers(self) -> dict:                      # src/lib.rs:339-345: addr -> identity
-        return {self.mesh.format_addr(p): p for p in self.mesh.peers(self.id)}
+        return {self.mesh.format_addr(p): self.mesh.identity(p) for p in self.mesh.peers(self.id)}
 
-    def discover_peers(self) -> Channel:          # src/lib.rs:221-236: (addr, id) per new peer
+    def identity(self) -> bytes:                  # the identity this peer announces (Kaboodle.identity)
+        return self.mesh.identity(self.id)
+
+    def discover_peers(self) -> Channel:          # src/lib.rs:221-236: (addr, identity) per new peer
         return self.mesh.subscribe(self.id, "peers", Channel())
 
     def discover_next_peer(self) -> Channel:      # src/lib.rs:238-263: the next one only
@@ -160,11 +163,15 @@ class Kaboodle:
     def discover_fingerprint_changes(self) -> Channel:   # src/lib.rs:201-219
         return self.mesh.subscribe(self.id, "fingerprints", Channel())
 
-    def peer_states(self) -> dict:                # src/lib.rs:348-354: addr -> (state, since, latency)
-        """PeerInfo per known peer: state name, round of its Instant (None = older than the stamp window),
-        latency in simulated ms (None = never measured, as PeerInfo.latency, src/structs.rs:18-22)."""
+    def peer_states(self) -> dict:                # src/lib.rs:348-354: addr -> PeerInfo
+        """PeerInfo per known peer (src/structs.rs:18-22): identity bytes, state name, round of its Instant
+        (None = older than the stamp window), latency in simulated ms (None = never measured)."""
         out = {}
-        for p, s, since, lat in self.mesh.peer_states(self.id):
-            out[self.mesh.format_addr(p)] = (STATE_NAMES[s], None if since == -2**31 else since,
-                                             None if lat == 0xFFFFFFFF else lat)
+        for p, s, since, lat, ident in self.mesh.peer_states(self.id):
+            out[self.mesh.format_addr(p)] = PeerInfo(ident, STATE_NAMES[s], None if since == -2**31 else since,
+                                                     None if lat == 0xFFFFFFFF else lat)
         return out
+
+
+class PeerInfo(collections.namedtuple("PeerInfo", "identity state since latency")):
+    """PeerInfo {identity, state, latency} (src/structs.rs:18-22), the state's Instant as a round."""

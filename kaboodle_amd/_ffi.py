@@ -10,14 +10,16 @@ import ctypes as C
 import os
 from dataclasses import dataclass
 
-KB_ABI_VERSION = 1
+KB_ABI_VERSION = 2
 KB_OK, KB_INVALID_OPERATION, KB_IO_ERROR, KB_NO_DEVICE, KB_STOPPING_FAILED, KB_INVALID_ARGUMENT, KB_CAPACITY = range(7)
 KB_INIT_JOIN, KB_INIT_CONVERGED = 0, 1
 KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL = 0, 1
 KB_DBG_PHASEB_HBM, KB_DBG_RESP_HBM, KB_DBG_KP_HBM, KB_DBG_KP_BIG_SMALL, KB_DBG_PROC_UNSORTED = 1, 2, 4, 8, 16
-KB_DBG_ALL = 31
+KB_DBG_ALL = 31                  # every wide-row variant
+KB_DBG_WAVE_GRAPH = 32           # the receive window as a replayed HIP graph
 KB_LATENCY_NONE = 0xFFFFFFFF
-KT_ROWPASS, KT_ROUND, KT_FOLD, KT_RESP = 0, 1, 2, 3   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
+KT_ROWPASS, KT_ROUND, KT_FOLD, KT_RESP, KT_PROC = 0, 1, 2, 3, 4   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
+KB_WAVE_SLOTS = 9
 STATE_NAMES = {0: "Known", 1: "WaitingForPing", 2: "WaitingForIndirectPing"}
 
 
@@ -33,7 +35,8 @@ class KbConfig(C.Structure):
 
 
 class KbPeerState(C.Structure):
-    _fields_ = [("peer", C.c_uint32), ("state", C.c_uint32), ("since", C.c_int32), ("latency_ms", C.c_uint32)]
+    _fields_ = [("peer", C.c_uint32), ("state", C.c_uint32), ("since", C.c_int32), ("latency_ms", C.c_uint32),
+                ("identity_len", C.c_uint32), ("identity", C.c_uint8 * 32)]
 
 
 class KbStats(C.Structure):
@@ -52,6 +55,11 @@ class KbStats(C.Structure):
 
     def as_dict(self) -> dict:
         return {n: getattr(self, n) for n, _ in self._fields_ if n != "reserved"}
+
+
+class KbKernelTime(C.Structure):
+    _fields_ = [("name", C.c_char * 24), ("ms", C.c_double), ("launches", C.c_uint64), ("bytes", C.c_uint64),
+                ("has_bytes", C.c_uint32), ("pad", C.c_uint32), ("wave_ms", C.c_double * KB_WAVE_SLOTS)]
 
 
 class KbError(RuntimeError):
@@ -105,6 +113,7 @@ _SIGS = {
     "sim_is_running": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_int)]),
     "sim_ping_addrs": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t]),
     "sim_set_identity": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]),
+    "sim_identity": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(C.c_size_t)]),
     "sim_fingerprint": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     "sim_fingerprints": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t]),
     "sim_true_fingerprint": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
@@ -137,6 +146,9 @@ _OPTIONAL = {
     "sim_reset_kernel_time": (C.c_int, [C.c_void_p]),
     "sim_kernel_bytes": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint64)]),
     "sim_debug_paths": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "sim_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "sim_kernel_breakdown": (C.c_int, [C.c_void_p, C.POINTER(KbKernelTime), C.c_size_t, C.POINTER(C.c_size_t)]),
+    "sim_host_syncs": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 }
 
 
@@ -248,6 +260,13 @@ class Sim:
         self.lib.call("sim_set_identity", self.h, node, identity, len(identity))
 
     # -- inspection --
+    def identity(self, node: int) -> bytes:
+        """The identity bytes of id `node` (what every view reports for it)."""
+        n = C.c_size_t()
+        buf = (C.c_uint8 * 32)()
+        self.lib.call("sim_identity", self.h, node, buf, 32, C.byref(n))
+        return bytes(buf[: n.value])
+
     def fingerprint(self, node: int) -> int:
         v = C.c_uint32()
         self.lib.call("sim_fingerprint", self.h, node, C.byref(v))
@@ -292,7 +311,7 @@ class Sim:
         self.lib.call("sim_peer_states", self.h, node, None, 0, C.byref(n))
         arr = (KbPeerState * max(n.value, 1))()
         self.lib.call("sim_peer_states", self.h, node, arr, n.value, C.byref(n))
-        return [(a.peer, a.state, a.since, a.latency_ms) for a in arr[: n.value]]
+        return [(a.peer, a.state, a.since, a.latency_ms, bytes(a.identity[: a.identity_len])) for a in arr[: n.value]]
 
     def stats(self) -> dict:
         st = KbStats()
@@ -350,7 +369,27 @@ class Sim:
         return v.value
 
     def kernel_bytes(self, kind: int = 0) -> int:
-        """Algorithmic bytes the kernel `kind` (KT_ROWPASS / KT_FOLD / KT_RESP) moved since reset_kernel_time."""
+        """Algorithmic bytes the kernel `kind` (KT_ROWPASS / KT_FOLD / KT_RESP / KT_PROC) moved since
+        reset_kernel_time."""
         v = C.c_uint64()
         self.lib.call("sim_kernel_bytes", self.h, kind, C.byref(v))
+        return v.value
+
+    def set_profiling(self, on: bool) -> None:
+        """Per-launch HIP events on every kernel of the round (kernel_breakdown); on by default."""
+        self.lib.call("sim_set_profiling", self.h, int(bool(on)))
+
+    def kernel_breakdown(self) -> dict:
+        """{kernel: {"ms", "launches", "bytes" (None if not counted), "wave_ms": [...]}} since reset_kernel_time."""
+        n = C.c_size_t()
+        self.lib.call("sim_kernel_breakdown", self.h, None, 0, C.byref(n))
+        arr = (KbKernelTime * max(n.value, 1))()
+        self.lib.call("sim_kernel_breakdown", self.h, arr, n.value, C.byref(n))
+        return {a.name.decode(): {"ms": a.ms, "launches": a.launches, "bytes": a.bytes if a.has_bytes else None,
+                                  "wave_ms": list(a.wave_ms)} for a in arr[: n.value]}
+
+    def host_syncs(self) -> int:
+        """Host waits on the device since creation (stream synchronisations, pinned hand-offs)."""
+        v = C.c_uint64()
+        self.lib.call("sim_host_syncs", self.h, C.byref(v))
         return v.value

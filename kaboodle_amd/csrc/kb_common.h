@@ -23,6 +23,7 @@ enum StatIdx {
   S_A3ROWS, S_A3DEEP, S_A3CHUNKS,  // A3 scans: rows, rows past their first chunk, chunks read (kb_sim_debug_counters)
   S_ALIVER,                       // running peers summed over the rounds (kb_stats.alive_rounds; counted by shard 0)
   S_RESPB,                        // bytes k_resp_wave moved (bench; not a kb_stats field)
+  S_PROCB,                        // bytes k_proc moved (bench; not a kb_stats field)
   NSTAT
 };
 enum CtrIdx {

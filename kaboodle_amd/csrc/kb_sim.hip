@@ -39,6 +39,32 @@
 
 using namespace kb;
 
+// Every launch of a round is tagged with one of these ids; with profiling on (kb_sim_set_profiling) it
+// carries start/stop events on its own dispatch packet and kb_sim_kernel_breakdown reports the sums.
+enum KId : int {
+  KI_REBASE, KI_EVENTS, KI_CHURN_LEAVE, KI_CHURN_JOIN, KI_ALIVE_BITS, KI_TRUEFP_PART, KI_TRUEFP_FIN, KI_LOG_MARK,
+  KI_LAT_MARK, KI_BFAIL_PREP, KI_ROWPASS, KI_LAT_SWEEP, KI_SCAN_TILES, KI_SCAN_APPLY, KI_SET_CAP, KI_RESP_WAVE,
+  KI_RESP_NODE, KI_TICK_SCAN, KI_TICK_PRE, KI_FOLD, KI_FP_ROWS, KI_TICK_POST, KI_BCAST_WRITE, KI_ROUTE, KI_ROUTE_X,
+  KI_XBOUND, KI_PACK, KI_ROUTE_RECV, KI_SCATTER, KI_SCATTER_FLAT, KI_KP_SMALL, KI_KP_GROUP, KI_SORT_INBOX,
+  KI_PROC_FAST, KI_PROC, KI_ROUND_END, NKI
+};
+static const char* const KNAME[NKI] = {
+  "k_rebase", "k_events", "k_churn_leave", "k_churn_join", "k_alive_bits", "k_truefp_part", "k_truefp_fin",
+  "k_log_mark", "k_lat_mark", "k_bfail_prep", "k_rowpass", "k_lat_sweep", "k_scan_tiles", "k_scan_apply",
+  "k_set_cap", "k_resp_wave", "k_resp_node", "k_tick_scan", "k_tick_pre", "k_fold", "k_fp_rows", "k_tick_post",
+  "k_bcast_write", "k_route", "k_route_x", "k_xbound", "k_pack", "k_route_recv", "k_scatter", "k_scatter_flat",
+  "k_kp_small", "k_kp_group", "k_sort_inbox", "k_proc_fast", "k_proc", "k_round_end"};
+// the in-kernel algorithmic byte counter of a kernel (StatIdx), or -1
+static int kbytes_stat(int kid) {
+  switch (kid) {
+    case KI_ROWPASS: return S_ROWB;
+    case KI_FOLD: return S_FOLDB;
+    case KI_RESP_WAVE: return S_RESPB;
+    case KI_PROC: return S_PROCB;
+    default: return -1;
+  }
+}
+
 // ================================================================================================
 // Exclusive scan over up to 4 arrays of length n (+ optional compaction of indices j with in[0][j] != 0),
 // two fully parallel passes over 1024-element tiles: per-tile sums, then per-tile offsets + local scan.
@@ -292,7 +318,7 @@ struct kb_sim {
   bool in_group;                       // a shard of a kb_sim_create_local group
   std::vector<void*> allocs;           // device memory owned by this handle
   int32_t round;
-  std::vector<uint8_t> h_ident, h_idlen, h_ever;
+  std::vector<uint8_t> h_ident, h_idlen;
   std::vector<Event> events;
   OutBuf ob[2];
   WaveCtl wc;
@@ -319,10 +345,23 @@ struct kb_sim {
   std::vector<uint32_t> h_xall;
   Msg* rmsg; uint32_t* rpay; uint8_t* rstatus; uint32_t* rinbox; uint32_t* rkp;
   size_t rmsg_cap, rpay_cap;
-  hipEvent_t ev0, ev1, er0, er1, ef0, ef1, ew0, ew1;   // row pass, whole round, fold, Join responses
-  double rowpass_ms, round_ms, fold_ms, resp_ms;
-  uint64_t rowpass_launches, round_launches, fold_launches, resp_launches, row_bytes0, fold_bytes0, resp_bytes0, bj_total, bf_total;
-  bool resp_timed = false;             // k_resp_wave ran (with its events) this round
+  hipEvent_t er0, er1;                 // the whole round (markers on the stream)
+  double round_ms;
+  uint64_t round_launches, bj_total, bf_total;
+  // per-kernel profile (kb_sim_kernel_breakdown): with prof_on every launch carries start/stop events
+  // on its own dispatch packet; a round's records are read back during the next round's final wait
+  // (the host is idle then), the last round's on query
+  struct KRec { int16_t kid, wave; hipEvent_t a, b; };
+  bool prof_on = true;
+  bool capturing = false;              // inside a HIP graph capture: launches carry no events
+  int cur_wave = -1;                   // the delivery wave being launched (-1: outside the window)
+  std::vector<hipEvent_t> ev_free;
+  std::vector<KRec> krec;
+  double k_ms[NKI] = {};
+  double k_wms[NKI][KB_WAVE_SLOTS] = {};
+  uint64_t k_n[NKI] = {};
+  uint64_t k_bytes0[NSTAT] = {};
+  uint64_t host_syncs = 0;             // host waits on the device (stream syncs, pinned hand-offs) since creation
   uint32_t ncu = 256;
   bool debug_waves = false;
   size_t lds_per_cu = 65536;
@@ -362,14 +401,49 @@ template <class T> static hipError_t ralloc(kb_sim* s, T** p, size_t per_row) {
 }
 template <class T> static T* L(const kb_sim* s, T* p) { return p + s->lo; }   // biased row table -> local base
 
+// ---- launches and their profile ------------------------------------------------------------------
+static void prof_events(kb_sim* s, int kid, hipEvent_t* a, hipEvent_t* b) {
+  *a = *b = nullptr;
+  if (!s->prof_on || s->capturing) return;
+  hipEvent_t e[2];
+  for (int k = 0; k < 2; ++k) {
+    if (!s->ev_free.empty()) { e[k] = s->ev_free.back(); s->ev_free.pop_back(); }
+    else if (hipEventCreate(&e[k]) != hipSuccess) { if (k) s->ev_free.push_back(e[0]); return; }
+  }
+  *a = e[0]; *b = e[1];
+  const int w = s->cur_wave < 0 ? -1 : (s->cur_wave < KB_WAVE_SLOTS ? s->cur_wave : KB_WAVE_SLOTS - 1);
+  s->krec.push_back(kb_sim::KRec{(int16_t)kid, (int16_t)w, e[0], e[1]});
+}
+// every kernel of the round is launched through here: the dispatch packet itself records the events
+template <typename F, typename... Args>
+static void klaunch(kb_sim* s, int kid, F kern, dim3 grid, dim3 block, uint32_t lds, Args... args) {
+  hipEvent_t a, b;
+  prof_events(s, kid, &a, &b);
+  hipExtLaunchKernelGGL(kern, grid, block, lds, s->st, a, b, 0, args...);
+}
+// fold the first n records (complete: their round has ended) into the per-kernel sums
+static void prof_resolve(kb_sim* s, size_t n) {
+  n = std::min(n, s->krec.size());
+  for (size_t k = 0; k < n; ++k) {
+    const kb_sim::KRec& q = s->krec[k];
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, q.a, q.b) == hipSuccess) {
+      s->k_ms[q.kid] += ms; s->k_n[q.kid]++;
+      if (q.wave >= 0) s->k_wms[q.kid][q.wave] += ms;
+    }
+    s->ev_free.push_back(q.a); s->ev_free.push_back(q.b);
+  }
+  s->krec.erase(s->krec.begin(), s->krec.begin() + n);
+}
+
 static ScanArgs scan_args(kb_sim* s, uint32_t n, uint32_t* totals) {
   ScanArgs a; memset(&a, 0, sizeof a); a.n = n; a.totals = totals;
   a.tiles = s->scan_tiles; a.ntiles = (n + 1023) / 1024; return a;
 }
-static void launch_scan(const ScanArgs& a, hipStream_t st) {
+static void launch_scan(kb_sim* s, const ScanArgs& a) {
   if (!a.n) return;
-  k_scan_tiles<<<a.ntiles, 1024, 0, st>>>(a);
-  k_scan_apply<<<a.ntiles, 1024, 0, st>>>(a);
+  klaunch(s, KI_SCAN_TILES, k_scan_tiles, dim3(a.ntiles), dim3(1024), 0, a);
+  klaunch(s, KI_SCAN_APPLY, k_scan_apply, dim3(a.ntiles), dim3(1024), 0, a);
 }
 
 extern "C" void kb_config_default(kb_config* c) {
@@ -443,7 +517,9 @@ static void destroy_shard(kb_sim* s) {
   (void)hipSetDevice(s->device);
   if (s->st) (void)hipStreamSynchronize(s->st);
   free_all(s);
-  for (hipEvent_t e : {s->ev0, s->ev1, s->er0, s->er1, s->ef0, s->ef1, s->ew0, s->ew1}) if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : {s->er0, s->er1}) if (e) (void)hipEventDestroy(e);
+  for (auto& q : s->krec) { (void)hipEventDestroy(q.a); (void)hipEventDestroy(q.b); }
+  for (hipEvent_t e : s->ev_free) (void)hipEventDestroy(e);
   if (s->h_pin) (void)hipHostFree(s->h_pin);
   if (s->wave_exec) (void)hipGraphExecDestroy(s->wave_exec);
   if (s->wave_graph) (void)hipGraphDestroy(s->wave_graph);
@@ -506,10 +582,10 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   d.dbg = cfg->debug_flags;
   if (const char* dv = getenv("KB_DEV")) d.dev = (uint32_t)atoi(dv);
   s->debug_waves = getenv("KB_DEBUG_WAVES") != nullptr;
-  s->graph_on = getenv("KB_WAVE_GRAPH") != nullptr;
-  s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid); s->h_ever.assign(C, 0);
+  if (const char* gv = getenv("KB_WAVE_GRAPH")) s->graph_on = atoi(gv) != 0;
+  if (cfg->debug_flags & KB_DBG_WAVE_GRAPH) s->graph_on = true;
+  s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid);
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &s->h_ident[(size_t)j * MAXID]);
-  for (uint32_t j = 0; j < cfg->initial_nodes; ++j) s->h_ever[j] = 1;
   hipError_t e = hipSuccess;
 #define A(ptr, n) if (e == hipSuccess) e = talloc(s, &(ptr), (n))     // per-id / global tables
 #define AR(ptr, n) if (e == hipSuccess) e = ralloc(s, &(ptr), (n))   // row tables: n entries per local row
@@ -559,7 +635,8 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
     s->h_pin = nullptr; destroy_shard(s); seterr("pinned buffer"); return KB_IO_ERROR;
   }
   if (hipHostGetDevicePointer((void**)&s->d_pin, s->h_pin, 0) != hipSuccess) { destroy_shard(s); seterr("pinned buffer mapping"); return KB_IO_ERROR; }
-  for (hipEvent_t* e : {&s->ev0, &s->ev1, &s->er0, &s->er1, &s->ef0, &s->ef1, &s->ew0, &s->ew1}) (void)hipEventCreate(e);
+  for (hipEvent_t* e : {&s->er0, &s->er1}) (void)hipEventCreate(e);
+  if (const char* pv = getenv("KB_PROF")) s->prof_on = atoi(pv) != 0;
   int rc = upload_segments(s);
   if (rc) { destroy_shard(s); return rc; }
   uint32_t ctr0[NCTR] = {0};
@@ -640,7 +717,12 @@ extern "C" int kb_sim_shard_info(kb_sim* s, int32_t* rank, int32_t* world, uint3
 // Host side of the pinned hand-offs: spin on the mapped sequence word (a stream synchronisation would
 // pay an interrupt wake-up, tens of microseconds with the GPU idle), with the stream's own status as
 // the way out when it drained without publishing (a fault).
+static hipError_t sync_st(kb_sim* s) {            // a counted host wait on the simulator's stream
+  s->host_syncs++;
+  return hipStreamSynchronize(s->st);
+}
 static int wait_pin(kb_sim* s, uint32_t seq) {
+  s->host_syncs++;
   volatile uint32_t* p = s->h_pin + PIN_SEQ;
   for (uint64_t it = 0;; ++it) {
     if (*p == seq) { std::atomic_thread_fence(std::memory_order_acquire); return KB_OK; }
@@ -667,7 +749,7 @@ static int err_status(uint32_t e) {
 static int check_err(kb_sim* s) {
   if (s->xf && !s->xf->allreduce_max_u32(s->d.ctr + C_ERR, 1, s->st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
   HIPCHK(hipMemcpyAsync(s->h_pin, s->d.ctr + C_ERR, 4, hipMemcpyDeviceToHost, s->st));
-  HIPCHK(hipStreamSynchronize(s->st));
+  HIPCHK(sync_st(s));
   return err_status(s->h_pin[0]);
 }
 
@@ -740,13 +822,13 @@ static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb,
     a.narr = 2;
     a.in[0] = x.xcnt; a.out[0] = x.xoff;
     a.in[1] = x.xpay; a.out[1] = x.xpoff;
-    launch_scan(a, st);
+    launch_scan(s, a);
   }
-  k_xbound<<<1, 64, 0, st>>>(x, s->scan_tot + 16);
-  k_pack<<<(s->R + 3) / 4, 256, 0, st>>>(s->d, ob, x);
+  klaunch(s, KI_XBOUND, k_xbound, dim3(1), dim3(64), 0, x, s->scan_tot + 16);
+  klaunch(s, KI_PACK, k_pack, dim3((s->R + 3) / 4), dim3(256), 0, s->d, ob, x);
   if (!s->xf->allgather_u32(x.xb, s->xall, 2 * W, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
   HIPCHK(hipMemcpyAsync(s->h_xall.data(), s->xall, 4ull * 2 * W * W, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(sync_st(s));
   size_t sc[XMAX], sd[XMAX], rc[XMAX], rd[XMAX], psc[XMAX], psd[XMAX], prc[XMAX], prd[XMAX];
   size_t so = 0, pso = 0, ro = 0, pro = 0;
   uint64_t total = 0;
@@ -781,7 +863,7 @@ static int gather_broadcasts(kb_sim* s, uint32_t nj_loc, uint32_t nf_loc) {
   hipStream_t st = s->st;
   if (!s->xf->allgather_u32(s->scan_tot, s->xall, 2, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
   HIPCHK(hipMemcpyAsync(s->h_xall.data(), s->xall, 4ull * 2 * W, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(sync_st(s));
   size_t sc[XMAX], sd[XMAX], rc[XMAX], rd[XMAX], fsc[XMAX], frc[XMAX], frd[XMAX];
   size_t oj = 0, of = 0;
   for (int k = 0; k < W; ++k) {
@@ -813,15 +895,16 @@ static int launch_waves(kb_sim* s, int32_t rk) {
     OutBuf& nb = s->ob[cur ^ 1];
     const int last = w == s->cfg.max_waves;
     d.wave = (int32_t)w;                               // latency clock of the wave's prologues
+    s->cur_wave = (int)w;
     OutBuf ib = ob;                                    // the wave's delivered records
     uint32_t nrecv = 0;
     if (!s->xf) {
-      k_route<<<gnode, tb, 0, st>>>(d, ob, s->wc, r, w, last);
+      klaunch(s, KI_ROUTE, k_route, dim3(gnode), dim3(tb), 0, d, ob, s->wc, r, w, last);
       if (last) break;
     } else {
       HIPCHK(hipMemsetAsync(s->xs.xcnt, 0, 4ull * s->world * R, st));
       HIPCHK(hipMemsetAsync(s->xs.xpay, 0, 4ull * s->world * R, st));
-      k_route_x<<<gnode, tb, 0, st>>>(d, ob, s->xs, r, w, last);
+      klaunch(s, KI_ROUTE_X, k_route_x, dim3(gnode), dim3(tb), 0, d, ob, s->xs, r, w, last);
       if (last) break;
       RecvBlocks rb;
       memset(&rb, 0, sizeof rb);
@@ -830,7 +913,7 @@ static int launch_waves(kb_sim* s, int32_t rk) {
       if (rc) return rc;
       if (!any) break;                                 // no record anywhere: the rest of the round's waves are empty
       ib.msgs = s->rmsg; ib.pay = s->rpay;
-      if (nrecv) k_route_recv<<<(nrecv + 255) / 256, 256, 0, st>>>(d, ib, s->wc, rb, nrecv);
+      if (nrecv) klaunch(s, KI_ROUTE_RECV, k_route_recv, dim3((nrecv + 255) / 256), dim3(256), 0, d, ib, s->wc, rb, nrecv);
     }
     {
       ScanArgs a = scan_args(s, R, s->scan_tot + 8);
@@ -840,7 +923,7 @@ static int launch_waves(kb_sim* s, int32_t rk) {
       a.in[2] = L(s, s->wc.bpay); a.out[2] = L(s, nb.poff);
       a.in[3] = L(s, s->wc.kcnt); a.out[3] = L(s, s->wc.koff);
       a.list = s->wc.active; a.list_count = d.ctr + C_ACTIVE; a.list_base = s->lo; a.list_or3 = 1;
-      launch_scan(a, st);
+      launch_scan(s, a);
     }
     if (s->debug_waves) {                               // KB_DEBUG_WAVES: inbox sizes per wave
       std::vector<uint32_t> c1(R);
@@ -851,21 +934,21 @@ static int launch_waves(kb_sim* s, int32_t rk) {
       fprintf(stderr, "[kb] round %d wave %u: in-order msgs %llu, max inbox %u (node %u), inboxes > 64: %u\n", r, w,
               (unsigned long long)sum, mx, arg, big);
     }
-    if (!s->xf) k_scatter<<<gnode, tb, 0, st>>>(d, ob, s->wc);
-    else if (nrecv) k_scatter_flat<<<(nrecv + 255) / 256, 256, 0, st>>>(ib, s->wc, nrecv);
+    if (!s->xf) klaunch(s, KI_SCATTER, k_scatter, dim3(gnode), dim3(tb), 0, d, ob, s->wc);
+    else if (nrecv) klaunch(s, KI_SCATTER_FLAT, k_scatter_flat, dim3((nrecv + 255) / 256), dim3(256), 0, ib, s->wc, nrecv);
     if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
-    k_kp_small<<<(R + 255) / 256, 256, 0, st>>>(d, ib, s->wc, r, nb);   // also sets up nb.cap / nb.cnt
+    klaunch(s, KI_KP_SMALL, k_kp_small, dim3((R + 255) / 256), dim3(256), 0, d, ib, s->wc, r, nb);   // also sets up nb.cap / nb.cnt
     {  // BIG groups in LDS: KP_COLS workgroups per destination group, one per column part
       const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
       const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
-      k_kp_group<true><<<ks * groups, 1024, kp_lds_bytes(d.NWR), st>>>(d, ib, s->wc, r);
+      klaunch(s, KI_KP_GROUP, k_kp_group<true>, dim3(ks * groups), dim3(1024), kp_lds_bytes(d.NWR), d, ib, s->wc, r);
     }
-    k_sort_inbox<<<256, 1024, 0, st>>>(d, s->wc, r);   // + the KPR oversize probe
-    k_proc_fast<<<gnode, tb, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
+    klaunch(s, KI_SORT_INBOX, k_sort_inbox, dim3(256), dim3(1024), 0, d, s->wc, r);   // + the KPR oversize probe
+    klaunch(s, KI_PROC_FAST, k_proc_fast, dim3(gnode), dim3(tb), 0, d, ib, nb, s->wc, r, s->slow);
     // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
     // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
     // on the late waves with few nodes.
-    k_proc<<<std::min<uint32_t>(4096, 2 * s->ncu), 256, 0, st>>>(d, ib, nb, s->wc, r, s->slow);
+    klaunch(s, KI_PROC, k_proc, dim3(std::min<uint32_t>(4096, 2 * s->ncu)), dim3(256), 0, d, ib, nb, s->wc, r, s->slow);
     if (s->debug_waves) {
       uint32_t dbg[13], slow = 0;
       HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost, st));
@@ -885,6 +968,7 @@ static int launch_waves(kb_sim* s, int32_t rk) {
     }
     cur ^= 1;
   }
+  s->cur_wave = -1;
   return KB_OK;
 }
 
@@ -894,9 +978,11 @@ static int step_round(kb_sim* s) {
   const uint32_t C = s->C, R = s->R;
   hipStream_t st = s->st;
   const uint32_t tb = 256, gnode = (R + tb - 1) / tb, gwave = (R + 3) / 4, gall = (C + tb - 1) / tb;
+  const size_t krec0 = s->krec.size();               // records of earlier rounds (complete)
+  s->cur_wave = -1;
   (void)hipEventRecord(s->er0, st);
   // 0. stamp window
-  if (r > 0 && r % EPOCH == 0) k_rebase<<<8192, 256, 0, st>>>(d);
+  if (r > 0 && r % EPOCH == 0) klaunch(s, KI_REBASE, k_rebase, dim3(8192), dim3(256), 0, d);
   // 1. lifecycle (every shard applies the same events and churn draws to the replicated per-id state)
   if (!s->events.empty()) {
     if (s->events.size() > s->events_cap) {
@@ -905,19 +991,19 @@ static int step_round(kb_sim* s) {
       HIPCHK(hipMalloc(&s->d_events, sizeof(Event) * s->events_cap));
     }
     HIPCHK(hipMemcpyAsync(s->d_events, s->events.data(), sizeof(Event) * s->events.size(), hipMemcpyHostToDevice, st));
-    k_events<<<1, 1, 0, st>>>(d, s->d_events, (uint32_t)s->events.size(), r);
-    HIPCHK(hipStreamSynchronize(st));
+    klaunch(s, KI_EVENTS, k_events, dim3(1), dim3(1), 0, d, s->d_events, (uint32_t)s->events.size(), r);
+    HIPCHK(sync_st(s));
     s->events.clear();
   }
   const bool faults_on = s->cfg.fault_end_round < 0 || r < s->cfg.fault_end_round;
   if (faults_on && s->cfg.churn_threshold) {
-    k_churn_leave<<<gall, tb, 0, st>>>(d, r);
-    k_churn_join<<<1, 1024, 0, st>>>(d, r);
+    klaunch(s, KI_CHURN_LEAVE, k_churn_leave, dim3(gall), dim3(tb), 0, d, r);
+    klaunch(s, KI_CHURN_JOIN, k_churn_join, dim3(1), dim3(1024), 0, d, r);
   }
-  k_alive_bits<<<(d.NWR + tb - 1) / tb, tb, 0, st>>>(d);
-  k_truefp_part<<<TRUEFP_G, 256, 0, st>>>(d, d.tfpart);
-  k_truefp_fin<<<1, 64, 0, st>>>(d, d.tfpart);
-  k_log_mark<<<gnode, tb, 0, st>>>(d, r);
+  klaunch(s, KI_ALIVE_BITS, k_alive_bits, dim3((d.NWR + tb - 1) / tb), dim3(tb), 0, d);
+  klaunch(s, KI_TRUEFP_PART, k_truefp_part, dim3(TRUEFP_G), dim3(256), 0, d, d.tfpart);
+  klaunch(s, KI_TRUEFP_FIN, k_truefp_fin, dim3(1), dim3(64), 0, d, d.tfpart);
+  klaunch(s, KI_LOG_MARK, k_log_mark, dim3(gnode), dim3(tb), 0, d, r);
   // 2. broadcasts of round r-1
   OutBuf& o0 = s->ob[0];
   PhaseB pb;
@@ -940,11 +1026,11 @@ static int step_round(kb_sim* s) {
   // latency upkeep for Failed removals; socket_faithful never honours Failed, so nothing to do there
   const bool lat_fail = d.lat && s->nf && d.failed_mode == KB_FAILED_SIM_SENDER;
   pb.fnamed = lat_fail ? s->fnamed : nullptr;
-  if (lat_fail) k_lat_mark<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->fnamed);
+  if (lat_fail) klaunch(s, KI_LAT_MARK, k_lat_mark, dim3((s->nf + 255) / 256), dim3(256), 0, (const BCast*)s->bfail, s->nf, s->fnamed);
   const bool have_b = s->nf + s->nj > 0;
   const bool pb_hbm = (d.dbg & KB_DBG_PHASEB_HBM) != 0;
-  if (s->nf > 2048 || (pb_hbm && s->nf)) k_bfail_prep<<<(s->nf + 255) / 256, 256, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep, d.ctr + C_PATHS);
-  else if (s->nf) k_bfail_prep_lds<<<1, 1024, 0, st>>>(s->bfail, s->nf, s->bf_gid, s->bf_dep);
+  if (s->nf > 2048 || (pb_hbm && s->nf)) klaunch(s, KI_BFAIL_PREP, k_bfail_prep, dim3((s->nf + 255) / 256), dim3(256), 0, (const BCast*)s->bfail, s->nf, s->bf_gid, s->bf_dep, d.ctr + C_PATHS);
+  else if (s->nf) klaunch(s, KI_BFAIL_PREP, k_bfail_prep_lds, dim3(1), dim3(1024), 0, (const BCast*)s->bfail, s->nf, s->bf_gid, s->bf_dep);
   {
     // the row pass (broadcast phase + A3 candidates), persistent waves; broadcast lists staged in LDS
     // once per workgroup when they fit.  Its events are taken by its own dispatch packet
@@ -970,11 +1056,12 @@ static int step_round(kb_sim* s) {
     if (s->debug_waves && r == 2)
       fprintf(stderr, "[kb] row pass: %u waves/workgroup, %zu B LDS, %u workgroups/CU (lds_per_cu %zu), %u workgroups\n", wpb,
               lds, per_cu, (size_t)s->lds_per_cu, blocks);
-    if (ldsb) hipExtLaunchKernelGGL(k_rowpass<true>, dim3(blocks), dim3(64 * wpb), lds, st, s->ev0, s->ev1, 0, d, pb, s->ro, r, lf, lj);
-    else hipExtLaunchKernelGGL(k_rowpass<false>, dim3(blocks), dim3(64 * wpb), lds, st, s->ev0, s->ev1, 0, d, pb, s->ro, r, lf, lj);
+    if (ldsb) klaunch(s, KI_ROWPASS, k_rowpass<true>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r, lf, lj);
+    else klaunch(s, KI_ROWPASS, k_rowpass<false>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r, lf, lj);
   }
   if (lat_fail)
-    k_lat_sweep<<<dim3((lat_stride(R) / 8 + 255) / 256, std::min<uint32_t>(s->nf, 16384)), 256, 0, st>>>(d, s->bfail, s->bf_gid, s->nf, s->fnamed);
+    klaunch(s, KI_LAT_SWEEP, k_lat_sweep, dim3((lat_stride(R) / 8 + 255) / 256, std::min<uint32_t>(s->nf, 16384)), dim3(256), 0, d,
+            (const BCast*)s->bfail, (const uint32_t*)s->bf_gid, s->nf, s->fnamed);
   {  // wave-0 outbox regions: responses first, then the tick's messages
     ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 3;
@@ -982,10 +1069,10 @@ static int step_round(kb_sim* s) {
     a.in[1] = L(s, s->paysum); a.out[1] = L(s, o0.poff);
     a.in[2] = L(s, s->nresp); a.out[2] = L(s, o0.off); a.addc[2] = TICK_MAX;
     a.list = s->resp_nodes; a.list_base = s->lo;
-    launch_scan(a, st);
+    launch_scan(s, a);
   }
   const bool need_tot = have_b && s->nj;
-  k_set_cap<<<gnode, tb, 0, st>>>(d, s->nresp, o0.cap, o0.cnt, s->scan_tot, s->d_pin, need_tot ? ++s->pin_seq : 0u);
+  klaunch(s, KI_SET_CAP, k_set_cap, dim3(gnode), dim3(tb), 0, d, s->nresp, o0.cap, o0.cnt, s->scan_tot, s->d_pin, need_tot ? ++s->pin_seq : 0u);
   if (need_tot) {
     const uint32_t* tot = s->h_pin;                 // written by k_set_cap through the host mapping
     { const int rc = wait_pin(s, s->pin_seq); if (rc) return rc; }
@@ -1014,11 +1101,11 @@ static int step_round(kb_sim* s) {
       const bool wave_on = wlds <= 65536 && !(d.dbg & KB_DBG_RESP_HBM);
       if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
       if (wave_on) {                                   // timed by events on its own dispatch packet
-        hipExtLaunchKernelGGL(k_resp_wave, dim3(std::min<uint32_t>((resp_nodes + 3) / 4, 4096)), dim3(256), wlds, st, s->ew0,
-                              s->ew1, 0, d, pb, (const uint32_t*)s->resp_nodes, (const uint32_t*)(s->scan_tot + 4), o0, r);
-        s->resp_timed = true;
+        klaunch(s, KI_RESP_WAVE, k_resp_wave, dim3(std::min<uint32_t>((resp_nodes + 3) / 4, 4096)), dim3(256), (uint32_t)wlds, d,
+                pb, (const uint32_t*)s->resp_nodes, (const uint32_t*)(s->scan_tot + 4), o0, r);
       }
-      k_resp_node<<<grid, 256, lds, st>>>(d, pb, s->resp_nodes, s->scan_tot + 4, o0, r, scratch, wave_on);
+      klaunch(s, KI_RESP_NODE, k_resp_node, dim3(grid), dim3(256), (uint32_t)lds, d, pb, (const uint32_t*)s->resp_nodes,
+              (const uint32_t*)(s->scan_tot + 4), o0, r, scratch, wave_on);
       if (s->debug_waves && (d.dev & 512)) {
         uint32_t dbg[13];
         HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost, st));
@@ -1029,24 +1116,21 @@ static int step_round(kb_sim* s) {
     }
   }
   // 3. tick
-  k_tick_scan<<<gnode, tb, 0, st>>>(d, s->bs, r, s->slow);                       // A1; list the A2 nodes
-  k_tick_pre<<<std::min<uint32_t>(gwave, 1024), 256, 0, st>>>(d, o0, s->bs, r, s->slow);   // A2 per listed node
-  // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded; timed by
-  // events on its own dispatch packet (a marker recorded before the launch can run while k_tick_pre
-  // is still executing)
-  if (d.uniform)
-    hipExtLaunchKernelGGL(k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, st, s->ef0, s->ef1, 0, d, FoldArgs{s->S});
-  if (d.uniform) k_fp_rows<<<(FP_LANES * R + tb - 1) / tb, tb, 0, st>>>(d);
-  k_tick_post<<<gnode, tb, 0, st>>>(d, s->ro, o0, r);
+  klaunch(s, KI_TICK_SCAN, k_tick_scan, dim3(gnode), dim3(tb), 0, d, s->bs, r, s->slow);                       // A1; list the A2 nodes
+  klaunch(s, KI_TICK_PRE, k_tick_pre, dim3(std::min<uint32_t>(gwave, 1024)), dim3(256), 0, d, o0, s->bs, r, s->slow);   // A2 per listed node
+  // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded
+  if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
+  if (d.uniform) klaunch(s, KI_FP_ROWS, k_fp_rows, dim3((FP_LANES * R + tb - 1) / tb), dim3(tb), 0, d);
+  klaunch(s, KI_TICK_POST, k_tick_post, dim3(gnode), dim3(tb), 0, d, s->ro, o0, r);
   {
     ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 2;
     a.in[0] = L(s, s->bs.join); a.out[0] = L(s, s->join_off);
     a.in[1] = L(s, s->bs.nfail); a.out[1] = L(s, s->fail_off);
-    launch_scan(a, st);
+    launch_scan(s, a);
   }
-  k_bcast_write<<<gnode, tb, 0, st>>>(d, s->bs, s->join_off, s->fail_off, s->xf ? s->bjoin_loc : s->bjoin,
-                                      s->xf ? s->bfail_loc : s->bfail);
+  klaunch(s, KI_BCAST_WRITE, k_bcast_write, dim3(gnode), dim3(tb), 0, d, s->bs, (const uint32_t*)s->join_off,
+          (const uint32_t*)s->fail_off, s->xf ? s->bjoin_loc : s->bjoin, s->xf ? s->bfail_loc : s->bfail);
   // 4. receive window: unicast waves.  Unsharded, the window has no host decision inside it, so with
   // KB_WAVE_GRAPH=1 its ≈ 80 launches are one HIP graph, captured once per buffer generation and
   // replayed each round: that removes host launch gaps in multi-round steps, but the benched one-round
@@ -1056,7 +1140,9 @@ static int step_round(kb_sim* s) {
       if (s->wave_exec) { (void)hipGraphExecDestroy(s->wave_exec); s->wave_exec = nullptr; }
       if (s->wave_graph) { (void)hipGraphDestroy(s->wave_graph); s->wave_graph = nullptr; }
       HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      s->capturing = true;                           // captured launches carry no profile events
       const int rc = launch_waves(s, -1);
+      s->capturing = false;
       hipGraph_t g = nullptr;
       const hipError_t e = hipStreamEndCapture(st, &g);
       if (rc) { if (g) (void)hipGraphDestroy(g); return rc; }
@@ -1071,12 +1157,14 @@ static int step_round(kb_sim* s) {
     if (rc) return rc;
   }
   if (s->xf && !s->xf->allreduce_sum_u32(d.ctr + C_AGREE, 1, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  k_round_end<<<1, 1, 0, st>>>(d, r, s->scan_tot, s->d_pin, ++s->pin_seq);
+  klaunch(s, KI_ROUND_END, k_round_end, dim3(1), dim3(1), 0, d, r, (const uint32_t*)s->scan_tot, s->d_pin, ++s->pin_seq);
   (void)hipEventRecord(s->er1, st);
+  // the earlier rounds' kernel events are complete: read them while this round runs
+  prof_resolve(s, krec0);
   // k_round_end wrote the next round's broadcast counts and the error flag straight into the
   // host-mapped pinned buffer; the host polls for them, then finds the stream drained
   { const int rc = wait_pin(s, s->pin_seq); if (rc) return rc; }
-  HIPCHK(hipStreamSynchronize(st));
+  HIPCHK(sync_st(s));
   const uint32_t nj_loc = s->h_pin[0], nf_loc = s->h_pin[1], err = s->h_pin[2];
   if (s->xf) {
     const int rc = gather_broadcasts(s, nj_loc, nf_loc);
@@ -1086,9 +1174,6 @@ static int step_round(kb_sim* s) {
   }
   s->bj_total += s->nj; s->bf_total += s->nf;
   float ms = 0;
-  (void)hipEventElapsedTime(&ms, s->ev0, s->ev1); s->rowpass_ms += ms; s->rowpass_launches++;
-  if (d.uniform) { (void)hipEventElapsedTime(&ms, s->ef0, s->ef1); s->fold_ms += ms; s->fold_launches++; }
-  if (s->resp_timed) { (void)hipEventElapsedTime(&ms, s->ew0, s->ew1); s->resp_ms += ms; s->resp_launches++; s->resp_timed = false; }
   (void)hipEventElapsedTime(&ms, s->er0, s->er1); s->round_ms += ms; s->round_launches++;
   s->round = r + 1;
   return s->xf ? check_err(s) : err_status(err);   // shards: the flag of any rank
@@ -1170,7 +1255,6 @@ extern "C" int kb_sim_start_node(kb_sim* s, uint32_t node) {
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_start_node(t, node); });
   s->events.push_back(Event{node, 0});
-  s->h_ever[node] = 1;
   return KB_OK;
 }
 extern "C" int kb_sim_stop_node(kb_sim* s, uint32_t node) {
@@ -1212,19 +1296,32 @@ extern "C" int kb_sim_ping_addrs(kb_sim* s, uint32_t node, const uint32_t* peers
 extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* identity, size_t len) {
   if (chk(s, node) || len > MAXID || (len && !identity)) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_set_identity(t, node, identity, len); });
-  uint8_t a = 0;
-  HIPCHK(hipMemcpy(&a, s->d.alive + node, 1, hipMemcpyDeviceToHost));
-  uint32_t nfree = 0;
-  HIPCHK(hipMemcpy(&nfree, s->d.ctr + C_NEXTFREE, 4, hipMemcpyDeviceToHost));
-  const bool ever = s->h_ever[node] || (node < nfree && node >= s->cfg.initial_nodes && s->cfg.churn_threshold);
-  if (a || ever) { seterr("Cannot change identity while the mesh is running; call .stop first"); return KB_INVALID_OPERATION; }
+  // running as the API sees it: the last start/stop queued for the node since the last step, else now
+  int run = -1;
+  for (size_t k = s->events.size(); k-- > 0;) if (s->events[k].node == node) { run = !s->events[k].stop; break; }
+  if (run < 0) {
+    uint8_t a = 0;
+    HIPCHK(hipMemcpy(&a, s->d.alive + node, 1, hipMemcpyDeviceToHost));
+    run = a;
+  }
+  if (run) { seterr("Cannot change identity while the mesh is running; call .stop first"); return KB_INVALID_OPERATION; }
   if (len != s->cfg.id_len && s->C > 200) { seterr("non-uniform identity length needs capacity <= 200"); return KB_INVALID_ARGUMENT; }
   memcpy(&s->h_ident[(size_t)node * MAXID], identity, len);
   s->h_idlen[node] = (uint8_t)len;
   int rc = upload_segments(s);
   if (rc) return rc;
+  s->buf_gen++;                                    // a captured receive window holds the old Dev (uniform, L)
   k_mark_all_dirty<<<(s->R + 255) / 256, 256, 0, s->st>>>(s->d);
   HIPCHK(hipStreamSynchronize(s->st));
+  return KB_OK;
+}
+extern "C" int kb_sim_identity(kb_sim* s, uint32_t node, uint8_t* buf, size_t cap, size_t* len) {
+  if (chk(s, node) || !len) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) return kb_sim_identity(s->shards[0], node, buf, cap, len);   // replicated per id
+  *len = s->h_idlen[node];
+  if (!buf) return KB_OK;
+  if (cap < *len) return KB_CAPACITY;
+  memcpy(buf, &s->h_ident[(size_t)node * MAXID], *len);
   return KB_OK;
 }
 extern "C" int kb_sim_fingerprint(kb_sim* s, uint32_t node, uint32_t* fp) {
@@ -1313,7 +1410,10 @@ extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, 
     if (!rw[j]) continue;
     if (out && c < cap) {
       kb_peer_state& o = out[c];
+      memset(&o, 0, sizeof o);
       o.peer = j;
+      o.identity_len = s->h_idlen[j];
+      memcpy(o.identity, &s->h_ident[(size_t)j * MAXID], s->h_idlen[j]);
       o.latency_ms = !lat.empty() && lat[j] != LAT_NONE ? lat[j] : KB_LATENCY_NONE;
       if (rw[j] == ST_SUSPECT) {
         const Susp* q = nullptr;
@@ -1507,14 +1607,24 @@ extern "C" uint32_t kb_fingerprint_of_set(const uint32_t* ids, size_t n, const u
   }
   return reg ^ 0xFFFFFFFFu;
 }
+static int kt_kid(int kind) {
+  return kind == KB_KT_ROWPASS ? KI_ROWPASS : kind == KB_KT_FOLD ? KI_FOLD : kind == KB_KT_RESP ? KI_RESP_WAVE
+       : kind == KB_KT_PROC ? KI_PROC : -1;
+}
+// the stream is idle: every pending kernel record can be read
+static void prof_flush(kb_sim* s) {
+  (void)hipSetDevice(s->device);
+  if (s->st) (void)hipStreamSynchronize(s->st);
+  prof_resolve(s, s->krec.size());
+}
 extern "C" int kb_sim_kernel_time(kb_sim* s, int kind, double* ms, uint64_t* launches) {
   if (!s || !ms || !launches) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_kernel_time(s->shards[0], kind, ms, launches);
-  if (kind == KB_KT_ROWPASS) { *ms = s->rowpass_ms; *launches = s->rowpass_launches; }
-  else if (kind == KB_KT_ROUND) { *ms = s->round_ms; *launches = s->round_launches; }
-  else if (kind == KB_KT_FOLD) { *ms = s->fold_ms; *launches = s->fold_launches; }
-  else if (kind == KB_KT_RESP) { *ms = s->resp_ms; *launches = s->resp_launches; }
-  else return KB_INVALID_ARGUMENT;
+  prof_flush(s);
+  if (kind == KB_KT_ROUND) { *ms = s->round_ms; *launches = s->round_launches; return KB_OK; }
+  const int k = kt_kid(kind);
+  if (k < 0) return KB_INVALID_ARGUMENT;
+  *ms = s->k_ms[k]; *launches = s->k_n[k];
   return KB_OK;
 }
 static uint64_t stat_counter(kb_sim* s, int idx) {
@@ -1526,11 +1636,13 @@ static uint64_t stat_counter(kb_sim* s, int idx) {
 extern "C" int kb_sim_reset_kernel_time(kb_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
   GROUP_ALL(kb_sim_reset_kernel_time);
-  s->rowpass_ms = s->round_ms = s->fold_ms = s->resp_ms = 0;
-  s->rowpass_launches = s->round_launches = s->fold_launches = s->resp_launches = 0;
-  s->resp_bytes0 = stat_counter(s, S_RESPB);
-  s->row_bytes0 = stat_counter(s, S_ROWB);        // baselines of the device-side byte counters
-  s->fold_bytes0 = stat_counter(s, S_FOLDB);
+  prof_flush(s);
+  s->round_ms = 0; s->round_launches = 0;
+  memset(s->k_ms, 0, sizeof s->k_ms); memset(s->k_wms, 0, sizeof s->k_wms); memset(s->k_n, 0, sizeof s->k_n);
+  for (int k = 0; k < NKI; ++k) {                   // baselines of the device-side byte counters
+    const int b = kbytes_stat(k);
+    if (b >= 0) s->k_bytes0[b] = stat_counter(s, b);
+  }
   return KB_OK;
 }
 // algorithmic bytes a kernel moved since the last reset, counted in-kernel; this handle's
@@ -1538,10 +1650,52 @@ extern "C" int kb_sim_reset_kernel_time(kb_sim* s) {
 extern "C" int kb_sim_kernel_bytes(kb_sim* s, int kind, uint64_t* bytes) {
   if (!s || !bytes) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_kernel_bytes(s->shards[0], kind, bytes);
-  if (kind == KB_KT_ROWPASS) *bytes = stat_counter(s, S_ROWB) - s->row_bytes0;
-  else if (kind == KB_KT_FOLD) *bytes = stat_counter(s, S_FOLDB) - s->fold_bytes0;
-  else if (kind == KB_KT_RESP) *bytes = stat_counter(s, S_RESPB) - s->resp_bytes0;
-  else return KB_INVALID_ARGUMENT;
+  const int k = kt_kid(kind), b = k < 0 ? -1 : kbytes_stat(k);
+  if (b < 0) return KB_INVALID_ARGUMENT;
+  *bytes = stat_counter(s, b) - s->k_bytes0[b];
+  return KB_OK;
+}
+extern "C" int kb_sim_set_profiling(kb_sim* s, int on) {
+  if (!s) return KB_INVALID_ARGUMENT;
+  GROUP_ALL([&](kb_sim* t) { return kb_sim_set_profiling(t, on); });
+  s->prof_on = on != 0;
+  return KB_OK;
+}
+// every kernel the rounds launched since the last reset: HIP-event time (sum and per delivery wave),
+// launches, algorithmic bytes where counted in-kernel; kernels never launched are omitted
+extern "C" int kb_sim_kernel_breakdown(kb_sim* s, kb_kernel_time* out, size_t cap, size_t* n) {
+  if (!s || !n) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) return kb_sim_kernel_breakdown(s->shards[0], out, cap, n);
+  prof_flush(s);
+  size_t c = 0;
+  for (int k = 0; k < NKI; ++k) {
+    if (!s->k_n[k]) continue;
+    if (out && c < cap) {
+      kb_kernel_time& o = out[c];
+      memset(&o, 0, sizeof o);
+      snprintf(o.name, sizeof o.name, "%s", KNAME[k]);
+      o.ms = s->k_ms[k]; o.launches = s->k_n[k];
+      const int b = kbytes_stat(k);
+      o.bytes = b >= 0 ? stat_counter(s, b) - s->k_bytes0[b] : 0;
+      o.has_bytes = b >= 0;
+      for (int w = 0; w < KB_WAVE_SLOTS; ++w) o.wave_ms[w] = s->k_wms[k][w];
+    }
+    c++;
+  }
+  *n = c;
+  return (out && cap < c) ? KB_CAPACITY : KB_OK;
+}
+// host waits on the device since creation (stream synchronisations and pinned hand-offs); for a
+// group, the largest over its shards
+extern "C" int kb_sim_host_syncs(kb_sim* s, uint64_t* n) {
+  if (!s || !n) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) {
+    uint64_t m = 0;
+    for (kb_sim* t : s->shards) m = std::max(m, t->host_syncs);
+    *n = m;
+    return KB_OK;
+  }
+  *n = s->host_syncs;
   return KB_OK;
 }
 // OR of the PATH_* bits (kb_common.h) of the kernel variants that did work since creation

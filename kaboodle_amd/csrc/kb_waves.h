@@ -829,6 +829,11 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
   const uint8_t now = enc(r, r);
   const uint8_t fresh_thr = enc(r - (SHARE_AGE - 1), r);
   unsigned long long w_over = 0, w_curovf = 0;      // flushed once per wave (see k_phaseB)
+  // algorithmic bytes (bench roofline): every table word the handlers must read or write —
+  // node header and slot tables, inbox indices and records, each sender's member word and stamp, the
+  // stamps / log entries / bits written, checkpoints and the member bytes + table words of every
+  // (partial) fold, freshness-log entries scanned, records and payload ids emitted
+  unsigned long long w_bytes = 0;
   for (uint32_t it = blockIdx.x * 4 + wv; it < nact; it += gridDim.x * 4) {
     const uint32_t i = list[it];
     const bool tdbg = (d.dev & 64) != 0;                // timing breakdown (KB_DEV=64, KB_DEBUG_WAVES)
@@ -845,6 +850,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
         else ob.msgs[ob_off + oseq] = Msg{dest, i, oseq, kind, a, efp, en, off};
       }
       oseq++;
+      w_bytes += sizeof(Msg);
     };
     int32_t kbig = d.kpr_big[i];
     bool dirty = d.dirty[i] != 0, need_sync = false;
@@ -854,6 +860,8 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     wait_lds();
     __builtin_amdgcn_wave_barrier();
     const uint32_t ibase = wc.in_off[i], icnt = wc.cnt1[i];
+    // header + slot tables read and written back, inbox index + record of every message
+    w_bytes += 2 * (28 + sizeof(Susp) * SLOTS + sizeof(Cur) * CSLOTS) + (4 + sizeof(Msg)) * (uint64_t)icnt;
     // canonical order = ascending outbox index = (sender, seq): one wave sorts <= 64 entries in
     // registers; k_sort_inbox has sorted longer inboxes up to SORT_MAX in place
     uint32_t mine = l < icnt ? wc.inbox[ibase + l] : 0xFFFFFFFFu;
@@ -883,6 +891,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       if (need_sync) { wave_mem_sync(); need_sync = false; }
       dbg_base++;
       const unsigned long long sd = d.sdirty[i] | segs;
+      w_bytes += 8 * NSEG + 4 * 64 + (uint64_t)__popcll(sd) * (5 * (d.SEGW / 8) + 8);   // checkpoints, Z^n row, refolds
       uint2 sp;
       if ((sd >> l) & 1ull) { sp = fold_segment(d, ztab, i, l); d.segp[(size_t)i * NSEG + l] = sp; }
       else sp = d.segp[(size_t)i * NSEG + l];
@@ -927,6 +936,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       }
       if (dirty) {
         dbg_fp++;
+        w_bytes += 8 * NSEG + (uint64_t)__popcll(d.sdirty[i] | segs) * (5 * (d.SEGW / 8) + 8);
         if (need_sync) { wave_mem_sync(); need_sync = false; }
         fp = wave_fp(d, ztab, i, segs);
         segs = 0;
@@ -965,6 +975,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           const uint32_t prev = __shfl_up(lm.sender, 1, 64);
           const bool ins = gl != 0xFFFFFFFFu && !pre_was && lm.sender != (l == 0 ? last_sender : prev);
           const unsigned long long insm = __ballot(ins);
+          w_bytes += 5ull * __popcll(__ballot(gl != 0xFFFFFFFFu));   // each sender's member word + stamp
           if (d.uniform && insm) {
             const uint64_t ta = tdbg ? wall_clock64() : 0;
             if (!inc) take_base();
@@ -990,11 +1001,13 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
                 const uint32_t Bx = multmodp(d.zpow[su.y], praw) ^ su.x;
                 Kx = mulzc(ztab, Bx, 1) ^ Bx ^ multmodp(d.zpow[pcnt + su.y], d.cseg[x]);
               }
+              w_bytes += wave_sum(ins ? 5u * ((seg_of(d, lm.sender) + 1) * (d.SEGW / 8) - (lm.sender >> 3)) + 12u : 0u);
             } else {                                  // few: the whole wave on each insertion
               for (unsigned long long mm = insm; mm; mm &= mm - 1) {
                 const int q = __ffsll((long long)mm) - 1;
                 const uint32_t x = bcast(lm.sender, q), k = seg_of(d, x);
                 const uint32_t hs = x >> 3, nh = (k + 1) * (d.SEGW / 8) - hs;
+                w_bytes += 5ull * nh + 12;
                 uint32_t praw = 0, pcnt = 0;
                 for (uint32_t h = hs + (l * nh) / 64; h < hs + ((l + 1) * nh) / 64; ++h) {
                   uint32_t m8 = hb[h];
@@ -1042,6 +1055,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           lat_sample(d, i, s, s_susp[wv][l].since, r);
           s_susp[wv][l].kind = 0;
         }
+        w_bytes += (!was ? 4u : 0u) + (b != now ? 5u : 0u);   // bit word, stamp + log entry written
         if (!was) {
           dbg_ins++;
           n++; segs |= seg_bit(d, s);
@@ -1146,6 +1160,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
               bv[u] = rw[j];
             }
             dbg_log += 64 * KPR_BATCH;
+            w_bytes += 9ull * (fn - k0 < 64u * KPR_BATCH ? fn - k0 : 64u * KPR_BATCH);   // log entry, member word, stamp
 #pragma unroll
             for (int u = 0; u < KPR_BATCH; ++u) {
               if (over) break;                          // wave-uniform
@@ -1175,7 +1190,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
           if (d.uniform && total > d.capk + 1) kbig = r;
           over = d.uniform ? total > d.capk : size > (uint64_t)BUFSZ;
           if (over) w_over++;
-          else { emit(s, K_KP, total, 0, 0, poff); pay_used += total; }
+          else { emit(s, K_KP, total, 0, 0, poff); pay_used += total; w_bytes += 4ull * total; }
           maybe_sync(s, m.fp, m.n);
           break;
         }
@@ -1209,6 +1224,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
   if (l == 0) {
     if (w_over) slot_add(d, S_OVERSIZE, w_over);
     if (w_curovf) slot_add(d, S_CUROVF, w_curovf);
+    if (w_bytes) slot_add(d, S_PROCB, w_bytes);
   }
 }
 

@@ -81,7 +81,6 @@ struct kbo_sim {
   uint8_t* stamp;             /* C x C */
   uint16_t* lat;              /* C x C PeerInfo.latency in ms, LAT_NONE = None (track_latency only) */
   uint8_t* alive;
-  uint8_t* ever;
   int32_t* start_round;
   uint32_t* n;
   uint32_t* fp;
@@ -320,7 +319,7 @@ static uint32_t kp_cap_uniform(kbo_sim* s) {   /* largest k with 20 + L + k(18+L
 
 /* ---- lifecycle (src/lib.rs:136-183, src/kaboodle.rs:114-185) ------------------------------------ */
 static void node_start(kbo_sim* s, uint32_t i, int32_t r) {
-  s->alive[i] = 1; s->ever[i] = 1; s->start_round[i] = r;
+  s->alive[i] = 1; s->start_round[i] = r;
   map_insert_known(s, i, i, r, r, -1);          /* known_peers.insert(self_addr, Known(now)) :145-152 */
   s->dirty[i] = 1;
   s->last_bcast[i] = INT32_MIN;             /* last_broadcast_time: None                    :170 */
@@ -354,7 +353,7 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   s->k0 = (uint32_t)cfg->seed; s->k1 = (uint32_t)(cfg->seed >> 32);
   size_t C = s->C;
   s->stamp = (uint8_t*)calloc(C * C, 1);
-  s->alive = (uint8_t*)calloc(C, 1); s->ever = (uint8_t*)calloc(C, 1);
+  s->alive = (uint8_t*)calloc(C, 1);
   s->start_round = (int32_t*)calloc(C, 4); s->n = (uint32_t*)calloc(C, 4); s->fp = (uint32_t*)calloc(C, 4);
   s->dirty = (uint8_t*)calloc(C, 1); s->last_bcast = (int32_t*)calloc(C, 4); s->a3cur = (uint32_t*)calloc(C, 4);
   s->susp = (osusp*)calloc(C * SLOTS, sizeof(osusp)); s->cur = (ocur*)calloc(C * CSLOTS, sizeof(ocur));
@@ -394,7 +393,7 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
 int kbo_sim_destroy(kbo_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
   for (uint32_t i = 0; i < s->C; ++i) free(s->out[i].v);
-  free(s->stamp); free(s->lat); free(s->alive); free(s->ever); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
+  free(s->stamp); free(s->lat); free(s->alive); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
   free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
   for (size_t k = 0; k < s->nwatch; ++k) free(s->wsnap[k]);
@@ -853,11 +852,18 @@ int kbo_sim_ping_addrs(kbo_sim* s, uint32_t node, const uint32_t* peers, size_t 
   }
   return KB_OK;
 }
-/* Kaboodle::set_identity (src/lib.rs:323-336); the simulator additionally requires that the id has
- * never run (identity is per id) and a uniform length when truncation is possible. */
+/* running as the API sees it: the last start/stop call queued for the node since the last step (they
+ * take effect at the next round start), else its current state */
+static int api_running(const kbo_sim* s, uint32_t node) {
+  for (uint32_t k = s->nev; k-- > 0;) if (s->ev[k].node == node) return !s->ev[k].stop;
+  return s->alive[node];
+}
+/* Kaboodle::set_identity (src/lib.rs:323-336): refused while running.  Identity belongs to the id
+ * (DESIGN.md §2.1): every view reports and fingerprints the new bytes from now on; a non-uniform length
+ * needs capacity <= 200 (the truncation sizes assume one length otherwise). */
 int kbo_sim_set_identity(kbo_sim* s, uint32_t node, const uint8_t* identity, size_t len) {
   if (check(s, node) || len > MAXID || (len && !identity)) return KB_INVALID_ARGUMENT;
-  if (s->alive[node] || s->ever[node]) {
+  if (api_running(s, node)) {
     seterr("Cannot change identity while the mesh is running; call .stop first");
     return KB_INVALID_OPERATION;
   }
@@ -871,6 +877,14 @@ int kbo_sim_set_identity(kbo_sim* s, uint32_t node, const uint8_t* identity, siz
   return KB_OK;
 }
 
+int kbo_sim_identity(kbo_sim* s, uint32_t node, uint8_t* buf, size_t cap, size_t* len) {
+  if (check(s, node) || !len) return KB_INVALID_ARGUMENT;
+  *len = s->id_len[node];
+  if (!buf) return KB_OK;
+  if (cap < *len) return KB_CAPACITY;
+  memcpy(buf, s->ident + (size_t)node * MAXID, *len);
+  return KB_OK;
+}
 int kbo_sim_fingerprint(kbo_sim* s, uint32_t node, uint32_t* fp) {
   if (check(s, node) || !fp) return KB_INVALID_ARGUMENT;
   *fp = cur_fp(s, node);
@@ -954,8 +968,11 @@ int kbo_sim_peer_states(kbo_sim* s, uint32_t node, kb_peer_state* out, size_t ca
     if (!rw[j]) continue;
     if (out && c < cap) {
       kb_peer_state* o = &out[c];
+      memset(o, 0, sizeof *o);
       o->peer = j;
       o->latency_ms = s->lat && s->lat[(size_t)node * s->C + j] != LAT_NONE ? s->lat[(size_t)node * s->C + j] : KB_LATENCY_NONE;
+      o->identity_len = s->id_len[j];
+      memcpy(o->identity, s->ident + (size_t)j * MAXID, s->id_len[j]);
       if (rw[j] == ST_SUSPECT) {
         osusp* q = susp_find(s, node, j);
         o->state = q && q->kind == SK_WFIP ? KB_STATE_WAITING_FOR_INDIRECT_PING : KB_STATE_WAITING_FOR_PING;

@@ -152,6 +152,8 @@ def apply_events(sims, case: dict, r: int) -> None:
                 s.stop_node(node)
             elif kind == "start":
                 s.start_node(node)
+            elif kind == "ident":
+                s.set_identity(node, arg)
             elif kind == "ping":
                 s.ping_addrs(node, arg)
 
@@ -227,6 +229,14 @@ def standard_cases() -> list[tuple[str, dict, int]]:
     # wave 0 (k_sort_inbox + k_proc's sorted path; with KB_DBG_PROC_UNSORTED the selection path)
     cases.append(("hot_inbox", {"cfg": SimConfig(capacity=256, initial_nodes=256, loss=0.02, seed=17),
                                 "events": {0: [("ping", i, [0]) for i in range(1, 201)]}}, 8))
+    # Kaboodle::set_identity on stopped peers (src/lib.rs:323-336), uniform and non-uniform lengths, restarted
+    cases.append(("identity_change", {"cfg": SimConfig(capacity=160, initial_nodes=150, init_mode=KB_INIT_CONVERGED,
+                                                       loss=0.02, id_len=6, seed=23),
+                                      "events": {2: [("stop", 9, None), ("stop", 70, None)],
+                                                 3: [("ident", 9, b"qwerty"), ("ident", 70, b"short"),
+                                                     ("start", 9, None)],
+                                                 5: [("ident", 155, b"fresh-peer-id"), ("start", 155, None),
+                                                     ("start", 70, None)]}}, 16))
     # stamps from before round 0 (early joiners' KnownPeers inserts) crossing three window rebases
     cases.append(("old_stamps", {"cfg": SimConfig(capacity=160, initial_nodes=128, init_mode=KB_INIT_CONVERGED, loss=0.02,
                                                   churn=0.03, fault_end_round=12, seed=31)}, 200))

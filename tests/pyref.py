@@ -457,17 +457,17 @@ class PyMesh:
 
     def peer_states(self, i):
         """Kaboodle::peer_states (src/lib.rs:348-354) as the ABI reports it: (peer, state, since,
-        latency); since = the exact instant, or INT32_MIN once the stamp window has saturated it
-        (DESIGN.md §2.2); latency in ms, 0xFFFFFFFF = None."""
+        latency, identity); since = the exact instant, or INT32_MIN once the stamp window has saturated
+        it; latency in ms, 0xFFFFFFFF = None."""
         rl = max(self.round - 1, 0)
         out = []
         p = self.peers[i]
         for q, (st, t) in sorted(p.known.items()):
             lat = p.latency.get(q, 0xFFFFFFFF)
             if st == KNOWN:
-                out.append((q, 0, t if stamp_key(t, rl) > 2 else -2 ** 31, lat))
+                out.append((q, 0, t if stamp_key(t, rl) > 2 else -2 ** 31, lat, self.identity[q]))
             else:
-                out.append((q, 1 if st == WFP else 2, t, lat))
+                out.append((q, 1 if st == WFP else 2, t, lat, self.identity[q]))
         return out
 
     def suspects(self, i):

@@ -45,6 +45,13 @@ SCENARIOS = [
     # rebases later (rounds 64, 128, 192) they sit at the bottom of the window: the saturation edge of k_rebase
     _sc("old_stamps", SimConfig(capacity=160, initial_nodes=128, init_mode=KB_INIT_CONVERGED, loss=0.02, churn=0.03,
                                 fault_end_round=12, seed=31), 200),
+    # Kaboodle::set_identity on stopped peers (src/lib.rs:323-336): one keeps the uniform length, one does not;
+    # both restart under the new identity and every view's fingerprint follows
+    _sc("identity_change", SimConfig(capacity=40, initial_nodes=36, init_mode=KB_INIT_CONVERGED, seed=19, loss=0.03,
+                                     id_len=4), 24,
+        events={2: [("stop", 5, None), ("stop", 11, None)], 3: [("ident", 5, b"wxyz"), ("ident", 11, b"zz"),
+                                                                ("start", 5, None)],
+                6: [("ident", 38, b"new-peer"), ("start", 38, None), ("start", 11, None)]}),
 ]
 
 BY_NAME = {s["name"]: s for s in SCENARIOS}
@@ -74,6 +81,8 @@ def apply_events(sim, sc, r):
             sim.stop_node(node)
         elif kind == "start":
             sim.start_node(node)
+        elif kind == "ident":
+            sim.set_identity(node, arg)
         else:
             sim.ping_addrs(node, arg)
 

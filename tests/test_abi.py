@@ -40,6 +40,7 @@ def test_hip_library_exports_every_symbol():
 def test_oracle_exports_every_symbol():
     lib = C.CDLL(ORACLE_SO)
     skip = {"kb_sim_kernel_time", "kb_sim_reset_kernel_time", "kb_sim_kernel_bytes",   # GPU timing surface
+            "kb_sim_set_profiling", "kb_sim_kernel_breakdown", "kb_sim_host_syncs",
             "kb_sim_debug_paths", "kb_sim_debug_counters",                             # GPU kernel variants
             "kb_rccl_unique_id", "kb_sim_create_rank", "kb_sim_create_local", "kb_sim_shard_info",  # sharding
             "kb_wire_encode", "kb_wire_decode", "kb_wire_addr_of_id", "kb_wire_id_of_addr"}     # wire codec (host)
@@ -51,6 +52,8 @@ def test_struct_layouts_match_header():
     # kb_config: 17 scalar fields (seed is u64) + reserved[4]; kb_stats: 6 x 4-byte + 20 x u64 + reserved[7]
     assert C.sizeof(KbConfig) == 4 * 4 + 8 + 4 * 12 + 4 * 4
     assert C.sizeof(KbStats) == 6 * 4 + 20 * 8 + 7 * 8
+    from kaboodle_amd._ffi import KbKernelTime
+    assert C.sizeof(KbKernelTime) == 24 + 8 + 8 + 8 + 4 + 4 + 9 * 8
 
 
 def test_config_default_matches_mirror():

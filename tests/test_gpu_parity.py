@@ -10,7 +10,7 @@ import pytest
 
 import parity
 import scenarios
-from kaboodle_amd._ffi import KB_DBG_ALL, KB_INIT_CONVERGED, Sim, SimConfig
+from kaboodle_amd._ffi import KB_DBG_ALL, KB_DBG_WAVE_GRAPH, KB_INIT_CONVERGED, KB_INVALID_OPERATION, KbError, Sim, SimConfig
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -38,6 +38,65 @@ def test_parity_wide_row_paths(gpu, name, case, rounds):
     k_proc's unsorted selection path), forced by kb_config.debug_flags at these sizes."""
     ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_ALL), rounds)
     assert ok, f"{name} (debug_flags={KB_DBG_ALL}): {msg}"
+
+
+@pytest.mark.parametrize("name", ["churn_loss_512", "partition_heal", "identity_change", "hot_inbox"])
+def test_parity_wave_graph(gpu, name):
+    """The receive window captured once as a HIP graph and replayed every round (KB_DBG_WAVE_GRAPH, the
+    env KB_WAVE_GRAPH=1 path): same results, including across set_identity (which must drop the graph)."""
+    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}[name]
+    ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_WAVE_GRAPH, track_latency=1), rounds,
+                                 peer_states=True)
+    assert ok, f"{name} (wave graph): {msg}"
+
+
+def test_identity_change_on_stopped_peer(gpu):
+    """Kaboodle::set_identity (src/lib.rs:323-336): refused while running (counting queued start/stop calls),
+    allowed once stopped; after the restart every view reports the new bytes (peers / peer_states) and
+    its fingerprint is generate_fingerprint over the new identities (kb_fingerprint_of_set)."""
+    import ctypes as C
+    cfg = SimConfig(capacity=512, initial_nodes=500, init_mode=KB_INIT_CONVERGED, id_len=6, seed=12)
+    lib = C.CDLL(parity.GPU_SO)
+    f = lib.kb_fingerprint_of_set
+    f.restype = C.c_uint32
+    f.argtypes = [C.POINTER(C.c_uint32), C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p]
+    with Sim(parity.oracle_lib(), cfg) as o, Sim(gpu, cfg) as g:
+        for s in (o, g):
+            s.step(2)
+            with pytest.raises(KbError) as e:
+                s.set_identity(7, b"abcdef")
+            assert e.value.code == KB_INVALID_OPERATION
+            s.stop_node(7)
+            s.set_identity(7, b"abcdef")           # stop queued: no longer running as the API sees it
+            s.start_node(7)
+            with pytest.raises(KbError):
+                s.set_identity(7, b"ghijkl")      # start queued: running again
+        fp_before = g.fingerprints()
+        o.step(1)
+        g.step(1)
+        assert g.identity(7) == o.identity(7) == b"abcdef"
+        fo, fg = o.fingerprints(), g.fingerprints()
+        assert np.array_equal(fo, fg)
+        idents = np.zeros((cfg.capacity, 32), dtype=np.uint8)
+        lens = np.zeros(cfg.capacity, dtype=np.uint8)
+        for j in range(cfg.capacity):
+            b = g.identity(j)
+            idents[j, :len(b)] = np.frombuffer(b, dtype=np.uint8)
+            lens[j] = len(b)
+        changed = 0
+        for i in range(0, 500, 37):
+            p = g.peers(i)
+            want = f((C.c_uint32 * len(p))(*p), len(p), idents.ctypes.data, 32, lens.ctypes.data)
+            assert want == fg[i], f"node {i}"
+            changed += 7 in p and fg[i] != fp_before[i]
+            ps = {e[0]: e[4] for e in g.peer_states(i)}
+            if 7 in ps:
+                assert ps[7] == b"abcdef"
+        assert changed > 0
+        for _ in range(3):
+            o.step(1)
+            g.step(1)
+            assert np.array_equal(o.fingerprints(), g.fingerprints())
 
 
 def test_wide_row_paths_are_hit(gpu):

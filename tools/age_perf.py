@@ -15,5 +15,5 @@ for b in range(R // Bk):
     sw, n = m.kernel_time(0)
     st = m.stats()
     print(f"rounds {b*Bk:4d}-{(b+1)*Bk-1:4d}: {dt/Bk*1e3:7.2f} ms/round  sweep {sw/n:6.3f} ms  "
-          f"sweep bytes/launch {m.sweep_bytes()/n/1e6:8.1f} MB  agree {st['agree']}/{st['alive']}  "
+          f"row-pass bytes/launch {m.kernel_bytes(0)/n/1e6:8.1f} MB  agree {st['agree']}/{st['alive']}  "
           f"kpr {st['sent_kpr']} oversize {st['drop_oversize']}", flush=True)

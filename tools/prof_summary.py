@@ -1,11 +1,15 @@
 """Summaries of rocprofv3 CSV output (dev tool).
 
-  prof_summary.py stats <dir> [K]        kernel_stats.csv -> compact table (name, calls, avg us, total %), and
-                                         k_sweep's average over its last K launches of the kernel trace
-                                         (bench's timed steps; the table's average includes the warmup)
-  prof_summary.py pmc <dir> <kernel> [bench args]
-                                         counter_collection.csv of the FETCH_SIZE / WRITE_SIZE passes ->
-                                         JSON with HBM bytes per launch of <kernel> (FETCH_SIZE x2, gfx950)
+  prof_summary.py stats <dir>                     kernel_stats.csv -> compact table (name, calls, avg us, total %)
+  prof_summary.py rounds <dir> <warmup> <steps>   kernel_trace.csv -> per-round kernel time over the timed rounds
+                                                  only (bench's timed region), kernels named as bench.py names them
+  prof_summary.py pmc <dir> <tag-json-fields...>  counter_collection.csv of the FETCH_SIZE / WRITE_SIZE passes
+                                                  (<dir>/FETCH_SIZE, <dir>/WRITE_SIZE) -> JSON: HBM bytes per launch
+                                                  and per round of every kernel over the timed rounds
+  prof_summary.py sq <dir>                        per-kernel averages of SQ counters
+
+Rounds are delimited by the dispatches of k_round_end (the last kernel of every round): the timed rounds
+of `bench.py --warmup W --steps K` are the dispatches after the W-th k_round_end up to the (W+K)-th.
 """
 import csv
 import glob
@@ -29,45 +33,82 @@ def short(name):
     return n
 
 
-def stats(d, k_last=0):
+def bench_name(name):
+    """The kernel as bench.py's breakdown names it (template arguments and LDS/HBM variants folded)."""
+    n = short(name).split("<")[0]
+    return {"k_bfail_prep_lds": "k_bfail_prep"}.get(n, n)
+
+
+def timed_window(rs, warmup, steps, id_key):
+    """(first, last] dispatch ids of the timed rounds, from the k_round_end dispatches."""
+    ends = sorted(int(r[id_key]) for r in rs if bench_name(r["Kernel_Name"]) == "k_round_end")
+    if len(ends) < warmup + steps:
+        raise SystemExit(f"only {len(ends)} rounds in the trace, need {warmup + steps}")
+    return (ends[warmup - 1] if warmup else -1), ends[warmup + steps - 1]
+
+
+def stats(d):
     rs = rows(os.path.join(d, "**", "*kernel_stats.csv"))
     rs.sort(key=lambda r: -float(r["TotalDurationNs"]))
     print(f"{'kernel':40s} {'calls':>7s} {'avg_us':>10s} {'pct':>6s}")
     for r in rs:
         print(f"{short(r['Name'])[:40]:40s} {r['Calls']:>7s} {float(r['AverageNs'])/1e3:10.2f} {float(r['Percentage']):6.2f}")
-    if k_last:
-        for kn in ("k_rowpass<true>", "k_rowpass<false>", "k_fold"):
-            tr = [r for r in rows(os.path.join(d, "**", "*kernel_trace.csv")) if short(r["Kernel_Name"]) == kn]
-            tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-            dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in tr][-k_last:]
-            if dur:
-                print(f"{kn} over its last {len(dur)} launches (the timed steps): avg {sum(dur) / len(dur):.2f} us")
 
 
-def pmc(d, kernel, args):
+def per_round(d, warmup, steps):
+    tr = rows(os.path.join(d, "**", "*kernel_trace.csv"))
+    lo, hi = timed_window(tr, warmup, steps, "Dispatch_Id")
+    agg = {}
+    span = [None, None]
+    for r in tr:
+        k = int(r["Dispatch_Id"])
+        if not lo < k <= hi:
+            continue
+        a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+        span[0] = a if span[0] is None else min(span[0], a)
+        span[1] = b if span[1] is None else max(span[1], b)
+        e = agg.setdefault(bench_name(r["Kernel_Name"]), [0, 0.0])
+        e[0] += 1
+        e[1] += (b - a) / 1e6
+    out = {"warmup": warmup, "steps": steps, "kernels": {}}
+    tot = 0.0
+    for n, (c, ms) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        out["kernels"][n] = {"ms_per_round": round(ms / steps, 4), "launches_per_round": round(c / steps, 2),
+                             "avg_launch_us": round(ms / c * 1e3, 2)}
+        tot += ms
+    out["kernel_ms_per_round"] = round(tot / steps, 4)
+    out["first_to_last_dispatch_ms_per_round"] = round((span[1] - span[0]) / 1e6 / steps, 4)
+    print(json.dumps(out, indent=1))
+
+
+def pmc(d, fields):
+    meta = json.loads(fields) if fields else {}
+    warmup, steps = meta.get("warmup", 5), meta.get("steps", 20)
     res = {}
     for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        vals = [float(r["Counter_Value"]) for r in rows(os.path.join(d, c, "**", "*counter_collection.csv"))
-                if kernel in r.get("Kernel_Name", "") and r.get("Counter_Name") == c]
-        res[c] = sum(vals) / len(vals) if vals else None
-        res[c + "_dispatches"] = len(vals)
-    # rocprofv3 reports both in KB; gfx950 FETCH_SIZE counts half of a wide streaming read (guide, HBM section)
-    fetch = res["FETCH_SIZE"] * 1024 * 2 if res["FETCH_SIZE"] is not None else None
-    write = res["WRITE_SIZE"] * 1024 if res["WRITE_SIZE"] is not None else None
-    nodes, loss, churn, steps, warmup = 65536, 0.01, 0.001, 50, 5
-    for k, v in zip(args[::2], args[1::2]):
-        if k == "--nodes":
-            nodes = int(v)
-        elif k == "--steps":
-            steps = int(v)
-        elif k == "--warmup":
-            warmup = int(v)
-    workload = f"configs[2]: {nodes} peers, converged start, {loss:.0%} loss, {churn:.1%}/round churn"
-    capacity = nodes + max(4096, int(nodes * churn * (steps + warmup + 8) * 1.5))      # bench.rank_config
-    out = {"kernel": kernel.split("<")[0], "workload": workload, "capacity": capacity, "raw_kb": res,
-           "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
-           "hbm_bytes_per_launch": (fetch or 0) + (write or 0) if fetch is not None else None,
-           "correction": "FETCH_SIZE(KB)*1024*2 (gfx950 half-count of 16B/lane streaming reads) + WRITE_SIZE(KB)*1024"}
+        rs = [r for r in rows(os.path.join(d, c, "**", "*counter_collection.csv")) if r.get("Counter_Name") == c]
+        lo, hi = timed_window(rs, warmup, steps, "Dispatch_Id")
+        for r in rs:
+            if lo < int(r["Dispatch_Id"]) <= hi:
+                e = res.setdefault(bench_name(r["Kernel_Name"]), {}).setdefault(c, [0, 0.0])
+                e[0] += 1
+                e[1] += float(r["Counter_Value"])
+    kern = {}
+    for n, e in res.items():
+        if "FETCH_SIZE" not in e or "WRITE_SIZE" not in e:
+            continue
+        launches = e["FETCH_SIZE"][0]
+        # rocprofv3 reports both in KB; gfx950 FETCH_SIZE counts half of a wide streaming read (guide, HBM section)
+        fetch = e["FETCH_SIZE"][1] * 1024 * 2
+        write = e["WRITE_SIZE"][1] * 1024
+        kern[n] = {"launches_per_round": launches / steps, "fetch_bytes_per_launch": int(fetch / launches),
+                   "write_bytes_per_launch": int(write / launches),
+                   "hbm_bytes_per_launch": int((fetch + write) / launches),
+                   "hbm_bytes_per_round": int((fetch + write) / steps)}
+    out = dict(meta)
+    out["kernels"] = dict(sorted(kern.items(), key=lambda kv: -kv[1]["hbm_bytes_per_round"]))
+    out["correction"] = "FETCH_SIZE(KB)*1024*2 (gfx950 half-count of 16B/lane streaming reads) + WRITE_SIZE(KB)*1024"
+    out["window"] = f"the {steps} timed rounds after {warmup} warmup rounds (k_round_end dispatches delimit rounds)"
     print(json.dumps(out, indent=1))
 
 
@@ -86,8 +127,10 @@ def sq(d):
 
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
-        stats(sys.argv[2], int(sys.argv[3]) if len(sys.argv) > 3 else 0)
+        stats(sys.argv[2])
+    elif sys.argv[1] == "rounds":
+        per_round(sys.argv[2], int(sys.argv[3]), int(sys.argv[4]))
     elif sys.argv[1] == "sq":
         sq(sys.argv[2])
     else:
-        pmc(sys.argv[2], sys.argv[3], sys.argv[4:])
+        pmc(sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "")
