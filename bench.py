@@ -20,8 +20,11 @@ Also reported, on the same JSON line:
   kernels       every kernel of the round: HIP-event ms per round (each launch timed by its own dispatch
                 packet on the simulator's stream), launches per round, wave-0 share, and for the kernels
                 with an in-kernel byte counter (k_rowpass, k_fold, k_resp_wave, k_proc) the algorithmic
-                bytes and GB/s; `gaps` = round_gpu_ms minus the kernels (launch gaps, host hand-offs), so
-                the rows sum to round_gpu_ms;
+                bytes and GB/s.  The timed rounds carry events on those four kernels only (an event pair
+                costs ≈5 us of dispatch overhead); the other kernels' times come from an untimed replay of
+                the same rounds (same seed: the simulation is deterministic, bit for bit) with events on
+                every launch.  `gaps` = round_gpu_ms minus the kernels (launch gaps, host hand-offs), so the
+                rows sum to round_gpu_ms;
   roofline      the kernel with the most time per round: algorithmic bytes per launch (counted in-kernel)
                 / its mean HIP-event launch duration, against 8 TB/s; `traffic` = measured HBM bytes per
                 launch from the rocprofv3 PMC summary committed under profiles/ for this exact command
@@ -67,16 +70,24 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="do not keep PeerInfo.latency (track_latency 0)")
     ap.add_argument("--no-conv", action="store_true")
+    ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (kernel breakdown)")
     ap.add_argument("--no-modes", action="store_true", help="skip the socket_faithful line (N = 1)")
     ap.add_argument("--failed-mode", choices=("sim_sender", "socket_faithful"), default="sim_sender",
                     help="Q1: Failed(p) honoured (sim_sender, the headline) or never (socket_faithful)")
     return ap.parse_args()
 
 
+def lib_sha16() -> str:
+    import hashlib
+    import kaboodle_amd
+    return hashlib.sha256(open(kaboodle_amd.LIB_PATH, "rb").read()).hexdigest()[:16]
+
+
 def pmc_summary(cfg_key: str, capacity: int, steps: int, warmup: int, failed_mode: str):
-    """The latest committed PMC summary (tools/gpu_pmc.sh -> profiles/*pmc*.json) taken on exactly this
-    workload, capacity, step and warmup counts: {kernel: {hbm_bytes_per_launch, hbm_bytes_per_round, ...}}
-    over the timed rounds, and the summary's path."""
+    """The latest committed PMC summary (tools/gpu_measure.sh -> profiles/*pmc*.json) taken on exactly this
+    workload, capacity, step and warmup counts, with this very library build (lib_sha16): {kernel:
+    {hbm_bytes_per_launch, hbm_bytes_per_round, ...}} over the timed rounds, and the summary's path."""
+    sha = lib_sha16()
     best, src = None, None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
@@ -84,7 +95,8 @@ def pmc_summary(cfg_key: str, capacity: int, steps: int, warmup: int, failed_mod
         except (OSError, ValueError):
             continue
         if (d.get("workload") == cfg_key and d.get("capacity") == capacity and d.get("steps") == steps and
-                d.get("warmup") == warmup and d.get("failed_mode", "sim_sender") == failed_mode and "kernels" in d):
+                d.get("warmup") == warmup and d.get("failed_mode", "sim_sender") == failed_mode and "kernels" in d
+                and d.get("lib_sha16") == sha):
             best, src = d["kernels"], os.path.relpath(p, ROOT)
     return best, src
 
@@ -298,6 +310,18 @@ def main() -> int:
             gap = np.abs(sc[live, 1].astype(np.int64) - int(live.sum()))
             conv["workload_view_size_match_frac_final"] = round(float((gap == 0).mean()), 4)
             conv["workload_view_size_mean_gap_final"] = round(float(gap.mean()), 2)
+
+    # every kernel's time: an untimed replay of the same rounds (deterministic) with events on every launch
+    if world == 1 and not a.no_replay:
+        mesh.close()
+        with kaboodle_amd.Mesh(cfg) as rp:
+            rp.set_profiling(2)
+            rp.step(a.warmup)
+            rp.reset_kernel_time()
+            rp.step(a.steps)
+            for name, k in rp.kernel_breakdown().items():
+                if name not in bd:
+                    bd[name] = k
 
     out = None
     if rank == 0:

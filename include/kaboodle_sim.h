@@ -263,10 +263,12 @@ int  kb_sim_reset_kernel_time(kb_sim* sim);
 /* Algorithmic HBM bytes moved by a kernel (KB_KT_ROWPASS, KB_KT_FOLD, KB_KT_RESP or KB_KT_PROC) since the
    last reset, counted in-kernel.                                                      */
 int  kb_sim_kernel_bytes(kb_sim* sim, int kind, uint64_t* bytes);
-/* Per-kernel profile of every launch of the rounds since the last reset (profiling on: the default;
-   env KB_PROF=0 or kb_sim_set_profiling(sim, 0) turns the per-launch events off).  wave_ms[w] is the
-   part spent in delivery wave w (slot KB_WAVE_SLOTS-1 holds waves >= KB_WAVE_SLOTS-1).  Kernels that
-   did not run are omitted; cap = 0 queries the count.                                               */
+/* Per-kernel profile of the launches of the rounds since the last reset.  Profiling level (env KB_PROF
+   or kb_sim_set_profiling): 0 = no per-launch events; 1 (default) = events on the kernels with an
+   in-kernel byte counter only (KB_KT_ROWPASS/FOLD/RESP/PROC); 2 = every launch (each event pair adds
+   ≈5 us of dispatch overhead, ≈0.5 ms on a 100-launch round: use it on an untimed replay).  wave_ms[w]
+   is the part spent in delivery wave w (slot KB_WAVE_SLOTS-1 holds waves >= KB_WAVE_SLOTS-1).  Kernels
+   without events are omitted; cap = 0 queries the count.                                            */
 #define KB_WAVE_SLOTS 9
 typedef struct kb_kernel_time {
   char     name[24];
@@ -276,7 +278,7 @@ typedef struct kb_kernel_time {
   uint32_t has_bytes, pad;
   double   wave_ms[KB_WAVE_SLOTS];
 } kb_kernel_time;
-int  kb_sim_set_profiling(kb_sim* sim, int on);
+int  kb_sim_set_profiling(kb_sim* sim, int level);
 int  kb_sim_kernel_breakdown(kb_sim* sim, kb_kernel_time* out, size_t cap, size_t* n);
 /* Host waits on the device since creation (stream synchronisations and pinned hand-offs).          */
 int  kb_sim_host_syncs(kb_sim* sim, uint64_t* n);

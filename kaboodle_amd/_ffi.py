@@ -375,9 +375,9 @@ class Sim:
         self.lib.call("sim_kernel_bytes", self.h, kind, C.byref(v))
         return v.value
 
-    def set_profiling(self, on: bool) -> None:
-        """Per-launch HIP events on every kernel of the round (kernel_breakdown); on by default."""
-        self.lib.call("sim_set_profiling", self.h, int(bool(on)))
+    def set_profiling(self, level: int) -> None:
+        """Per-launch HIP events (kernel_breakdown): 0 none, 1 the byte-counted kernels (default), 2 every launch."""
+        self.lib.call("sim_set_profiling", self.h, int(level))
 
     def kernel_breakdown(self) -> dict:
         """{kernel: {"ms", "launches", "bytes" (None if not counted), "wave_ms": [...]}} since reset_kernel_time."""

@@ -155,6 +155,11 @@ __global__ void k_set_cap(Dev d, const uint32_t* nresp, uint32_t* cap, uint32_t*
   if (i < d.hi) { cap[i] = nresp[i] + TICK_MAX; cnt[i] = nresp[i]; }
   if (blockIdx.x == 0 && threadIdx.x == 0) pin_publish(hpin, tot, 5, seq);
 }
+// device values -> the host's mapped pinned buffer, then the sequence number it polls for (sharded
+// hand-offs of all-gathered counts)
+__global__ void k_publish(const uint32_t* v, uint32_t n, uint32_t* hpin, uint32_t seq) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) pin_publish(hpin, v, n, seq);
+}
 __global__ void k_init_nodes(Dev d, uint32_t n0) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.C) return;
@@ -200,11 +205,11 @@ __global__ void k_init_converged_nodes(Dev d, uint32_t n0) {
   d.start_round[i] = NONE_ROUND;
   if (i >= n0) return;
   d.alive[i] = 1; d.start_round[i] = 0;
-  if (loc) { d.dirty[i] = 1; d.n[i] = n0; d.last_bcast[i] = -1000; d.paq_n[i] = 0; d.sdirty[i] = ~0ull; }
+  if (loc) { d.dirty[i] = 1; d.n[i] = n0; d.last_bcast[i] = -1000; d.paq_n[i] = 0; d.sdirty[i] = ~0ull; d.sfull[i] = ~0ull; }
 }
 __global__ void k_mark_all_dirty(Dev d) {
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < d.hi) { d.dirty[i] = 1; d.sdirty[i] = ~0ull; }
+  if (i < d.hi) { d.dirty[i] = 1; d.sdirty[i] = ~0ull; d.sfull[i] = ~0ull; }
 }
 __global__ __launch_bounds__(64) void k_fp_one(Dev d, uint32_t i) {
   __shared__ uint32_t ztab[ZT * 128];
@@ -345,14 +350,14 @@ struct kb_sim {
   std::vector<uint32_t> h_xall;
   Msg* rmsg; uint32_t* rpay; uint8_t* rstatus; uint32_t* rinbox; uint32_t* rkp;
   size_t rmsg_cap, rpay_cap;
-  hipEvent_t er0, er1;                 // the whole round (markers on the stream)
-  double round_ms;
+  double round_ms;                     // the whole round: markers on the stream, read back like the kernels'
+  uint32_t* rr = nullptr;              // [3] the round's {Join, Failed, error} on the device (sharded gather)
   uint64_t round_launches, bj_total, bf_total;
   // per-kernel profile (kb_sim_kernel_breakdown): with prof_on every launch carries start/stop events
   // on its own dispatch packet; a round's records are read back during the next round's final wait
   // (the host is idle then), the last round's on query
   struct KRec { int16_t kid, wave; hipEvent_t a, b; };
-  bool prof_on = true;
+  int prof_level = 1;                  // 0 none, 1 the kernels with byte counters, 2 every launch
   bool capturing = false;              // inside a HIP graph capture: launches carry no events
   int cur_wave = -1;                   // the delivery wave being launched (-1: outside the window)
   std::vector<hipEvent_t> ev_free;
@@ -404,7 +409,7 @@ template <class T> static T* L(const kb_sim* s, T* p) { return p + s->lo; }   //
 // ---- launches and their profile ------------------------------------------------------------------
 static void prof_events(kb_sim* s, int kid, hipEvent_t* a, hipEvent_t* b) {
   *a = *b = nullptr;
-  if (!s->prof_on || s->capturing) return;
+  if (s->capturing || s->prof_level <= 0 || (s->prof_level == 1 && kbytes_stat(kid) < 0)) return;
   hipEvent_t e[2];
   for (int k = 0; k < 2; ++k) {
     if (!s->ev_free.empty()) { e[k] = s->ev_free.back(); s->ev_free.pop_back(); }
@@ -428,8 +433,11 @@ static void prof_resolve(kb_sim* s, size_t n) {
     const kb_sim::KRec& q = s->krec[k];
     float ms = 0;
     if (hipEventElapsedTime(&ms, q.a, q.b) == hipSuccess) {
-      s->k_ms[q.kid] += ms; s->k_n[q.kid]++;
-      if (q.wave >= 0) s->k_wms[q.kid][q.wave] += ms;
+      if (q.kid == NKI) { s->round_ms += ms; s->round_launches++; }          // the whole round
+      else {
+        s->k_ms[q.kid] += ms; s->k_n[q.kid]++;
+        if (q.wave >= 0) s->k_wms[q.kid][q.wave] += ms;
+      }
     }
     s->ev_free.push_back(q.a); s->ev_free.push_back(q.b);
   }
@@ -495,10 +503,17 @@ static int upload_segments(kb_sim* s) {
     HIPCHK(hipMemcpy(s->d.zfin, zf.data(), 4ull * (C + 2), hipMemcpyHostToDevice));
   }
   HIPCHK(hipMemcpy(s->d.ztab, ztab.data(), 4ull * ztab.size(), hipMemcpyHostToDevice));
-  std::vector<uint32_t> zb(9 * 1024);
-  for (uint32_t c = 0; c < 9; ++c)
-    for (uint32_t k = 0; k < 4; ++k)
-      for (uint32_t v = 0; v < 256; ++v) zb[c * 1024 + k * 256 + v] = multmodp(zpow[c], v << (8 * k));
+  std::vector<uint32_t> zb(ZB2);                  // Z^0..Z^8, then Z^16, Z^24, ..., Z^128
+  {
+    uint32_t z = 0x80000000u;                      // Z^c for the tables, independent of the capacity
+    std::vector<uint32_t> zp(129);
+    for (uint32_t c = 0; c <= 128; ++c) { zp[c] = z; z = multmodp(Z, z); }
+    for (uint32_t t = 0; t < 24; ++t) {
+      const uint32_t c = t <= 8 ? t : 8 * (t - 7);
+      for (uint32_t k = 0; k < 4; ++k)
+        for (uint32_t v = 0; v < 256; ++v) zb[t * 1024 + k * 256 + v] = multmodp(zp[c], v << (8 * k));
+    }
+  }
   HIPCHK(hipMemcpy(s->d.zbtab, zb.data(), 4ull * zb.size(), hipMemcpyHostToDevice));
   const size_t hn = (size_t)(s->W / 8) * 256;
   k_build_htab<<<(unsigned)((hn + 255) / 256), 256>>>(s->d);
@@ -517,7 +532,6 @@ static void destroy_shard(kb_sim* s) {
   (void)hipSetDevice(s->device);
   if (s->st) (void)hipStreamSynchronize(s->st);
   free_all(s);
-  for (hipEvent_t e : {s->er0, s->er1}) if (e) (void)hipEventDestroy(e);
   for (auto& q : s->krec) { (void)hipEventDestroy(q.a); (void)hipEventDestroy(q.b); }
   for (hipEvent_t e : s->ev_free) (void)hipEventDestroy(e);
   if (s->h_pin) (void)hipHostFree(s->h_pin);
@@ -571,6 +585,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   d.C = C; d.W = W; d.SEGW = W / NSEG; d.NWR = W / 32;
   d.segq = d.SEGW / 128;
   d.segm = d.segq > 1 ? (uint32_t)(((1ull << 32) + d.segq - 1) / d.segq) : 0u;
+  d.NSW = W / 4096;
   d.k0 = (uint32_t)cfg->seed; d.k1 = (uint32_t)(cfg->seed >> 32);
   d.loss_thr = cfg->loss_threshold; d.churn_thr = cfg->churn_threshold; d.fault_end = cfg->fault_end_round;
   d.failed_mode = cfg->failed_mode; d.pgroups = cfg->partition_groups; d.pstart = cfg->partition_start;
@@ -590,10 +605,11 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
 #define A(ptr, n) if (e == hipSuccess) e = talloc(s, &(ptr), (n))     // per-id / global tables
 #define AR(ptr, n) if (e == hipSuccess) e = ralloc(s, &(ptr), (n))   // row tables: n entries per local row
   AR(d.stamp, W); AR(d.bits, d.NWR); AR(d.segp, NSEG); AR(d.sdirty, 1);
+  AR(d.stp, W / 128); AR(d.sfull, 1); AR(d.stepd, d.NSW);
   AR(d.dirty, 1); A(d.alive, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
   AR(d.last_bcast, 1); AR(d.a3cur, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
   AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
-  A(d.ztab, 17 * 128); A(d.zbtab, 9 * 1024);
+  A(d.ztab, 17 * 128); A(d.zbtab, ZB2);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.sacc, (size_t)NACC * NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
   if (cfg->track_latency) { A(d.lat, (size_t)W * lat_stride(R)); A(s->lat_col, C); A(s->fnamed, d.NWR); }   // peer-major
@@ -610,7 +626,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (!xf) { A(s->wc.status, s->msg_cap); A(s->wc.inbox, s->msg_cap); A(s->wc.kin, s->msg_cap); }
   A(s->bfail, (size_t)C * SLOTS); A(s->bjoin, C);
   AR(s->bs.join, 1); AR(s->bs.nfail, 1); AR(s->bs.fail, SLOTS); AR(s->join_off, 1); AR(s->fail_off, 1);
-  A(s->scan_tot, 32); A(s->scan_tiles, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
+  A(s->scan_tot, 32); A(s->rr, 4); A(s->scan_tiles, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
   AR(s->nresp, 1); AR(s->paysum, 1); AR(s->nbase, 1); AR(s->resp_off, 1);
   A(s->resp_nodes, R); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS); A(s->slow, R);
   AR(s->ro.part, 10);
@@ -631,12 +647,11 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (d.lat) { (void)hipMemset(d.lat, 0xFF, 2ull * lat_stride(R) * W); (void)hipMemset(s->fnamed, 0, 4ull * d.NWR); }   // all None
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
-  if (hipHostMalloc((void**)&s->h_pin, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+  if (hipHostMalloc((void**)&s->h_pin, 4 * PIN_WORDS, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
     s->h_pin = nullptr; destroy_shard(s); seterr("pinned buffer"); return KB_IO_ERROR;
   }
   if (hipHostGetDevicePointer((void**)&s->d_pin, s->h_pin, 0) != hipSuccess) { destroy_shard(s); seterr("pinned buffer mapping"); return KB_IO_ERROR; }
-  for (hipEvent_t* e : {&s->er0, &s->er1}) (void)hipEventCreate(e);
-  if (const char* pv = getenv("KB_PROF")) s->prof_on = atoi(pv) != 0;
+  if (const char* pv = getenv("KB_PROF")) s->prof_level = atoi(pv);
   int rc = upload_segments(s);
   if (rc) { destroy_shard(s); return rc; }
   uint32_t ctr0[NCTR] = {0};
@@ -746,13 +761,6 @@ static int err_status(uint32_t e) {
   }
   return KB_OK;
 }
-static int check_err(kb_sim* s) {
-  if (s->xf && !s->xf->allreduce_max_u32(s->d.ctr + C_ERR, 1, s->st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  HIPCHK(hipMemcpyAsync(s->h_pin, s->d.ctr + C_ERR, 4, hipMemcpyDeviceToHost, s->st));
-  HIPCHK(sync_st(s));
-  return err_status(s->h_pin[0]);
-}
-
 // replace a tracked device allocation by a larger one (contents are not kept)
 template <class T> static hipError_t regrow(kb_sim* s, T** p, size_t n) {
   for (auto& q : s->allocs) if (q == (void*)*p) { (void)hipFree(q); q = nullptr; }
@@ -827,8 +835,9 @@ static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb,
   klaunch(s, KI_XBOUND, k_xbound, dim3(1), dim3(64), 0, x, s->scan_tot + 16);
   klaunch(s, KI_PACK, k_pack, dim3((s->R + 3) / 4), dim3(256), 0, s->d, ob, x);
   if (!s->xf->allgather_u32(x.xb, s->xall, 2 * W, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  HIPCHK(hipMemcpyAsync(s->h_xall.data(), s->xall, 4ull * 2 * W * W, hipMemcpyDeviceToHost, st));
-  HIPCHK(sync_st(s));
+  k_publish<<<1, 1, 0, st>>>(s->xall, 2 * W * W, s->d_pin, ++s->pin_seq);   // counts -> host, then the wait
+  { const int rc = wait_pin(s, s->pin_seq); if (rc) return rc; }
+  memcpy(s->h_xall.data(), s->h_pin, 4ull * 2 * W * W);
   size_t sc[XMAX], sd[XMAX], rc[XMAX], rd[XMAX], psc[XMAX], psd[XMAX], prc[XMAX], prd[XMAX];
   size_t so = 0, pso = 0, ro = 0, pro = 0;
   uint64_t total = 0;
@@ -843,11 +852,12 @@ static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb,
   }
   int rcode = ensure_recv(s, ro, pro);
   if (rcode) return rcode;
-  if (!s->xf->group_begin() ||                                     // records and payload as one grouped exchange
-      !s->xf->alltoallv(x.smsg, sc, sd, s->rmsg, rc, rd, sizeof(Msg), st) ||
-      !s->xf->alltoallv(x.spay, psc, psd, s->rpay, prc, prd, 4, st) || !s->xf->group_end()) {
-    seterr(s->xf->error()); return KB_IO_ERROR;
-  }
+  // records and payload as one grouped exchange; once the group is open it is always closed
+  if (!s->xf->group_begin()) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  const bool sent = s->xf->alltoallv(x.smsg, sc, sd, s->rmsg, rc, rd, sizeof(Msg), st) &&
+                    s->xf->alltoallv(x.spay, psc, psd, s->rpay, prc, prd, 4, st);
+  const std::string e1 = sent ? std::string() : s->xf->error();
+  if (!s->xf->group_end() || !sent) { seterr(sent ? s->xf->error() : e1); return KB_IO_ERROR; }
   rb.world = (uint32_t)W;
   for (int k = 0; k <= W && k <= (int)XMAX; ++k) {
     rb.m0[k] = k < W ? (uint32_t)rd[k] : (uint32_t)ro;
@@ -857,25 +867,28 @@ static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb,
   return KB_OK;
 }
 
-// the round's broadcast lists of every shard, concatenated in shard order = sender order
-static int gather_broadcasts(kb_sim* s, uint32_t nj_loc, uint32_t nf_loc) {
+// the round's broadcast lists of every shard, concatenated in shard order = sender order; the same
+// all-gather carries every rank's error flag (*err = the largest): one host wait per round for both
+static int gather_broadcasts(kb_sim* s, uint32_t* err) {
   const int W = s->world;
   hipStream_t st = s->st;
-  if (!s->xf->allgather_u32(s->scan_tot, s->xall, 2, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  HIPCHK(hipMemcpyAsync(s->h_xall.data(), s->xall, 4ull * 2 * W, hipMemcpyDeviceToHost, st));
-  HIPCHK(sync_st(s));
+  if (!s->xf->allgather_u32(s->rr, s->xall, 3, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  k_publish<<<1, 1, 0, st>>>(s->xall, 3 * W, s->d_pin, ++s->pin_seq);
+  { const int rc = wait_pin(s, s->pin_seq); if (rc) return rc; }
   size_t sc[XMAX], sd[XMAX], rc[XMAX], rd[XMAX], fsc[XMAX], frc[XMAX], frd[XMAX];
   size_t oj = 0, of = 0;
+  uint32_t e = 0;
   for (int k = 0; k < W; ++k) {
-    sc[k] = nj_loc; fsc[k] = nf_loc; sd[k] = 0;
-    rc[k] = s->h_xall[2 * k]; frc[k] = s->h_xall[2 * k + 1];
+    rc[k] = s->h_pin[3 * k]; frc[k] = s->h_pin[3 * k + 1]; e = std::max(e, s->h_pin[3 * k + 2]);
     rd[k] = oj; oj += rc[k]; frd[k] = of; of += frc[k];
   }
-  if (!s->xf->group_begin() ||
-      !s->xf->alltoallv(s->bjoin_loc, sc, sd, s->bjoin, rc, rd, sizeof(BCast), st) ||
-      !s->xf->alltoallv(s->bfail_loc, fsc, sd, s->bfail, frc, frd, sizeof(BCast), st) || !s->xf->group_end()) {
-    seterr(s->xf->error()); return KB_IO_ERROR;
-  }
+  for (int k = 0; k < W; ++k) { sc[k] = rc[s->rank]; fsc[k] = frc[s->rank]; sd[k] = 0; }
+  *err = e;
+  if (!s->xf->group_begin()) { seterr(s->xf->error()); return KB_IO_ERROR; }
+  const bool sent = s->xf->alltoallv(s->bjoin_loc, sc, sd, s->bjoin, rc, rd, sizeof(BCast), st) &&
+                    s->xf->alltoallv(s->bfail_loc, fsc, sd, s->bfail, frc, frd, sizeof(BCast), st);
+  const std::string e1 = sent ? std::string() : s->xf->error();
+  if (!s->xf->group_end() || !sent) { seterr(sent ? s->xf->error() : e1); return KB_IO_ERROR; }
   s->nj = (uint32_t)oj; s->nf = (uint32_t)of;
   return KB_OK;
 }
@@ -980,7 +993,12 @@ static int step_round(kb_sim* s) {
   const uint32_t tb = 256, gnode = (R + tb - 1) / tb, gwave = (R + 3) / 4, gall = (C + tb - 1) / tb;
   const size_t krec0 = s->krec.size();               // records of earlier rounds (complete)
   s->cur_wave = -1;
-  (void)hipEventRecord(s->er0, st);
+  hipEvent_t er[2] = {nullptr, nullptr};              // the whole round, read back next round
+  for (int k = 0; k < 2; ++k) {
+    if (!s->ev_free.empty()) { er[k] = s->ev_free.back(); s->ev_free.pop_back(); }
+    else (void)hipEventCreate(&er[k]);
+  }
+  (void)hipEventRecord(er[0], st);
   // 0. stamp window
   if (r > 0 && r % EPOCH == 0) klaunch(s, KI_REBASE, k_rebase, dim3(8192), dim3(256), 0, d);
   // 1. lifecycle (every shard applies the same events and churn draws to the replicated per-id state)
@@ -1039,9 +1057,10 @@ static int step_round(kb_sim* s) {
     uint32_t lf = s->nf <= PB_FMAX, lj = s->nj <= PB_JMAX;
     uint32_t listw = (lf ? 2 * s->nf : 0) + (lj ? s->nj : 0);
     if (listw > budget / 2 || pb_hbm) { lf = lj = 0; listw = 0; }
-    const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR && !pb_hbm;
-    const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / d.NWR) : RP_WAVES;
-    const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
+    const uint32_t per_wave = d.NWR + d.NSW;          // bitset + changed-step flags
+    const bool ldsb = s->W <= PB_LDS_W && budget - listw >= per_wave && !pb_hbm;
+    const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / per_wave) : RP_WAVES;
+    const size_t lds = 4ull * ((ldsb ? (size_t)wpb * per_wave : 0) + listw);
     int occ = 0;                                       // resident workgroups per CU (LDS, registers)
     const uint64_t okey = ((uint64_t)ldsb << 63) | ((uint64_t)wpb << 40) | (uint64_t)lds;   // queried once per shape
     if (okey == s->occ_key) occ = s->occ_val;
@@ -1119,7 +1138,8 @@ static int step_round(kb_sim* s) {
   klaunch(s, KI_TICK_SCAN, k_tick_scan, dim3(gnode), dim3(tb), 0, d, s->bs, r, s->slow);                       // A1; list the A2 nodes
   klaunch(s, KI_TICK_PRE, k_tick_pre, dim3(std::min<uint32_t>(gwave, 1024)), dim3(256), 0, d, o0, s->bs, r, s->slow);   // A2 per listed node
   // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded
-  if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
+  if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + FOLD_WAVES - 1) / FOLD_WAVES * s->S), dim3(64 * FOLD_WAVES),
+                         (uint32_t)(4 * ZB2), d, FoldArgs{s->S});
   if (d.uniform) klaunch(s, KI_FP_ROWS, k_fp_rows, dim3((FP_LANES * R + tb - 1) / tb), dim3(tb), 0, d);
   klaunch(s, KI_TICK_POST, k_tick_post, dim3(gnode), dim3(tb), 0, d, s->ro, o0, r);
   {
@@ -1157,26 +1177,27 @@ static int step_round(kb_sim* s) {
     if (rc) return rc;
   }
   if (s->xf && !s->xf->allreduce_sum_u32(d.ctr + C_AGREE, 1, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
-  klaunch(s, KI_ROUND_END, k_round_end, dim3(1), dim3(1), 0, d, r, (const uint32_t*)s->scan_tot, s->d_pin, ++s->pin_seq);
-  (void)hipEventRecord(s->er1, st);
+  klaunch(s, KI_ROUND_END, k_round_end, dim3(1), dim3(1), 0, d, r, (const uint32_t*)s->scan_tot, s->d_pin,
+          s->xf ? 0u : ++s->pin_seq, s->rr);
+  (void)hipEventRecord(er[1], st);
+  s->krec.push_back(kb_sim::KRec{(int16_t)NKI, (int16_t)-1, er[0], er[1]});
   // the earlier rounds' kernel events are complete: read them while this round runs
   prof_resolve(s, krec0);
-  // k_round_end wrote the next round's broadcast counts and the error flag straight into the
-  // host-mapped pinned buffer; the host polls for them, then finds the stream drained
-  { const int rc = wait_pin(s, s->pin_seq); if (rc) return rc; }
-  HIPCHK(sync_st(s));
-  const uint32_t nj_loc = s->h_pin[0], nf_loc = s->h_pin[1], err = s->h_pin[2];
+  uint32_t err = 0;
   if (s->xf) {
-    const int rc = gather_broadcasts(s, nj_loc, nf_loc);
+    // every shard's broadcast lists and error flag in one all-gather, one host wait
+    const int rc = gather_broadcasts(s, &err);
     if (rc) return rc;
   } else {
-    s->nj = nj_loc; s->nf = nf_loc;
+    // k_round_end wrote the next round's broadcast counts and the error flag straight into the
+    // host-mapped pinned buffer; the host polls for them (the stream then drains by itself)
+    const int rc = wait_pin(s, s->pin_seq);
+    if (rc) return rc;
+    s->nj = s->h_pin[0]; s->nf = s->h_pin[1]; err = s->h_pin[2];
   }
   s->bj_total += s->nj; s->bf_total += s->nf;
-  float ms = 0;
-  (void)hipEventElapsedTime(&ms, s->er0, s->er1); s->round_ms += ms; s->round_launches++;
   s->round = r + 1;
-  return s->xf ? check_err(s) : err_status(err);   // shards: the flag of any rank
+  return err_status(err);                            // shards: the flag of any rank
 }
 
 static bool is_group(const kb_sim* s) { return !s->shards.empty(); }
@@ -1197,6 +1218,7 @@ static int group_step(kb_sim* g, uint32_t rounds) {
       kb_sim* s = g->shards[k];
       (void)hipSetDevice(s->device);
       for (uint32_t q = 0; q < rounds && rc[k] == KB_OK; ++q) rc[k] = step_round(s);
+      if (rc[k] == KB_OK && sync_st(s) != hipSuccess) { rc[k] = KB_IO_ERROR; g_err = "stream"; }
       if (rc[k] != KB_OK) { err[k] = g_err; g->hub->abort(); }
     });
   for (auto& t : th) t.join();
@@ -1218,6 +1240,7 @@ extern "C" int kb_sim_step(kb_sim* s, uint32_t rounds) {
     int rc = step_round(s);
     if (rc) { if (s->xf) s->xf->abort(); return rc; }
   }
+  HIPCHK(sync_st(s));                                  // synchronous: the rounds' work has completed on return
   return KB_OK;
 }
 
@@ -1655,10 +1678,10 @@ extern "C" int kb_sim_kernel_bytes(kb_sim* s, int kind, uint64_t* bytes) {
   *bytes = stat_counter(s, b) - s->k_bytes0[b];
   return KB_OK;
 }
-extern "C" int kb_sim_set_profiling(kb_sim* s, int on) {
-  if (!s) return KB_INVALID_ARGUMENT;
-  GROUP_ALL([&](kb_sim* t) { return kb_sim_set_profiling(t, on); });
-  s->prof_on = on != 0;
+extern "C" int kb_sim_set_profiling(kb_sim* s, int level) {
+  if (!s || level < 0 || level > 2) return KB_INVALID_ARGUMENT;
+  GROUP_ALL([&](kb_sim* t) { return kb_sim_set_profiling(t, level); });
+  s->prof_level = level;
   return KB_OK;
 }
 // every kernel the rounds launched since the last reset: HIP-event time (sum and per delivery wave),

@@ -63,6 +63,8 @@ def test_identity_change_on_stopped_peer(gpu):
     with Sim(parity.oracle_lib(), cfg) as o, Sim(gpu, cfg) as g:
         for s in (o, g):
             s.step(2)
+        fp_before = g.fingerprints()
+        for s in (o, g):
             with pytest.raises(KbError) as e:
                 s.set_identity(7, b"abcdef")
             assert e.value.code == KB_INVALID_OPERATION
@@ -71,7 +73,6 @@ def test_identity_change_on_stopped_peer(gpu):
             s.start_node(7)
             with pytest.raises(KbError):
                 s.set_identity(7, b"ghijkl")      # start queued: running again
-        fp_before = g.fingerprints()
         o.step(1)
         g.step(1)
         assert g.identity(7) == o.identity(7) == b"abcdef"
@@ -169,6 +170,27 @@ def test_sharded_parity_every_round(gpu, name, case, rounds, shards):
     the unsharded oracle bit for bit, every round."""
     ok, msg, _ = parity.run_case(case, rounds, shards=shards)
     assert ok, f"{name}: {msg}"
+
+
+def test_host_waits_per_round(gpu):
+    """Host waits on the device per round (kb_sim_host_syncs): unsharded at most two pinned hand-offs (the
+    wave-0 outbox size when Join responses exist, the round's results); a row-sharded round one hand-off
+    for the broadcast lists and every rank's error flag (one all-gather) plus one per delivery wave for
+    the all-to-all-v counts; plus one stream synchronisation per kb_sim_step call."""
+    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}["churn_loss_512"]
+    cfg = case["cfg"]
+    with Sim(gpu, cfg) as g:
+        g.step(1)
+        n0 = g.host_syncs()
+        g.step(rounds)
+        assert g.host_syncs() - n0 <= 2 * rounds + 1
+    with Sim(gpu, cfg, shards=3) as g:
+        g.step(1)
+        n0 = g.host_syncs()
+        for _ in range(rounds):
+            g.step(1)
+        per_round = (g.host_syncs() - n0) / rounds
+        assert per_round <= 1 + cfg.max_waves + 1 + 1, per_round
 
 
 def test_rccl_rank_path_world1(gpu):

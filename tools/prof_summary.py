@@ -106,6 +106,9 @@ def pmc(d, fields):
                    "hbm_bytes_per_launch": int((fetch + write) / launches),
                    "hbm_bytes_per_round": int((fetch + write) / steps)}
     out = dict(meta)
+    import hashlib
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "kaboodle_amd", "libkaboodle_sim.so")
+    out["lib_sha16"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]   # the build the counters measured
     out["kernels"] = dict(sorted(kern.items(), key=lambda kv: -kv[1]["hbm_bytes_per_round"]))
     out["correction"] = "FETCH_SIZE(KB)*1024*2 (gfx950 half-count of 16B/lane streaming reads) + WRITE_SIZE(KB)*1024"
     out["window"] = f"the {steps} timed rounds after {warmup} warmup rounds (k_round_end dispatches delimit rounds)"
