@@ -77,8 +77,15 @@ typedef struct kb_config {
                                 are identical with any value (test surface, ignored by the oracle)   */
   uint32_t track_latency;    /* 1: keep the per-(node, peer) ping latency EWMA of peer_states
                                 (src/kaboodle.rs:789-817); 0: latency reported as none (no table)    */
-  uint32_t reserved[4];
+  uint32_t variant;          /* KB_VARIANT_*: 0 = round semantics v1.  Nonzero selects an alternative
+                                reading of a declared deviation, implemented by the
+                                CPU oracle only, to measure what the declaration changes; the HIP
+                                library refuses it (KB_INVALID_ARGUMENT)                            */
+  uint32_t reserved[3];
 } kb_config;
+enum { KB_VARIANT_SAME_WINDOW_BCAST = 1u,   /* Join/Failed delivered in the round they are sent, right after
+                                               the tick (src/kaboodle.rs:770-778), not at the next round start */
+       KB_VARIANT_EXACT_LRU = 2u };         /* A3 orders by the exact instant (no stamp window, no ancient ties) */
 
 /* debug_flags: each forces the code path a mesh of >= 1M ids takes, so that path is
    parity-tested at sizes the oracle finishes in seconds. */

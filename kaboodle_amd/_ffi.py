@@ -17,6 +17,7 @@ KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL = 0, 1
 KB_DBG_PHASEB_HBM, KB_DBG_RESP_HBM, KB_DBG_KP_HBM, KB_DBG_KP_BIG_SMALL, KB_DBG_PROC_UNSORTED = 1, 2, 4, 8, 16
 KB_DBG_ALL = 31                  # every wide-row variant
 KB_DBG_WAVE_GRAPH = 32           # the receive window as a replayed HIP graph
+KB_VARIANT_SAME_WINDOW_BCAST, KB_VARIANT_EXACT_LRU = 1, 2   # oracle-only
 KB_LATENCY_NONE = 0xFFFFFFFF
 KT_ROWPASS, KT_ROUND, KT_FOLD, KT_RESP, KT_PROC = 0, 1, 2, 3, 4   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
 KB_WAVE_SLOTS = 9
@@ -30,7 +31,8 @@ class KbConfig(C.Structure):
         ("churn_threshold", C.c_uint32), ("fault_end_round", C.c_int32), ("max_waves", C.c_uint32),
         ("failed_mode", C.c_uint32), ("id_len", C.c_uint32), ("partition_groups", C.c_uint32),
         ("partition_start", C.c_int32), ("partition_end", C.c_int32), ("device", C.c_int32),
-        ("debug_flags", C.c_uint32), ("track_latency", C.c_uint32), ("reserved", C.c_uint32 * 4),
+        ("debug_flags", C.c_uint32), ("track_latency", C.c_uint32), ("variant", C.c_uint32),
+        ("reserved", C.c_uint32 * 3),
     ]
 
 
@@ -87,6 +89,7 @@ class SimConfig:
     device: int = -1
     debug_flags: int = 0         # KB_DBG_*: force the wide-row kernel variants (test surface)
     track_latency: int = 0       # 1: keep the ping-latency EWMA reported by peer_states
+    variant: int = 0             # KB_VARIANT_*: oracle-only alternative semantics (deviation measurements)
 
     def to_c(self) -> KbConfig:
         c = KbConfig()
@@ -100,7 +103,7 @@ class SimConfig:
         c.partition_groups, c.partition_start, c.partition_end = (
             self.partition_groups, self.partition_start, self.partition_end)
         c.device = self.device
-        c.debug_flags, c.track_latency = self.debug_flags, self.track_latency
+        c.debug_flags, c.track_latency, c.variant = self.debug_flags, self.track_latency, self.variant
         return c
 
 

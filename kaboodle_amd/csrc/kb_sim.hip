@@ -548,6 +548,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (!cfg || !out || cfg->abi_version != KB_ABI_VERSION) { seterr("bad config"); delete xf; return KB_INVALID_ARGUMENT; }
   if (cfg->capacity == 0 || cfg->capacity > 7800000u || cfg->initial_nodes > cfg->capacity || cfg->id_len > MAXID ||
       cfg->max_waves == 0 || cfg->max_waves > 64) { seterr("config out of range"); delete xf; return KB_INVALID_ARGUMENT; }
+  if (cfg->variant) { seterr("semantic variants are measurement-only (CPU oracle)"); delete xf; return KB_INVALID_ARGUMENT; }
   const uint32_t C = cfg->capacity;
   const uint32_t rows_per = (C + (uint32_t)world - 1) / (uint32_t)world;
   if (world < 1 || world > (int)XMAX || rank < 0 || rank >= world || (uint64_t)(world - 1) * rows_per >= C) {

@@ -78,7 +78,8 @@ struct kbo_sim {
   kb_config cfg;
   uint32_t C;
   uint32_t k0, k1;
-  uint8_t* stamp;             /* C x C */
+  uint8_t* stamp;
+  int32_t* tst;        /* KB_VARIANT_EXACT_LRU: the exact instant of every Known entry (no window) */             /* C x C */
   uint16_t* lat;              /* C x C PeerInfo.latency in ms, LAT_NONE = None (track_latency only) */
   uint8_t* alive;
   int32_t* start_round;
@@ -236,6 +237,7 @@ static int map_insert_known(kbo_sim* s, uint32_t i, uint32_t p, int32_t t, int32
     if (q) q->kind = 0;
   }
   *b = enc(t, r);
+  if (s->tst) s->tst[(size_t)i * s->C + p] = t;
   if (was == ST_UNKNOWN) { if (lt) *lt = LAT_NONE; s->n[i]++; s->dirty[i] = 1; return 1; }
   return 0;
 }
@@ -361,6 +363,13 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   s->ident = (uint8_t*)calloc(C * MAXID, 1); s->id_len = (uint8_t*)calloc(C, 1);
   s->cseg = (uint32_t*)calloc(C, 4); s->segmul = (uint32_t*)calloc(C, 4); s->seglen = (uint32_t*)calloc(C, 4);
   s->out = (ovec*)calloc(C, sizeof(ovec)); s->oseq = (uint32_t*)calloc(C, 4);
+  if (cfg->variant & ~(uint32_t)(KB_VARIANT_SAME_WINDOW_BCAST | KB_VARIANT_EXACT_LRU)) {
+    seterr("unknown variant"); free(s); return KB_INVALID_ARGUMENT;
+  }
+  if (cfg->variant & KB_VARIANT_EXACT_LRU) {
+    s->tst = (int32_t*)malloc(C * C * sizeof(int32_t));
+    if (s->tst) for (size_t k = 0; k < C * C; ++k) s->tst[k] = INT32_MIN / 2;   /* converged start: ancient, ties */
+  }
   if (cfg->track_latency) {
     s->lat = (uint16_t*)malloc(C * C * sizeof(uint16_t));
     if (s->lat) memset(s->lat, 0xFF, C * C * sizeof(uint16_t));
@@ -393,7 +402,7 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
 int kbo_sim_destroy(kbo_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
   for (uint32_t i = 0; i < s->C; ++i) free(s->out[i].v);
-  free(s->stamp); free(s->lat); free(s->alive); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
+  free(s->stamp); free(s->tst); free(s->lat); free(s->alive); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
   free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
   for (size_t k = 0; k < s->nwatch; ++k) free(s->wsnap[k]);
@@ -576,7 +585,7 @@ static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
     for (uint32_t j = 0; j < s->C; ++j) {
       uint8_t b = rw[j];
       if (b < ST_ANCIENT || j == i) continue;
-      uint32_t kh = b, kl = rot_key(j, s->a3cur[i], s->C);
+      uint32_t kh = s->tst ? (uint32_t)(s->tst[(size_t)i * s->C + j] - INT32_MIN) : b, kl = rot_key(j, s->a3cur[i], s->C);
       if (nb == NUM_CANDIDATES && (kh > bkey_hi[nb - 1] || (kh == bkey_hi[nb - 1] && kl > bkey_lo[nb - 1]))) continue;
       int pos = nb < NUM_CANDIDATES ? nb : NUM_CANDIDATES - 1;
       while (pos > 0 && (bkey_hi[pos - 1] > kh || (bkey_hi[pos - 1] == kh && bkey_lo[pos - 1] > kl))) {
@@ -778,10 +787,13 @@ static int step_round(kbo_sim* s) {
     s->st.churn_leaves += leaves;
     for (uint32_t k = 0; k < leaves && s->next_free < C; ++k) { node_start(s, s->next_free++, r); s->st.churn_joins++; }
   }
-  /* 2. broadcasts emitted during round r-1 */
+  /* 2. broadcasts emitted during round r-1 (KB_VARIANT_SAME_WINDOW_BCAST: after this round's tick) */
+  const int same_window = (s->cfg.variant & KB_VARIANT_SAME_WINDOW_BCAST) != 0;
+  if (!same_window) {
 #pragma omp parallel for schedule(dynamic, 64)
-  for (uint32_t i = 0; i < C; ++i)
-    if (s->alive[i] && s->start_round[i] < r) phase_broadcasts(s, i, r);
+    for (uint32_t i = 0; i < C; ++i)
+      if (s->alive[i] && s->start_round[i] < r) phase_broadcasts(s, i, r);
+  }
   /* 3. tick */
   otick_bc* bc = (otick_bc*)calloc(C, sizeof(otick_bc));
   int err = KB_OK;
@@ -802,6 +814,11 @@ static int step_round(kbo_sim* s) {
     for (int q = 0; q < bc[i].nfail; ++q) { bpush(&s->bfail, &s->nbfail, &s->capbfail, i, bc[i].fail_peers[q], bseq++); s->st.bcast_failed++; }
   }
   free(bc);
+  if (same_window) {            /* the tick's broadcasts reach every running peer inside this window */
+#pragma omp parallel for schedule(dynamic, 64)
+    for (uint32_t i = 0; i < C; ++i)
+      if (s->alive[i]) phase_broadcasts(s, i, r);
+  }
   /* 4. receive window: unicast waves */
   err = run_waves(s, r);
   if (err) return err;
