@@ -127,7 +127,8 @@ typedef struct kb_stats {
   uint64_t removed_timeout, removed_failed, join_responses, curious_overflow, churn_leaves, churn_joins;
   uint64_t sent_kp_ids;           /* peer entries carried by the KnownPeers messages sent               */
   uint64_t alive_rounds;          /* sum over the simulated rounds of the peers running in that round  */
-  uint64_t reserved[6];
+  uint64_t probe_responses;       /* ProbeResponses sent (maybe_respond_to_probe), lost ones included   */
+  uint64_t reserved[5];
 } kb_stats;
 
 typedef struct kb_sim kb_sim;
@@ -174,6 +175,33 @@ int  kb_sim_true_fingerprint(kb_sim* sim, uint32_t* fp);
 int  kb_sim_watch(kb_sim* sim, uint32_t node);
 int  kb_sim_events(kb_sim* sim, uint32_t node, uint32_t* discovered, size_t cap_d, size_t* n_d,
                    uint32_t* departed, size_t cap_p, size_t* n_p, uint32_t* fp, int* fp_changed);
+
+/* An IPv4 socket address as the wire carries it (SocketAddr::V4). */
+typedef struct kb_wire_addr { uint8_t ip[4]; uint16_t port; uint16_t pad; } kb_wire_addr;
+
+/* ---- discovery (src/discovery.rs:30-89, src/kaboodle.rs:305-331) ----------------------------------
+ * kb_sim_probe queues SwimBroadcast::Probe(prober) from an address outside the mesh; it is delivered at
+ * the next round start with that round's other broadcasts (after the Failed and Join groups, DESIGN.md
+ * §2.4).  Every running peer that receives it answers with ProbeResponse{identity} iff
+ * should_respond_to_broadcast (:333-354, the integer restatement of §2.4, its own Philox counter).
+ * Deliveries and responses are subject to the loss of the round.  kb_sim_probe_responses drains the
+ * responses produced since the last drain, ordered by (round, responder, probe); with out = NULL only
+ * the count is reported.  Sharded ranks (kb_sim_create_rank) report the responders among their rows. */
+typedef struct kb_probe_response {
+  uint32_t responder;        /* the answering peer (its canonical address is the datagram's source) */
+  uint32_t probe;            /* index of the probe among those queued for that round                */
+  int32_t  round;
+  kb_wire_addr prober;       /* where the ProbeResponse is sent                                      */
+  uint32_t identity_len;     /* ProbeResponse.identity: the responder's identity                     */
+  uint8_t  identity[32];
+} kb_probe_response;
+int  kb_sim_probe(kb_sim* sim, const kb_wire_addr* prober);
+int  kb_sim_probe_responses(kb_sim* sim, kb_probe_response* out, size_t cap, size_t* n);
+/* The round's broadcast lists as the transport carries them (what a bridge sends on the multicast socket,
+   src/kaboodle.rs:188-195): the Join and Failed broadcasts emitted by the last simulated round (delivered
+   at the next round start), sender order.  kind: KB_WIRE_JOIN or KB_WIRE_FAILED.                    */
+typedef struct kb_broadcast { uint32_t kind, sender, peer, pad; } kb_broadcast;
+int  kb_sim_broadcasts(kb_sim* sim, kb_broadcast* out, size_t cap, size_t* n);
 
 /* ---- sharding across GPUs --------------------------------------------------------
  * A mesh of C ids can be split into `world` (1..8) contiguous row shards: shard k holds the observer
@@ -238,7 +266,6 @@ enum { KB_WIRE_PING = 0, KB_WIRE_PING_REQUEST = 1, KB_WIRE_ACK = 2, KB_WIRE_KNOW
        KB_WIRE_JOIN = 16, KB_WIRE_FAILED = 17, KB_WIRE_PROBE = 18,   /* SwimBroadcast variants           */
        KB_WIRE_PROBE_RESPONSE = 32 };
 enum { KB_WIRE_CHANNEL_UNICAST = 0, KB_WIRE_CHANNEL_BROADCAST = 1, KB_WIRE_CHANNEL_PROBE_RESPONSE = 2 };
-typedef struct kb_wire_addr { uint8_t ip[4]; uint16_t port; uint16_t pad; } kb_wire_addr;
 typedef struct kb_wire_entry { kb_wire_addr addr; uint32_t id_off, id_len; } kb_wire_entry;   /* KnownPeers */
 typedef struct kb_wire_msg {
   uint32_t kind;                       /* KB_WIRE_*                                                     */

@@ -90,6 +90,28 @@ class Mesh(Sim):
                 subs[k] = [c for c in subs[k] if not c.closed]
 
 
+def discover_mesh_member(mesh: "Mesh", prober=("192.0.2.1", 40000), max_rounds: int = 64):
+    """Kaboodle::discover_mesh_member (src/lib.rs, src/discovery.rs:30-89) against a simulated mesh: broadcast
+    Probe(prober), wait for a ProbeResponse, re-broadcast with the reference's back-off (1 s, x1.25, at most
+    10 s; one protocol period = one round = 1000 ms).  Steps the mesh.  Returns (responder address,
+    identity) of the first response (canonical order), or None after max_rounds."""
+    interval_ms, last_ms, now_ms, waited = 1000, None, 0, 0
+    for _ in range(max_rounds):
+        if last_ms is None or last_ms <= now_ms - interval_ms:
+            mesh.probe(prober)
+            last_ms, waited = now_ms, 0
+        mesh.step(1)
+        now_ms += 1000
+        waited += 1000
+        got = [r for r in mesh.probe_responses() if r[3] == tuple(prober)]
+        if got:
+            return mesh.format_addr(got[0][1]), got[0][4]
+        if waited >= interval_ms:                  # timeout: longer wait, then probe again (discovery.rs:62-73)
+            interval_ms = min(10000, int(interval_ms * 1.25))
+            waited = 0
+    return None
+
+
 class Channel:
     """The receiving end of a discover_* channel (tokio UnboundedReceiver / oneshot Receiver in the
     reference, src/lib.rs:186-263), filled by Mesh.step."""

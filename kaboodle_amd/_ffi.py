@@ -52,7 +52,8 @@ class KbStats(C.Structure):
         ("drop_oversize", C.c_uint64), ("drop_partition", C.c_uint64), ("drop_bcast", C.c_uint64),
         ("removed_timeout", C.c_uint64), ("removed_failed", C.c_uint64), ("join_responses", C.c_uint64),
         ("curious_overflow", C.c_uint64), ("churn_leaves", C.c_uint64), ("churn_joins", C.c_uint64),
-        ("sent_kp_ids", C.c_uint64), ("alive_rounds", C.c_uint64), ("reserved", C.c_uint64 * 6),
+        ("sent_kp_ids", C.c_uint64), ("alive_rounds", C.c_uint64), ("probe_responses", C.c_uint64),
+        ("reserved", C.c_uint64 * 5),
     ]
 
     def as_dict(self) -> dict:
@@ -62,6 +63,29 @@ class KbStats(C.Structure):
 class KbKernelTime(C.Structure):
     _fields_ = [("name", C.c_char * 24), ("ms", C.c_double), ("launches", C.c_uint64), ("bytes", C.c_uint64),
                 ("has_bytes", C.c_uint32), ("pad", C.c_uint32), ("wave_ms", C.c_double * KB_WAVE_SLOTS)]
+
+
+class KbWireAddrC(C.Structure):
+    _fields_ = [("ip", C.c_uint8 * 4), ("port", C.c_uint16), ("pad", C.c_uint16)]
+
+
+class KbProbeResponse(C.Structure):
+    _fields_ = [("responder", C.c_uint32), ("probe", C.c_uint32), ("round", C.c_int32), ("prober", KbWireAddrC),
+                ("identity_len", C.c_uint32), ("identity", C.c_uint8 * 32)]
+
+
+class KbBroadcast(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("sender", C.c_uint32), ("peer", C.c_uint32), ("pad", C.c_uint32)]
+
+
+def wire_addr(addr) -> KbWireAddrC:
+    """("a.b.c.d", port) -> kb_wire_addr"""
+    ip, port = addr
+    a = KbWireAddrC()
+    for k, part in enumerate(ip.split(".")):
+        a.ip[k] = int(part)
+    a.port = port
+    return a
 
 
 class KbError(RuntimeError):
@@ -134,6 +158,9 @@ _SIGS = {
     "sim_events": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t),
                              C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_uint32),
                              C.POINTER(C.c_int)]),
+    "sim_probe": (C.c_int, [C.c_void_p, C.POINTER(KbWireAddrC)]),
+    "sim_probe_responses": (C.c_int, [C.c_void_p, C.POINTER(KbProbeResponse), C.c_size_t, C.POINTER(C.c_size_t)]),
+    "sim_broadcasts": (C.c_int, [C.c_void_p, C.POINTER(KbBroadcast), C.c_size_t, C.POINTER(C.c_size_t)]),
     "format_addr": (C.c_int, [C.c_uint32, C.c_char_p, C.c_size_t]),
     "last_error": (C.c_char_p, []),
 }
@@ -315,6 +342,28 @@ class Sim:
         arr = (KbPeerState * max(n.value, 1))()
         self.lib.call("sim_peer_states", self.h, node, arr, n.value, C.byref(n))
         return [(a.peer, a.state, a.since, a.latency_ms, bytes(a.identity[: a.identity_len])) for a in arr[: n.value]]
+
+    # -- discovery (src/discovery.rs:30-89, src/kaboodle.rs:305-331) --
+    def probe(self, prober) -> None:
+        """Queue SwimBroadcast::Probe(prober) for the next round; prober = ("a.b.c.d", port) outside the mesh."""
+        self.lib.call("sim_probe", self.h, C.byref(wire_addr(prober)))
+
+    def probe_responses(self):
+        """Drain the ProbeResponses: [(round, responder id, probe index, prober addr, identity)] in canonical order."""
+        n = C.c_size_t()
+        self.lib.call("sim_probe_responses", self.h, None, 0, C.byref(n))
+        arr = (KbProbeResponse * max(n.value, 1))()
+        self.lib.call("sim_probe_responses", self.h, arr, n.value, C.byref(n))
+        return [(a.round, a.responder, a.probe, (".".join(str(a.prober.ip[k]) for k in range(4)), a.prober.port),
+                 bytes(a.identity[: a.identity_len])) for a in arr[: n.value]]
+
+    def broadcasts(self):
+        """The last round's Join / Failed broadcasts: [("Join" | "Failed", sender id, peer id)], sender order."""
+        n = C.c_size_t()
+        self.lib.call("sim_broadcasts", self.h, None, 0, C.byref(n))
+        arr = (KbBroadcast * max(n.value, 1))()
+        self.lib.call("sim_broadcasts", self.h, arr, n.value, C.byref(n))
+        return [("Join" if a.kind == 16 else "Failed", a.sender, a.peer) for a in arr[: n.value]]
 
     def stats(self) -> dict:
         st = KbStats()

@@ -27,6 +27,7 @@ enum StatIdx {
   S_ALIVER,                       // running peers summed over the rounds (kb_stats.alive_rounds; counted by shard 0)
   S_RESPB,                        // bytes k_resp_wave moved (bench; not a kb_stats field)
   S_PROCB,                        // bytes k_proc moved (bench; not a kb_stats field)
+  S_PROBERESP,                    // ProbeResponses sent (kb_stats.probe_responses)
   NSTAT
 };
 enum CtrIdx {

@@ -570,6 +570,42 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
   }
 }
 
+// ---- SwimBroadcast::Probe (src/kaboodle.rs:305-331), after the Failed and Join groups: every running
+// peer that receives probe e answers with ProbeResponse{identity} iff should_respond_to_broadcast holds
+// for its map as it stands (its own Philox counter, bit 23).  Thread per local row; the
+// (responder, probe) pairs that were not lost on the way back are listed for the host (few per round).
+__global__ __launch_bounds__(256) void k_probe(Dev d, uint32_t np, int32_t r, uint2* out, uint32_t* cnt, uint32_t cap) {
+  const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long lost_in = 0, sent = 0, lost_out = 0;
+  if (i < d.hi && d.alive[i] && d.start_round[i] < r) {
+    const bool f = faults(d, r) && d.loss_thr;
+    const uint32_t n = d.n[i];
+    for (uint32_t e = 0; e < np; ++e) {
+      if (f) {
+        const U4 w = philox(i, (uint32_t)r, ((uint32_t)P_PROBE << 24) | (e >> 2), 0, d.k0, d.k1);
+        const uint32_t u = (e & 3) == 0 ? w.x : (e & 3) == 1 ? w.y : (e & 3) == 2 ? w.z : w.w;
+        if (u < d.loss_thr) { lost_in++; continue; }
+      }
+      const int64_t o = (int64_t)n - 2;
+      bool resp = o <= 0;
+      if (!resp) {
+        int64_t pct = 100 - o * o; if (pct < 1) pct = 1;
+        const uint32_t u = philox(i, (uint32_t)r, ((uint32_t)P_RESPOND << 24) | (1u << 23) | e, 0, d.k0, d.k1).x;
+        resp = (int64_t)mulhi(u, 100) < pct;
+      }
+      if (!resp) continue;
+      sent++;
+      if (f && philox(i, (uint32_t)r, ((uint32_t)P_PROBE << 24) | (1u << 23) | e, 1, d.k0, d.k1).x < d.loss_thr) { lost_out++; continue; }
+      const uint32_t k = atomicAdd(cnt, 1u);
+      if (k < cap) out[k] = make_uint2(i, e);
+      else set_err(d, DERR_OUTBOX);
+    }
+  }
+  const int idx[3] = {S_BDROP, S_PROBERESP, S_LOSS};
+  const unsigned long long v[3] = {lost_in, sent, lost_out};
+  stat_add_n(d, idx, v);
+}
+
 // ================================================================================================
 // Join responses: KnownPeers of every map entry (src/kaboodle.rs:356-392).  One workgroup per
 // responding node: the row's member bitset goes to LDS once; for each response (list order) the

@@ -46,14 +46,14 @@ enum KId : int {
   KI_LAT_MARK, KI_BFAIL_PREP, KI_ROWPASS, KI_LAT_SWEEP, KI_SCAN_TILES, KI_SCAN_APPLY, KI_SET_CAP, KI_RESP_WAVE,
   KI_RESP_NODE, KI_TICK_SCAN, KI_TICK_PRE, KI_FOLD, KI_FP_ROWS, KI_TICK_POST, KI_BCAST_WRITE, KI_ROUTE, KI_ROUTE_X,
   KI_XBOUND, KI_PACK, KI_ROUTE_RECV, KI_SCATTER, KI_SCATTER_FLAT, KI_KP_SMALL, KI_KP_GROUP, KI_SORT_INBOX,
-  KI_PROC_FAST, KI_PROC, KI_ROUND_END, NKI
+  KI_PROC_FAST, KI_PROC, KI_ROUND_END, KI_PROBE, NKI
 };
 static const char* const KNAME[NKI] = {
   "k_rebase", "k_events", "k_churn_leave", "k_churn_join", "k_alive_bits", "k_truefp_part", "k_truefp_fin",
   "k_log_mark", "k_lat_mark", "k_bfail_prep", "k_rowpass", "k_lat_sweep", "k_scan_tiles", "k_scan_apply",
   "k_set_cap", "k_resp_wave", "k_resp_node", "k_tick_scan", "k_tick_pre", "k_fold", "k_fp_rows", "k_tick_post",
   "k_bcast_write", "k_route", "k_route_x", "k_xbound", "k_pack", "k_route_recv", "k_scatter", "k_scatter_flat",
-  "k_kp_small", "k_kp_group", "k_sort_inbox", "k_proc_fast", "k_proc", "k_round_end"};
+  "k_kp_small", "k_kp_group", "k_sort_inbox", "k_proc_fast", "k_proc", "k_round_end", "k_probe"};
 // the in-kernel algorithmic byte counter of a kernel (StatIdx), or -1
 static int kbytes_stat(int kid) {
   switch (kid) {
@@ -325,6 +325,10 @@ struct kb_sim {
   int32_t round;
   std::vector<uint8_t> h_ident, h_idlen;
   std::vector<Event> events;
+  // discovery: Probes queued for the next round, those delivered this round, responses not yet drained
+  std::vector<kb_wire_addr> probe_q, probes;
+  std::vector<kb_probe_response> presp;
+  uint2* d_presp = nullptr; uint32_t* d_presp_n = nullptr; size_t presp_cap = 0;
   OutBuf ob[2];
   WaveCtl wc;
   uint32_t msg_cap, pay_cap;
@@ -525,7 +529,7 @@ static void free_all(kb_sim* s) {
   for (void* p : s->allocs) (void)hipFree(p);
   s->allocs.clear();
   void* dyn[] = {s->newmask_base, s->respmask_base, s->resp_scratch, s->d_events, s->rmsg, s->rpay, s->rstatus,
-                 s->rinbox, s->rkp};
+                 s->rinbox, s->rkp, s->d_presp, s->d_presp_n};
   for (void* p : dyn) if (p) (void)hipFree(p);
 }
 static void destroy_shard(kb_sim* s) {
@@ -1082,6 +1086,22 @@ static int step_round(kb_sim* s) {
   if (lat_fail)
     klaunch(s, KI_LAT_SWEEP, k_lat_sweep, dim3((lat_stride(R) / 8 + 255) / 256, std::min<uint32_t>(s->nf, 16384)), dim3(256), 0, d,
             (const BCast*)s->bfail, (const uint32_t*)s->bf_gid, s->nf, s->fnamed);
+  // the Probes queued since the last round travel with this round's broadcasts (after Failed and Join)
+  s->probes.swap(s->probe_q);
+  s->probe_q.clear();
+  const uint32_t np = (uint32_t)s->probes.size();
+  if (np) {
+    const size_t need = (size_t)np * R;
+    if (need > s->presp_cap) {
+      if (s->d_presp) (void)hipFree(s->d_presp);
+      s->d_presp = nullptr;
+      HIPCHK(hipMalloc(&s->d_presp, sizeof(uint2) * need));
+      s->presp_cap = need;
+    }
+    if (!s->d_presp_n) HIPCHK(hipMalloc(&s->d_presp_n, 4));
+    HIPCHK(hipMemsetAsync(s->d_presp_n, 0, 4, st));
+    klaunch(s, KI_PROBE, k_probe, dim3(gnode), dim3(tb), 0, d, np, r, s->d_presp, s->d_presp_n, (uint32_t)s->presp_cap);
+  }
   {  // wave-0 outbox regions: responses first, then the tick's messages
     ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 3;
@@ -1197,6 +1217,22 @@ static int step_round(kb_sim* s) {
     s->nj = s->h_pin[0]; s->nf = s->h_pin[1]; err = s->h_pin[2];
   }
   s->bj_total += s->nj; s->bf_total += s->nf;
+  if (np) {                                          // the round's ProbeResponses, (responder, probe) order
+    uint32_t k = 0;
+    HIPCHK(hipMemcpy(&k, s->d_presp_n, 4, hipMemcpyDeviceToHost));
+    k = std::min<uint32_t>(k, (uint32_t)s->presp_cap);
+    std::vector<uint2> v(k);
+    if (k) HIPCHK(hipMemcpy(v.data(), s->d_presp, sizeof(uint2) * k, hipMemcpyDeviceToHost));
+    std::sort(v.begin(), v.end(), [](const uint2& a, const uint2& b) { return a.x != b.x ? a.x < b.x : a.y < b.y; });
+    for (const uint2& q : v) {
+      kb_probe_response o;
+      memset(&o, 0, sizeof o);
+      o.responder = q.x; o.probe = q.y; o.round = r; o.prober = s->probes[q.y];
+      o.identity_len = s->h_idlen[q.x];
+      memcpy(o.identity, &s->h_ident[(size_t)q.x * MAXID], o.identity_len);
+      s->presp.push_back(o);
+    }
+  }
   s->round = r + 1;
   return err_status(err);                            // shards: the flag of any rank
 }
@@ -1347,6 +1383,57 @@ extern "C" int kb_sim_identity(kb_sim* s, uint32_t node, uint8_t* buf, size_t ca
   if (cap < *len) return KB_CAPACITY;
   memcpy(buf, &s->h_ident[(size_t)node * MAXID], *len);
   return KB_OK;
+}
+// ---- discovery (src/discovery.rs:30-89, src/kaboodle.rs:305-331) ----------------------------------
+extern "C" int kb_sim_probe(kb_sim* s, const kb_wire_addr* prober) {
+  if (!s || !prober) return KB_INVALID_ARGUMENT;
+  GROUP_ALL([&](kb_sim* t) { return kb_sim_probe(t, prober); });
+  s->probe_q.push_back(*prober);
+  return KB_OK;
+}
+extern "C" int kb_sim_probe_responses(kb_sim* s, kb_probe_response* out, size_t cap, size_t* n) {
+  if (!s || !n) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) {                                 // every shard's responders, merged in canonical order
+    std::vector<kb_probe_response> all;
+    for (kb_sim* t : s->shards) all.insert(all.end(), t->presp.begin(), t->presp.end());
+    std::stable_sort(all.begin(), all.end(), [](const kb_probe_response& a, const kb_probe_response& b) {
+      return a.round != b.round ? a.round < b.round : a.responder != b.responder ? a.responder < b.responder : a.probe < b.probe;
+    });
+    *n = all.size();
+    if (!out) return KB_OK;
+    if (cap < all.size()) return KB_CAPACITY;
+    if (!all.empty()) memcpy(out, all.data(), all.size() * sizeof(kb_probe_response));
+    for (kb_sim* t : s->shards) t->presp.clear();
+    return KB_OK;
+  }
+  *n = s->presp.size();
+  if (!out) return KB_OK;
+  if (cap < s->presp.size()) return KB_CAPACITY;
+  if (!s->presp.empty()) memcpy(out, s->presp.data(), s->presp.size() * sizeof(kb_probe_response));
+  s->presp.clear();
+  return KB_OK;
+}
+// the last round's Join / Failed broadcasts (whole mesh; sender order, a node's Join before its Failed)
+extern "C" int kb_sim_broadcasts(kb_sim* s, kb_broadcast* out, size_t cap, size_t* n) {
+  if (!s || !n) return KB_INVALID_ARGUMENT;
+  if (is_group(s)) return kb_sim_broadcasts(s->shards[0], out, cap, n);   // every shard holds the lists
+  std::vector<BCast> j(s->nj), f(s->nf);
+  if (s->nj) HIPCHK(hipMemcpy(j.data(), s->bjoin, sizeof(BCast) * s->nj, hipMemcpyDeviceToHost));
+  if (s->nf) HIPCHK(hipMemcpy(f.data(), s->bfail, sizeof(BCast) * s->nf, hipMemcpyDeviceToHost));
+  size_t c = 0, a = 0, b = 0;
+  while (a < j.size() || b < f.size()) {
+    const bool tj = b == f.size() || (a < j.size() && j[a].sender <= f[b].sender);
+    if (out && c < cap) {
+      kb_broadcast& o = out[c];
+      memset(&o, 0, sizeof o);
+      if (tj) { o.kind = KB_WIRE_JOIN; o.sender = j[a].sender; o.peer = j[a].peer; }
+      else { o.kind = KB_WIRE_FAILED; o.sender = f[b].sender; o.peer = f[b].peer; }
+    }
+    if (tj) a++; else b++;
+    c++;
+  }
+  *n = c;
+  return (out && cap < c) ? KB_CAPACITY : KB_OK;
 }
 extern "C" int kb_sim_fingerprint(kb_sim* s, uint32_t node, uint32_t* fp) {
   if (chk(s, node) || !fp) return KB_INVALID_ARGUMENT;
@@ -1558,6 +1645,7 @@ extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
   out->curious_overflow = st[S_CUROVF]; out->churn_leaves = st[S_CLEAVE]; out->churn_joins = st[S_CJOIN];
   out->sent_kp_ids = st[S_KPIDS];
   out->alive_rounds = st[S_ALIVER];
+  out->probe_responses = st[S_PROBERESP];
   return KB_OK;
 }
 // per id: alive, n, last_bcast, start_round; n and last_bcast only for the rows this handle holds

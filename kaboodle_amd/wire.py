@@ -18,6 +18,7 @@ KINDS = {"Ping": 0, "PingRequest": 1, "Ack": 2, "KnownPeers": 3, "KnownPeersRequ
 NAMES = {v: k for k, v in KINDS.items()}
 CHANNELS = {"unicast": 0, "broadcast": 1, "probe_response": 2}
 INCOMING_BUFFER_SIZE = 10240       # src/kaboodle.rs:43: longer datagrams arrive truncated
+DISCOVERY_BUFFER_SIZE = 1024       # src/discovery.rs:16: discover_mesh_member's receive buffer
 
 
 class KbWireAddr(C.Structure):
@@ -103,9 +104,23 @@ def encode(kind: str, identity: bytes = b"", peer=None, fingerprint: int = 0, nu
     return out.raw[: size.value]
 
 
+def receive(datagram: bytes, channel: str = "unicast") -> dict:
+    """The message as the reference's receivers decode it: they deserialize the whole reused receive
+    buffer, not the datagram's length (`bincode::deserialize(&buf)`, src/kaboodle.rs:259,397): the bytes
+    past the datagram are zeros (a fresh buffer), so a short datagram can still decode.  Channel
+    "discovery" is discover_mesh_member's reply socket (src/discovery.rs:16,81): a 1024-byte buffer read
+    as a SwimEnvelope, so a ProbeResponse{identity} decodes as SwimEnvelope{identity, Ping}."""
+    size = DISCOVERY_BUFFER_SIZE if channel == "discovery" else INCOMING_BUFFER_SIZE
+    buf = bytearray(size)
+    k = min(len(datagram), size)
+    buf[:k] = datagram[:k]
+    return decode(bytes(buf), "unicast" if channel == "discovery" else channel)
+
+
 def decode(datagram: bytes, channel: str = "unicast") -> dict:
-    """The message in a datagram as the receiver sees it: at most INCOMING_BUFFER_SIZE bytes are read,
-    so an oversize datagram fails (ValueError), as in the reference (Q3)."""
+    """The message in a datagram: at most INCOMING_BUFFER_SIZE bytes are read, so an oversize datagram
+    fails (ValueError), as in the reference (Q3).  Decodes the datagram's own bytes only; `receive`
+    reproduces the reference receivers' zero-padded buffer."""
     buf = bytes(datagram[:INCOMING_BUFFER_SIZE])
     m = KbWireMsg()
     cd = _lib()

@@ -60,7 +60,7 @@
 /* message kinds (SwimMessage, src/structs.rs:94-116) */
 enum { K_PING = 0, K_PINGREQ = 1, K_ACK = 2, K_KP = 3, K_KPR = 4 };
 /* Philox purposes */
-enum { P_PING = 1, P_INDIRECT = 2, P_RESPOND = 3, P_TRUNC = 4, P_LOSS = 5, P_BLOSS = 6, P_CHURN = 7 };
+enum { P_PING = 1, P_INDIRECT = 2, P_RESPOND = 3, P_TRUNC = 4, P_LOSS = 5, P_BLOSS = 6, P_CHURN = 7, P_PROBE = 8 };
 enum { SK_WFP = 1, SK_WFIP = 2 };
 
 typedef struct { uint32_t peer; int32_t since; int32_t kind; } osusp;       /* kind 0 = free */
@@ -79,7 +79,7 @@ struct kbo_sim {
   uint32_t C;
   uint32_t k0, k1;
   uint8_t* stamp;
-  int32_t* tst;        /* KB_VARIANT_EXACT_LRU: the exact instant of every Known entry (no window) */             /* C x C */
+  int32_t* tst;               /* C x C, KB_VARIANT_EXACT_LRU: the exact instant of every Known entry */
   uint16_t* lat;              /* C x C PeerInfo.latency in ms, LAT_NONE = None (track_latency only) */
   uint8_t* alive;
   int32_t* start_round;
@@ -100,6 +100,9 @@ struct kbo_sim {
   obcast* bfail; size_t nbfail, capbfail;
   obcast* bjoin; size_t nbjoin, capbjoin;
   oevent* ev; size_t nev, capev;
+  kb_wire_addr* probe_q; size_t nprobe_q, capprobe_q;   /* Probes queued for the next round (kbo_sim_probe) */
+  kb_wire_addr* probes; size_t nprobes;                   /* the Probes delivered this round */
+  kb_probe_response* presp; size_t npresp, cappresp;     /* responses not yet drained */
   ovec* out;                  /* per-node outbox of the wave being produced */
   uint32_t* oseq;             /* per-node emission counter for the wave being produced */
   kb_stats st;
@@ -402,7 +405,7 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
 int kbo_sim_destroy(kbo_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
   for (uint32_t i = 0; i < s->C; ++i) free(s->out[i].v);
-  free(s->stamp); free(s->tst); free(s->lat); free(s->alive); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
+  free(s->probe_q); free(s->probes); free(s->presp); free(s->stamp); free(s->tst); free(s->lat); free(s->alive); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
   free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
   for (size_t k = 0; k < s->nwatch; ++k) free(s->wsnap[k]);
@@ -426,6 +429,15 @@ static int bcast_lost(kbo_sim* s, uint32_t recv, const obcast* b, int32_t r, uin
          s->cfg.loss_threshold;
 }
 
+/* should_respond_to_broadcast for the e-th Probe of the round: its own counter (bit 23 set) */
+static int probe_should_respond(kbo_sim* s, uint32_t i, uint32_t e, int32_t r) {
+  const int64_t o = (int64_t)s->n[i] - 2;
+  if (o <= 0) return 1;
+  int64_t pct = 100 - o * o;
+  if (pct < 1) pct = 1;
+  const uint32_t u = ph(s, i, (uint32_t)r, ((uint32_t)P_RESPOND << 24) | (1u << 23) | e, 0).v[0];
+  return (int64_t)o_mulhi(u, 100) < pct;
+}
 /* should_respond_to_broadcast (src/kaboodle.rs:333-354), integer restatement of gen_bool */
 static int should_respond(kbo_sim* s, uint32_t i, uint32_t joiner, int32_t r) {
   int64_t o = (int64_t)s->n[i] - 2;
@@ -504,6 +516,32 @@ static void phase_broadcasts(kbo_sim* s, uint32_t i, int32_t r) {
     if (bcast_lost(s, i, b, r, 1, k)) { lost++; continue; }
     int is_new = map_insert_known(s, i, b->sender, r, r, -1);
     if (is_new && should_respond(s, i, b->sender, r)) join_response(s, i, b->sender, r);
+  }
+  /* Probe(addr) (src/kaboodle.rs:305-331): maybe_respond_to_probe with the map as it stands now */
+  for (size_t e = 0; e < s->nprobes; ++e) {
+    if (active_faults(s, r) && s->cfg.loss_threshold &&
+        ph(s, i, (uint32_t)r, ((uint32_t)P_PROBE << 24) | (uint32_t)(e / 4), 0).v[e % 4] < s->cfg.loss_threshold) {
+      lost++; continue;
+    }
+    if (!probe_should_respond(s, i, (uint32_t)e, r)) continue;
+    const int rlost = active_faults(s, r) && s->cfg.loss_threshold &&
+        ph(s, i, (uint32_t)r, ((uint32_t)P_PROBE << 24) | (1u << 23) | (uint32_t)e, 1).v[0] < s->cfg.loss_threshold;
+#pragma omp critical(kbo_probe)
+    {
+      s->st.probe_responses++;
+      if (rlost) s->st.drop_loss++;
+      else {
+        if (s->npresp == s->cappresp) {
+          s->cappresp = s->cappresp ? 2 * s->cappresp : 64;
+          s->presp = (kb_probe_response*)realloc(s->presp, s->cappresp * sizeof(kb_probe_response));
+        }
+        kb_probe_response* o = &s->presp[s->npresp++];
+        memset(o, 0, sizeof *o);
+        o->responder = i; o->probe = (uint32_t)e; o->round = r; o->prober = s->probes[e];
+        o->identity_len = s->id_len[i];
+        memcpy(o->identity, s->ident + (size_t)i * MAXID, s->id_len[i]);
+      }
+    }
   }
 #pragma omp atomic
   s->st.drop_bcast += lost;
@@ -787,12 +825,29 @@ static int step_round(kbo_sim* s) {
     s->st.churn_leaves += leaves;
     for (uint32_t k = 0; k < leaves && s->next_free < C; ++k) { node_start(s, s->next_free++, r); s->st.churn_joins++; }
   }
+  /* the Probes queued since the last round travel with this round's broadcasts */
+  free(s->probes);
+  s->probes = s->probe_q; s->nprobes = s->nprobe_q;
+  s->probe_q = NULL; s->nprobe_q = 0; s->capprobe_q = 0;
+  const size_t presp0 = s->npresp;
   /* 2. broadcasts emitted during round r-1 (KB_VARIANT_SAME_WINDOW_BCAST: after this round's tick) */
   const int same_window = (s->cfg.variant & KB_VARIANT_SAME_WINDOW_BCAST) != 0;
   if (!same_window) {
 #pragma omp parallel for schedule(dynamic, 64)
     for (uint32_t i = 0; i < C; ++i)
       if (s->alive[i] && s->start_round[i] < r) phase_broadcasts(s, i, r);
+  }
+  if (s->npresp > presp0) {               /* canonical order within the round: (responder, probe) */
+    kb_probe_response* v = s->presp + presp0;
+    const size_t m = s->npresp - presp0;
+    for (size_t a = 1; a < m; ++a) {
+      kb_probe_response t = v[a];
+      size_t b = a;
+      while (b > 0 && (v[b - 1].responder > t.responder || (v[b - 1].responder == t.responder && v[b - 1].probe > t.probe))) {
+        v[b] = v[b - 1]; --b;
+      }
+      v[b] = t;
+    }
   }
   /* 3. tick */
   otick_bc* bc = (otick_bc*)calloc(C, sizeof(otick_bc));
@@ -901,6 +956,44 @@ int kbo_sim_identity(kbo_sim* s, uint32_t node, uint8_t* buf, size_t cap, size_t
   if (cap < *len) return KB_CAPACITY;
   memcpy(buf, s->ident + (size_t)node * MAXID, *len);
   return KB_OK;
+}
+/* SwimBroadcast::Probe from outside the mesh (src/discovery.rs:30-89), delivered next round */
+int kbo_sim_probe(kbo_sim* s, const kb_wire_addr* prober) {
+  if (!s || !prober) return KB_INVALID_ARGUMENT;
+  if (s->nprobe_q == s->capprobe_q) {
+    s->capprobe_q = s->capprobe_q ? 2 * s->capprobe_q : 8;
+    s->probe_q = (kb_wire_addr*)realloc(s->probe_q, s->capprobe_q * sizeof(kb_wire_addr));
+  }
+  s->probe_q[s->nprobe_q++] = *prober;
+  return KB_OK;
+}
+int kbo_sim_probe_responses(kbo_sim* s, kb_probe_response* out, size_t cap, size_t* n) {
+  if (!s || !n) return KB_INVALID_ARGUMENT;
+  *n = s->npresp;
+  if (!out) return KB_OK;
+  if (cap < s->npresp) return KB_CAPACITY;
+  memcpy(out, s->presp, s->npresp * sizeof(kb_probe_response));
+  s->npresp = 0;
+  return KB_OK;
+}
+/* the last round's Join / Failed broadcasts (to be delivered at the next round start), sender order */
+int kbo_sim_broadcasts(kbo_sim* s, kb_broadcast* out, size_t cap, size_t* n) {
+  if (!s || !n) return KB_INVALID_ARGUMENT;
+  /* canonical order: by sender, then bseq (a node's Join comes before its Failed entries) */
+  size_t c = 0, a = 0, b = 0;
+  while (a < s->nbjoin || b < s->nbfail) {
+    int take_join = b == s->nbfail || (a < s->nbjoin && s->bjoin[a].sender <= s->bfail[b].sender);
+    if (out && c < cap) {
+      kb_broadcast* o = &out[c];
+      memset(o, 0, sizeof *o);
+      if (take_join) { o->kind = KB_WIRE_JOIN; o->sender = s->bjoin[a].sender; o->peer = s->bjoin[a].peer; }
+      else { o->kind = KB_WIRE_FAILED; o->sender = s->bfail[b].sender; o->peer = s->bfail[b].peer; }
+    }
+    if (take_join) a++; else b++;
+    c++;
+  }
+  *n = c;
+  return (out && cap < c) ? KB_CAPACITY : KB_OK;
 }
 int kbo_sim_fingerprint(kbo_sim* s, uint32_t node, uint32_t* fp) {
   if (check(s, node) || !fp) return KB_INVALID_ARGUMENT;

@@ -41,6 +41,8 @@ def state_of(sim: Sim, full_rows: bool = True) -> dict:
         st["rows"] = sim.rows()
     st["susp"] = [sim.suspects(i) for i in range(C)]
     st["cur"] = [sim.curious(i) for i in range(C)]
+    st["probe"] = sim.probe_responses()          # drained: the round's ProbeResponses
+    st["bcasts"] = sim.broadcasts()              # the broadcast lists the next round delivers
     return st
 
 
@@ -65,6 +67,9 @@ def diff_states(a: dict, b: dict) -> list[str]:
             if x != y:
                 out.append(f"{k}[{i}]: {x} != {y}")
                 break
+    for k in ("probe", "bcasts"):
+        if k in a and k in b and a[k] != b[k]:
+            out.append(f"{k}: {len(a[k])} vs {len(b[k])} entries, first {a[k][:2]} vs {b[k][:2]}")
     return out
 
 
@@ -154,6 +159,8 @@ def apply_events(sims, case: dict, r: int) -> None:
                 s.start_node(node)
             elif kind == "ident":
                 s.set_identity(node, arg)
+            elif kind == "probe":
+                s.probe(arg)
             elif kind == "ping":
                 s.ping_addrs(node, arg)
 
@@ -237,6 +244,16 @@ def standard_cases() -> list[tuple[str, dict, int]]:
                                                      ("start", 9, None)],
                                                  5: [("ident", 155, b"fresh-peer-id"), ("start", 155, None),
                                                      ("start", 70, None)]}}, 16))
+    # SwimBroadcast::Probe from outside the mesh (src/discovery.rs:30-89): ProbeResponses of the peers that
+    # should_respond, in a small mesh (everyone answers: n <= 2) and a lossy converged one (about 1 %)
+    cases.append(("probes", {"cfg": SimConfig(capacity=400, initial_nodes=396, init_mode=KB_INIT_CONVERGED, loss=0.03,
+                                              churn=0.01, fault_end_round=8, seed=29),
+                             "events": {1: [("probe", 0, ("192.0.2.10", 41000))],
+                                        3: [("probe", 0, ("192.0.2.10", 41000)), ("probe", 0, ("198.51.100.3", 5000))],
+                                        6: [("probe", 0, ("192.0.2.11", 41001))] * 3}}, 10))
+    cases.append(("probe_tiny", {"cfg": SimConfig(capacity=4, initial_nodes=2, seed=2),
+                                 "events": {0: [("probe", 0, ("192.0.2.1", 9000))], 2: [("probe", 0, ("192.0.2.1", 9000))],
+                                            3: [("start", 3, None)], 5: [("probe", 0, ("192.0.2.2", 9001))]}}, 8))
     # stamps from before round 0 (early joiners' KnownPeers inserts) crossing three window rebases
     cases.append(("old_stamps", {"cfg": SimConfig(capacity=160, initial_nodes=128, init_mode=KB_INIT_CONVERGED, loss=0.02,
                                                   churn=0.03, fault_end_round=12, seed=31)}, 200))
