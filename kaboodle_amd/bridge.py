@@ -1,0 +1,106 @@
+"""A bridge between a simulated mesh and real Kaboodle instances on a network.
+
+Each round (`Bridge.run_round`):
+  1. every datagram waiting on the broadcast socket is read as the reference's broadcast receiver reads it
+     (a zeroed 10240-byte buffer, src/kaboodle.rs:256-262) and decoded as a SwimBroadcast:
+       Probe(addr)  -> queued into the mesh (kb_sim_probe): the running peers that should respond answer
+                       it in the next round (maybe_respond_to_probe, src/kaboodle.rs:305-331);
+       Join/Failed  -> counted and dropped: a real instance's unicast address is not a peer of the
+                       simulated mesh (its ids are the canonical 10.100.100.x addresses), so it cannot be
+                       inserted into simulated views or answered over the mesh;
+  2. the mesh steps one round (one protocol period);
+  3. the round's outbound traffic is encoded with the wire codec and sent:
+       ProbeResponse{identity} of every responder, to the prober, from the unicast socket
+       (src/kaboodle.rs:316-330: send_bytes on self.sock);
+       SwimBroadcast::Join / Failed of the round's broadcast lists, to the broadcast address, from the
+       broadcast socket (broadcast_msg, src/kaboodle.rs:188-195).
+A real `Kaboodle::discover_mesh_member` on the same network therefore discovers a simulated peer, and real
+instances see the simulated mesh's Join/Failed broadcasts.  Not carried (declared): unicast
+envelopes between real and simulated peers.
+
+`mesh` is a kaboodle_amd.Mesh (or any object with step / probe / probe_responses / broadcasts / identity).
+"""
+from __future__ import annotations
+
+import socket
+
+from . import wire
+from .networking import Interface, create_broadcast_sockets
+
+
+class Bridge:
+    def __init__(self, mesh, broadcast_port: int | None = None, interface: Interface | None = None,
+                 sockets=None):
+        """sockets = (broadcast_in, broadcast_out, broadcast_addr, unicast) overrides the network setup
+        (tests use loopback sockets); otherwise the reference's sockets are created on `interface`."""
+        self.mesh = mesh
+        if sockets is not None:
+            self.bin, self.bout, self.baddr, self.usock = sockets
+        else:
+            self.bin, self.bout, self.baddr = create_broadcast_sockets(interface, broadcast_port)
+            fam = socket.AF_INET6 if interface.is_ipv6 else socket.AF_INET
+            self.usock = socket.socket(fam, socket.SOCK_DGRAM)
+            self.usock.bind((interface.ip, 0))
+        self.stats = {"probes_in": 0, "external_join": 0, "external_failed": 0, "undecodable": 0,
+                      "probe_responses_out": 0, "broadcasts_out": 0}
+
+    # ---- inbound ----
+    def ingest(self, datagram: bytes, sender) -> str | None:
+        """One datagram from the broadcast socket; returns the SwimBroadcast kind (None if undecodable)."""
+        try:
+            msg = wire.receive(datagram, "broadcast")
+        except ValueError:
+            self.stats["undecodable"] += 1
+            return None
+        if msg["kind"] == "Probe":
+            self.mesh.probe(msg["peer"])
+            self.stats["probes_in"] += 1
+        elif msg["kind"] == "Join":
+            self.stats["external_join"] += 1
+        else:
+            self.stats["external_failed"] += 1
+        return msg["kind"]
+
+    def pump(self) -> int:
+        """Read every datagram waiting on the broadcast socket."""
+        n = 0
+        while True:
+            try:
+                data, sender = self.bin.recvfrom(wire.INCOMING_BUFFER_SIZE)
+            except (BlockingIOError, InterruptedError):
+                return n
+            self.ingest(data, sender)
+            n += 1
+
+    # ---- outbound ----
+    def egress(self):
+        """The round's datagrams: [(destination, datagram, "unicast" | "broadcast")]."""
+        out = []
+        for rnd, responder, probe, prober, ident in self.mesh.probe_responses():
+            out.append((prober, wire.encode("ProbeResponse", identity=ident), "unicast"))
+        for kind, sender, peer in self.mesh.broadcasts():
+            if kind == "Join":
+                out.append((self.baddr, wire.encode("Join", identity=self.mesh.identity(sender),
+                                                    peer=wire.addr_of(sender)), "broadcast"))
+            else:
+                out.append((self.baddr, wire.encode("Failed", peer=wire.addr_of(peer)), "broadcast"))
+        return out
+
+    def run_round(self) -> dict:
+        """pump the inbound broadcasts, step the mesh one round, send its outbound datagrams"""
+        self.pump()
+        self.mesh.step(1)
+        for dest, dg, ch in self.egress():
+            try:
+                (self.usock if ch == "unicast" else self.bout).sendto(dg, dest)
+            except OSError:
+                continue                       # the reference logs send failures and carries on (:324-329)
+            self.stats["probe_responses_out" if ch == "unicast" else "broadcasts_out"] += 1
+        return dict(self.stats)
+
+    def close(self) -> None:
+        for s in {self.bin, self.bout, self.usock}:
+            try:
+                s.close()
+            except OSError:
+                pass
