@@ -124,9 +124,10 @@ def test_gpu_discover_channels_2x2():
         for x in k:
             x.start()
         m.step(6)
-        got = peers.drain()
-        assert sorted(i for _, i in got) == [0, 1, 2, 3]
-        assert got[0][0] == m.format_addr(got[0][1])
+        got = peers.drain()                       # (addr, identity) per discovered peer (src/lib.rs:221-236)
+        ids = {m.format_addr(i): i for i in range(4)}
+        assert sorted(ids[a] for a, _ in got) == [0, 1, 2, 3]
+        assert all(ident == names[ids[a]] for a, ident in got)
         assert len(nxt.drain()) == 1 and nxt.closed
         f = fps.drain()
         assert f and f[-1] == 0x981285C8 == k[0].fingerprint()
