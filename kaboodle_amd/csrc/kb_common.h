@@ -5,9 +5,6 @@
 //   bits   [C][W/32] u32 membership bitset (the authority for "peer in known_peers")
 //   segp   [C][64] {raw, cnt} crc0 of the members of each W/64-id segment (fingerprint checkpoints)
 //   sdirty [C] u64  segments whose checkpoint is stale; dirty[C] u8: cached fingerprint stale
-//   stp    [C][W/128] {raw, cnt} crc0 of the members of each 128-id step (k_fold's sub-checkpoints); a
-//          step's entry is current unless the step is flagged: its bit in stepd [C][W/4096] u32 (set by
-//          the row pass, exact) or its segment's bit in sfull [C] u64 (every other writer: all steps)
 //   susp   [C][8]   WaitingForPing / WaitingForIndirectPing slots; cur [C][8] curious_peers entries
 //   flog   [C][LOGCAP] u32 freshness log: (peer << 8 | round & 255) each time a stamp becomes
 //          Known(now); flog_n [C] entries appended; fstart [C][16] flog_n at the start of each round
@@ -47,7 +44,6 @@ enum : uint32_t { PATH_PHASEB_HBM = 1, PATH_RESP_SCRATCH_SAMPLED = 2, PATH_RESP_
 constexpr int NSEG = 64;          // fingerprint checkpoints per row
 constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
 constexpr int ZB = 9 * 1024;      // byte tables for Z^0..Z^8 (4 lookups per multiply)
-constexpr int ZB2 = 24 * 1024;    // ... and Z^16, Z^24, ..., Z^128 (tables 9..23): Z^c for c <= 128 in two
 
 // Row shards: a shard holds the rows of ids [lo, hi) — the observer state of those
 // peers.  Row-indexed tables are allocated for the local rows only and their pointers are biased by
@@ -57,7 +53,6 @@ struct Dev {
   uint32_t lo, hi;                // local rows (unsharded: 0, C)
   uint32_t C, W, SEGW, NWR;       // capacity, row stride, ids per segment (W/64), bitset words per row (W/32)
   uint32_t segq, segm;            // SEGW = 128 * segq; segm = ceil(2^32 / segq) (segment of id j without a divide)
-  uint32_t NSW;                   // step-flag words per row (W / 4096)
   uint32_t k0, k1;
   uint32_t loss_thr, churn_thr;
   int32_t fault_end;
@@ -73,9 +68,6 @@ struct Dev {
   uint32_t* bits;
   uint2* segp;
   unsigned long long* sdirty;
-  uint2* stp;                     // [R][W/128] step checkpoints (k_fold)
-  unsigned long long* sfull;      // [R] segments whose every step is flagged stale
-  uint32_t* stepd;                // [R][NSW] steps flagged stale by the row pass
   uint8_t* dirty;
   uint8_t* alive;
   uint32_t* abits;                // running set bitset [W/32]
@@ -94,7 +86,7 @@ struct Dev {
   uint32_t* zpow;                 // Z^k, Z = x^(8L), k in [0, C+1]
   uint32_t* zfin;                 // Z^k * 0xFFFFFFFF (the init term of a k-member fingerprint)
   uint32_t* ztab;                 // [17][8][16] nibble tables of multiplication by Z^c
-  uint32_t* zbtab;                // [24][4][256] byte tables of multiplication by Z^c (c <= 8) and Z^(8q) (2 <= q <= 16)
+  uint32_t* zbtab;                // [9][4][256] byte tables of multiplication by Z^c
   uint32_t* htab;                 // [(W/8)][256] crc0 of every member pattern of every 8-id half block
   unsigned long long* stats;
   unsigned long long* sacc;       // [NACC][NSTAT] per-workgroup partial counters, folded into stats on read
@@ -171,7 +163,7 @@ __device__ inline bool mem_clr(const Dev& d, uint32_t i, uint32_t j) {   // retu
   return (atomicAnd(&bits_of(d, i)[j >> 5], ~m) & m) != 0;
 }
 __device__ inline void mark(const Dev& d, uint32_t i, unsigned long long segs) {
-  if (segs) { atomicOr(&d.sdirty[i], segs); atomicOr(&d.sfull[i], segs); d.dirty[i] = 1; }
+  if (segs) { atomicOr(&d.sdirty[i], segs); d.dirty[i] = 1; }
 }
 
 // multiplication by Z^c (c in 0..8) through LDS nibble tables (conflict-free: 16 words per table)
@@ -185,14 +177,9 @@ __device__ inline uint32_t mulzb(const uint32_t* tab, uint32_t x, uint32_t c) {
   const uint32_t* t = tab + c * 1024;
   return t[x & 255] ^ t[256 + ((x >> 8) & 255)] ^ t[512 + ((x >> 16) & 255)] ^ t[768 + (x >> 24)];
 }
-__device__ inline void load_zbtab(const Dev& d, uint32_t* lds, uint32_t n = ZB) {
-  for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) lds[k] = d.zbtab[k];
+__device__ inline void load_zbtab(const Dev& d, uint32_t* lds) {
+  for (uint32_t k = threadIdx.x; k < ZB; k += blockDim.x) lds[k] = d.zbtab[k];
   __syncthreads();
-}
-// multiplication by Z^c for c <= 128 (ZB2 tables): Z^(8q) then Z^r, c = 8q + r
-__device__ inline uint32_t mulz_cnt(const uint32_t* tab, uint32_t x, uint32_t c) {
-  const uint32_t q = c >> 3;
-  return mulzb(tab, mulzb(tab, x, q == 0 ? 0u : (q == 1 ? 8u : 7u + q)), c & 7u);
 }
 __device__ inline void load_ztab(const Dev& d, uint32_t* lds) {
   for (uint32_t k = threadIdx.x; k < ZT * 128; k += blockDim.x) lds[k] = d.ztab[k];
@@ -308,7 +295,6 @@ __device__ __attribute__((always_inline)) inline uint32_t wave_fp(const Dev& d, 
   wave_combine(d, raw, cnt);
   raw = bcast(raw, 0); cnt = bcast(cnt, 0);
   if (l == 0 && sd) atomicAnd(&d.sdirty[i], ~sd);
-  if (l == 0 && extra) atomicOr(&d.sfull[i], extra);   // the caller's changes: k_fold's step checkpoints are stale
   return finish_fp(d, raw, cnt);
 }
 // fingerprint of row i from its checkpoints by one thread (checkpoints must be fresh)

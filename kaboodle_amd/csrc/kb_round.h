@@ -334,11 +334,8 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t l = lane();
-  // LDS: [wpb][NWR] bitsets, [wpb][NSW] changed-step flags (LDSB), then the lists
-  uint32_t* SM = pb_dyn + (LDSB ? (size_t)wpb * d.NWR + (size_t)wv * d.NSW : 0);
-  uint32_t* FL = pb_dyn + (LDSB ? (size_t)wpb * (d.NWR + d.NSW) : 0);   // [2 * nf] when lf
+  uint32_t* FL = pb_dyn + (LDSB ? (size_t)wpb * d.NWR : 0);   // [2 * nf] when lf
   uint32_t* JL = FL + (lf ? 2 * pb.nf : 0);                    // [nj] when lj
-  if (LDSB) for (uint32_t k = threadIdx.x; k < wpb * d.NSW; k += blockDim.x) pb_dyn[(size_t)wpb * d.NWR + k] = 0;
   if (lf) for (uint32_t e = threadIdx.x; e < pb.nf; e += blockDim.x) {
     const BCast b = pb.bfail[e];
     FL[2 * e] = b.sender | (b.bseq << 23) | ((uint32_t)pb.dep[e] << 31);
@@ -447,7 +444,6 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
             removed_cnt++;
             if (is_susp(b.peer)) susp_clear(d, i, b.peer);
             segs |= seg_bit(d, b.peer);
-            if (LDSB) atomicOr(&SM[b.peer >> 12], 1u << ((b.peer >> 7) & 31u));   // its 128-id step changed
           }
         }
         if (!LDSB) { __builtin_amdgcn_s_waitcnt(0); }
@@ -496,7 +492,6 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
           rw[b.sender] = now;
           if (isnew) {
             atomicOr(&B[b.sender >> 5], 1u << (b.sender & 31)); segs |= seg_bit(d, b.sender);
-            if (LDSB) atomicOr(&SM[b.sender >> 12], 1u << ((b.sender >> 7) & 31u));
             if (pb.fnamed && ((pb.fnamed[b.sender >> 5] >> (b.sender & 31)) & 1u)) lat_none(d, i, b.sender);
           }
         }
@@ -511,18 +506,10 @@ __global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, in
         }
       }
       segs = (unsigned long long)wave_or((uint32_t)segs) | ((unsigned long long)wave_or((uint32_t)(segs >> 32)) << 32);
-      if (LDSB && segs) {                             // the changed steps, exact: k_fold refolds only those
-        wait_lds();
-        __builtin_amdgcn_wave_barrier();
-        uint32_t* gsw = d.stepd + (size_t)i * d.NSW;
-        for (uint32_t w = l; w < d.NSW; w += 64) { const uint32_t m = SM[w]; if (m) { gsw[w] |= m; SM[w] = 0; } }
-        w_bytes += 8ull * d.NSW;
-      }
       if (l == 0) {
         d.n[i] = n;
         d.flog_n[i] = fn;
-        if (LDSB) { if (segs) { atomicOr(&d.sdirty[i], segs); d.dirty[i] = 1; } }   // steps flagged above
-        else mark(d, i, segs);                                                          // every step of the segments
+        mark(d, i, segs);
         if (n != n0) d.dirty[i] = 1;
         pb.nresp[i] = nresp; pb.paysum[i] = paysum; pb.nbase[i] = nbase;
       }

@@ -43,14 +43,14 @@ using namespace kb;
 // carries start/stop events on its own dispatch packet and kb_sim_kernel_breakdown reports the sums.
 enum KId : int {
   KI_REBASE, KI_EVENTS, KI_CHURN_LEAVE, KI_CHURN_JOIN, KI_ALIVE_BITS, KI_TRUEFP_PART, KI_TRUEFP_FIN, KI_LOG_MARK,
-  KI_LAT_MARK, KI_BFAIL_PREP, KI_ROWPASS, KI_LAT_SWEEP, KI_SCAN, KI_SET_CAP, KI_RESP_WAVE,
+  KI_LAT_MARK, KI_BFAIL_PREP, KI_ROWPASS, KI_LAT_SWEEP, KI_SCAN_TILES, KI_SCAN_APPLY, KI_SET_CAP, KI_RESP_WAVE,
   KI_RESP_NODE, KI_TICK_SCAN, KI_TICK_PRE, KI_FOLD, KI_FP_ROWS, KI_TICK_POST, KI_BCAST_WRITE, KI_ROUTE, KI_ROUTE_X,
   KI_XBOUND, KI_PACK, KI_ROUTE_RECV, KI_SCATTER, KI_SCATTER_FLAT, KI_KP_SMALL, KI_KP_GROUP, KI_SORT_INBOX,
   KI_PROC_FAST, KI_PROC, KI_ROUND_END, KI_PROBE, NKI
 };
 static const char* const KNAME[NKI] = {
   "k_rebase", "k_events", "k_churn_leave", "k_churn_join", "k_alive_bits", "k_truefp_part", "k_truefp_fin",
-  "k_log_mark", "k_lat_mark", "k_bfail_prep", "k_rowpass", "k_lat_sweep", "k_scan",
+  "k_log_mark", "k_lat_mark", "k_bfail_prep", "k_rowpass", "k_lat_sweep", "k_scan_tiles", "k_scan_apply",
   "k_set_cap", "k_resp_wave", "k_resp_node", "k_tick_scan", "k_tick_pre", "k_fold", "k_fp_rows", "k_tick_post",
   "k_bcast_write", "k_route", "k_route_x", "k_xbound", "k_pack", "k_route_recv", "k_scatter", "k_scatter_flat",
   "k_kp_small", "k_kp_group", "k_sort_inbox", "k_proc_fast", "k_proc", "k_round_end", "k_probe"};
@@ -66,12 +66,8 @@ static int kbytes_stat(int kid) {
 }
 
 // ================================================================================================
-// Exclusive scan over up to 4 arrays of length n (+ optional compaction of indices j with in[0][j] != 0)
-// in ONE launch over 1024-element tiles, with decoupled look-back: a tile takes a ticket (tiles run in
-// ticket order, so every predecessor has started), publishes its aggregate, then walks back over the
-// predecessors' published values until it meets an inclusive prefix, and publishes its own.  Status
-// words carry the launch's epoch; the last tile to finish resets the tickets and advances the epoch
-// (ctl = {ticket, done, epoch} on the device), so launches need no host state and replay in a graph.
+// Exclusive scan over up to 4 arrays of length n (+ optional compaction of indices j with in[0][j] != 0),
+// two fully parallel passes over 1024-element tiles: per-tile sums, then per-tile offsets + local scan.
 // ================================================================================================
 struct ScanArgs {
   const uint32_t* in[4]; uint32_t* out[4]; int narr; uint32_t n;
@@ -79,23 +75,45 @@ struct ScanArgs {
   uint32_t* list; uint32_t* list_count; uint32_t list_base;   // list entries are j + list_base
   uint32_t list_or3;  // list flag: in[0][j] != 0, or also in[3][j] != 0 when set
   uint32_t addc[4];   // constant added to every element of array q before scanning
-  unsigned long long* status;   // [5][ntiles] {epoch:30 | state:2 | value:32}: 1 aggregate, 2 inclusive prefix
-  uint32_t* ctl;      // {next ticket, tiles done, epoch}
+  uint32_t* tiles;    // workspace [5 * ntiles]
   uint32_t ntiles;
 };
 __device__ inline uint32_t scan_val(const ScanArgs& a, int q, uint32_t j) {
   if (q == 4) return a.in[0][j] != 0 || (a.list_or3 && a.in[3][j] != 0);
   return (a.in[q] ? a.in[q][j] : 0) + a.addc[q];
 }
-__global__ __launch_bounds__(1024) void k_scan(ScanArgs a) {
-  __shared__ uint32_t s_tile, s_epoch, base[5], wpre[5][16];
-  const uint32_t t = threadIdx.x;
-  if (t == 0) {
-    s_tile = atomicAdd(&a.ctl[0], 1u);
-    s_epoch = __hip_atomic_load(&a.ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0x3FFFFFFFu;
+__global__ __launch_bounds__(1024) void k_scan_tiles(ScanArgs a) {
+  __shared__ uint32_t red[5][16];
+  const uint32_t j = blockIdx.x * 1024 + threadIdx.x;
+  const int nq = a.list ? 5 : a.narr;
+  for (int q = 0; q < 5; ++q) {
+    if (q >= a.narr && !(q == 4 && a.list)) continue;
+    uint32_t v = j < a.n ? scan_val(a, q, j) : 0;
+    v = wave_sum(v);
+    if (lane() == 0) red[q][threadIdx.x >> 6] = v;
   }
   __syncthreads();
-  const uint32_t tile = s_tile, epoch = s_epoch, j = tile * 1024 + t;
+  if (threadIdx.x < 5 && (threadIdx.x < (uint32_t)a.narr || (threadIdx.x == 4 && a.list))) {
+    uint32_t t = 0;
+    for (int w = 0; w < 16; ++w) t += red[threadIdx.x][w];
+    a.tiles[threadIdx.x * a.ntiles + blockIdx.x] = t;
+  }
+  (void)nq;
+}
+__global__ __launch_bounds__(1024) void k_scan_apply(ScanArgs a) {
+  __shared__ uint32_t base[5], red[5][16], wpre[5][16];
+  const uint32_t tile = blockIdx.x, t = threadIdx.x;
+  const uint32_t j = tile * 1024 + t;
+  for (int q = 0; q < 5; ++q) {
+    const bool on = q < a.narr || (q == 4 && a.list);
+    uint32_t s = 0;
+    if (on) for (uint32_t k = t; k < tile; k += 1024) s += a.tiles[q * a.ntiles + k];
+    s = wave_sum(s);
+    if (lane() == 0) red[q][t >> 6] = s;
+  }
+  __syncthreads();
+  if (t < 5) { uint32_t s = 0; for (int w = 0; w < 16; ++w) s += red[t][w]; base[t] = s; }
+  __syncthreads();
   uint32_t v[5], ex[5];
   for (int q = 0; q < 5; ++q) {
     const bool on = q < a.narr || (q == 4 && a.list);
@@ -105,36 +123,13 @@ __global__ __launch_bounds__(1024) void k_scan(ScanArgs a) {
     if (lane() == 0) wpre[q][t >> 6] = tot;
   }
   __syncthreads();
-  if (t < 5 && ((int)t < a.narr || (t == 4 && a.list))) {
-    uint32_t run = 0;
-    for (int w = 0; w < 16; ++w) { const uint32_t x = wpre[t][w]; wpre[t][w] = run; run += x; }
-    unsigned long long* st = a.status + (size_t)t * a.ntiles;
-    const unsigned long long ep = (unsigned long long)epoch << 34;
-    uint32_t excl = 0;
-    if (tile > 0) {
-      __hip_atomic_store(&st[tile], ep | (1ull << 32) | run, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      for (uint32_t p = tile - 1;; --p) {
-        unsigned long long x;
-        do {
-          x = __hip_atomic_load(&st[p], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        } while ((x >> 34) != epoch || ((x >> 32) & 3u) == 0);
-        excl += (uint32_t)x;
-        if (((x >> 32) & 3u) == 2) break;
-      }
-    }
-    __hip_atomic_store(&st[tile], ep | (2ull << 32) | (uint32_t)(excl + run), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    base[t] = excl;
-  }
+  if (t < 5) { uint32_t run = 0; for (int w = 0; w < 16; ++w) { uint32_t x = wpre[t][w]; wpre[t][w] = run; run += x; } }
   __syncthreads();
   for (int q = 0; q < a.narr; ++q) if (j < a.n) a.out[q][j] = base[q] + wpre[q][t >> 6] + ex[q];
   if (a.list && j < a.n && v[4]) a.list[base[4] + wpre[4][t >> 6] + ex[4]] = j + a.list_base;
-  if (tile == a.ntiles - 1 && t == 1023) {
+  if (tile == gridDim.x - 1 && t == 1023) {
     for (int q = 0; q < a.narr; ++q) a.totals[q] = base[q] + wpre[q][15] + ex[q] + v[q];
     if (a.list) { const uint32_t c = base[4] + wpre[4][15] + ex[4] + v[4]; a.totals[4] = c; if (a.list_count) *a.list_count = c; }
-  }
-  if (t == 0 && atomicAdd(&a.ctl[1], 1u) == a.ntiles - 1) {   // the last tile: next launch starts afresh
-    a.ctl[0] = 0; a.ctl[1] = 0;
-    __hip_atomic_store(&a.ctl[2], a.ctl[2] + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -210,11 +205,11 @@ __global__ void k_init_converged_nodes(Dev d, uint32_t n0) {
   d.start_round[i] = NONE_ROUND;
   if (i >= n0) return;
   d.alive[i] = 1; d.start_round[i] = 0;
-  if (loc) { d.dirty[i] = 1; d.n[i] = n0; d.last_bcast[i] = -1000; d.paq_n[i] = 0; d.sdirty[i] = ~0ull; d.sfull[i] = ~0ull; }
+  if (loc) { d.dirty[i] = 1; d.n[i] = n0; d.last_bcast[i] = -1000; d.paq_n[i] = 0; d.sdirty[i] = ~0ull; }
 }
 __global__ void k_mark_all_dirty(Dev d) {
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < d.hi) { d.dirty[i] = 1; d.sdirty[i] = ~0ull; d.sfull[i] = ~0ull; }
+  if (i < d.hi) { d.dirty[i] = 1; d.sdirty[i] = ~0ull; }
 }
 __global__ __launch_bounds__(64) void k_fp_one(Dev d, uint32_t i) {
   __shared__ uint32_t ztab[ZT * 128];
@@ -342,8 +337,7 @@ struct kb_sim {
   uint32_t nf, nj;
   BcastSlots bs;
   uint32_t* join_off; uint32_t* fail_off;
-  uint32_t* scan_tot;
-  unsigned long long* scan_status; uint32_t* scan_ctl;     // single-pass scan: tile status, {ticket, done, epoch}
+  uint32_t* scan_tot; uint32_t* scan_tiles;
   unsigned long long* newmask; unsigned long long* respmask; size_t mask_words;
   unsigned long long* newmask_base; unsigned long long* respmask_base;
   uint32_t* nresp; uint32_t* paysum; uint32_t* nbase; uint32_t* resp_off;
@@ -456,11 +450,12 @@ static void prof_resolve(kb_sim* s, size_t n) {
 
 static ScanArgs scan_args(kb_sim* s, uint32_t n, uint32_t* totals) {
   ScanArgs a; memset(&a, 0, sizeof a); a.n = n; a.totals = totals;
-  a.status = s->scan_status; a.ctl = s->scan_ctl; a.ntiles = (n + 1023) / 1024; return a;
+  a.tiles = s->scan_tiles; a.ntiles = (n + 1023) / 1024; return a;
 }
 static void launch_scan(kb_sim* s, const ScanArgs& a) {
   if (!a.n) return;
-  klaunch(s, KI_SCAN, k_scan, dim3(a.ntiles), dim3(1024), 0, a);
+  klaunch(s, KI_SCAN_TILES, k_scan_tiles, dim3(a.ntiles), dim3(1024), 0, a);
+  klaunch(s, KI_SCAN_APPLY, k_scan_apply, dim3(a.ntiles), dim3(1024), 0, a);
 }
 
 extern "C" void kb_config_default(kb_config* c) {
@@ -512,17 +507,10 @@ static int upload_segments(kb_sim* s) {
     HIPCHK(hipMemcpy(s->d.zfin, zf.data(), 4ull * (C + 2), hipMemcpyHostToDevice));
   }
   HIPCHK(hipMemcpy(s->d.ztab, ztab.data(), 4ull * ztab.size(), hipMemcpyHostToDevice));
-  std::vector<uint32_t> zb(ZB2);                  // Z^0..Z^8, then Z^16, Z^24, ..., Z^128
-  {
-    uint32_t z = 0x80000000u;                      // Z^c for the tables, independent of the capacity
-    std::vector<uint32_t> zp(129);
-    for (uint32_t c = 0; c <= 128; ++c) { zp[c] = z; z = multmodp(Z, z); }
-    for (uint32_t t = 0; t < 24; ++t) {
-      const uint32_t c = t <= 8 ? t : 8 * (t - 7);
-      for (uint32_t k = 0; k < 4; ++k)
-        for (uint32_t v = 0; v < 256; ++v) zb[t * 1024 + k * 256 + v] = multmodp(zp[c], v << (8 * k));
-    }
-  }
+  std::vector<uint32_t> zb(ZB);
+  for (uint32_t c = 0; c < 9; ++c)
+    for (uint32_t k = 0; k < 4; ++k)
+      for (uint32_t v = 0; v < 256; ++v) zb[c * 1024 + k * 256 + v] = multmodp(zpow[c], v << (8 * k));
   HIPCHK(hipMemcpy(s->d.zbtab, zb.data(), 4ull * zb.size(), hipMemcpyHostToDevice));
   const size_t hn = (size_t)(s->W / 8) * 256;
   k_build_htab<<<(unsigned)((hn + 255) / 256), 256>>>(s->d);
@@ -595,7 +583,6 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   d.C = C; d.W = W; d.SEGW = W / NSEG; d.NWR = W / 32;
   d.segq = d.SEGW / 128;
   d.segm = d.segq > 1 ? (uint32_t)(((1ull << 32) + d.segq - 1) / d.segq) : 0u;
-  d.NSW = W / 4096;
   d.k0 = (uint32_t)cfg->seed; d.k1 = (uint32_t)(cfg->seed >> 32);
   d.loss_thr = cfg->loss_threshold; d.churn_thr = cfg->churn_threshold; d.fault_end = cfg->fault_end_round;
   d.failed_mode = cfg->failed_mode; d.pgroups = cfg->partition_groups; d.pstart = cfg->partition_start;
@@ -615,11 +602,10 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
 #define A(ptr, n) if (e == hipSuccess) e = talloc(s, &(ptr), (n))     // per-id / global tables
 #define AR(ptr, n) if (e == hipSuccess) e = ralloc(s, &(ptr), (n))   // row tables: n entries per local row
   AR(d.stamp, W); AR(d.bits, d.NWR); AR(d.segp, NSEG); AR(d.sdirty, 1);
-  AR(d.stp, W / 128); AR(d.sfull, 1); AR(d.stepd, d.NSW);
   AR(d.dirty, 1); A(d.alive, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
   AR(d.last_bcast, 1); AR(d.a3cur, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
   AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
-  A(d.ztab, 17 * 128); A(d.zbtab, ZB2);
+  A(d.ztab, 17 * 128); A(d.zbtab, ZB);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.sacc, (size_t)NACC * NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
   if (cfg->track_latency) { A(d.lat, (size_t)W * lat_stride(R)); A(s->lat_col, C); A(s->fnamed, d.NWR); }   // peer-major
@@ -636,8 +622,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (!xf) { A(s->wc.status, s->msg_cap); A(s->wc.inbox, s->msg_cap); A(s->wc.kin, s->msg_cap); }
   A(s->bfail, (size_t)C * SLOTS); A(s->bjoin, C);
   AR(s->bs.join, 1); AR(s->bs.nfail, 1); AR(s->bs.fail, SLOTS); AR(s->join_off, 1); AR(s->fail_off, 1);
-  A(s->scan_tot, 32); A(s->rr, 4); A(s->scan_ctl, 4);
-  A(s->scan_status, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
+  A(s->scan_tot, 32); A(s->rr, 4); A(s->scan_tiles, 5 * ((std::max<size_t>(C, (size_t)world * R) + 1023) / 1024) + 5);
   AR(s->nresp, 1); AR(s->paysum, 1); AR(s->nbase, 1); AR(s->resp_off, 1);
   A(s->resp_nodes, R); A(s->bf_gid, (size_t)C * SLOTS); A(s->bf_dep, (size_t)C * SLOTS); A(s->slow, R);
   AR(s->ro.part, 10);
@@ -1069,10 +1054,9 @@ static int step_round(kb_sim* s) {
     uint32_t lf = s->nf <= PB_FMAX, lj = s->nj <= PB_JMAX;
     uint32_t listw = (lf ? 2 * s->nf : 0) + (lj ? s->nj : 0);
     if (listw > budget / 2 || pb_hbm) { lf = lj = 0; listw = 0; }
-    const uint32_t per_wave = d.NWR + d.NSW;          // bitset + changed-step flags
-    const bool ldsb = s->W <= PB_LDS_W && budget - listw >= per_wave && !pb_hbm;
-    const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / per_wave) : RP_WAVES;
-    const size_t lds = 4ull * ((ldsb ? (size_t)wpb * per_wave : 0) + listw);
+    const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR && !pb_hbm;
+    const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / d.NWR) : RP_WAVES;
+    const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
     int occ = 0;                                       // resident workgroups per CU (LDS, registers)
     const uint64_t okey = ((uint64_t)ldsb << 63) | ((uint64_t)wpb << 40) | (uint64_t)lds;   // queried once per shape
     if (okey == s->occ_key) occ = s->occ_val;
@@ -1166,8 +1150,7 @@ static int step_round(kb_sim* s) {
   klaunch(s, KI_TICK_SCAN, k_tick_scan, dim3(gnode), dim3(tb), 0, d, s->bs, r, s->slow);                       // A1; list the A2 nodes
   klaunch(s, KI_TICK_PRE, k_tick_pre, dim3(std::min<uint32_t>(gwave, 1024)), dim3(256), 0, d, o0, s->bs, r, s->slow);   // A2 per listed node
   // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded
-  if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + FOLD_WAVES - 1) / FOLD_WAVES * s->S), dim3(64 * FOLD_WAVES),
-                         (uint32_t)(4 * ZB2), d, FoldArgs{s->S});
+  if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
   if (d.uniform) klaunch(s, KI_FP_ROWS, k_fp_rows, dim3((FP_LANES * R + tb - 1) / tb), dim3(tb), 0, d);
   klaunch(s, KI_TICK_POST, k_tick_post, dim3(gnode), dim3(tb), 0, d, s->ro, o0, r);
   {

@@ -165,90 +165,62 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
 
 // ================================================================================================
 // THE FOLD: generate_fingerprint's checkpoints (:71-83).  Every segment whose membership changed since
-// its checkpoint (sdirty) gets a fresh checkpoint, combined from its 128-id step checkpoints (stp): a
-// flagged step (the row pass's exact stepd bits, or every step of an sfull segment) is refolded from the
-// member bits — per 8-id block raw = raw·Z^popc ⊕ htab[block][mask], the multiply through LDS byte
-// tables — the others are read back.  The round's Failed/Join broadcasts name the same few hundred
-// peers in every row, so the same few steps are flagged across the rows of a wave, and the refolds
-// skip most of the row.  Lane = node: a wave folds 64 rows over one column split; workgroups take
-// split blockIdx % S, so each XCD (workgroups are dealt round-robin to the 8 XCDs) stays on
-// 1/min(S, 8) of the columns and its slice of htab stays in that XCD's 4 MB L2.  Runs after A2 (the
-// last membership change of the tick), so the tick ends with every checkpoint fresh.
+// its checkpoint (sdirty) is refolded from the member bits: per 8-id block, raw = raw·Z^popc ⊕
+// htab[block][mask], the multiply through four LDS byte tables.  Lane = node: a wave folds 64 rows over
+// one column split; workgroups take split blockIdx % S, so each XCD (workgroups are dealt round-robin to
+// the 8 XCDs) stays on 1/min(S, 8) of the columns and its slice of htab stays in that XCD's 4 MB L2.
+// Runs after A2 (the last membership change of the tick), so the tick ends with every checkpoint fresh.
 // ================================================================================================
 struct FoldArgs { uint32_t S; };
-constexpr uint32_t FOLD_WAVES = 16;               // 1024-thread workgroups share the 96 KB of Z tables
-constexpr uint32_t FOLD_BATCH = 8;                // step checkpoints loaded ahead
 
-__global__ __launch_bounds__(1024) void k_fold(Dev d, FoldArgs fa) {
-  extern __shared__ uint32_t zb[];                // ZB2 words: Z^c byte tables, c <= 8 and Z^(8q)
-  load_zbtab(d, zb, ZB2);
+__global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
+  __shared__ uint32_t zb[ZB];
+  load_zbtab(d, zb);
   const uint32_t S = fa.S;
   const uint32_t s = blockIdx.x % S;
-  const uint32_t nwv = blockDim.x >> 6;
-  const uint32_t g = (blockIdx.x / S) * nwv + (threadIdx.x >> 6);
+  const uint32_t g = (blockIdx.x / S) * 4 + (threadIdx.x >> 6);
   const uint32_t i0 = d.lo + g * 64 + lane();
   const bool act = i0 < d.hi && d.alive[i0] && d.uniform;
   const unsigned long long actm = __ballot(act);
   // the fold's byte counter (bench roofline) is summed over the workgroup and added once: one atomic
   // per wave on one address serialises thousands of waves in the memory system
-  __shared__ uint32_t s_nb[FOLD_WAVES];
+  __shared__ uint32_t s_nb[4];
   uint32_t nbytes = 0;
   if (actm) {
     const uint32_t i = act ? i0 : d.lo + g * 64 + (uint32_t)(__ffsll((long long)actm) - 1);   // idle lanes shadow a live one
     const uint32_t* bw = bits_of(d, i);
-    uint2* st = d.stp + (size_t)i * (d.W / 128);
-    const uint32_t* sw = d.stepd + (size_t)i * d.NSW;
-    const uint32_t spp = NSEG / S, segq = d.segq;
-    const unsigned long long sd = act ? d.sdirty[i] : 0ull, sf = act ? d.sfull[i] : 0ull;
+    const uint32_t spp = NSEG / S;
+    const unsigned long long sd = act ? d.sdirty[i] : 0ull;
     unsigned long long folded = 0;
     for (uint32_t k = s * spp; k < (s + 1) * spp; ++k) {
       const bool mine = (sd >> k) & 1ull;
-      if (!__ballot(mine)) continue;                // wave-uniform: no row of this wave changed here
-      const bool full = (sf >> k) & 1ull;
-      uint32_t raw = 0, cnt = 0, wcur = 0xFFFFFFFFu, wbits = 0;
-      for (uint32_t t0 = k * segq; t0 < (k + 1) * segq; t0 += FOLD_BATCH) {
-        uint2 sp[FOLD_BATCH];
+      if (!__ballot(mine)) continue;                  // wave-uniform: no row of this wave changed here
+      const uint32_t c0 = k * d.SEGW, c1 = c0 + d.SEGW;
+      uint32_t raw = 0, cnt = 0;
+      uint4 mb = *reinterpret_cast<const uint4*>(bw + (c0 >> 5));
+      for (uint32_t col = c0; col < c1; col += 128) {
+        const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
+        uint32_t hv[16];
+        const uint32_t* ht = d.htab + (size_t)(col >> 3) * 256;
 #pragma unroll
-        for (uint32_t u = 0; u < FOLD_BATCH; ++u)   // the batch's checkpoints, in flight together
-          sp[u] = (mine && t0 + u < (k + 1) * segq) ? st[t0 + u] : make_uint2(0, 0);
-        for (uint32_t u = 0; u < FOLD_BATCH && t0 + u < (k + 1) * segq; ++u) {
-          const uint32_t t = t0 + u;
-          if ((t >> 5) != wcur) { wcur = t >> 5; wbits = (mine && !full) ? sw[wcur] : 0u; }
-          const bool need = mine && (full || ((wbits >> (t & 31)) & 1u));
-          if (need) {                               // refold the step from its member bits
-            const uint4 mb = *reinterpret_cast<const uint4*>(bw + t * 4);
-            const uint32_t mw[4] = {mb.x, mb.y, mb.z, mb.w};
-            const uint32_t* ht = d.htab + (size_t)t * 16 * 256;
-            uint32_t hv[16];
+        for (int h = 0; h < 16; ++h) hv[h] = ht[h * 256 + ((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu)];   // entry 0 is 0
+        if (col + 128 < c1) mb = *reinterpret_cast<const uint4*>(bw + ((col + 128) >> 5));   // next step's bits
 #pragma unroll
-            for (int h = 0; h < 16; ++h) hv[h] = ht[h * 256 + ((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu)];   // entry 0 is 0
-            uint32_t r2 = 0, c2 = 0;
-#pragma unroll
-            for (int h = 0; h < 16; ++h) {
-              const uint32_t c = __popc((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu);   // Z^0 table is the identity
-              r2 = mulzb(zb, r2, c) ^ hv[h];
-              c2 += c;
-            }
-            sp[u] = make_uint2(r2, c2);
-            st[t] = sp[u];
-            nbytes += 16 + 64 + 8;                  // member bits, 16 table words, the new step checkpoint
-          }
-          if (mine) { raw = mulz_cnt(zb, raw, sp[u].y) ^ sp[u].x; cnt += sp[u].y; nbytes += need ? 0u : 8u; }
+        for (int h = 0; h < 16; ++h) {
+          const uint32_t c = __popc((mw[h >> 2] >> (8 * (h & 3))) & 0xFFu);   // Z^0 table is the identity
+          raw = mulzb(zb, raw, c) ^ hv[h];
+          cnt += c;
         }
       }
-      if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; nbytes += 8 + (full ? 0u : 4u); }
+      if (mine) { d.segp[(size_t)i * NSEG + k] = make_uint2(raw, cnt); folded |= 1ull << k; nbytes += d.SEGW / 8; }
     }
-    if (folded) {
-      atomicAnd(&d.sdirty[i], ~folded);
-      if (sf & folded) atomicAnd(&d.sfull[i], ~folded);
-    }
+    if (folded) atomicAnd(&d.sdirty[i], ~folded);
   }
   const uint32_t wb = wave_sum(act ? nbytes : 0u);
   if (lane() == 0) s_nb[threadIdx.x >> 6] = wb;
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t t = 0;
-    for (uint32_t w = 0; w < nwv; ++w) t += s_nb[w];
+    const uint32_t t = s_nb[0] + s_nb[1] + s_nb[2] + s_nb[3];
     if (t) slot_add(d, S_FOLDB, t);
   }
 }
@@ -285,7 +257,6 @@ __global__ __launch_bounds__(256) void k_fp_rows(Dev d) {
     if (on && (part & (2 * st - 1)) == 0) { raw = multmodp(d.zpow[c2], raw) ^ r2; cnt += c2; }
   }
   if (on && part == 0) { d.fp[i] = finish_fp(d, raw, cnt); d.dirty[i] = 0; }
-  if (on) for (uint32_t w = part; w < d.NSW; w += FP_LANES) d.stepd[(size_t)i * d.NSW + w] = 0;   // k_fold consumed them
 }
 
 // ---- pick the ping target (one of the oldest 5), WaitingForPing(now), Ping; ping_addrs (:550-556);

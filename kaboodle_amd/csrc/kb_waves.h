@@ -504,9 +504,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
     }
     if (t == 0 && (s_add || sg)) {
       if (KS > 1) atomicAdd(&d.n[i], s_add); else d.n[i] += s_add;
-      if (refolded) {                                  // checkpoints fresh, fp stale; step checkpoints stale
-        atomicAnd(&d.sdirty[i], ~refolded); atomicOr(&d.sfull[i], refolded); d.dirty[i] = 1;
-      }
+      if (refolded) { atomicAnd(&d.sdirty[i], ~refolded); d.dirty[i] = 1; }   // checkpoints fresh, fp stale
       else mark(d, i, sg);
     }
     if (BIG && t == 0 && li == 0) path_hit(d, lds ? PATH_KP_BIG_LDS : PATH_KP_BIG_HBM);
@@ -922,7 +920,6 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       R = bcast(raw, 0);
       if (bcast(cnt, 0) != n) set_err(d, DERR_FP);
       if (l == 0 && sd) atomicAnd(&d.sdirty[i], ~sd);
-      if (l == 0 && segs) atomicOr(&d.sfull[i], segs);   // this node's changes: k_fold's step checkpoints are stale
       segs = 0;
       inc = true; dirty = false; fpstale = true;
       zf_n = n;
@@ -1205,7 +1202,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     if (l < CSLOTS) d.cur[(size_t)i * CSLOTS + l] = s_cur[wv][l];
     if (inc) fp_now();                              // exact: the touched checkpoints stay marked stale
     if (l == 0) {
-      if (segs) { atomicOr(&d.sdirty[i], segs); atomicOr(&d.sfull[i], segs); }
+      if (segs) atomicOr(&d.sdirty[i], segs);
       d.n[i] = n; d.fp[i] = fp; d.dirty[i] = dirty ? 1 : 0; d.flog_n[i] = fn; d.kpr_big[i] = kbig;
       ob.cnt[i] = oseq;
       wave_ctr_clear(wc, i);
