@@ -45,15 +45,15 @@ enum KId : int {
   KI_REBASE, KI_EVENTS, KI_CHURN_LEAVE, KI_CHURN_JOIN, KI_ALIVE_BITS, KI_TRUEFP_PART, KI_TRUEFP_FIN, KI_LOG_MARK,
   KI_LAT_MARK, KI_BFAIL_PREP, KI_ROWPASS, KI_LAT_SWEEP, KI_SCAN_TILES, KI_SCAN_APPLY, KI_SET_CAP, KI_RESP_WAVE,
   KI_RESP_NODE, KI_TICK_SCAN, KI_TICK_PRE, KI_FOLD, KI_FP_ROWS, KI_TICK_POST, KI_BCAST_WRITE, KI_ROUTE, KI_ROUTE_X,
-  KI_XBOUND, KI_PACK, KI_ROUTE_RECV, KI_SCATTER, KI_SCATTER_FLAT, KI_KP_SMALL, KI_KP_GROUP, KI_SORT_INBOX,
-  KI_PROC_FAST, KI_PROC, KI_ROUND_END, KI_PROBE, NKI
+  KI_XBOUND, KI_PACK, KI_ROUTE_RECV, KI_SCATTER, KI_SCATTER_FLAT, KI_KP, KI_SORTFAST, KI_PROC, KI_ROUND_END,
+  KI_PROBE, NKI
 };
 static const char* const KNAME[NKI] = {
   "k_rebase", "k_events", "k_churn_leave", "k_churn_join", "k_alive_bits", "k_truefp_part", "k_truefp_fin",
   "k_log_mark", "k_lat_mark", "k_bfail_prep", "k_rowpass", "k_lat_sweep", "k_scan_tiles", "k_scan_apply",
   "k_set_cap", "k_resp_wave", "k_resp_node", "k_tick_scan", "k_tick_pre", "k_fold", "k_fp_rows", "k_tick_post",
   "k_bcast_write", "k_route", "k_route_x", "k_xbound", "k_pack", "k_route_recv", "k_scatter", "k_scatter_flat",
-  "k_kp_small", "k_kp_group", "k_sort_inbox", "k_proc_fast", "k_proc", "k_round_end", "k_probe"};
+  "k_kp", "k_sortfast", "k_proc", "k_round_end", "k_probe"};
 // the in-kernel algorithmic byte counter of a kernel (StatIdx), or -1
 static int kbytes_stat(int kid) {
   switch (kid) {
@@ -947,14 +947,16 @@ static int launch_waves(kb_sim* s, int32_t rk) {
     if (!s->xf) klaunch(s, KI_SCATTER, k_scatter, dim3(gnode), dim3(tb), 0, d, ob, s->wc);
     else if (nrecv) klaunch(s, KI_SCATTER_FLAT, k_scatter_flat, dim3((nrecv + 255) / 256), dim3(256), 0, ib, s->wc, nrecv);
     if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
-    klaunch(s, KI_KP_SMALL, k_kp_small, dim3((R + 255) / 256), dim3(256), 0, d, ib, s->wc, r, nb);   // also sets up nb.cap / nb.cnt
-    {  // BIG groups in LDS: KP_COLS workgroups per destination group, one per column part
+    {  // the KnownPeers groups: BIG ones KP_COLS workgroups per destination group (one per column part),
+       // then the small ones (a wave per destination), which also set up nb.cap / nb.cnt
       const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
       const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
-      klaunch(s, KI_KP_GROUP, k_kp_group<true>, dim3(ks * groups), dim3(1024), kp_lds_bytes(d.NWR), d, ib, s->wc, r);
+      klaunch(s, KI_KP, k_kp, dim3(ks * groups + (R + 1023) / 1024), dim3(1024), (uint32_t)kp_lds_bytes(d.NWR), d, ib, s->wc, r,
+              nb, ks * groups);
     }
-    klaunch(s, KI_SORT_INBOX, k_sort_inbox, dim3(256), dim3(1024), 0, d, s->wc, r);   // + the KPR oversize probe
-    klaunch(s, KI_PROC_FAST, k_proc_fast, dim3(gnode), dim3(tb), 0, d, ib, nb, s->wc, r, s->slow);
+    // inbox sorts + the KPR oversize probe, and the fast handlers
+    klaunch(s, KI_SORTFAST, k_sortfast, dim3(SORT_GROUPS + (R + 1023) / 1024), dim3(1024), 0, d, ib, nb, s->wc, r, s->slow,
+            SORT_GROUPS);
     // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
     // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
     // on the late waves with few nodes.

@@ -324,9 +324,10 @@ __host__ __device__ constexpr size_t kp_lds_bytes(uint32_t nwr) {
   return 4ull * (nwr <= KP_LDS_WORDS ? nwr : 4);
 }
 
+// (the body of k_kp's first nblk workgroups, bid = the workgroup among them)
 template <bool BIG>
-__global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib, WaveCtl wc, int32_t r_arg) {
-  const int32_t r = round_of(d, r_arg);
+__device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d, const OutBuf& ib, const WaveCtl& wc, int32_t r,
+                                                                   uint32_t bid, uint32_t nblk) {
   extern __shared__ __attribute__((aligned(16))) uint32_t kp_lds[];
   __shared__ unsigned long long s_segs;
   __shared__ uint32_t s_add, s_nl;
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
   const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
   const bool lds = BIG && d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM);
   const uint32_t kpb = (d.dbg & KB_DBG_KP_BIG_SMALL) ? 0u : KP_BIG;
-  const uint32_t KS = lds ? KP_COLS : 1u, part = blockIdx.x % KS, G = gridDim.x / KS, g = blockIdx.x / KS;
+  const uint32_t KS = lds ? KP_COLS : 1u, part = bid % KS, G = nblk / KS, g = bid / KS;
   const uint32_t w0 = part * (d.NWR / KS), w1 = w0 + d.NWR / KS;   // this workgroup's bitset words
   // the active list T entries per workgroup group at a time, interleaved over the groups (consecutive
   // ids, e.g. the round's joiners, go to different groups): the destinations of this kind are
@@ -522,21 +523,20 @@ __global__ __launch_bounds__(BIG ? 1024 : 256) void k_kp_group(Dev d, OutBuf ib,
 }
 
 // The groups under KP_BIG ids (KnownPeersRequest replies, small Join lists): a wave per destination,
-// in place on the row's bitset, the same arms-then-prologues order as k_kp_group.
-__global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, int32_t r_arg, OutBuf nb) {
-  const int32_t r = round_of(d, r_arg);
-  __shared__ uint32_t s_list[256], s_nl;
-  const uint32_t t = threadIdx.x, wv = t >> 6, l = lane();
-  {  // the next outbox of every local row: capacity = the wave's reservation, empty (was a copy + memset)
-    const uint32_t i = d.lo + blockIdx.x * blockDim.x + t;
-    if (i < d.hi) { nb.cap[i] = wc.bnd[i]; nb.cnt[i] = 0; }
-    if (blockIdx.x == 0 && t == 0) d.ctr[C_SLOW] = 0;   // k_proc_fast lists this wave's slow nodes afresh
-  }
+// in place on the row's bitset, the same arms-then-prologues order as the BIG groups.  (The body of
+// k_kp's last nblk workgroups.)
+__device__ __attribute__((always_inline)) inline void kp_small_body(const Dev& d, const OutBuf& ib, const WaveCtl& wc, int32_t r,
+                                                                   const OutBuf& nb, uint32_t bid, uint32_t nblk) {
+  __shared__ uint32_t s_list[1024], s_nl;
+  const uint32_t t = threadIdx.x, T = blockDim.x, nwv = T >> 6, wv = t >> 6, l = lane();
+  // the next outbox of every local row: capacity = the wave's reservation, empty (was a copy + memset)
+  for (uint32_t i = d.lo + bid * T + t; i < d.hi; i += nblk * T) { nb.cap[i] = wc.bnd[i]; nb.cnt[i] = 0; }
+  if (bid == 0 && t == 0) d.ctr[C_SLOW] = 0;             // the fast handlers list this wave's slow nodes afresh
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint8_t old = enc(r - SHARE_AGE, r), now = enc(r, r);
   const uint32_t kpb = (d.dbg & KB_DBG_KP_BIG_SMALL) ? 0u : KP_BIG;
-  for (uint32_t c0 = 0; c0 < nact; c0 += gridDim.x * 256) {
-    const uint32_t it = c0 + t * gridDim.x + blockIdx.x;   // interleaved over the workgroups
+  for (uint32_t c0 = 0; c0 < nact; c0 += nblk * T) {
+    const uint32_t it = c0 + t * nblk + bid;             // interleaved over the workgroups
     if (t == 0) s_nl = 0;
     __syncthreads();
     if (it < nact) {
@@ -545,7 +545,7 @@ __global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, 
     }
     __syncthreads();
     const uint32_t nl = s_nl;
-    for (uint32_t li = wv; li < nl; li += 4) {
+    for (uint32_t li = wv; li < nl; li += nwv) {
       const uint32_t i = s_list[li], nk = wc.kcnt[i], k0 = wc.koff[i];
       uint32_t* B = bits_of(d, i);
       uint8_t* rw = row_of(d, i);
@@ -596,6 +596,15 @@ __global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, 
   }
 }
 
+// The KnownPeers group of every destination of the wave in ONE launch: workgroups [0, nbig) serve the
+// BIG groups (KP_COLS per destination group, bitset in LDS), the rest the small groups (a wave per
+// destination) and set up the next outbox.  The two kinds never share a destination.
+__global__ __launch_bounds__(1024) void k_kp(Dev d, OutBuf ib, WaveCtl wc, int32_t r_arg, OutBuf nb, uint32_t nbig) {
+  const int32_t r = round_of(d, r_arg);
+  if (blockIdx.x < nbig) kp_group_body<true>(d, ib, wc, r, blockIdx.x, nbig);
+  else kp_small_body(d, ib, wc, r, nb, blockIdx.x - nbig, gridDim.x - nbig);
+}
+
 // ---- KnownPeersRequest oversize probe (:473-512, Q3) -----------------------------------------------
 // A KPR reply lists every fresh entry (Known, stamped within SHARE_AGE, not self, not the requester);
 // above capk entries it is lost at the receiver, so only its size matters.  The fresh set only grows
@@ -605,10 +614,11 @@ __global__ __launch_bounds__(256) void k_kp_small(Dev d, OutBuf ib, WaveCtl wc, 
 // takes its constant-time path.  A wave per node with a KPR delivery this wave, all of its log window
 // in flight at once (up to 8 x 64 entries per step); run by the small, high-occupancy k_sort_inbox
 // after its sorts, in front of the register-heavy k_proc.
-__device__ __attribute__((always_inline)) inline void kpr_probe(const Dev& d, const WaveCtl& wc, int32_t r) {
+__device__ __attribute__((always_inline)) inline void kpr_probe(const Dev& d, const WaveCtl& wc, int32_t r, uint32_t bid,
+                                                               uint32_t nblk) {
   const uint32_t nact = d.ctr[C_ACTIVE];
   const uint32_t nwv = blockDim.x >> 6, wv = threadIdx.x >> 6, l = lane();
-  for (uint32_t it = blockIdx.x * nwv + wv; it < nact; it += gridDim.x * nwv) {
+  for (uint32_t it = bid * nwv + wv; it < nact; it += nblk * nwv) {
     const uint32_t i = wc.active[it];
     if (!wc.bpay[i] || d.kpr_big[i] == r) continue;  // wave-uniform: no KPR, or already proven
     const uint8_t* rw = row_of(d, i);
@@ -647,16 +657,17 @@ __device__ __attribute__((always_inline)) inline void kpr_probe(const Dev& d, co
 // index, one workgroup per node, bitonic in LDS (up to SORT_MAX entries; longer ones keep the
 // selection path of k_proc)
 constexpr uint32_t SORT_MAX = 8192;
+constexpr uint32_t SORT_GROUPS = 256;      // k_sortfast workgroups that sort inboxes and run the KPR probe
 __device__ inline uint32_t sort_max(const Dev& d) { return (d.dbg & KB_DBG_PROC_UNSORTED) ? 64u : SORT_MAX; }
-__global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc, int32_t r_arg) {
-  const int32_t r = round_of(d, r_arg);
+__device__ __attribute__((always_inline)) inline void sort_body(const Dev& d, const WaveCtl& wc, int32_t r, uint32_t bid,
+                                                               uint32_t nblk) {
   __shared__ uint32_t v[SORT_MAX];
   __shared__ uint32_t s_list[1024], s_nl;
   const uint32_t nact = d.ctr[C_ACTIVE];
   // the active list 1024 entries per workgroup at a time, interleaved over the workgroups: its long
   // inboxes are listed in LDS by all threads at once
-  for (uint32_t c0 = 0; c0 < nact; c0 += gridDim.x * 1024) {
-  const uint32_t it = c0 + threadIdx.x * gridDim.x + blockIdx.x;
+  for (uint32_t c0 = 0; c0 < nact; c0 += nblk * 1024) {
+  const uint32_t it = c0 + threadIdx.x * nblk + bid;
   if (threadIdx.x == 0) s_nl = 0;
   __syncthreads();
   if (it < nact) {
@@ -689,7 +700,7 @@ __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc, int32_t 
     __syncthreads();
   }
   }
-  if (d.uniform) kpr_probe(d, wc, r);               // then the KPR oversize probe, wave per node
+  if (d.uniform) kpr_probe(d, wc, r, bid, nblk);     // then the KPR oversize probe, wave per node
 }
 
 // ---- the per-node in-order program for Ping / PingRequest / Ack / KnownPeersRequest ---------------
@@ -702,10 +713,10 @@ __global__ __launch_bounds__(1024) void k_sort_inbox(Dev d, WaveCtl wc, int32_t 
 // `slow` list for k_proc (same semantics: prologue :406-415, Ping :513-532, PingRequest :533-545,
 // Ack :418-447, maybe_sync :707-740).
 constexpr uint32_t FAST_MAX = 8;
-__global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, uint32_t* slow) {
-  const int32_t r = round_of(d, r_arg);
+__device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, const OutBuf& ib, const OutBuf& ob, const WaveCtl& wc,
+                                                               int32_t r, uint32_t* slow, uint32_t bid) {
   const uint32_t nact = d.ctr[C_ACTIVE];
-  const uint32_t it = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t it = bid * blockDim.x + threadIdx.x;
   const uint8_t now = enc(r, r);
   unsigned long long curovf = 0, over = 0;
   bool to_slow = false;
@@ -795,16 +806,16 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
     if (!to_slow) wave_ctr_clear(wc, i);              // done with this node for the wave
   }
   // the rest goes to k_proc: listed with one atomic per workgroup (the list counter is one word)
-  __shared__ uint32_t s_wn[4], s_wb[4];
+  __shared__ uint32_t s_wn[16], s_wb[16];
   const unsigned long long sm = __ballot(to_slow);
-  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
   if (lane() == 0) s_wn[wv] = (uint32_t)__popcll(sm);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t a = s_wn[0], b = s_wn[1], c = s_wn[2], e = s_wn[3], tot = a + b + c + e;
-    const uint32_t base = tot ? atomicAdd(&d.ctr[C_SLOW], tot) : 0u;
-    s_wb[0] = base; s_wb[1] = base + a; s_wb[2] = base + a + b; s_wb[3] = base + a + b + c;
-    (void)e;
+    uint32_t tot = 0;
+    for (uint32_t k = 0; k < nwv; ++k) tot += s_wn[k];
+    uint32_t base = tot ? atomicAdd(&d.ctr[C_SLOW], tot) : 0u;
+    for (uint32_t k = 0; k < nwv; ++k) { s_wb[k] = base; base += s_wn[k]; }
   }
   __syncthreads();
   if (to_slow) slow[s_wb[wv] + __popcll(sm & ((1ull << lane()) - 1ull))] = i;
@@ -813,6 +824,17 @@ __global__ __launch_bounds__(256) void k_proc_fast(Dev d, OutBuf ib, OutBuf ob, 
     const unsigned long long v[2] = {curovf, over};
     stat_add_n(d, idx, v);
   }
+}
+
+// Inbox sorts + KPR oversize probe (workgroups [0, nsort)) and the fast in-order handlers (the rest) in ONE
+// launch.  They touch disjoint nodes: the sorts take inboxes > 64 entries, the fast lane <= FAST_MAX; a
+// node with a KnownPeersRequest is fast only once the probe has proven its replies oversize (kpr_big = r,
+// written by the probe after its last read of that row), else it goes to k_proc, which reads the proof.
+__global__ __launch_bounds__(1024) void k_sortfast(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, uint32_t* slow,
+                                                   uint32_t nsort) {
+  const int32_t r = round_of(d, r_arg);
+  if (blockIdx.x < nsort) sort_body(d, wc, r, blockIdx.x, nsort);
+  else fast_body(d, ib, ob, wc, r, slow, blockIdx.x - nsort);
 }
 
 __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32_t* list) {
