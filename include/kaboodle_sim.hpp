@@ -61,7 +61,7 @@ class Mesh {
       check(kb_sim_set_identity(h_, id_, ident.data(), ident.size()), "kb_sim_set_identity");
     }
     uint32_t fingerprint() const { uint32_t f; check(kb_sim_fingerprint(h_, id_, &f), "kb_sim_fingerprint"); return f; }
-    std::vector<uint32_t> peers() const {                                               // :339
+    std::vector<uint32_t> peers() const {                                               // :339 (ids)
       size_t n = 0;
       check(kb_sim_peers(h_, id_, nullptr, 0, &n), "kb_sim_peers");
       std::vector<uint32_t> v(n);
@@ -69,6 +69,13 @@ class Mesh {
       v.resize(n);
       return v;
     }
+    // Kaboodle::peers as the reference returns it (:339-345): address -> identity bytes
+    std::vector<std::pair<std::string, std::vector<uint8_t>>> peers_with_identity() const {
+      std::vector<std::pair<std::string, std::vector<uint8_t>>> out;
+      for (uint32_t p : peers()) out.emplace_back(format_addr(p), identity_of(h_, p));
+      return out;
+    }
+    std::vector<uint8_t> identity() const { return identity_of(h_, id_); }
     std::vector<kb_peer_state> peer_states() const {                                   // :348
       size_t n = 0;
       check(kb_sim_peer_states(h_, id_, nullptr, 0, &n), "kb_sim_peer_states");
@@ -94,6 +101,12 @@ class Mesh {
       return e;
     }
    private:
+    static std::vector<uint8_t> identity_of(kb_sim* h, uint32_t id) {
+      uint8_t buf[32];
+      size_t len = 0;
+      check(kb_sim_identity(h, id, buf, sizeof buf, &len), "kb_sim_identity");
+      return std::vector<uint8_t>(buf, buf + len);
+    }
     kb_sim* h_;
     uint32_t id_;
   };

@@ -1048,6 +1048,14 @@ static int step_round(kb_sim* s) {
   const bool pb_hbm = (d.dbg & KB_DBG_PHASEB_HBM) != 0;
   if (s->nf > 2048 || (pb_hbm && s->nf)) klaunch(s, KI_BFAIL_PREP, k_bfail_prep, dim3((s->nf + 255) / 256), dim3(256), 0, (const BCast*)s->bfail, s->nf, s->bf_gid, s->bf_dep, d.ctr + C_PATHS);
   else if (s->nf) klaunch(s, KI_BFAIL_PREP, k_bfail_prep_lds, dim3(1), dim3(1024), 0, (const BCast*)s->bfail, s->nf, s->bf_gid, s->bf_dep);
+  if (s->debug_waves && s->nf) {                     // KB_DEBUG_WAVES: broadcast list shape
+    std::vector<uint8_t> dep(s->nf);
+    HIPCHK(hipMemcpyAsync(dep.data(), s->bf_dep, s->nf, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    size_t nd = 0;
+    for (uint8_t x : dep) nd += x != 0;
+    fprintf(stderr, "[kb] round %d broadcasts: Failed %u (sender named earlier: %zu), Join %u\n", r, s->nf, nd, s->nj);
+  }
   {
     // the row pass (broadcast phase + A3 candidates), persistent waves; broadcast lists staged in LDS
     // once per workgroup when they fit.  Its events are taken by its own dispatch packet
