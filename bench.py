@@ -30,7 +30,9 @@ Also reported, on the same JSON line:
                 launch from the rocprofv3 PMC summary committed under profiles/ for this exact command
                 (FETCH_SIZE x2 per the gfx950 correction + WRITE_SIZE, timed rounds only), else null;
   cpu_baseline  the CPU oracle (oracle/, OpenMP build, same semantics and seeds) on a bounded sample of
-                the same workload, on rank 0 only;
+                the same workload, on rank 0 only; `single_thread`: the same oracle on one thread for the
+                rounds that follow;
+  seeds         seeds 2 and 3 of the same workload (SURVEY.md §8(d)), timed the same way (N = 1);
   convergence   after the timed rounds faults stop (fault_end_round); untimed rounds continue until every
                 live peer's fingerprint equals the fingerprint of the true live set (or a cap).
 """
@@ -67,6 +69,8 @@ def parse():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--conv-cap", type=int, default=100, help="max untimed quiescent rounds for convergence")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU baseline sample budget")
+    ap.add_argument("--cpu1-seconds", type=float, default=15.0, help="single-thread CPU sample budget (0: skip)")
+    ap.add_argument("--seeds", default="2,3", help="extra seeds of the same workload timed the same way (N = 1)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-latency", action="store_true", help="do not keep PeerInfo.latency (track_latency 0)")
     ap.add_argument("--no-conv", action="store_true")
@@ -150,8 +154,9 @@ def round_model_bytes(s0: dict, s1: dict, alive_mean: float, steps: int) -> floa
     return (alive_mean * alive_mean * steps + 32.0 * msgs + 4.0 * ids) / steps
 
 
-def cpu_baseline(cfg, budget_s: float, nodes: int) -> dict:
-    """The OpenMP oracle on a bounded sample of the same workload (rank 0, N=1 only)."""
+def cpu_baseline(cfg, budget_s: float, nodes: int, budget_1t: float) -> dict:
+    """The OpenMP oracle on a bounded sample of the same workload (rank 0, N=1 only); then the same oracle
+    restricted to one thread on the rounds that follow (BASELINE.md's single-thread CPU figure)."""
     import ctypes as C
     from kaboodle_amd._ffi import Sim
     so = os.path.join(ROOT, "oracle", "_build", "libkb_oracle_omp.so")
@@ -162,20 +167,31 @@ def cpu_baseline(cfg, budget_s: float, nodes: int) -> dict:
     lib = SimLib(so, "kbo_")
     lib.lib.kbo_num_threads.restype = C.c_int
     cores = int(lib.lib.kbo_num_threads())
-    with Sim(lib, cfg) as o:
-        o.step(1)                                # one warmup round (first touch of the dense table)
+
+    def sample(o, budget, cap):
         t0 = time.perf_counter()
         rounds, alive_sum = 0, 0
         while True:
             o.step(1)
             rounds += 1
             alive_sum += o.stats()["alive"]
-            if time.perf_counter() - t0 >= budget_s or rounds >= 200:
-                break
-        dt = time.perf_counter() - t0
+            if time.perf_counter() - t0 >= budget or rounds >= cap:
+                return rounds, alive_sum, time.perf_counter() - t0
+
+    with Sim(lib, cfg) as o:
+        o.step(1)                                # one warmup round (first touch of the dense table)
+        rounds, alive_sum, dt = sample(o, budget_s, 200)
+        one = None
+        if budget_1t > 0:
+            lib.lib.kbo_set_num_threads(1)
+            r1, a1, dt1 = sample(o, budget_1t, 50)
+            lib.lib.kbo_set_num_threads(cores)
+            one = {"value": a1 / dt1, "unit": "peer-rounds/s", "cores": 1,
+                   "sample": f"the next {r1} rounds of the same run on one thread ({dt1:.1f} s)"}
     return {"value": alive_sum / dt, "unit": "peer-rounds/s", "cores": cores, "kind": "port",
             "sample": f"{rounds} rounds of the same {nodes}-peer workload after 1 warmup round "
-                      f"(oracle/kb_oracle.c, OpenMP over peers, {dt:.1f} s)"}
+                      f"(oracle/kb_oracle.c, OpenMP over peers, {dt:.1f} s)",
+            "single_thread": one}
 
 
 def sharded(a, world: int) -> bool:
@@ -377,7 +393,7 @@ def main() -> int:
         }
         if world == 1 and not a.no_cpu:
             ccfg = SimConfig(**{**cfg.__dict__, "device": -1})
-            out["cpu_baseline"] = cpu_baseline(ccfg, a.cpu_seconds, a.nodes)
+            out["cpu_baseline"] = cpu_baseline(ccfg, a.cpu_seconds, a.nodes, a.cpu1_seconds)
         else:
             out["cpu_baseline"] = None
     mesh.close()
@@ -398,8 +414,23 @@ def main() -> int:
                 "round_model_frac": round(rb2 / (dt2 / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "agree_frac_at_fault_end": round(s21["agree"] / max(s21["alive"], 1), 4),
                 "workload_full_tail": committed_tail(f"configs[2]: {a.nodes} peers", "socket_faithful")}}
+    seeds = None
+    if world == 1 and a.seeds:
+        # seeds 2 and 3 of the same synthetic workload, same K and W, each its own mesh
+        import copy
+        seeds = {}
+        for sd in (int(x) for x in a.seeds.split(",") if x.strip()):
+            b = copy.copy(a)
+            b.seed = sd
+            with kaboodle_amd.Mesh(rank_config(b, rank, world, local)) as m3:
+                m3.step(a.warmup)
+                torch.cuda.synchronize()
+                dt3, alive3, _, s31 = timed_rounds(m3, a.steps, world)
+                seeds[str(sd)] = {"value": alive3 / dt3, "ms_per_step": dt3 / a.steps * 1e3,
+                                  "agree_frac_at_fault_end": round(s31["agree"] / max(s31["alive"], 1), 4)}
     if out is not None:
         out["modes"] = modes
+        out["seeds"] = seeds
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1178,3 +1178,11 @@ int kbo_num_threads(void) {
   return 1;
 #endif
 }
+/* bench.py's single-thread figure: the OpenMP build restricted to n threads for the calls that follow */
+void kbo_set_num_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+#else
+  (void)n;
+#endif
+}
