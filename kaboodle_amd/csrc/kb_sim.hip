@@ -944,9 +944,16 @@ static int launch_waves(kb_sim* s, int32_t rk) {
       fprintf(stderr, "[kb] round %d wave %u: in-order msgs %llu, max inbox %u (node %u), inboxes > 64: %u\n", r, w,
               (unsigned long long)sum, mx, arg, big);
     }
-    if (!s->xf) klaunch(s, KI_SCATTER, k_scatter, dim3(gnode), dim3(tb), 0, d, ob, s->wc);
-    else if (nrecv) klaunch(s, KI_SCATTER_FLAT, k_scatter_flat, dim3((nrecv + 255) / 256), dim3(256), 0, ib, s->wc, nrecv);
-    if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
+    // (the inbox placement, and in PROBE_GROUPS more workgroups the KPR oversize probe)
+    if (!s->xf) klaunch(s, KI_SCATTER, k_scatter, dim3(gnode + PROBE_GROUPS), dim3(tb), 0, d, ob, s->wc, r, gnode);
+    else if (nrecv) {
+      const uint32_t nsc = (nrecv + 255) / 256;
+      klaunch(s, KI_SCATTER_FLAT, k_scatter_flat, dim3(nsc + PROBE_GROUPS), dim3(256), 0, d, ib, s->wc, nrecv, r, nsc);
+    }
+    if (s->debug_waves) {
+      HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
+      HIPCHK(hipMemsetAsync(d.ctr + C_DBG_SLOW_LONG, 0, 20, st));
+    }
     {  // the KnownPeers groups: BIG ones KP_COLS workgroups per destination group (one per column part),
        // then the small ones (a wave per destination), which also set up nb.cap / nb.cnt
       const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
@@ -969,6 +976,12 @@ static int launch_waves(kb_sim* s, int32_t rk) {
       fprintf(stderr, "[kb] round %d wave %u: k_proc nodes %u, prologue inserts %u, fingerprint refreshes %u (max per "
               "node %u), KPR scans %u (log entries %u), incremental bases %u\n", r, w, slow, dbg[0], dbg[1], dbg[2], dbg[3],
               dbg[4], dbg[5]);
+      if (d.dev & 256) {
+        uint32_t why[5];
+        HIPCHK(hipMemcpy(why, d.ctr + C_DBG_SLOW_LONG, 20, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[kb] round %d wave %u: to k_proc because inbox > %u: %u, sender not a member: %u, fingerprint stale: %u, "
+                "KPR not proven oversize: %u, other: %u\n", r, w, FAST_MAX, why[0], why[1], why[2], why[3], why[4]);
+      }
       if (d.dev & 128)
         fprintf(stderr, "[kb] round %d wave %u: k_kp_group BIG workgroup-destinations %u, messages %u: stage+arms %.1f us, "
                 "prologues %.1f, write-back+refold %.1f (sums), max total %.1f\n", r, w, dbg[10], dbg[12], dbg[6] * 0.01,
@@ -1140,7 +1153,10 @@ static int step_round(kb_sim* s) {
       // a wave per responder where its LDS slice fits (4 responders per 64 KB workgroup), else a workgroup
       const size_t wlds = 16ull * rwave_words(d.NWR, s->W / 256);
       const bool wave_on = wlds <= 65536 && !(d.dbg & KB_DBG_RESP_HBM);
-      if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
+      if (s->debug_waves) {
+      HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
+      HIPCHK(hipMemsetAsync(d.ctr + C_DBG_SLOW_LONG, 0, 20, st));
+    }
       if (wave_on) {                                   // timed by events on its own dispatch packet
         klaunch(s, KI_RESP_WAVE, k_resp_wave, dim3(std::min<uint32_t>((resp_nodes + 3) / 4, 4096)), dim3(256), (uint32_t)wlds, d,
                 pb, (const uint32_t*)s->resp_nodes, (const uint32_t*)(s->scan_tot + 4), o0, r);

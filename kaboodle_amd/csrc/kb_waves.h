@@ -114,10 +114,66 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
   }
 }
 
+// ---- KnownPeersRequest oversize probe (:473-512, Q3) -----------------------------------------------
+// A KPR reply lists every fresh entry (Known, stamped within SHARE_AGE, not self, not the requester);
+// above capk entries it is lost at the receiver, so only its size matters.  The fresh set only grows
+// while a round's waves run (stamps rise to now; removals happen before the waves), so counting it
+// once, as it stands when the wave starts, proves every reply of the rest of the round oversize as
+// soon as the count exceeds capk + 1 (one requester excluded): kpr_big = r, and k_proc's KPR handler
+// takes its constant-time path.  A wave per node with a KPR delivery this wave, all of its log window
+// in flight at once (up to 8 x 64 entries per step), in extra workgroups of the k_scatter launch: no
+// kernel writes a row while the inboxes are built (a row read while a prologue moves a stamp to
+// Known(now) and logs it could count that peer twice), and the proof is in place before the fast
+// handlers of k_sortfast decide.  The KnownPeers prologues of k_kp in between only add fresh entries.
+constexpr uint32_t PROBE_GROUPS = 512;     // workgroups of the scatter launch that run the probe
+__device__ __attribute__((always_inline)) inline void kpr_probe(const Dev& d, const WaveCtl& wc, int32_t r, uint32_t bid,
+                                                               uint32_t nblk) {
+  const uint32_t nact = d.ctr[C_ACTIVE];
+  const uint32_t nwv = blockDim.x >> 6, wv = threadIdx.x >> 6, l = lane();
+  for (uint32_t it = bid * nwv + wv; it < nact; it += nblk * nwv) {
+    const uint32_t i = wc.active[it];
+    if (!wc.bpay[i] || d.kpr_big[i] == r) continue;  // wave-uniform: no KPR, or already proven
+    const uint8_t* rw = row_of(d, i);
+    const uint32_t* bw = bits_of(d, i);
+    const uint32_t fn = d.flog_n[i], ws = log_window_start(d, i, r);
+    const uint32_t k_lo = fn - ws <= LOGCAP ? ws : fn - LOGCAP;
+    uint32_t total = 0;
+    constexpr int PB = 8;
+    for (uint32_t k0 = k_lo; k0 < fn && total <= d.capk + 1; k0 += 64 * PB) {
+      uint32_t ev[PB], wv4[PB], bv[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const uint32_t k = k0 + 64u * u + l;
+        ev[u] = k < fn ? d.flog[(size_t)i * LOGCAP + (k & (LOGCAP - 1))] : LOG_INVALID;
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const uint32_t j = ev[u] == LOG_INVALID ? i : ev[u] >> 8;
+        wv4[u] = bw[j >> 5];
+        bv[u] = rw[j];
+      }
+      uint32_t c = 0;
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const uint32_t e = ev[u], j = e >> 8;
+        c += e != LOG_INVALID && j != i && r - log_round(e, r) < SHARE_AGE && ((wv4[u] >> (j & 31)) & 1u) &&
+             bv[u] == enc(log_round(e, r), r);
+      }
+      total += wave_sum(c);
+    }
+    if (total > d.capk + 1 && l == 0) d.kpr_big[i] = r;
+  }
+}
+
+
 // KnownPeers records are placed in two passes (their order within a destination's group is free: the
 // group commutes): count per destination in LDS, reserve each destination's block once,
 // then place; in-order records take their global cursor directly (in-order inboxes are sorted later).
-__global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc) {
+__global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc, int32_t r_arg, uint32_t nscat) {
+  if (blockIdx.x >= nscat) {                           // the KPR oversize probe (workgroups past the scatter's)
+    if (d.uniform) kpr_probe(d, wc, round_of(d, r_arg), blockIdx.x - nscat, gridDim.x - nscat);
+    return;
+  }
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
   __shared__ uint32_t s_kd[KAGG], s_kc[KAGG], s_kb[KAGG];
   const uint32_t wv = threadIdx.x >> 6, l = lane();
@@ -292,7 +348,11 @@ __global__ __launch_bounds__(256) void k_route_recv(Dev d, OutBuf ib, WaveCtl wc
     }
   }
 }
-__global__ void k_scatter_flat(OutBuf ib, WaveCtl wc, uint32_t n) {
+__global__ void k_scatter_flat(Dev d, OutBuf ib, WaveCtl wc, uint32_t n, int32_t r, uint32_t nscat) {
+  if (blockIdx.x >= nscat) {                           // the KPR oversize probe, as in k_scatter
+    if (d.uniform) kpr_probe(d, wc, r, blockIdx.x - nscat, gridDim.x - nscat);
+    return;
+  }
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n) return;
   const uint8_t st = wc.status[g];
@@ -605,54 +665,6 @@ __global__ __launch_bounds__(1024) void k_kp(Dev d, OutBuf ib, WaveCtl wc, int32
   else kp_small_body(d, ib, wc, r, nb, blockIdx.x - nbig, gridDim.x - nbig);
 }
 
-// ---- KnownPeersRequest oversize probe (:473-512, Q3) -----------------------------------------------
-// A KPR reply lists every fresh entry (Known, stamped within SHARE_AGE, not self, not the requester);
-// above capk entries it is lost at the receiver, so only its size matters.  The fresh set only grows
-// while a round's waves run (stamps rise to now; removals happen before the waves), so counting it
-// once, as it stands when the wave starts, proves every reply of the rest of the round oversize as
-// soon as the count exceeds capk + 1 (one requester excluded): kpr_big = r, and k_proc's KPR handler
-// takes its constant-time path.  A wave per node with a KPR delivery this wave, all of its log window
-// in flight at once (up to 8 x 64 entries per step); run by the small, high-occupancy k_sort_inbox
-// after its sorts, in front of the register-heavy k_proc.
-__device__ __attribute__((always_inline)) inline void kpr_probe(const Dev& d, const WaveCtl& wc, int32_t r, uint32_t bid,
-                                                               uint32_t nblk) {
-  const uint32_t nact = d.ctr[C_ACTIVE];
-  const uint32_t nwv = blockDim.x >> 6, wv = threadIdx.x >> 6, l = lane();
-  for (uint32_t it = bid * nwv + wv; it < nact; it += nblk * nwv) {
-    const uint32_t i = wc.active[it];
-    if (!wc.bpay[i] || d.kpr_big[i] == r) continue;  // wave-uniform: no KPR, or already proven
-    const uint8_t* rw = row_of(d, i);
-    const uint32_t* bw = bits_of(d, i);
-    const uint32_t fn = d.flog_n[i], ws = log_window_start(d, i, r);
-    const uint32_t k_lo = fn - ws <= LOGCAP ? ws : fn - LOGCAP;
-    uint32_t total = 0;
-    constexpr int PB = 8;
-    for (uint32_t k0 = k_lo; k0 < fn && total <= d.capk + 1; k0 += 64 * PB) {
-      uint32_t ev[PB], wv4[PB], bv[PB];
-#pragma unroll
-      for (int u = 0; u < PB; ++u) {
-        const uint32_t k = k0 + 64u * u + l;
-        ev[u] = k < fn ? d.flog[(size_t)i * LOGCAP + (k & (LOGCAP - 1))] : LOG_INVALID;
-      }
-#pragma unroll
-      for (int u = 0; u < PB; ++u) {
-        const uint32_t j = ev[u] == LOG_INVALID ? i : ev[u] >> 8;
-        wv4[u] = bw[j >> 5];
-        bv[u] = rw[j];
-      }
-      uint32_t c = 0;
-#pragma unroll
-      for (int u = 0; u < PB; ++u) {
-        const uint32_t e = ev[u], j = e >> 8;
-        c += e != LOG_INVALID && j != i && r - log_round(e, r) < SHARE_AGE && ((wv4[u] >> (j & 31)) & 1u) &&
-             bv[u] == enc(log_round(e, r), r);
-      }
-      total += wave_sum(c);
-    }
-    if (total > d.capk + 1 && l == 0) d.kpr_big[i] = r;
-  }
-}
-
 // ---- inboxes longer than one wave: sorted into canonical (sender, seq) order = ascending outbox
 // index, one workgroup per node, bitonic in LDS (up to SORT_MAX entries; longer ones keep the
 // selection path of k_proc)
@@ -700,13 +712,12 @@ __device__ __attribute__((always_inline)) inline void sort_body(const Dev& d, co
     __syncthreads();
   }
   }
-  if (d.uniform) kpr_probe(d, wc, r, bid, nblk);     // then the KPR oversize probe, wave per node
 }
 
 // ---- the per-node in-order program for Ping / PingRequest / Ack / KnownPeersRequest ---------------
 // ---- fast lane of the in-order handlers: a THREAD per node --------------------------------------
 // The common inbox — at most FAST_MAX Ping / PingRequest / Ack envelopes (and KnownPeersRequests
-// once kpr_probe (in k_sort_inbox) has proven this round's replies oversize), every sender already a member, the
+// once kpr_probe (run with k_scatter) has proven this round's replies oversize), every sender already a member, the
 // node's fingerprint current — changes no membership, so no fingerprint work: the handlers reduce
 // to stamp/log/slot updates and emissions.  Such nodes are handled here, one per
 // thread, in canonical (sender, seq) order; every other node with in-order deliveries goes to the
@@ -745,6 +756,19 @@ __device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, co
       }
     }
     to_slow = icnt && !fast;
+    if (to_slow && (d.dev & 256)) {                   // why nodes go to k_proc (KB_DEV=256, KB_DEBUG_WAVES)
+      bool kpr = false, nonmem = false;
+      if (icnt <= FAST_MAX) {
+        const uint32_t* bw = bits_of(d, i);
+        for (uint32_t k = 0; k < icnt; ++k) {
+          const Msg m = ib.msgs[wc.inbox[wc.in_off[i] + k]];
+          kpr |= m.kind == K_KPR && d.kpr_big[i] != r;
+          nonmem |= !((bw[m.sender >> 5] >> (m.sender & 31)) & 1u);
+        }
+      }
+      atomicAdd(&d.ctr[icnt > FAST_MAX ? C_DBG_SLOW_LONG : nonmem ? C_DBG_SLOW_NONMEM : d.dirty[i] ? C_DBG_SLOW_DIRTY
+                                                                                                : kpr ? C_DBG_SLOW_KPR : C_DBG_SLOW_OTHER], 1u);
+    }
     if (fast) {
       const uint32_t n = d.n[i], fp = d.fp[i];
       const uint32_t ob_cap = ob.cap[i], ob_off = ob.off[i];   // this node's outbox region, loaded once
@@ -885,7 +909,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
     // header + slot tables read and written back, inbox index + record of every message
     w_bytes += 2 * (28 + sizeof(Susp) * SLOTS + sizeof(Cur) * CSLOTS) + (4 + sizeof(Msg)) * (uint64_t)icnt;
     // canonical order = ascending outbox index = (sender, seq): one wave sorts <= 64 entries in
-    // registers; k_sort_inbox has sorted longer inboxes up to SORT_MAX in place
+    // registers; k_sortfast has sorted longer inboxes up to SORT_MAX in place
     uint32_t mine = l < icnt ? wc.inbox[ibase + l] : 0xFFFFFFFFu;
     const bool small = icnt <= 64, sorted = icnt <= sort_max(d);
     if (small) {
