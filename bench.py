@@ -54,7 +54,7 @@ KT_ROUND = 1                    # kb_sim_kernel_time kind of the whole round
 CHURN_RESERVE = 8192            # fresh ids kept for churn joins: capacity does not depend on --steps
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--no-modes", action="store_true", help="skip the socket_faithful line (N = 1)")
     ap.add_argument("--failed-mode", choices=("sim_sender", "socket_faithful"), default="sim_sender",
                     help="Q1: Failed(p) honoured (sim_sender, the headline) or never (socket_faithful)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def lib_sha16() -> str:

@@ -1,10 +1,11 @@
 """Full-size parity on an MI355X: the HIP library against the OpenMP oracle at the sizes the bench and the
 wide-row configs run, through the C ABI.
 
-- configs[2] exactly as bench.py runs it (65,536 peers, capacity 69,632, 1 % loss, 0.1 %/round churn,
-  faults until round 25) over the whole benched horizon (25 faulty rounds) plus a 10-round quiet tail,
-  every round: counters, every fingerprint and per-node scalar, and sampled whole rows, suspect and
-  curious tables and peer_states (src/kaboodle.rs:746-779 per round).
+- configs[2] exactly as the driver's `bench.py --steps 20 --warmup 5` runs it (65,536 peers, capacity
+  73,728, 1 % loss, 0.1 %/round churn, faults until round 25, the latency EWMA on; tests/test_bench.py
+  checks this config against bench.rank_config) over the whole benched horizon (25 faulty rounds) plus a
+  10-round quiet tail, every round: counters, every fingerprint and per-node scalar, and sampled whole
+  rows, suspect and curious tables and peer_states with latency (src/kaboodle.rs:746-779, :789-817).
 - a 140K-id mesh: rows wider than RESP_LDS_W = 131,072 ids, so Join responses take the HBM-scratch
   path a >= 1M-id mesh takes (kb_sim.hip, the W > RESP_LDS_W branch), unsharded and as 8 row shards.
 - configs[4] scaled to one GPU: 65,536 peers, 5 % loss, a two-way partition, then the heal by injected
@@ -20,8 +21,8 @@ from kaboodle_amd._ffi import KB_INIT_CONVERGED, Sim, SimConfig
 
 pytestmark = pytest.mark.gpu
 
-BENCH_CFG = SimConfig(capacity=65536 + 4096, initial_nodes=65536, init_mode=KB_INIT_CONVERGED, loss=0.01,
-                      churn=0.001, fault_end_round=25, seed=1)     # bench.rank_config at --steps 20 --warmup 5
+BENCH_CFG = SimConfig(capacity=65536 + 8192, initial_nodes=65536, init_mode=KB_INIT_CONVERGED, loss=0.01,
+                      churn=0.001, fault_end_round=25, seed=1, track_latency=1)   # bench.rank_config, --steps 20 --warmup 5
 
 
 class Pair:
