@@ -259,6 +259,7 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
   const uint32_t a0 = p & ~15u;
   uint32_t K[5] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
   uint32_t anc = 0, nbytes = 0;                   // ancient candidates in the scanned address-order prefix
+  bool fast = false;                              // out[] already holds the five (first-five-ancient case)
   // chunk order: ids [a0, W) then [0, a0), 1024 ids per chunk; the first step loads one chunk (it
   // usually decides), later steps A3_U chunks at once (rows with few ancient stamps: recent joiners)
   constexpr int A3_U = 4;
@@ -307,7 +308,25 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
       uint32_t am = cm & (eqmask4(x.x, ST_ANCIENT) | (eqmask4(x.y, ST_ANCIENT) << 4) | (eqmask4(x.z, ST_ANCIENT) << 8) |
                           (eqmask4(x.w, ST_ANCIENT) << 12));
       if (!wr[u] && j < p) am &= p - j >= 16 ? 0u : ~((1u << (p - j)) - 1u);   // [a0, p) comes last in order
-      anc += wave_sum(__popc(am));
+      const uint32_t pc = __popc(am), ta = wave_sum(pc);
+      if (u == 0 && anc == 0 && ta >= (uint32_t)NUM_CANDIDATES) {   // (first chunk of a step)
+        // (the usual case) no ancient candidate before this chunk and at least five in it: every earlier
+        // key is newer, so the five oldest are this chunk's first five ancient members in address order
+        // (= rotated order inside a chunk) — taken by a prefix count, no per-lane top-5 and no merge
+        const uint32_t pre = wave_excl(pc);
+#pragma unroll
+        for (uint32_t q = 0; q < (uint32_t)NUM_CANDIDATES; ++q) {
+          const bool owns = pre <= q && q < pre + pc;    // the lane holding the q-th ancient member
+          const uint32_t jj = j + select_in_word(am, owns ? q - pre : 0u);
+          const uint32_t key = ((uint32_t)ST_ANCIENT << 24) | (jj >= p ? jj - p : jj + C - p);
+          out[q] = (uint32_t)__builtin_amdgcn_readlane((int)key, __ffsll((long long)__ballot(owns)) - 1);
+        }
+        anc = ta;
+        fast = true;
+        done = true;
+        continue;
+      }
+      anc += ta;
       for (uint32_t m = cm; m; m &= m - 1) {
         const uint32_t t = __ffs(m) - 1, jj = j + t;
         const uint32_t word = (t & 8) ? ((t & 4) ? x.w : x.z) : ((t & 4) ? x.y : x.x);
@@ -319,6 +338,7 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
     if (done || (d.dev & 1)) break;               // dev 1: first chunk only (timing experiments)
   }
   a3c.x += 1; a3c.y += (next != a0 + 1024 || wrapped) ? 1u : 0u;   // scan depth (kb_sim_debug_counters)
+  if (fast) return wave_sum(nbytes);
 #pragma unroll
   for (int q = 0; q < 5; ++q) {                     // merge the lanes' lists (keys are distinct)
     const uint32_t mn = wave_min(K[0]);
@@ -329,7 +349,7 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
 }
 
 template <bool LDSB>
-__global__ __launch_bounds__(512) void k_rowpass(Dev d, PhaseB pb, RowOut ro, int32_t r, uint32_t lf, uint32_t lj) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_rowpass(Dev d, PhaseB pb, RowOut ro, int32_t r, uint32_t lf, uint32_t lj) {
   extern __shared__ uint32_t pb_dyn[];
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wv = threadIdx.x >> 6;
