@@ -111,17 +111,37 @@ __device__ inline int32_t log_round(uint32_t e, int32_t r) { return r - (int32_t
 __device__ inline uint32_t log_window_start(const Dev& d, uint32_t i, int32_t r) {
   return r >= SHARE_AGE - 1 ? d.fstart[(size_t)i * 16 + ((uint32_t)(r - (SHARE_AGE - 1)) & 15u)] : 0u;
 }
-// copy n 16-byte words global -> LDS with `lanes` cooperating threads (index t), 8 loads in flight each
+// copy n 16-byte words global -> LDS with `lanes` cooperating threads (index t, waves of consecutive t),
+// as LDS-DMA loads (global_load_lds_dwordx4: no VGPR destination, every load of the copy in flight at
+// once), then one vmcnt(0).  Register staging had let the compiler sink each load into its guarded store
+// and wait for it there — one HBM round trip per 16 B per lane.  The LDS destination of one wave's load
+// is its base + 16 B × lane, which is the layout of consecutive words.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void glb_void_t;
 __device__ __attribute__((always_inline)) inline void stage16(uint4* dst, const uint4* src, uint32_t n, uint32_t t,
                                                              uint32_t lanes) {
-  constexpr int U = 8;                                  // independent loads in flight per lane, then the stores
-  for (uint32_t w0 = t; w0 < n; w0 += lanes * U) {
+  const uint32_t wb = t - lane();                        // the wave's first word of each pass
+  for (uint32_t w0 = 0; wb + w0 < n; w0 += lanes) {
+    if (t + w0 < n)
+      __builtin_amdgcn_global_load_lds((glb_void_t*)(src + t + w0), (lds_void_t*)(dst + wb + w0), 16, 0, 0);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0F70);                    // vmcnt(0): the copies have landed
+  asm volatile("" ::: "memory");
+}
+// the same copy into global memory (a scratch destination): register staged, full groups of 8 loads with
+// no condition between the loads and their stores
+__device__ __attribute__((always_inline)) inline void copy16(uint4* dst, const uint4* src, uint32_t n, uint32_t t,
+                                                            uint32_t lanes) {
+  constexpr int U = 8;
+  uint32_t w0 = t;
+  for (; w0 + lanes * (U - 1) < n; w0 += lanes * U) {
     uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) { const uint32_t w = w0 + lanes * u; v[u] = src[w < n ? w : w0]; }
+    for (int u = 0; u < U; ++u) v[u] = src[w0 + lanes * u];
 #pragma unroll
-    for (int u = 0; u < U; ++u) { const uint32_t w = w0 + lanes * u; if (w < n) dst[w] = v[u]; }
+    for (int u = 0; u < U; ++u) dst[w0 + lanes * u] = v[u];
   }
+  for (; w0 < n; w0 += lanes) dst[w0] = src[w0];
 }
 // hand-off to the host through mapped pinned memory: the values, a system-scope release, then the
 // sequence number the host polls for (one thread)

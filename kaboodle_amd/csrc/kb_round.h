@@ -832,9 +832,9 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
     uint32_t bc = 0, last = 0;
     uint4* S4 = reinterpret_cast<uint4*>(S);
+    stage16(S4, B4, NW / 4, l, 64);                         // the row into LDS, every load in flight
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) {
-      const uint4 q0 = B4[2 * k], q1 = B4[2 * k + 1];
-      S4[2 * k] = q0; S4[2 * k + 1] = q1;
+      const uint4 q0 = S4[2 * k], q1 = S4[2 * k + 1];
       const uint32_t c = __popc(q0.x) + __popc(q0.y) + __popc(q0.z) + __popc(q0.w) + __popc(q1.x) + __popc(q1.y) +
                          __popc(q1.z) + __popc(q1.w);
       BP[k] = c; bc += c;
@@ -932,7 +932,8 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
     uint32_t nnew = 0;
     for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
     if (resp_by_wave(d, i, nnew, wave_on)) continue;        // uniform: served by k_resp_wave
-    stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(bits_of(d, i)), NW / 4, t, T);
+    if (gscratch) copy16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(bits_of(d, i)), NW / 4, t, T);
+    else stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(bits_of(d, i)), NW / 4, t, T);
     __syncthreads();
     const uint32_t nB = block_prefix(B, BP, NB, s_red);
     const bool jl = nnew <= RESP_JCAP;

@@ -1153,10 +1153,7 @@ static int step_round(kb_sim* s) {
       // a wave per responder where its LDS slice fits (4 responders per 64 KB workgroup), else a workgroup
       const size_t wlds = 16ull * rwave_words(d.NWR, s->W / 256);
       const bool wave_on = wlds <= 65536 && !(d.dbg & KB_DBG_RESP_HBM);
-      if (s->debug_waves) {
-      HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
-      HIPCHK(hipMemsetAsync(d.ctr + C_DBG_SLOW_LONG, 0, 20, st));
-    }
+      if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
       if (wave_on) {                                   // timed by events on its own dispatch packet
         klaunch(s, KI_RESP_WAVE, k_resp_wave, dim3(std::min<uint32_t>((resp_nodes + 3) / 4, 4096)), dim3(256), (uint32_t)wlds, d,
                 pb, (const uint32_t*)s->resp_nodes, (const uint32_t*)(s->scan_tot + 4), o0, r);
