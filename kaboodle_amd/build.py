@@ -27,7 +27,8 @@ def needs_build() -> bool:
 def build(force: bool = False) -> str:
     if force or needs_build():
         hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-        cmd = [hipcc, f"--offload-arch={ARCH}", *FLAGS, "-o", OUT + ".tmp", SRC]
+        extra = os.environ.get("KB_EXTRA_FLAGS", "").split()   # e.g. -DKB_RP_PROF (dev profiling builds)
+        cmd = [hipcc, f"--offload-arch={ARCH}", *FLAGS, *extra, "-o", OUT + ".tmp", SRC]
         subprocess.run(cmd, check=True)
         os.replace(OUT + ".tmp", OUT)
     return OUT

@@ -382,7 +382,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
   // address atomics from every node would serialise in L2 and stall the waves that wait on them)
   unsigned long long w_lost = 0, w_removed = 0, w_resp = 0, w_nodes = 0, w_bytes = 0;
   uint3 a3c = make_uint3(0, 0, 0);
+  // phase timing (a build with -DKB_RP_PROF, run with KB_DEBUG_WAVES=1 KB_DEV=2048): wall-clock ticks per
+  // phase summed in registers, added once per workgroup at the end; compiled out otherwise (its registers
+  // would cost the pass spills)
+#ifdef KB_RP_PROF
+  const bool prof = (d.dev & 2048) != 0;
+  uint64_t tph[5] = {0, 0, 0, 0, 0}, tmark = 0;
+  auto tick = [&](int k) __attribute__((always_inline)) {
+    if (prof) { const uint64_t t = wall_clock64(); if (k >= 0) tph[k] += t - tmark; tmark = t; }
+  };
+#else
+  auto tick = [](int) __attribute__((always_inline)) {};
+#endif
   for (uint32_t i = d.lo + blockIdx.x * wpb + wv; i < d.hi; i += gridDim.x * wpb) {
+    tick(-1);
     // the node's header loads are issued together, ahead of the bitset staging (one memory round trip
     // for all of them instead of one per dependent use)
     const uint8_t alive = d.alive[i];
@@ -397,6 +410,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     uint32_t* gB = bits_of(d, i);
     uint32_t* B = LDSB ? pb_dyn + (size_t)wv * d.NWR : gB;
     if (LDSB) { stage16(reinterpret_cast<uint4*>(B), reinterpret_cast<const uint4*>(gB), d.NWR / 4, l, 64); w_bytes += 4ull * d.NWR; }
+    tick(0);
     unsigned long long segs = 0;
     uint32_t nresp = 0;
     if (sr < r) {                                     // ---- (1) broadcast phase ----
@@ -469,6 +483,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
         if (!LDSB) { __builtin_amdgcn_s_waitcnt(0); }
         __builtin_amdgcn_wave_barrier();
       }
+      tick(1);
       removed_cnt = wave_sum(removed_cnt);
       n -= removed_cnt;
       if (!LDSB) { __builtin_amdgcn_s_waitcnt(0); }
@@ -544,10 +559,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
     }
     wait_lds();
     __builtin_amdgcn_wave_barrier();
+    tick(2);
     // ---- (2) A3 candidates ----
     uint32_t top[5];
     w_bytes += a3_scan<LDSB>(d, i, cur, rw, B, top, a3c);
     if (l < 10) ro.part[(size_t)i * 10 + l] = l < 5 ? (l == 0 ? top[0] : l == 1 ? top[1] : l == 2 ? top[2] : l == 3 ? top[3] : top[4]) : 0xFFFFFFFFu;
+    tick(3);
     // ---- (3) write back the changed segments of the bitset ----
     if (LDSB && segs) {
       const uint32_t wps4 = d.SEGW / 128;             // 16-byte words per segment
@@ -557,11 +574,23 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) voi
       w_bytes += (unsigned long long)__popcll(segs) * (d.SEGW / 8);
     }
     w_resp += nresp; w_nodes++;
+    tick(4);
     wait_lds();                                       // LDS bitset is reused by the next node
     __builtin_amdgcn_wave_barrier();
   }
   // the counters are summed over the workgroup's waves in LDS and added once per workgroup (one atomic
   // per wave and counter on the same few addresses would serialise in the memory system)
+#ifdef KB_RP_PROF
+  if (prof) {
+    __shared__ unsigned long long s_t[5];
+    if (threadIdx.x < 5) s_t[threadIdx.x] = 0;
+    __syncthreads();
+    if (l == 0) for (int k = 0; k < 5; ++k) atomicAdd(&s_t[k], tph[k]);
+    __syncthreads();
+    const int ci[5] = {C_DBG_TSTART, C_DBG_TBASE, C_DBG_TINS, C_DBG_TNODE, C_DBG_TEND};
+    if (threadIdx.x < 5) atomicAdd(&d.ctr[ci[threadIdx.x]], (uint32_t)(s_t[threadIdx.x] / 64));   // in 64-tick units
+  }
+#endif
   __shared__ unsigned long long s_cnt[RP_WAVES][7];
   if (l == 0) {
     s_cnt[wv][0] = w_lost; s_cnt[wv][1] = w_removed; s_cnt[wv][2] = w_resp; s_cnt[wv][3] = w_bytes;

@@ -1094,8 +1094,22 @@ static int step_round(kb_sim* s) {
     if (s->debug_waves && r == 2)
       fprintf(stderr, "[kb] row pass: %u waves/workgroup, %zu B LDS, %u workgroups/CU (lds_per_cu %zu), %u workgroups\n", wpb,
               lds, per_cu, (size_t)s->lds_per_cu, blocks);
+    const bool rp_prof = s->debug_waves && (d.dev & 2048);
+    if (rp_prof) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_TNODE, 0, 4 * (C_DBG_MSGS - C_DBG_TNODE), st));
     if (ldsb) klaunch(s, KI_ROWPASS, k_rowpass<true>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r, lf, lj);
     else klaunch(s, KI_ROWPASS, k_rowpass<false>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r, lf, lj);
+    if (rp_prof) {                                     // KB_DEV=2048: the row pass's phases, summed over its waves
+      uint32_t t[13];
+      HIPCHK(hipMemcpy(t, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost));
+      const double u = 100.0 / ((double)blocks * wpb);   // shares of the summed wall-clock ticks
+      double tot = 0;
+      for (int k = C_DBG_TNODE; k <= C_DBG_TEND; ++k) if (k != C_DBG_TMAX) tot += t[k - C_DBG_INS];
+      const double sc = tot > 0 ? (double)blocks * wpb / tot : 0;   // -> percent
+      fprintf(stderr, "[kb] round %d row pass time shares: stage %.1f %%, Failed %.1f %%, Join %.1f %%, A3 %.1f %%, write-back "
+              "%.1f %% (%u rows, %u waves)\n", r, t[C_DBG_TSTART - C_DBG_INS] * u * sc, t[C_DBG_TBASE - C_DBG_INS] * u * sc,
+              t[C_DBG_TINS - C_DBG_INS] * u * sc, t[C_DBG_TNODE - C_DBG_INS] * u * sc, t[C_DBG_TEND - C_DBG_INS] * u * sc, R,
+              blocks * wpb);
+    }
   }
   if (lat_fail)
     klaunch(s, KI_LAT_SWEEP, k_lat_sweep, dim3((lat_stride(R) / 8 + 255) / 256, std::min<uint32_t>(s->nf, 16384)), dim3(256), 0, d,
