@@ -286,12 +286,12 @@ __device__ inline void wave_combine(const Dev& d, uint32_t& raw, uint32_t& cnt) 
   cnt = c;
 }
 
-// Current fingerprint of row i with the whole wave: stale checkpoints are refolded (one per lane
-// when many are stale; all 64 lanes on each one when few are — the in-order handlers typically
-// dirty one segment per newly heard sender), then the 64 checkpoints are combined.
-__device__ __attribute__((always_inline)) inline uint32_t wave_fp(const Dev& d, const uint32_t* ztab, uint32_t i, unsigned long long extra) {
+// Checkpoint of segment `lane` of row i with the stale ones (sd) refolded and stored: one per lane when
+// many are stale; all 64 lanes on each one when few are (a lane alone on a segment is a chain of up to
+// 144 dependent table steps — the in-order handlers typically dirty one segment per newly heard sender).
+__device__ __attribute__((always_inline)) inline uint2 refold_stale(const Dev& d, const uint32_t* ztab, uint32_t i,
+                                                                   unsigned long long sd) {
   const uint32_t l = lane();
-  const unsigned long long sd = d.sdirty[i] | extra;
   uint2 sp = make_uint2(0, 0);
   if (d.uniform && sd && __popcll(sd) <= 4) {
     sp = d.segp[(size_t)i * NSEG + l];
@@ -312,6 +312,14 @@ __device__ __attribute__((always_inline)) inline uint32_t wave_fp(const Dev& d, 
   } else {
     sp = d.segp[(size_t)i * NSEG + l];
   }
+  return sp;
+}
+// Current fingerprint of row i with the whole wave: the stale checkpoints refolded, then the 64
+// checkpoints combined.
+__device__ __attribute__((always_inline)) inline uint32_t wave_fp(const Dev& d, const uint32_t* ztab, uint32_t i, unsigned long long extra) {
+  const uint32_t l = lane();
+  const unsigned long long sd = d.sdirty[i] | extra;
+  const uint2 sp = refold_stale(d, ztab, i, sd);
   uint32_t raw = sp.x, cnt = sp.y;
   wave_combine(d, raw, cnt);
   raw = bcast(raw, 0); cnt = bcast(cnt, 0);

@@ -938,9 +938,7 @@ __global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveC
       dbg_base++;
       const unsigned long long sd = d.sdirty[i] | segs;
       w_bytes += 8 * NSEG + 4 * 64 + (uint64_t)__popcll(sd) * (5 * (d.SEGW / 8) + 8);   // checkpoints, Z^n row, refolds
-      uint2 sp;
-      if ((sd >> l) & 1ull) { sp = fold_segment(d, ztab, i, l); d.segp[(size_t)i * NSEG + l] = sp; }
-      else sp = d.segp[(size_t)i * NSEG + l];
+      const uint2 sp = refold_stale(d, ztab, i, sd);
       uint32_t raw = sp.x, cnt = sp.y, c = sp.y;
       uint32_t oc[6], zp[6];
 #pragma unroll
