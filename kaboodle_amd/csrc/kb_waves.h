@@ -737,8 +737,16 @@ __device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, co
     const uint32_t icnt = wc.cnt1[i];
     bool fast = icnt && icnt <= FAST_MAX && !d.dirty[i];
     uint32_t g[FAST_MAX];
+    // Everything the handlers read is loaded up front, each group of loads in flight together: the
+    // records (kept in registers), the senders' member words and stamps (a handler changes only its own
+    // sender's stamp, and equal senders are adjacent), the node's header.  The fast lane is a chain of
+    // dependent loads per node, so its length is the launch's duration in the late waves.
+    uint32_t ms[FAST_MAX], mk[FAST_MAX], ma[FAST_MAX], mf[FAST_MAX], mn[FAST_MAX];
+    uint8_t sb[FAST_MAX];
+    uint32_t n = 0, fp = 0, ob_cap = 0, ob_off = 0, fn = 0;
     if (fast) {
       const uint32_t base = wc.in_off[i];
+      n = d.n[i]; fp = d.fp[i]; ob_cap = ob.cap[i]; ob_off = ob.off[i]; fn = d.flog_n[i];
 #pragma unroll
       for (uint32_t k = 0; k < FAST_MAX; ++k) g[k] = k < icnt ? wc.inbox[base + k] : 0xFFFFFFFFu;
 #pragma unroll
@@ -747,12 +755,21 @@ __device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, co
         for (uint32_t b = a; b > 0; --b)
           if (g[b - 1] > g[b]) { const uint32_t x = g[b]; g[b] = g[b - 1]; g[b - 1] = x; }
       const uint32_t* bw = bits_of(d, i);
+      const uint8_t* rw = row_of(d, i);
       const bool kpr_over = d.uniform && d.kpr_big[i] == r;      // every KPR reply of the round oversize
 #pragma unroll
       for (uint32_t k = 0; k < FAST_MAX; ++k) {
-        if (k >= icnt) break;
-        const Msg m = ib.msgs[g[k]];
-        if ((m.kind == K_KPR && !kpr_over) || !((bw[m.sender >> 5] >> (m.sender & 31)) & 1u)) fast = false;
+        ms[k] = 0; mk[k] = 0; ma[k] = 0; mf[k] = 0; mn[k] = 0;
+        if (k < icnt) { const Msg m = ib.msgs[g[k]]; ms[k] = m.sender; mk[k] = m.kind; ma[k] = m.a; mf[k] = m.fp; mn[k] = m.n; }
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < FAST_MAX; ++k) {
+        sb[k] = 0;
+        if (k < icnt) {
+          const uint32_t w = bw[ms[k] >> 5];
+          sb[k] = rw[ms[k]];
+          if ((mk[k] == K_KPR && !kpr_over) || !((w >> (ms[k] & 31)) & 1u)) fast = false;
+        }
       }
     }
     to_slow = icnt && !fast;
@@ -770,9 +787,7 @@ __device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, co
                                                                                                 : kpr ? C_DBG_SLOW_KPR : C_DBG_SLOW_OTHER], 1u);
     }
     if (fast) {
-      const uint32_t n = d.n[i], fp = d.fp[i];
-      const uint32_t ob_cap = ob.cap[i], ob_off = ob.off[i];   // this node's outbox region, loaded once
-      uint32_t fn = d.flog_n[i], oseq = 0, last_sender = 0xFFFFFFFFu;
+      uint32_t oseq = 0, last_sender = 0xFFFFFFFFu;
       auto emit = [&](uint32_t dest, uint32_t kind, uint32_t a, uint32_t efp, uint32_t en) __attribute__((always_inline)) {
         if (oseq >= ob_cap || ob_off + oseq >= ob.msg_cap) set_err(d, DERR_OUTBOX);
         else ob.msgs[ob_off + oseq] = Msg{dest, i, oseq, kind, a, efp, en, 0};
@@ -781,26 +796,34 @@ __device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, co
       uint8_t* rw = row_of(d, i);
       Susp* sl = d.susp + (size_t)i * SLOTS;
       Cur* cu = d.cur + (size_t)i * CSLOTS;
+      // curious_peers entry of peer p: the slots' (used, peer) words read together, not slot by slot
+      auto cur_find = [&](uint32_t p) __attribute__((always_inline)) -> int {
+        uint32_t cp[CSLOTS], cf[CSLOTS];
+#pragma unroll
+        for (int j = 0; j < CSLOTS; ++j) { cp[j] = cu[j].peer; cf[j] = cu[j].used; }
+        int e = -1;
+#pragma unroll
+        for (int j = CSLOTS - 1; j >= 0; --j) if (cf[j] && cp[j] == p) e = j;
+        return e;
+      };
 #pragma unroll
       for (uint32_t k = 0; k < FAST_MAX; ++k) {
         if (k >= icnt) break;
-        const Msg m = ib.msgs[g[k]];
-        const uint32_t s = m.sender;
+        const uint32_t s = ms[k], kind = mk[k], ma_k = ma[k];
         if (s != last_sender) {                        // prologue: insert(sender, Known(now))
-          const uint8_t b = rw[s];
+          const uint8_t b = sb[k];
           if (b == ST_SUSPECT)
             for (int j = 0; j < SLOTS; ++j) if (sl[j].kind && sl[j].peer == s) { lat_sample(d, i, s, sl[j].since, r); sl[j].kind = 0; }
           if (b != now) { rw[s] = now; d.flog[(size_t)i * LOGCAP + (fn & (LOGCAP - 1))] = log_entry(s, r); fn++; }
           last_sender = s;
         }
-        if (m.kind == K_PING) {
+        if (kind == K_PING) {
           emit(s, K_ACK, i, fp, n);
-        } else if (m.kind == K_PINGREQ) {
-          int e = -1;
-          for (int j = 0; j < CSLOTS && e < 0; ++j) if (cu[j].used && cu[j].peer == m.a) e = j;
+        } else if (kind == K_PINGREQ) {
+          int e = cur_find(ma_k);
           if (e < 0) {
             for (int j = 0; j < CSLOTS && e < 0; ++j) if (!cu[j].used) e = j;
-            if (e >= 0) { cu[e].used = 1; cu[e].peer = m.a; cu[e].nobs = 0; }
+            if (e >= 0) { cu[e].used = 1; cu[e].peer = ma_k; cu[e].nobs = 0; }
           }
           if (e < 0) curovf++;
           else {
@@ -809,19 +832,22 @@ __device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, co
             for (uint32_t q = 0; q < nobs; ++q) dup |= cu[e].obs[q] == s;
             if (!dup) { if (nobs == NOBS) curovf++; else { cu[e].obs[nobs] = s; cu[e].nobs = nobs + 1; } }
           }
-          emit(m.a, K_PING, 0, 0, 0);
-        } else if (m.kind == K_ACK) {
-          int e = -1;
-          for (int j = 0; j < CSLOTS && e < 0; ++j) if (cu[j].used && cu[j].peer == m.a) e = j;
+          emit(ma_k, K_PING, 0, 0, 0);
+        } else if (kind == K_ACK) {
+          const int e = cur_find(ma_k);
           if (e >= 0) {
             const uint32_t nobs = cu[e].nobs;
-            for (uint32_t q = 0; q < nobs; ++q) emit(cu[e].obs[q], K_ACK, m.a, m.fp, m.n);
+            uint32_t ob4[NOBS];
+#pragma unroll
+            for (int q = 0; q < NOBS; ++q) ob4[q] = cu[e].obs[q];
+#pragma unroll
+            for (uint32_t q = 0; q < (uint32_t)NOBS; ++q) if (q < nobs) emit(ob4[q], K_ACK, ma_k, mf[k], mn[k]);
             cu[e].used = 0;
           }
-          if (fp != m.fp && !(n > m.n)) emit(m.a, K_KPR, 0, fp, n);
-        } else if (m.kind == K_KPR) {                  // :473-512, reply lost as oversize (Q3), then :507
+          if (fp != mf[k] && !(n > mn[k])) emit(ma_k, K_KPR, 0, fp, n);
+        } else if (kind == K_KPR) {                  // :473-512, reply lost as oversize (Q3), then :507
           over++;
-          if (fp != m.fp && !(n > m.n)) emit(s, K_KPR, 0, fp, n);
+          if (fp != mf[k] && !(n > mn[k])) emit(s, K_KPR, 0, fp, n);
         }
       }
       ob.cnt[i] = oseq;
