@@ -20,8 +20,9 @@ Also reported, on the same JSON line:
   kernels       every kernel of the round: HIP-event ms per round (each launch timed by its own dispatch
                 packet on the simulator's stream), launches per round, wave-0 share, and for the kernels
                 with an in-kernel byte counter (k_rowpass, k_fold, k_resp_wave, k_proc) the algorithmic
-                bytes and GB/s.  The timed rounds carry events on those four kernels only (an event pair
-                costs ≈5 us of dispatch overhead); the other kernels' times come from an untimed replay of
+                bytes and GB/s.  The timed rounds carry events on the three once-per-round ones only (an
+                event pair costs ≈5 us of dispatch overhead; k_proc's eight launches a round would add
+                ≈0.05 ms); the other kernels' times, k_proc's included, come from an untimed replay of
                 the same rounds (same seed: the simulation is deterministic, bit for bit) with events on
                 every launch.  `gaps` = round_gpu_ms minus the kernels (launch gaps, host hand-offs), so the
                 rows sum to round_gpu_ms;

@@ -298,9 +298,10 @@ int  kb_sim_reset_kernel_time(kb_sim* sim);
    last reset, counted in-kernel.                                                      */
 int  kb_sim_kernel_bytes(kb_sim* sim, int kind, uint64_t* bytes);
 /* Per-kernel profile of the launches of the rounds since the last reset.  Profiling level (env KB_PROF
-   or kb_sim_set_profiling): 0 = no per-launch events; 1 (default) = events on the kernels with an
-   in-kernel byte counter only (KB_KT_ROWPASS/FOLD/RESP/PROC); 2 = every launch (each event pair adds
-   ≈5 us of dispatch overhead, ≈0.5 ms on a 100-launch round: use it on an untimed replay).  wave_ms[w]
+   or kb_sim_set_profiling): 0 = no per-launch events; 1 (default) = events on the once-per-round
+   kernels with an in-kernel byte counter only (KB_KT_ROWPASS/FOLD/RESP); 2 = every launch, KB_KT_PROC's
+   included (each event pair adds ≈5 us of dispatch overhead, ≈0.5 ms on a 100-launch round: use it on
+   an untimed replay).  wave_ms[w]
    is the part spent in delivery wave w (slot KB_WAVE_SLOTS-1 holds waves >= KB_WAVE_SLOTS-1).  Kernels
    without events are omitted; cap = 0 queries the count.                                            */
 #define KB_WAVE_SLOTS 9

@@ -413,7 +413,9 @@ template <class T> static T* L(const kb_sim* s, T* p) { return p + s->lo; }   //
 // ---- launches and their profile ------------------------------------------------------------------
 static void prof_events(kb_sim* s, int kid, hipEvent_t* a, hipEvent_t* b) {
   *a = *b = nullptr;
-  if (s->capturing || s->prof_level <= 0 || (s->prof_level == 1 && kbytes_stat(kid) < 0)) return;
+  // level 1 times the once-per-round kernels with byte counters only: k_proc's eight launches a round
+  // would add ≈ 0.05 ms of event dispatch overhead to the round (tools/ev_cost.py)
+  if (s->capturing || s->prof_level <= 0 || (s->prof_level == 1 && (kbytes_stat(kid) < 0 || kid == KI_PROC))) return;
   hipEvent_t e[2];
   for (int k = 0; k < 2; ++k) {
     if (!s->ev_free.empty()) { e[k] = s->ev_free.back(); s->ev_free.pop_back(); }
