@@ -304,3 +304,26 @@ def test_kaboodle_view(gpu):
     assert fps == {0x981285C8}
     assert m.node(0).self_addr() == "10.100.100.100:10000"
     assert sorted(m.node(2).peers()) == [f"10.100.100.100:1000{i}" for i in range(4)]
+
+
+def test_profiling_levels(gpu):
+    """Level 1 (the timed rounds' default) times the once-per-round counted kernels only, level 2 every
+    launch, level 0 none; results do not depend on the level (kb_sim_set_profiling)."""
+    cfg = SimConfig(capacity=5000, initial_nodes=4096, init_mode=KB_INIT_CONVERGED, loss=0.02, churn=0.002, seed=9)
+    fps = []
+    for level in (1, 2, 0):
+        with Sim(gpu, cfg) as g:
+            g.set_profiling(level)
+            g.step(2)
+            g.reset_kernel_time()
+            g.step(3)
+            names = set(g.kernel_breakdown())
+            if level == 1:
+                assert "k_rowpass" in names and "k_proc" not in names and "k_sortfast" not in names
+            elif level == 2:
+                assert {"k_rowpass", "k_proc", "k_sortfast", "k_route"} <= names
+            else:
+                assert not names
+            fps.append((g.stats(), g.fingerprints().copy()))
+    assert fps[0][0] == fps[1][0] == fps[2][0]
+    assert np.array_equal(fps[0][1], fps[1][1]) and np.array_equal(fps[0][1], fps[2][1])
