@@ -7,7 +7,9 @@
  *
  *   kb_sim_create / kb_sim_destroy   Kaboodle::new            src/lib.rs:93-133   (per mesh, not per peer)
  *   kb_sim_step                      KaboodleInner::run/tick  src/kaboodle.rs:746-786 (all peers, R rounds)
- *   kb_sim_start_node                Kaboodle::start          src/lib.rs:136-156, src/kaboodle.rs:114-185
+ *   kb_sim_start_node                Kaboodle::start          src/lib.rs:136-156, src/kaboodle.rs:114-185 (first start)
+ *   kb_sim_restart_node              Kaboodle::start          the same, on a stopped instance: a fresh address
+ *                                                             (src/kaboodle.rs:138-152) keeping its map (src/lib.rs:104,167-170)
  *   kb_sim_stop_node                 Kaboodle::stop           src/lib.rs:159-183
  *   kb_sim_ping_addrs                Kaboodle::ping_addrs     src/lib.rs:268-297
  *   kb_sim_fingerprint               Kaboodle::fingerprint    src/lib.rs:301-304 -> generate_fingerprint
@@ -37,7 +39,8 @@
 extern "C" {
 #endif
 
-#define KB_ABI_VERSION 2u   /* 2: kernel breakdown, identities on the inspection surface */
+#define KB_ABI_VERSION 3u   /* 2: kernel breakdown, identities on the inspection surface; 3: restarts bind a
+                                fresh address (kb_sim_restart_node) */
 
 /* ---- status codes (mirror KaboodleError, src/errors.rs:8-24) ------------------------------------ */
 enum {
@@ -141,13 +144,30 @@ int  kb_sim_destroy(kb_sim* sim);
 /* Advance every running peer by `rounds` protocol periods. */
 int  kb_sim_step(kb_sim* sim, uint32_t rounds);
 
-int  kb_sim_start_node(kb_sim* sim, uint32_t node);                 /* takes effect next round start */
+/* The first start of the instance at address `node` (a no-op while it runs); takes effect at the next
+   round start.  A stopped instance that has run restarts at a fresh address instead: KB_INVALID_OPERATION
+   here, use kb_sim_restart_node. */
+int  kb_sim_start_node(kb_sim* sim, uint32_t node);
 int  kb_sim_stop_node(kb_sim* sim, uint32_t node);                  /* takes effect next round start */
+/* Kaboodle::start for the instance last bound to address `node` (src/lib.rs:136-156).  Running: a no-op,
+   *new_node = node.  Never bound: its first start, *new_node = node.  Stopped after running: the reference
+   binds a fresh ephemeral socket on every start (src/kaboodle.rs:138-152) while the instance's known_peers
+   map persists across stop/start (src/lib.rs:104, minus the old self removed by stop, :167-170).  So the
+   next fresh id (the churn reserve, allocated now, in order) becomes the instance's address: at the next
+   round start it inherits the old address's map (entries, states, instants, latencies), with fresh curious
+   peers, ping queue and Join timer (a new KaboodleInner), and the old address stays in other views until
+   pinged out.  Its identity is the instance's (the one set while stopped, if any).  Watches follow the
+   instance.  KB_CAPACITY: no fresh id left.                                                           */
+int  kb_sim_restart_node(kb_sim* sim, uint32_t node, uint32_t* new_node);
 int  kb_sim_is_running(kb_sim* sim, uint32_t node, int* running);
 int  kb_sim_ping_addrs(kb_sim* sim, uint32_t node, const uint32_t* peers, size_t n);
 /* Kaboodle::set_identity (src/lib.rs:323-336): only while the node is not running, counting the start /
-   stop calls queued since the last step (they take effect at the next round start).  Identity belongs
-   to the id: the new bytes are what every view reports and fingerprints from then on. */
+   stop calls queued since the last step (they take effect at the next round start).  Views hold the
+   identity an address announced (PeerInfo.identity, src/kaboodle.rs:409-414, :291-298, :461-468); since an
+   instance changes identity only while stopped and restarts at a fresh address, one identity per address
+   is what every view holds.  An address never bound takes the bytes at once; for an instance stopped at
+   an address that ran they are kept for its next address (kb_sim_restart_node) and kb_sim_identity(node)
+   keeps reporting the bytes the views hold.                                                            */
 int  kb_sim_set_identity(kb_sim* sim, uint32_t node, const uint8_t* identity, size_t len);
 /* The identity bytes of id `node` (Kaboodle::peers / peer_states values, src/lib.rs:339-354): *len is
    the length; copied into buf when cap suffices (buf = NULL: length query).                         */

@@ -50,7 +50,8 @@ class Mesh {
   class Peer {
    public:
     Peer(kb_sim* h, uint32_t id) : h_(h), id_(id) {}
-    void start() { check(kb_sim_start_node(h_, id_), "kb_sim_start_node"); }            // :136
+    // :136 — a stopped peer comes back at a fresh address (src/kaboodle.rs:138-152) with its map
+    void start() { check(kb_sim_restart_node(h_, id_, &id_), "kb_sim_restart_node"); }
     void stop() { check(kb_sim_stop_node(h_, id_), "kb_sim_stop_node"); }               // :159
     bool is_running() const { int r; check(kb_sim_is_running(h_, id_, &r), "kb_sim_is_running"); return r != 0; }
     std::string self_addr() const { return format_addr(id_); }                          // :312

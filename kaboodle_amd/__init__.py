@@ -145,9 +145,17 @@ class Kaboodle:
 
     def __init__(self, mesh: Mesh, node: int):
         self.mesh, self.id = mesh, node
+        self._identity = None                     # set while stopped: announced from the next start
 
     def start(self) -> None:                      # src/lib.rs:136-156 (effective next round)
-        self.mesh.start_node(self.id)
+        """Start, or restart after stop: the reference binds a fresh ephemeral socket on every start
+        (src/kaboodle.rs:138-152) and keeps its known_peers map, so a restarted peer has a new address
+        (kb_sim_restart_node); its event channels follow it."""
+        old = self.id
+        self.id = self.mesh.restart_node(old)
+        self._identity = None
+        if self.id != old and old in self.mesh._subs:
+            self.mesh._subs[self.id] = self.mesh._subs.pop(old)
 
     def stop(self) -> None:                       # src/lib.rs:159-183
         self.mesh.stop_node(self.id)
@@ -163,6 +171,7 @@ class Kaboodle:
 
     def set_identity(self, identity: bytes) -> None:   # src/lib.rs:323-336
         self.mesh.set_identity(self.id, identity)
+        self._identity = bytes(identity)
 
     def fingerprint(self) -> int:                 # src/lib.rs:301-304
         return self.mesh.fingerprint(self.id)
@@ -171,7 +180,7 @@ class Kaboodle:
         return {self.mesh.format_addr(p): self.mesh.identity(p) for p in self.mesh.peers(self.id)}
 
     def identity(self) -> bytes:                  # the identity this peer announces (Kaboodle.identity)
-        return self.mesh.identity(self.id)
+        return self._identity if self._identity is not None else self.mesh.identity(self.id)
 
     def discover_peers(self) -> Channel:          # src/lib.rs:221-236: (addr, identity) per new peer
         return self.mesh.subscribe(self.id, "peers", Channel())

@@ -10,7 +10,7 @@ import ctypes as C
 import os
 from dataclasses import dataclass
 
-KB_ABI_VERSION = 2
+KB_ABI_VERSION = 3
 KB_OK, KB_INVALID_OPERATION, KB_IO_ERROR, KB_NO_DEVICE, KB_STOPPING_FAILED, KB_INVALID_ARGUMENT, KB_CAPACITY = range(7)
 KB_INIT_JOIN, KB_INIT_CONVERGED = 0, 1
 KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL = 0, 1
@@ -137,6 +137,7 @@ _SIGS = {
     "sim_step": (C.c_int, [C.c_void_p, C.c_uint32]),
     "sim_start_node": (C.c_int, [C.c_void_p, C.c_uint32]),
     "sim_stop_node": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sim_restart_node": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     "sim_is_running": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_int)]),
     "sim_ping_addrs": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t]),
     "sim_set_identity": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]),
@@ -276,6 +277,13 @@ class Sim:
 
     def stop_node(self, node: int) -> None:
         self.lib.call("sim_stop_node", self.h, node)
+
+    def restart_node(self, node: int) -> int:
+        """Kaboodle::start for the instance at `node`: returns its address from then on (a fresh id when it
+        had run and is stopped; kb_sim_restart_node)."""
+        v = C.c_uint32()
+        self.lib.call("sim_restart_node", self.h, node, C.byref(v))
+        return v.value
 
     def is_running(self, node: int) -> bool:
         v = C.c_int()

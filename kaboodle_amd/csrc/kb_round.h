@@ -29,14 +29,72 @@ __global__ void k_rebase(Dev d) {
 }
 
 // ---- lifecycle: API start/stop in call order, then churn (src/lib.rs:136-183) ------------------
-struct Event { uint32_t node, stop; };
+// kind: EV_START, EV_STOP, or EV_RESTART (node = the instance's fresh address, src = its old one; the
+// map was moved by k_row_pack / k_row_unpack just before, so here it is a start at the new address)
+enum : uint32_t { EV_START = 0, EV_STOP = 1, EV_RESTART = 2 };
+struct Event { uint32_t node, kind, src, pad; };
 __global__ void k_events(Dev d, const Event* ev, uint32_t nev, int32_t r) {
   if (threadIdx.x || blockIdx.x) return;
   for (uint32_t k = 0; k < nev; ++k) {
     const uint32_t i = ev[k].node;
-    if (ev[k].stop) { if (d.alive[i]) node_stop(d, i); }
+    if (ev[k].kind == EV_STOP) { if (d.alive[i]) node_stop(d, i); }
     else if (!d.alive[i]) node_start(d, i, r);
   }
+}
+
+// ---- a restart's map (kb_sim_restart_node): Kaboodle::start on a stopped instance binds a fresh address
+// (src/kaboodle.rs:138-152) while its known_peers map persists (src/lib.rs:104, 167-170).  The old row is
+// packed into one u32 buffer (every row table of the node: stamps, member bits, checkpoints, suspect slots,
+// freshness log, latency column, plus the event observer's snapshot), moved to the shard holding the new
+// row (an all-to-all-v with one non-empty pair; unsharded: in place) and unpacked there.
+struct RowPack { uint32_t hdr, fstart, susp, segp, flog, bits, snap, stamp, lat, words; };
+enum { RP_N, RP_FP, RP_DIRTY, RP_FLOGN, RP_WATCHED, RP_WFP, RP_SD0, RP_SD1, RP_HDR = 16 };
+__host__ __device__ inline RowPack row_pack_layout(uint32_t W, uint32_t NWR, bool lat) {
+  RowPack L;
+  L.hdr = 0; L.fstart = RP_HDR; L.susp = L.fstart + 16; L.segp = L.susp + SLOTS * 4; L.flog = L.segp + 2 * NSEG;
+  L.bits = L.flog + LOGCAP; L.snap = L.bits + NWR; L.stamp = L.snap + NWR; L.lat = L.stamp + W / 4;
+  L.words = L.lat + (lat ? W / 2 : 0);
+  return L;
+}
+__global__ __launch_bounds__(256) void k_row_pack(Dev d, uint32_t i, uint32_t* __restrict__ out, RowPack L,
+                                                  const uint32_t* __restrict__ snap, uint32_t wfp) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, T = gridDim.x * blockDim.x;
+  if (t == 0) {
+    const unsigned long long sd = d.sdirty[i];
+    out[RP_N] = d.n[i]; out[RP_FP] = d.fp[i]; out[RP_DIRTY] = d.dirty[i]; out[RP_FLOGN] = d.flog_n[i];
+    out[RP_WATCHED] = snap != nullptr; out[RP_WFP] = wfp; out[RP_SD0] = (uint32_t)sd; out[RP_SD1] = (uint32_t)(sd >> 32);
+  }
+  if (t < 16) out[L.fstart + t] = d.fstart[(size_t)i * 16 + t];
+  if (t < SLOTS * 4) out[L.susp + t] = reinterpret_cast<const uint32_t*>(d.susp + (size_t)i * SLOTS)[t];
+  if (t < 2 * NSEG) out[L.segp + t] = reinterpret_cast<const uint32_t*>(d.segp + (size_t)i * NSEG)[t];
+  for (uint32_t k = t; k < LOGCAP; k += T) out[L.flog + k] = d.flog[(size_t)i * LOGCAP + k];
+  const uint32_t* b = bits_of(d, i);
+  for (uint32_t k = t; k < d.NWR; k += T) { out[L.bits + k] = b[k]; out[L.snap + k] = snap ? snap[k] : 0u; }
+  const uint32_t* st = reinterpret_cast<const uint32_t*>(row_of(d, i));
+  for (uint32_t k = t; k < d.W / 4; k += T) out[L.stamp + k] = st[k];
+  if (d.lat)
+    for (uint32_t k = t; k < d.W / 2; k += T) out[L.lat + k] = (uint32_t)*lat_at(d, i, 2 * k) | ((uint32_t)*lat_at(d, i, 2 * k + 1) << 16);
+}
+__global__ __launch_bounds__(256) void k_row_unpack(Dev d, uint32_t i, const uint32_t* __restrict__ in, RowPack L,
+                                                    uint32_t* __restrict__ snap) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x, T = gridDim.x * blockDim.x;
+  if (t == 0) {
+    d.n[i] = in[RP_N]; d.fp[i] = in[RP_FP]; d.dirty[i] = (uint8_t)in[RP_DIRTY]; d.flog_n[i] = in[RP_FLOGN];
+    d.sdirty[i] = (unsigned long long)in[RP_SD0] | ((unsigned long long)in[RP_SD1] << 32);
+  }
+  if (t < 16) d.fstart[(size_t)i * 16 + t] = in[L.fstart + t];
+  if (t < SLOTS * 4) reinterpret_cast<uint32_t*>(d.susp + (size_t)i * SLOTS)[t] = in[L.susp + t];
+  if (t < 2 * NSEG) reinterpret_cast<uint32_t*>(d.segp + (size_t)i * NSEG)[t] = in[L.segp + t];
+  for (uint32_t k = t; k < LOGCAP; k += T) d.flog[(size_t)i * LOGCAP + k] = in[L.flog + k];
+  uint32_t* b = bits_of(d, i);
+  for (uint32_t k = t; k < d.NWR; k += T) { b[k] = in[L.bits + k]; if (snap) snap[k] = in[L.snap + k]; }
+  uint32_t* st = reinterpret_cast<uint32_t*>(row_of(d, i));
+  for (uint32_t k = t; k < d.W / 4; k += T) st[k] = in[L.stamp + k];
+  if (d.lat)
+    for (uint32_t k = t; k < d.W / 2; k += T) {
+      const uint32_t v = in[L.lat + k];
+      *lat_at(d, i, 2 * k) = (uint16_t)v; *lat_at(d, i, 2 * k + 1) = (uint16_t)(v >> 16);
+    }
 }
 __global__ void k_churn_leave(Dev d, int32_t r) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

@@ -324,7 +324,11 @@ struct kb_sim {
   std::vector<void*> allocs;           // device memory owned by this handle
   int32_t round;
   std::vector<uint8_t> h_ident, h_idlen;
+  std::vector<uint8_t> h_pend; std::vector<int16_t> h_pendlen;   // identity set on a stopped instance that ran:
+                                                                 // its next address takes it (-1: none)
+  std::vector<uint8_t> h_moved;                                  // the instance bound here restarted elsewhere
   std::vector<Event> events;
+  uint32_t* rpack = nullptr; uint32_t* rpack_in = nullptr;       // a restart's packed row (send / receive)
   // discovery: Probes queued for the next round, those delivered this round, responses not yet drained
   std::vector<kb_wire_addr> probe_q, probes;
   std::vector<kb_probe_response> presp;
@@ -524,7 +528,7 @@ static void free_all(kb_sim* s) {
   for (void* p : s->allocs) (void)hipFree(p);
   s->allocs.clear();
   void* dyn[] = {s->newmask_base, s->respmask_base, s->resp_scratch, s->d_events, s->rmsg, s->rpay, s->rstatus,
-                 s->rinbox, s->rkp, s->d_presp, s->d_presp_n};
+                 s->rinbox, s->rkp, s->d_presp, s->d_presp_n, s->rpack, s->rpack_in};
   for (void* p : dyn) if (p) (void)hipFree(p);
 }
 static void destroy_shard(kb_sim* s) {
@@ -599,6 +603,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (const char* gv = getenv("KB_WAVE_GRAPH")) s->graph_on = atoi(gv) != 0;
   if (cfg->debug_flags & KB_DBG_WAVE_GRAPH) s->graph_on = true;
   s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid);
+  s->h_pend.assign((size_t)C * MAXID, 0); s->h_pendlen.assign(C, (int16_t)-1); s->h_moved.assign(C, 0);
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &s->h_ident[(size_t)j * MAXID]);
   hipError_t e = hipSuccess;
 #define A(ptr, n) if (e == hipSuccess) e = talloc(s, &(ptr), (n))     // per-id / global tables
@@ -999,6 +1004,49 @@ static int launch_waves(kb_sim* s, int32_t rk) {
   return KB_OK;
 }
 
+// A restart's map: the old address's row packed on the shard holding it, moved (sharded: an all-to-all-v
+// in which only that shard sends, to the shard holding the new row) and unpacked; the event observer
+// moves with it (src/lib.rs:104: the map and its observer belong to the Kaboodle, not to its socket).
+static int move_row(kb_sim* s, uint32_t from, uint32_t to) {
+  const RowPack LP = row_pack_layout(s->W, s->d.NWR, s->d.lat != nullptr);
+  if (!s->rpack) HIPCHK(hipMalloc(&s->rpack, 4ull * LP.words));
+  if (s->xf && !s->rpack_in) HIPCHK(hipMalloc(&s->rpack_in, 4ull * LP.words));
+  const bool have = from >= s->lo && from < s->hi, take = to >= s->lo && to < s->hi;
+  size_t wk = 0;
+  while (wk < s->watch_node.size() && s->watch_node[wk] != from) ++wk;
+  const bool watched = have && wk < s->watch_node.size();
+  const uint32_t g = (LP.words + 255) / 256 < 1024 ? (LP.words + 255) / 256 : 1024;
+  if (have) k_row_pack<<<g, 256, 0, s->st>>>(s->d, from, s->rpack, LP, watched ? s->watch_snap[wk] : nullptr,
+                                            watched ? s->watch_fp[wk] : 0u);
+  if (watched) { s->watch_node.erase(s->watch_node.begin() + wk); s->watch_fp.erase(s->watch_fp.begin() + wk);
+                 s->watch_snap.erase(s->watch_snap.begin() + wk); }
+  const uint32_t* src = s->rpack;
+  if (s->xf) {
+    const int W = s->world, S = (int)s->xs.S;
+    const int ofrom = (int)(from / (uint32_t)S), oto = (int)(to / (uint32_t)S);
+    size_t sc[XMAX] = {}, sd[XMAX] = {}, rc[XMAX] = {}, rd[XMAX] = {};
+    if (s->rank == ofrom) sc[oto] = LP.words;
+    if (s->rank == oto) rc[ofrom] = LP.words;
+    (void)W;
+    if (!s->xf->group_begin()) { seterr(s->xf->error()); return KB_IO_ERROR; }
+    const bool sent = s->xf->alltoallv(s->rpack, sc, sd, s->rpack_in, rc, rd, 4, s->st);
+    const std::string e1 = sent ? std::string() : s->xf->error();
+    if (!s->xf->group_end() || !sent) { seterr(sent ? s->xf->error() : e1); return KB_IO_ERROR; }
+    src = s->rpack_in;
+  }
+  if (!take) return KB_OK;
+  uint32_t hdr[RP_HDR];
+  HIPCHK(hipMemcpyAsync(hdr, src, sizeof hdr, hipMemcpyDeviceToHost, s->st));
+  HIPCHK(sync_st(s));
+  uint32_t* snap = nullptr;
+  if (hdr[RP_WATCHED]) {
+    HIPCHK(talloc(s, &snap, (size_t)s->d.NWR));
+    s->watch_node.push_back(to); s->watch_fp.push_back(hdr[RP_WFP]); s->watch_snap.push_back(snap);
+  }
+  k_row_unpack<<<g, 256, 0, s->st>>>(s->d, to, src, LP, snap);
+  return KB_OK;
+}
+
 static int step_round(kb_sim* s) {
   Dev& d = s->d;
   const int32_t r = s->round;
@@ -1023,7 +1071,17 @@ static int step_round(kb_sim* s) {
       HIPCHK(hipMalloc(&s->d_events, sizeof(Event) * s->events_cap));
     }
     HIPCHK(hipMemcpyAsync(s->d_events, s->events.data(), sizeof(Event) * s->events.size(), hipMemcpyHostToDevice, st));
-    klaunch(s, KI_EVENTS, k_events, dim3(1), dim3(1), 0, d, s->d_events, (uint32_t)s->events.size(), r);
+    // in call order; a restart first moves the instance's map to its new address (the events before it
+    // have been applied: its stop removed the old self), then starts it there
+    size_t k0 = 0;
+    for (size_t k = 0; k <= s->events.size(); ++k) {
+      const bool rs = k < s->events.size() && s->events[k].kind == EV_RESTART;
+      if (k == s->events.size() || rs) {
+        if (k > k0) klaunch(s, KI_EVENTS, k_events, dim3(1), dim3(1), 0, d, s->d_events + k0, (uint32_t)(k - k0), r);
+        if (rs) { const int rc = move_row(s, s->events[k].src, s->events[k].node); if (rc) return rc; }
+        k0 = k;
+      }
+    }
     HIPCHK(sync_st(s));
     s->events.clear();
   }
@@ -1340,17 +1398,79 @@ static int read_row(kb_sim* s, uint32_t node, std::vector<uint8_t>& rw) {   // c
     return call(owner(s, node));                                          \
   }
 
+// running as the API sees it: the last lifecycle call queued for the node since the last step (they take
+// effect at the next round start), else its current state; a queued restart moves the instance away
+static int api_running(kb_sim* s, uint32_t node, int* run) {
+  for (size_t k = s->events.size(); k-- > 0;) {
+    if (s->events[k].node == node) { *run = s->events[k].kind != EV_STOP; return KB_OK; }
+    if (s->events[k].kind == EV_RESTART && s->events[k].src == node) { *run = 0; return KB_OK; }
+  }
+  uint8_t a = 0;
+  HIPCHK(hipMemcpy(&a, s->d.alive + node, 1, hipMemcpyDeviceToHost));
+  *run = a;
+  return KB_OK;
+}
+// the address has been bound by an instance: it ran (start_round, replicated), or a start of it is queued
+static int ever_bound(kb_sim* s, uint32_t node, int* ever) {
+  for (const Event& e : s->events) if (e.node == node && e.kind != EV_STOP) { *ever = 1; return KB_OK; }
+  int32_t sr = 0;
+  HIPCHK(hipMemcpy(&sr, s->d.start_round + node, 4, hipMemcpyDeviceToHost));
+  *ever = sr != NONE_ROUND;
+  return KB_OK;
+}
 extern "C" int kb_sim_start_node(kb_sim* s, uint32_t node) {
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
-  GROUP_ALL([&](kb_sim* t) { return kb_sim_start_node(t, node); });
-  s->events.push_back(Event{node, 0});
+  kb_sim* h = is_group(s) ? s->shards[0] : s;        // lifecycle facts are replicated on every shard
+  int run = 0, ever = 0;
+  { int rc = api_running(h, node, &run); if (!rc) rc = ever_bound(h, node, &ever); if (rc) return rc; }
+  if (!run && ever) { seterr("a stopped instance restarts at a fresh address (kb_sim_restart_node)"); return KB_INVALID_OPERATION; }
+  GROUP_ALL([&](kb_sim* t) { t->events.push_back(Event{node, EV_START, node, 0}); return KB_OK; });
+  s->events.push_back(Event{node, EV_START, node, 0});
   return KB_OK;
 }
 extern "C" int kb_sim_stop_node(kb_sim* s, uint32_t node) {
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_stop_node(t, node); });
-  s->events.push_back(Event{node, 1});
+  s->events.push_back(Event{node, EV_STOP, node, 0});
   return KB_OK;
+}
+// Kaboodle::start of the instance at `node` (include/kaboodle_sim.h): a stopped instance that ran comes
+// back at the next fresh id, allocated now (the churn reserve's counter, replicated on every shard)
+static int restart_apply(kb_sim* s, uint32_t node, uint32_t to) {
+  const int pl = s->h_pendlen[node];
+  const uint8_t* src = pl >= 0 ? &s->h_pend[(size_t)node * MAXID] : &s->h_ident[(size_t)node * MAXID];
+  const uint32_t len = pl >= 0 ? (uint32_t)pl : s->h_idlen[node];
+  memmove(&s->h_ident[(size_t)to * MAXID], src, len);
+  s->h_idlen[to] = (uint8_t)len;
+  s->h_pendlen[node] = -1; s->h_pendlen[to] = -1;
+  const int rc = upload_segments(s);
+  if (rc) return rc;
+  s->buf_gen++;                                    // a captured receive window holds the old Dev (uniform)
+  const uint32_t nf = to + 1;
+  HIPCHK(hipMemcpy(s->d.ctr + C_NEXTFREE, &nf, 4, hipMemcpyHostToDevice));
+  s->events.push_back(Event{to, EV_RESTART, node, 0});
+  s->h_moved[node] = 1;
+  return KB_OK;
+}
+extern "C" int kb_sim_restart_node(kb_sim* s, uint32_t node, uint32_t* new_node) {
+  if (chk(s, node) || !new_node) return KB_INVALID_ARGUMENT;
+  kb_sim* h = is_group(s) ? s->shards[0] : s;
+  if (h->h_moved[node]) { seterr("the instance bound here restarted at a fresh address"); return KB_INVALID_OPERATION; }
+  int run = 0, ever = 0;
+  { int rc = api_running(h, node, &run); if (!rc) rc = ever_bound(h, node, &ever); if (rc) return rc; }
+  if (run) { *new_node = node; return KB_OK; }
+  if (!ever) {
+    *new_node = node;
+    GROUP_ALL([&](kb_sim* t) { t->events.push_back(Event{node, EV_START, node, 0}); return KB_OK; });
+    s->events.push_back(Event{node, EV_START, node, 0});
+    return KB_OK;
+  }
+  uint32_t nf = 0;
+  HIPCHK(hipMemcpy(&nf, h->d.ctr + C_NEXTFREE, 4, hipMemcpyDeviceToHost));
+  if (nf >= s->C) { seterr("no fresh address left for the restart (capacity)"); return KB_CAPACITY; }
+  *new_node = nf;
+  GROUP_ALL([&](kb_sim* t) { (void)hipSetDevice(t->device); return restart_apply(t, node, nf); });
+  return restart_apply(s, node, nf);
 }
 extern "C" int kb_sim_is_running(kb_sim* s, uint32_t node, int* running) {
   if (chk(s, node) || !running) return KB_INVALID_ARGUMENT;
@@ -1385,16 +1505,16 @@ extern "C" int kb_sim_ping_addrs(kb_sim* s, uint32_t node, const uint32_t* peers
 extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* identity, size_t len) {
   if (chk(s, node) || len > MAXID || (len && !identity)) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_set_identity(t, node, identity, len); });
-  // running as the API sees it: the last start/stop queued for the node since the last step, else now
-  int run = -1;
-  for (size_t k = s->events.size(); k-- > 0;) if (s->events[k].node == node) { run = !s->events[k].stop; break; }
-  if (run < 0) {
-    uint8_t a = 0;
-    HIPCHK(hipMemcpy(&a, s->d.alive + node, 1, hipMemcpyDeviceToHost));
-    run = a;
-  }
+  if (s->h_moved[node]) { seterr("the instance bound here restarted at a fresh address"); return KB_INVALID_OPERATION; }
+  int run = 0, ever = 0;
+  { int rc = api_running(s, node, &run); if (!rc) rc = ever_bound(s, node, &ever); if (rc) return rc; }
   if (run) { seterr("Cannot change identity while the mesh is running; call .stop first"); return KB_INVALID_OPERATION; }
   if (len != s->cfg.id_len && s->C > 200) { seterr("non-uniform identity length needs capacity <= 200"); return KB_INVALID_ARGUMENT; }
+  if (ever) {                                      // views keep what the address announced; the instance's
+    memcpy(&s->h_pend[(size_t)node * MAXID], identity, len);   // next address takes the new bytes
+    s->h_pendlen[node] = (int16_t)len;
+    return KB_OK;
+  }
   memcpy(&s->h_ident[(size_t)node * MAXID], identity, len);
   s->h_idlen[node] = (uint8_t)len;
   int rc = upload_segments(s);

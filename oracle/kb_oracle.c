@@ -72,7 +72,8 @@ typedef struct {
 } omsg;
 typedef struct { omsg* v; size_t n, cap; } ovec;
 typedef struct { uint32_t sender, peer, bseq; } obcast;
-typedef struct { int stop; uint32_t node; } oevent;
+typedef struct { int kind; uint32_t node, src; } oevent;   /* kind: EV_START / EV_STOP / EV_RESTART (node = new id, src = old) */
+enum { EV_START = 0, EV_STOP = 1, EV_RESTART = 2 };
 
 struct kbo_sim {
   kb_config cfg;
@@ -92,6 +93,8 @@ struct kbo_sim {
   ocur* cur;                  /* C x CSLOTS */
   uint32_t* paq; uint32_t* paq_n;
   uint8_t* ident; uint8_t* id_len;
+  uint8_t* pend_ident; int16_t* pend_len;   /* identity set on a stopped instance, taken by its next address (-1: none) */
+  uint8_t* moved;                           /* the instance bound here restarted at a fresh address */
   uint32_t* cseg; uint32_t* segmul;   /* crc0(addr||identity), x^(8*seglen) */
   uint32_t* seglen;
   uint32_t mulz_tab[4][256]; int uniform; uint32_t ulen;
@@ -337,6 +340,23 @@ static void node_stop(kbo_sim* s, uint32_t i) {
   s->alive[i] = 0;
   s->paq_n[i] = 0;
 }
+/* Kaboodle::start on a stopped instance (src/lib.rs:136-156): KaboodleInner::start binds a fresh
+ * ephemeral socket (src/kaboodle.rs:138-152), so the instance comes back at a NEW address (`to`, a fresh
+ * id) while its known_peers map persists (the Arc'd ObservableHashMap of src/lib.rs:104, minus the old
+ * self removed by stop, :167-170): every entry with its state, instant and latency.  The old address
+ * stays in other views until pinged out.  Curious peers, the ping queue and last_broadcast_time belong to
+ * the new KaboodleInner (fresh); the A3 sweep front starts after the new self. */
+static void node_restart(kbo_sim* s, uint32_t from, uint32_t to, int32_t r) {
+  const size_t C = s->C;
+  memcpy(row(s, to), row(s, from), C);
+  if (s->lat) memcpy(s->lat + (size_t)to * C, s->lat + (size_t)from * C, C * sizeof(uint16_t));
+  if (s->tst) memcpy(s->tst + (size_t)to * C, s->tst + (size_t)from * C, C * sizeof(int32_t));
+  memcpy(s->susp + (size_t)to * SLOTS, s->susp + (size_t)from * SLOTS, SLOTS * sizeof(osusp));
+  s->n[to] = s->n[from];
+  s->dirty[to] = 1;
+  for (size_t k = 0; k < s->nwatch; ++k) if (s->wnode[k] == from) s->wnode[k] = to;   /* the map's observer */
+  node_start(s, to, r);
+}
 
 /* ---- creation ----------------------------------------------------------------------------------- */
 void kbo_config_default(kb_config* c) {
@@ -364,6 +384,9 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   s->susp = (osusp*)calloc(C * SLOTS, sizeof(osusp)); s->cur = (ocur*)calloc(C * CSLOTS, sizeof(ocur));
   s->paq = (uint32_t*)calloc(C * PAQ, 4); s->paq_n = (uint32_t*)calloc(C, 4);
   s->ident = (uint8_t*)calloc(C * MAXID, 1); s->id_len = (uint8_t*)calloc(C, 1);
+  s->pend_ident = (uint8_t*)calloc(C * MAXID, 1); s->pend_len = (int16_t*)malloc(C * sizeof(int16_t));
+  if (s->pend_len) for (size_t k = 0; k < C; ++k) s->pend_len[k] = -1;
+  s->moved = (uint8_t*)calloc(C, 1);
   s->cseg = (uint32_t*)calloc(C, 4); s->segmul = (uint32_t*)calloc(C, 4); s->seglen = (uint32_t*)calloc(C, 4);
   s->out = (ovec*)calloc(C, sizeof(ovec)); s->oseq = (uint32_t*)calloc(C, 4);
   if (cfg->variant & ~(uint32_t)(KB_VARIANT_SAME_WINDOW_BCAST | KB_VARIANT_EXACT_LRU)) {
@@ -406,7 +429,7 @@ int kbo_sim_destroy(kbo_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
   for (uint32_t i = 0; i < s->C; ++i) free(s->out[i].v);
   free(s->probe_q); free(s->probes); free(s->presp); free(s->stamp); free(s->tst); free(s->lat); free(s->alive); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
-  free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len);
+  free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len); free(s->pend_ident); free(s->pend_len); free(s->moved);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
   for (size_t k = 0; k < s->nwatch; ++k) free(s->wsnap[k]);
   free(s->wnode); free(s->wsnap); free(s->wfp);
@@ -623,7 +646,8 @@ static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
     for (uint32_t j = 0; j < s->C; ++j) {
       uint8_t b = rw[j];
       if (b < ST_ANCIENT || j == i) continue;
-      uint32_t kh = s->tst ? (uint32_t)(s->tst[(size_t)i * s->C + j] - INT32_MIN) : b, kl = rot_key(j, s->a3cur[i], s->C);
+      uint32_t kh = s->tst ? ((uint32_t)s->tst[(size_t)i * s->C + j] ^ 0x80000000u) : b,   /* order-preserving */
+                kl = rot_key(j, s->a3cur[i], s->C);
       if (nb == NUM_CANDIDATES && (kh > bkey_hi[nb - 1] || (kh == bkey_hi[nb - 1] && kl > bkey_lo[nb - 1]))) continue;
       int pos = nb < NUM_CANDIDATES ? nb : NUM_CANDIDATES - 1;
       while (pos > 0 && (bkey_hi[pos - 1] > kh || (bkey_hi[pos - 1] == kh && bkey_lo[pos - 1] > kl))) {
@@ -812,7 +836,8 @@ static int step_round(kbo_sim* s) {
   /* 1. lifecycle: API events in call order, then churn (leaves in id order, joins with fresh ids) */
   for (size_t k = 0; k < s->nev; ++k) {
     uint32_t i = s->ev[k].node;
-    if (s->ev[k].stop) { if (s->alive[i]) node_stop(s, i); }
+    if (s->ev[k].kind == EV_STOP) { if (s->alive[i]) node_stop(s, i); }
+    else if (s->ev[k].kind == EV_RESTART) node_restart(s, s->ev[k].src, i, r);
     else if (!s->alive[i]) node_start(s, i, r);
   }
   s->nev = 0;
@@ -895,16 +920,67 @@ int kbo_sim_step(kbo_sim* s, uint32_t rounds) {
 /* ---- API ---------------------------------------------------------------------------------------- */
 static int check(kbo_sim* s, uint32_t node) { return (!s || node >= s->C) ? KB_INVALID_ARGUMENT : KB_OK; }
 
+static void push_ev(kbo_sim* s, int kind, uint32_t node, uint32_t src) {
+  if (s->nev == s->capev) { s->capev = s->capev ? s->capev * 2 : 16; s->ev = (oevent*)realloc(s->ev, s->capev * sizeof(oevent)); }
+  s->ev[s->nev].kind = kind; s->ev[s->nev].node = node; s->ev[s->nev].src = src; s->nev++;
+}
+/* running as the API sees it: the last lifecycle call queued for the node since the last step (they
+ * take effect at the next round start), else its current state.  A queued restart moves the instance
+ * away from its old address, which stays stopped. */
+static int api_running(const kbo_sim* s, uint32_t node) {
+  for (uint32_t k = s->nev; k-- > 0;) {
+    if (s->ev[k].node == node) return s->ev[k].kind != EV_STOP;
+    if (s->ev[k].kind == EV_RESTART && s->ev[k].src == node) return 0;
+  }
+  return s->alive[node];
+}
+/* the address has been bound by an instance (it ran, or a start of it is queued) */
+static int ever_bound(const kbo_sim* s, uint32_t node) {
+  if (s->start_round[node] != INT32_MIN) return 1;
+  for (uint32_t k = 0; k < s->nev; ++k) if (s->ev[k].node == node && s->ev[k].kind != EV_STOP) return 1;
+  return 0;
+}
+/* the first start of an instance at address `node` (src/lib.rs:136-156); a no-op while running.  A stopped
+ * instance restarts at a fresh address: kbo_sim_restart_node. */
 int kbo_sim_start_node(kbo_sim* s, uint32_t node) {
   if (check(s, node)) return KB_INVALID_ARGUMENT;
-  if (s->nev == s->capev) { s->capev = s->capev ? s->capev * 2 : 16; s->ev = (oevent*)realloc(s->ev, s->capev * sizeof(oevent)); }
-  s->ev[s->nev].stop = 0; s->ev[s->nev].node = node; s->nev++;
+  if (!api_running(s, node) && ever_bound(s, node)) {
+    seterr("a stopped instance restarts at a fresh address (kb_sim_restart_node)");
+    return KB_INVALID_OPERATION;
+  }
+  push_ev(s, EV_START, node, node);
   return KB_OK;
 }
 int kbo_sim_stop_node(kbo_sim* s, uint32_t node) {
   if (check(s, node)) return KB_INVALID_ARGUMENT;
-  if (s->nev == s->capev) { s->capev = s->capev ? s->capev * 2 : 16; s->ev = (oevent*)realloc(s->ev, s->capev * sizeof(oevent)); }
-  s->ev[s->nev].stop = 1; s->ev[s->nev].node = node; s->nev++;
+  push_ev(s, EV_STOP, node, node);
+  return KB_OK;
+}
+/* Kaboodle::start for the instance last bound to `node` (src/lib.rs:136-156): running -> no-op (*out =
+ * node); never bound -> its first start at `node`; stopped -> it binds a fresh ephemeral address
+ * (src/kaboodle.rs:138-152): the next fresh id (the churn reserve, in allocation order) inherits its
+ * known_peers map at the next round start, and carries the instance's identity (the one set while
+ * stopped, if any).  *out = the instance's address from then on. */
+int kbo_sim_restart_node(kbo_sim* s, uint32_t node, uint32_t* out) {
+  if (check(s, node) || !out) return KB_INVALID_ARGUMENT;
+  if (s->moved[node]) { seterr("the instance bound here restarted at a fresh address"); return KB_INVALID_OPERATION; }
+  if (api_running(s, node)) { *out = node; return KB_OK; }
+  if (!ever_bound(s, node)) { push_ev(s, EV_START, node, node); *out = node; return KB_OK; }
+  if (s->next_free >= s->C) { seterr("no fresh address left for the restart (capacity)"); return KB_CAPACITY; }
+  const uint32_t to = s->next_free++;
+  const int pl = s->pend_len[node];
+  const uint8_t* src = pl >= 0 ? s->pend_ident + (size_t)node * MAXID : s->ident + (size_t)node * MAXID;
+  const uint32_t len = pl >= 0 ? (uint32_t)pl : s->id_len[node];
+  memmove(s->ident + (size_t)to * MAXID, src, len);
+  s->id_len[to] = (uint8_t)len;
+  s->pend_len[to] = -1;
+  s->pend_len[node] = -1;
+  compute_seg(s, to);
+  s->uniform = 1;
+  for (uint32_t j = 0; j < s->C; ++j) if (s->id_len[j] != s->cfg.id_len) { s->uniform = 0; break; }
+  push_ev(s, EV_RESTART, to, node);
+  s->moved[node] = 1;
+  *out = to;
   return KB_OK;
 }
 int kbo_sim_is_running(kbo_sim* s, uint32_t node, int* running) {
@@ -924,22 +1000,26 @@ int kbo_sim_ping_addrs(kbo_sim* s, uint32_t node, const uint32_t* peers, size_t 
   }
   return KB_OK;
 }
-/* running as the API sees it: the last start/stop call queued for the node since the last step (they
- * take effect at the next round start), else its current state */
-static int api_running(const kbo_sim* s, uint32_t node) {
-  for (uint32_t k = s->nev; k-- > 0;) if (s->ev[k].node == node) return !s->ev[k].stop;
-  return s->alive[node];
-}
-/* Kaboodle::set_identity (src/lib.rs:323-336): refused while running.  Identity belongs to the id
- * (DESIGN.md §2.1): every view reports and fingerprints the new bytes from now on; a non-uniform length
- * needs capacity <= 200 (the truncation sizes assume one length otherwise). */
+/* Kaboodle::set_identity (src/lib.rs:323-336): refused while running.  Each view holds the identity an
+ * address announced (PeerInfo.identity, written by the envelope prologue, a Join or a KnownPeers entry:
+ * src/kaboodle.rs:409-414, :291-298, :461-468).  An instance changes identity only while stopped and comes
+ * back at a fresh address (kbo_sim_restart_node), so every address keeps one identity for its lifetime
+ * and one table per address equals every view's copy.  Hence: an address never bound takes the bytes
+ * now; the instance stopped at an address that did run keeps them for its next address.  A non-uniform
+ * length needs capacity <= 200 (the truncation sizes assume one length otherwise). */
 int kbo_sim_set_identity(kbo_sim* s, uint32_t node, const uint8_t* identity, size_t len) {
   if (check(s, node) || len > MAXID || (len && !identity)) return KB_INVALID_ARGUMENT;
+  if (s->moved[node]) { seterr("the instance bound here restarted at a fresh address"); return KB_INVALID_OPERATION; }
   if (api_running(s, node)) {
     seterr("Cannot change identity while the mesh is running; call .stop first");
     return KB_INVALID_OPERATION;
   }
   if (len != s->cfg.id_len && s->C > 200) { seterr("non-uniform identity length needs capacity <= 200"); return KB_INVALID_ARGUMENT; }
+  if (ever_bound(s, node)) {
+    memcpy(s->pend_ident + (size_t)node * MAXID, identity, len);
+    s->pend_len[node] = (int16_t)len;
+    return KB_OK;
+  }
   memcpy(s->ident + (size_t)node * MAXID, identity, len);
   s->id_len[node] = (uint8_t)len;
   compute_seg(s, node);
@@ -972,7 +1052,7 @@ int kbo_sim_probe_responses(kbo_sim* s, kb_probe_response* out, size_t cap, size
   *n = s->npresp;
   if (!out) return KB_OK;
   if (cap < s->npresp) return KB_CAPACITY;
-  memcpy(out, s->presp, s->npresp * sizeof(kb_probe_response));
+  if (s->npresp) memcpy(out, s->presp, s->npresp * sizeof(kb_probe_response));
   s->npresp = 0;
   return KB_OK;
 }

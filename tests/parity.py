@@ -150,19 +150,29 @@ def compare_sampled(o: Sim, g: Sim, rng, nrows: int = 24) -> list[str]:
     return out
 
 
-def apply_events(sims, case: dict, r: int) -> None:
+def apply_events(sims, case: dict, r: int) -> dict:
+    """The case's API calls of round r on every implementation; returns {old address: new address} of
+    the restarts (each implementation must allocate the same fresh id)."""
+    moved = {}
     for kind, node, arg in case.get("events", {}).get(r, []):
+        got = set()
         for s in sims:
             if kind == "stop":
                 s.stop_node(node)
             elif kind == "start":
                 s.start_node(node)
+            elif kind == "restart":
+                got.add(s.restart_node(node))
             elif kind == "ident":
                 s.set_identity(node, arg)
             elif kind == "probe":
                 s.probe(arg)
             elif kind == "ping":
                 s.ping_addrs(node, arg)
+        if kind == "restart":
+            assert len(got) == 1, f"restart of {node}: implementations allocated {got}"
+            moved[node] = got.pop()
+    return moved
 
 
 def run_events_case(case: dict, rounds: int, watched, drain_every: int = 1, shards: int = 0,
@@ -184,8 +194,12 @@ def run_events_case(case: dict, rounds: int, watched, drain_every: int = 1, shar
     prev = {i: set() for i in watched}
     last_fp = {i: 0 for i in watched}
     n = 0
+    watched = list(watched)
     for r in range(rounds):
-        apply_events((o, g), case, r)
+        for a, b in apply_events((o, g), case, r).items():     # the observer follows the instance
+            if a in watched:
+                watched[watched.index(a)] = b
+                prev[b], last_fp[b] = prev.pop(a), last_fp.pop(a)
         o.step(1)
         g.step(1)
         if (r + 1) % drain_every and r != rounds - 1:
@@ -228,7 +242,8 @@ def standard_cases() -> list[tuple[str, dict, int]]:
     cases.append(("stop_start", {"cfg": SimConfig(capacity=128, initial_nodes=100, init_mode=KB_INIT_CONVERGED,
                                                   seed=2),
                                  "events": {2: [("stop", 5, None), ("stop", 17, None)], 4: [("start", 120, None)],
-                                            9: [("start", 5, None)]}}, 20))
+                                            9: [("restart", 5, None)], 12: [("stop", 100, None)],
+                                            14: [("restart", 100, None), ("restart", 17, None)]}}, 20))
     cases.append(("rebase_window", {"cfg": SimConfig(capacity=192, initial_nodes=192, init_mode=KB_INIT_CONVERGED,
                                                      loss=0.01, churn=0.002, seed=4)}, 140))
     cases.append(("waves_2", {"cfg": SimConfig(capacity=256, initial_nodes=256, loss=0.03, max_waves=2, seed=13)}, 15))
@@ -241,9 +256,9 @@ def standard_cases() -> list[tuple[str, dict, int]]:
                                                        loss=0.02, id_len=6, seed=23),
                                       "events": {2: [("stop", 9, None), ("stop", 70, None)],
                                                  3: [("ident", 9, b"qwerty"), ("ident", 70, b"short"),
-                                                     ("start", 9, None)],
+                                                     ("restart", 9, None)],
                                                  5: [("ident", 155, b"fresh-peer-id"), ("start", 155, None),
-                                                     ("start", 70, None)]}}, 16))
+                                                     ("restart", 70, None)]}}, 16))
     # SwimBroadcast::Probe from outside the mesh (src/discovery.rs:30-89): ProbeResponses of the peers that
     # should_respond, in a small mesh (everyone answers: n <= 2) and a lossy converged one (about 1 %)
     cases.append(("probes", {"cfg": SimConfig(capacity=400, initial_nodes=396, init_mode=KB_INIT_CONVERGED, loss=0.03,

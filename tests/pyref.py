@@ -73,11 +73,21 @@ def default_identity(i: int, n: int) -> bytes:
 
 
 def fingerprint(ids, identity) -> int:
-    """generate_fingerprint (src/kaboodle.rs:71-83), literally."""
+    """generate_fingerprint (src/kaboodle.rs:71-83), literally, over ids with one identity table."""
     h = 0
     for p in sorted(ids):
         h = zlib.crc32(addr(p).encode(), h)
         h = zlib.crc32(identity[p], h)
+    return h
+
+
+def view_fingerprint(known) -> int:
+    """generate_fingerprint of one peer's map: every entry's address and the identity THIS view holds for
+    it (PeerInfo.identity, src/kaboodle.rs:77-79)."""
+    h = 0
+    for p in sorted(known):
+        h = zlib.crc32(addr(p).encode(), h)
+        h = zlib.crc32(known[p][2], h)
     return h
 
 
@@ -96,7 +106,7 @@ class Peer:
         self.running = False
         self.ever = False
         self.start_round = None
-        self.known = {}          # peer -> [state, instant]
+        self.known = {}          # peer -> [state, instant, identity]: PeerInfo (src/structs.rs:18-22)
         self.latency = {}        # peer -> PeerInfo.latency in ms (absent = None)
         self.a3cur = i           # A3's rotation base: just before the last round's oldest candidate (§2.6)
         self.curious = {}        # peer -> [observers]
@@ -114,7 +124,8 @@ class PyMesh:
         self.fault_end, self.max_waves, self.failed_honoured = fault_end, max_waves, failed_honoured
         self.partition = partition      # (groups, start, end) or None
         self.id_len = id_len
-        self.identity = [default_identity(i, id_len) for i in range(capacity)]
+        self.identity = [default_identity(i, id_len) for i in range(capacity)]   # what each address announces
+        self.pending = {}        # identity set on a stopped instance, taken by its next address
         self.peers = [Peer(i) for i in range(capacity)]
         self.round = 0
         self.next_free = initial_nodes
@@ -132,7 +143,7 @@ class PyMesh:
                 p = self.peers[i]
                 for j in range(initial_nodes):
                     if j != i:
-                        p.known[j] = [KNOWN, -(10 ** 6)]    # an instant long before the stamp window
+                        p.known[j] = [KNOWN, -(10 ** 6), self.identity[j]]   # long before the stamp window
                 p.last_bcast = -1000
 
     # ---------------------------------------------------------------- helpers
@@ -155,7 +166,7 @@ class PyMesh:
         p.running, p.ever, p.start_round = True, True, r
         if i not in p.known:
             p.latency.pop(i, None)
-        p.known[i] = [KNOWN, r]
+        p.known[i] = [KNOWN, r, self.identity[i]]
         p.a3cur = i
         p.last_bcast = None
         p.curious = {}
@@ -167,14 +178,46 @@ class PyMesh:
         p.running = False
         p.paq = []
 
+    def _api_running(self, i):
+        for ev in reversed(self.events):
+            if ev[1] == i:
+                return ev[0] != "stop"
+            if ev[0] == "restart" and ev[2] == i:
+                return False
+        return self.peers[i].running
+
+    def _ever(self, i):
+        return self.peers[i].ever or any(ev[1] == i and ev[0] != "stop" for ev in self.events)
+
     def set_identity(self, i, ident: bytes):
-        self.identity[i] = ident
+        """Kaboodle::set_identity (src/lib.rs:323-336) on a stopped instance: the identity it will announce
+        from its next start on (a never-bound address takes it at once)."""
+        assert not self._api_running(i)
+        if self._ever(i):
+            self.pending[i] = ident
+        else:
+            self.identity[i] = ident
 
     def start_node(self, i):
-        self.events.append(("start", i))
+        assert self._api_running(i) or not self._ever(i)
+        self.events.append(("start", i, i))
 
     def stop_node(self, i):
-        self.events.append(("stop", i))
+        self.events.append(("stop", i, i))
+
+    def restart_node(self, i):
+        """Kaboodle::start of the instance at address i: a stopped instance binds a fresh ephemeral socket
+        (src/kaboodle.rs:138-152) and keeps its known_peers map (src/lib.rs:104, 167-170)."""
+        if self._api_running(i):
+            return i
+        if not self._ever(i):
+            self.events.append(("start", i, i))
+            return i
+        new = self.next_free
+        self.next_free += 1
+        self.identity[new] = self.pending.pop(i, self.identity[i])
+        self.events.append(("restart", new, i))
+        return new
 
     def ping_addrs(self, i, addrs):
         p = self.peers[i]
@@ -189,10 +232,15 @@ class PyMesh:
     def step(self):
         r = self.round
         self.out = {}
-        for kind, i in self.events:
+        for kind, i, src in self.events:
             if kind == "stop" and self.peers[i].running:
                 self._stop(i)
             elif kind == "start" and not self.peers[i].running:
+                self._start(i, r)
+            elif kind == "restart":                       # the map moves with the instance
+                old, new = self.peers[src], self.peers[i]
+                new.known = {q: list(v) for q, v in old.known.items()}
+                new.latency = dict(old.latency)
                 self._start(i, r)
         self.events = []
         if self.faults(r) and self.churn_thr:
@@ -218,12 +266,12 @@ class PyMesh:
             j, f = self.tick(self.peers[i], r)
             bseq = 0
             if j:
-                bjoin.append((i, i, bseq))
+                bjoin.append((i, i, bseq, self.identity[i]))    # Join{addr, identity} (:228-251)
                 bseq += 1
             for q in f:
-                bfail.append((i, q, bseq))
+                bfail.append((i, q, bseq, None))
                 bseq += 1
-            agree += fingerprint(self.peers[i].known, self.identity) == true_fp
+            agree += view_fingerprint(self.peers[i].known) == true_fp
         self.bjoin, self.bfail = bjoin, bfail
         self.stats["bcast_join"] += len(bjoin)
         self.stats["bcast_failed"] += len(bfail)
@@ -239,7 +287,7 @@ class PyMesh:
 
     # handle_incoming_broadcasts (src/kaboodle.rs:256-311)
     def broadcasts(self, p, r):
-        for e, (s, peer, bseq) in enumerate(self.bfail):
+        for e, (s, peer, bseq, _) in enumerate(self.bfail):
             if s == p.id:
                 continue
             if self.lost_b(p.id, s, 0, e, r):
@@ -249,13 +297,13 @@ class PyMesh:
             if self.failed_honoured and s in p.known and peer in p.known:
                 del p.known[peer]
                 self.stats["removed_failed"] += 1
-        for e, (a, _, bseq) in enumerate(self.bjoin):
+        for e, (a, _, bseq, ident) in enumerate(self.bjoin):
             if a == p.id or self.lost_b(p.id, a, 1, e, r):
                 continue
             is_new = a not in p.known
             if is_new:
                 p.latency.pop(a, None)                    # :294-296 keeps an existing entry's latency
-            p.known[a] = [KNOWN, r]
+            p.known[a] = [KNOWN, r, ident]                # Join{addr, identity} (:284-298)
             if is_new and self.should_respond(p, a, r):
                 self.send_known_peers_to(p, a, r)
 
@@ -287,7 +335,7 @@ class PyMesh:
             key = self.ph(p.id, r, P_TRUNC << 24, joiner)
             chosen = {prp_walk(t, n, key) for t in range(cap)}
             members = [members[k] for k in sorted(chosen)]
-        self.emit(p.id, joiner, "KnownPeers", peers=members)
+        self.emit(p.id, joiner, "KnownPeers", peers=[(q, p.known[q][2]) for q in members])
         self.stats["join_responses"] += 1
 
     # tick (src/kaboodle.rs:746-779)
@@ -297,10 +345,10 @@ class PyMesh:
             join = True
             p.last_bcast = r
         # handle_suspected_peers :558-653
-        cands = sorted(q for q, (st, _) in p.known.items() if st == KNOWN and q != p.id)
+        cands = sorted(q for q, (st, _, _) in p.known.items() if st == KNOWN and q != p.id)
         removed, indirect = [], []
         for q in sorted(p.known):
-            st, t = p.known[q]
+            st, t, _ = p.known[q]
             if st == KNOWN or r - t < PING_TIMEOUT:
                 continue
             if st == WFP:
@@ -326,7 +374,7 @@ class PyMesh:
             else:
                 removed.append(q)
         for q in indirect:
-            p.known[q] = [WFIP, r]
+            p.known[q] = [WFIP, r, p.known[q][2]]
         fails = []
         for q in removed:
             del p.known[q]
@@ -334,13 +382,13 @@ class PyMesh:
             fails.append(q)
             self.stats["removed_timeout"] += 1
         # ping_random_peer :655-703
-        c = [q for q, (st, _) in p.known.items() if st == KNOWN and q != p.id]
+        c = [q for q, (st, _, _) in p.known.items() if st == KNOWN and q != p.id]
         c.sort(key=lambda q: (stamp_key(p.known[q][1], r), (q - p.a3cur - 1) % self.C))
         c = c[:NUM_CANDIDATES]
         if c:
             t = c[mulhi(self.ph(p.id, r, P_PING << 24, 0)[0], len(c))]
             p.a3cur = (c[0] - 1) % self.C           # the sweep front: just before the oldest candidate
-            p.known[t] = [WFP, r]
+            p.known[t] = [WFP, r, p.known[t][2]]
             self.emit(p.id, t, "Ping")
         for a in p.paq:                                   # :550-556
             self.emit(p.id, a, "Ping")
@@ -387,7 +435,7 @@ class PyMesh:
     def handle(self, p, m, r, w=0):
         s = m["sender"]
         self.observe_latency(p, s, r, w)
-        p.known[s] = [KNOWN, r]                                   # :406-415
+        p.known[s] = [KNOWN, r, self.identity[s]]                 # :406-415: the envelope's identity
         kind = m["kind"]
         if kind == "Ack":                                         # :418-447
             peer = m["peer"]
@@ -397,20 +445,20 @@ class PyMesh:
                     self.emit(p.id, o, "Ack", peer=peer, fp=m["fp"], n=m["n"])
             self.maybe_sync(p, peer, m["fp"], m["n"])
         elif kind == "KnownPeers":                                # :448-472
-            for q in m["peers"]:
+            for q, ident in m["peers"]:
                 if q not in p.known:
                     p.latency.pop(q, None)                        # latency: None (:467)
-                    p.known[q] = [KNOWN, r - SHARE_AGE]
+                    p.known[q] = [KNOWN, r - SHARE_AGE, ident]    # the listed PeerInfo's identity (:461-468)
         elif kind == "KnownPeersRequest":                         # :473-512
-            lst = sorted(q for q, (st, t) in p.known.items()
+            lst = sorted(q for q, (st, t, _) in p.known.items()
                          if st == KNOWN and q != p.id and q != s and r - t < SHARE_AGE)
             if self.kp_size(p.id, lst) > BUFSZ:
                 self.stats["drop_oversize"] += 1
             else:
-                self.emit(p.id, s, "KnownPeers", peers=lst)
+                self.emit(p.id, s, "KnownPeers", peers=[(q, p.known[q][2]) for q in lst])
             self.maybe_sync(p, s, m["fp"], m["n"])
         elif kind == "Ping":                                      # :513-532
-            self.emit(p.id, s, "Ack", peer=p.id, fp=fingerprint(p.known, self.identity), n=len(p.known))
+            self.emit(p.id, s, "Ack", peer=p.id, fp=view_fingerprint(p.known), n=len(p.known))
         elif kind == "PingRequest":                               # :533-545
             peer = m["peer"]
             if peer in p.curious:
@@ -434,7 +482,7 @@ class PyMesh:
         if old is None:
             p.latency.pop(s, None)
             return
-        st, t = old
+        st, t, _ = old
         if st == KNOWN:
             return
         sample = 1000 * (r - t) + w + 1
@@ -442,7 +490,7 @@ class PyMesh:
         p.latency[s] = sample if prev is None else int((sample * 0.8) + (prev * (1.0 - 0.8)))
 
     def maybe_sync(self, p, peer, their_fp, their_n):           # :707-740
-        f = fingerprint(p.known, self.identity)
+        f = view_fingerprint(p.known)
         if f == their_fp or len(p.known) > their_n:
             return
         self.emit(p.id, peer, "KnownPeersRequest", fp=f, n=len(p.known))
@@ -451,7 +499,7 @@ class PyMesh:
     def row(self, i):
         """the dense stamp-byte view of peer i's map, for comparison with the oracle"""
         out = [0] * self.C
-        for q, (st, t) in self.peers[i].known.items():
+        for q, (st, t, _) in self.peers[i].known.items():
             out[q] = 1 if st != KNOWN else stamp_key(t, max(self.round - 1, 0))
         return out
 
@@ -462,16 +510,16 @@ class PyMesh:
         rl = max(self.round - 1, 0)
         out = []
         p = self.peers[i]
-        for q, (st, t) in sorted(p.known.items()):
+        for q, (st, t, ident) in sorted(p.known.items()):
             lat = p.latency.get(q, 0xFFFFFFFF)
             if st == KNOWN:
-                out.append((q, 0, t if stamp_key(t, rl) > 2 else -2 ** 31, lat, self.identity[q]))
+                out.append((q, 0, t if stamp_key(t, rl) > 2 else -2 ** 31, lat, ident))
             else:
-                out.append((q, 1 if st == WFP else 2, t, lat, self.identity[q]))
+                out.append((q, 1 if st == WFP else 2, t, lat, ident))
         return out
 
     def suspects(self, i):
-        return sorted((q, 1 if st == WFP else 2, t) for q, (st, t) in self.peers[i].known.items() if st != KNOWN)
+        return sorted((q, 1 if st == WFP else 2, t) for q, (st, t, _) in self.peers[i].known.items() if st != KNOWN)
 
     def curious_view(self, i):
         return sorted((q, len(o), *(list(o) + [-1] * (NOBS - len(o)))) for q, o in self.peers[i].curious.items())

@@ -33,8 +33,10 @@ SCENARIOS = [
     _sc("partition", SimConfig(capacity=32, initial_nodes=32, init_mode=KB_INIT_CONVERGED, seed=4, loss=0.02,
                                partition_groups=2, partition_start=3, partition_end=10), 25,
         events={10: [("ping", i, [(i + 16) % 32]) for i in range(0, 32, 4)]}),
+    # a stopped instance restarts at a fresh address (src/kaboodle.rs:138-152) with its map (src/lib.rs:104):
+    # 3 comes back as id 20, the first fresh id; 22 is a first start
     _sc("stop_start", SimConfig(capacity=24, initial_nodes=20, init_mode=KB_INIT_CONVERGED, seed=6), 15,
-        events={2: [("stop", 3, None)], 4: [("start", 22, None)], 8: [("start", 3, None)]}),
+        events={2: [("stop", 3, None)], 4: [("start", 22, None)], 8: [("restart", 3, None)]}),
     _sc("rebase", SimConfig(capacity=24, initial_nodes=24, init_mode=KB_INIT_CONVERGED, seed=8, loss=0.02,
                             churn=0.01), 140),
     _sc("waves2", SimConfig(capacity=40, initial_nodes=40, seed=13, loss=0.03, max_waves=2), 15),
@@ -46,12 +48,13 @@ SCENARIOS = [
     _sc("old_stamps", SimConfig(capacity=160, initial_nodes=128, init_mode=KB_INIT_CONVERGED, loss=0.02, churn=0.03,
                                 fault_end_round=12, seed=31), 200),
     # Kaboodle::set_identity on stopped peers (src/lib.rs:323-336): one keeps the uniform length, one does not;
-    # both restart under the new identity and every view's fingerprint follows
+    # both restart at fresh addresses (36, 37) under the new identity, while the views that still hold 5 and 11
+    # keep the identities those addresses announced; 38 is set before its first start
     _sc("identity_change", SimConfig(capacity=40, initial_nodes=36, init_mode=KB_INIT_CONVERGED, seed=19, loss=0.03,
                                      id_len=4), 24,
         events={2: [("stop", 5, None), ("stop", 11, None)], 3: [("ident", 5, b"wxyz"), ("ident", 11, b"zz"),
-                                                                ("start", 5, None)],
-                6: [("ident", 38, b"new-peer"), ("start", 38, None), ("start", 11, None)]}),
+                                                                ("restart", 5, None)],
+                6: [("ident", 38, b"new-peer"), ("start", 38, None), ("restart", 11, None)]}),
 ]
 
 BY_NAME = {s["name"]: s for s in SCENARIOS}
@@ -81,6 +84,8 @@ def apply_events(sim, sc, r):
             sim.stop_node(node)
         elif kind == "start":
             sim.start_node(node)
+        elif kind == "restart":
+            sim.restart_node(node)
         elif kind == "ident":
             sim.set_identity(node, arg)
         else:
@@ -107,7 +112,7 @@ def digest_pymesh(pm) -> dict:
     import pyref
     C = pm.C
     rows = np.array([pm.row(i) for i in range(C)], dtype=np.uint8)
-    fps = np.array([pyref.fingerprint(p.known, pm.identity) if p.running else 0 for p in pm.peers], np.uint32)
+    fps = np.array([pyref.view_fingerprint(p.known) if p.running else 0 for p in pm.peers], np.uint32)
     susp = [s for i in range(C) for s in [(i,) + tuple(x) for x in pm.suspects(i)]]
     cur = [s for i in range(C) for s in [(i,) + tuple(x) for x in pm.curious_view(i)]]
     return {"rows": _crc(rows.tobytes()), "fps": _crc(fps.tobytes()), "susp": _crc(repr(susp).encode()),

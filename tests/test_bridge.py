@@ -1,8 +1,10 @@
 """The bridge between a simulated mesh and real instances (kaboodle_amd.bridge) and the networking.rs
-plumbing (kaboodle_amd.networking), on loopback sockets with the CPU oracle standing in for the mesh: a
-real discover_mesh_member's Probe datagram reaches the mesh, the ProbeResponse comes back to the prober's
-socket and decodes as discovery.rs decodes it, and the mesh's Join broadcasts go out as SwimBroadcast
-datagrams a real instance decodes."""
+plumbing (kaboodle_amd.networking), on loopback sockets: a real discover_mesh_member's Probe datagram
+reaches the mesh, the ProbeResponse comes back to the prober's socket and decodes as discovery.rs decodes
+it; the mesh's Join broadcasts go out only when forwarding is asked for (by default they would fill real
+views with unreachable members, kaboodle_amd/bridge.py), as SwimBroadcast datagrams a real instance
+decodes.  The CPU oracle stands in for the mesh here; test_bridge_hip_mesh runs the same exchange against
+the HIP library on an MI355X."""
 import os
 import socket
 import time
@@ -22,43 +24,75 @@ def _udp():
     return s
 
 
-def test_probe_over_udp_and_join_broadcasts():
+def _exchange(mesh):
+    """one Probe in, the ProbeResponses out; Joins forwarded only by the opted-in bridge"""
     from kaboodle_amd import wire
     from kaboodle_amd.bridge import Bridge
     bin_ = _udp()
     bin_.setblocking(False)
     listener = _udp()                      # stands in for the broadcast address: what real instances receive
+    listener.settimeout(0.3)
     uni = _udp()
     prober = _udp()                        # a real discover_mesh_member's socket
-    with Sim(parity.oracle_lib(), SimConfig(capacity=8, initial_nodes=0, id_len=5, seed=3)) as o:
-        for i in range(2):
-            o.start_node(i)
-        br = Bridge(o, sockets=(bin_, bin_, listener.getsockname(), uni))
-        br.run_round()                     # round 0: the two Joins go out
-        got = []
-        for _ in range(2):
-            dg, _src = listener.recvfrom(wire.INCOMING_BUFFER_SIZE)
-            got.append(wire.receive(dg, "broadcast"))
-        assert [(g["kind"], wire.id_of(g["peer"]), g["identity"]) for g in got] == \
-            [("Join", 0, o.identity(0)), ("Join", 1, o.identity(1))]
-        # discover_mesh_member: Probe(self_addr) to the broadcast port
-        paddr = prober.getsockname()
-        prober.sendto(wire.encode("Probe", peer=paddr), bin_.getsockname())
-        time.sleep(0.05)
-        br.run_round()                     # ingested, delivered with round 1's broadcasts
-        assert br.stats["probes_in"] == 1
-        dg, src = prober.recvfrom(1024)
-        env = wire.receive(dg, "discovery")          # discovery.rs:81 reads it as a SwimEnvelope
-        assert src == uni.getsockname() and env["identity"] in (o.identity(0), o.identity(1))
-        assert br.stats["probe_responses_out"] == 2  # n = 2: both answer (o = 0)
-        # a real instance's Join is not a simulated peer: counted, dropped
-        prober.sendto(wire.encode("Join", identity=b"real", peer=paddr), bin_.getsockname())
-        time.sleep(0.05)
-        br.run_round()
-        assert br.stats["external_join"] == 1
-        br.close()
+    for i in range(2):
+        mesh.start_node(i)
+    br = Bridge(mesh, sockets=(bin_, bin_, listener.getsockname(), uni))
+    br.run_round()                         # round 0: the two Joins stay inside the mesh
+    with pytest.raises(socket.timeout):
+        listener.recvfrom(wire.INCOMING_BUFFER_SIZE)
+    assert br.stats["broadcasts_out"] == 0
+    # discover_mesh_member: Probe(self_addr) to the broadcast port
+    paddr = prober.getsockname()
+    prober.sendto(wire.encode("Probe", peer=paddr), bin_.getsockname())
+    time.sleep(0.05)
+    br.run_round()                         # ingested, delivered with round 1's broadcasts
+    assert br.stats["probes_in"] == 1
+    dg, src = prober.recvfrom(1024)
+    env = wire.receive(dg, "discovery")    # discovery.rs:81 reads it as a SwimEnvelope
+    assert src == uni.getsockname() and env["identity"] in (mesh.identity(0), mesh.identity(1))
+    assert br.stats["probe_responses_out"] == 2  # n = 2: both answer (o = 0)
+    # a real instance's Join is not a simulated peer: counted, dropped
+    prober.sendto(wire.encode("Join", identity=b"real", peer=paddr), bin_.getsockname())
+    time.sleep(0.05)
+    br.run_round()
+    assert br.stats["external_join"] == 1
+    # forwarding on: the next Join broadcasts go out as SwimBroadcast::Join datagrams
+    mesh.start_node(2)
+    br.forward_broadcasts = True
+    br.run_round()                         # round 3: node 2's Join
+    dg, _src = listener.recvfrom(wire.INCOMING_BUFFER_SIZE)
+    g = wire.receive(dg, "broadcast")
+    assert (g["kind"], wire.id_of(g["peer"]), g["identity"]) == ("Join", 2, mesh.identity(2))
+    br.close()
     for s in (listener, prober):
         s.close()
+
+
+def test_probe_over_udp_and_join_broadcasts():
+    with Sim(parity.oracle_lib(), SimConfig(capacity=8, initial_nodes=0, id_len=5, seed=3)) as o:
+        _exchange(o)
+
+
+@pytest.mark.gpu
+def test_bridge_hip_mesh():
+    """The same exchange against the HIP library's mesh (kaboodle_amd.Mesh) on an MI355X."""
+    import kaboodle_amd
+    kaboodle_amd.require_gpu()
+    with kaboodle_amd.Mesh(SimConfig(capacity=8, initial_nodes=0, id_len=5, seed=3)) as m:
+        _exchange(m)
+
+
+def test_bridge_default_interface_and_ipv6(monkeypatch):
+    """Bridge(mesh) with no interface takes best_available_interface() (Kaboodle::new, src/lib.rs:98);
+    an IPv6 interface is refused with a clear error (the codec carries IPv4 addresses)."""
+    from kaboodle_amd import bridge, networking
+    monkeypatch.setattr(bridge, "best_available_interface", lambda: networking.Interface("lo", "127.0.0.1", None))
+    br = bridge.Bridge(object(), broadcast_port=0)
+    assert br.usock.getsockname()[0] == "127.0.0.1" and not br.forward_broadcasts
+    br.close()
+    monkeypatch.setattr(bridge, "best_available_interface", lambda: networking.Interface("v6", "fe80::1", 2))
+    with pytest.raises(ValueError, match="IPv6"):
+        bridge.Bridge(object(), broadcast_port=0)
 
 
 def test_networking_plumbing():

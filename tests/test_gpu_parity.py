@@ -51,9 +51,11 @@ def test_parity_wave_graph(gpu, name):
 
 
 def test_identity_change_on_stopped_peer(gpu):
-    """Kaboodle::set_identity (src/lib.rs:323-336): refused while running (counting queued start/stop calls),
-    allowed once stopped; after the restart every view reports the new bytes (peers / peer_states) and
-    its fingerprint is generate_fingerprint over the new identities (kb_fingerprint_of_set)."""
+    """Kaboodle::set_identity (src/lib.rs:323-336) and start after stop (:136-156): refused while running
+    (counting queued start/stop calls), allowed once stopped; the restarted instance binds a fresh address
+    (src/kaboodle.rs:138-152) that inherits its map and announces the new bytes, while the views holding
+    the old address keep the identity it announced.  Every fingerprint is generate_fingerprint over one
+    identity per address (kb_fingerprint_of_set), on both implementations."""
     import ctypes as C
     cfg = SimConfig(capacity=512, initial_nodes=500, init_mode=KB_INIT_CONVERGED, id_len=6, seed=12)
     lib = C.CDLL(parity.GPU_SO)
@@ -63,41 +65,45 @@ def test_identity_change_on_stopped_peer(gpu):
     with Sim(parity.oracle_lib(), cfg) as o, Sim(gpu, cfg) as g:
         for s in (o, g):
             s.step(2)
-        fp_before = g.fingerprints()
+        old7 = g.identity(7)
+        news = set()
         for s in (o, g):
             with pytest.raises(KbError) as e:
                 s.set_identity(7, b"abcdef")
             assert e.value.code == KB_INVALID_OPERATION
             s.stop_node(7)
             s.set_identity(7, b"abcdef")           # stop queued: no longer running as the API sees it
-            s.start_node(7)
             with pytest.raises(KbError):
-                s.set_identity(7, b"ghijkl")      # start queued: running again
+                s.start_node(7)                    # it ran: a restart binds a fresh address
+            news.add(s.restart_node(7))
+            with pytest.raises(KbError):
+                s.set_identity(7, b"ghijkl")       # the instance moved on: address 7 stays stopped, but
+        new = news.pop()                           # ... its restart is queued under the new address
+        assert new == 500 and not news
         o.step(1)
         g.step(1)
-        assert g.identity(7) == o.identity(7) == b"abcdef"
+        assert g.identity(7) == o.identity(7) == old7 and g.identity(new) == o.identity(new) == b"abcdef"
+        assert g.is_running(new) and not g.is_running(7)
         fo, fg = o.fingerprints(), g.fingerprints()
         assert np.array_equal(fo, fg)
+        assert g.peer_states(new) == o.peer_states(new)
         idents = np.zeros((cfg.capacity, 32), dtype=np.uint8)
         lens = np.zeros(cfg.capacity, dtype=np.uint8)
         for j in range(cfg.capacity):
             b = g.identity(j)
             idents[j, :len(b)] = np.frombuffer(b, dtype=np.uint8)
             lens[j] = len(b)
-        changed = 0
-        for i in range(0, 500, 37):
+        for i in list(range(0, 500, 37)) + [new]:
             p = g.peers(i)
             want = f((C.c_uint32 * len(p))(*p), len(p), idents.ctypes.data, 32, lens.ctypes.data)
             assert want == fg[i], f"node {i}"
-            changed += 7 in p and fg[i] != fp_before[i]
             ps = {e[0]: e[4] for e in g.peer_states(i)}
-            if 7 in ps:
-                assert ps[7] == b"abcdef"
-        assert changed > 0
+            assert ps.get(7, old7) == old7 and ps.get(new, b"abcdef") == b"abcdef"
         for _ in range(3):
             o.step(1)
             g.step(1)
             assert np.array_equal(o.fingerprints(), g.fingerprints())
+            assert np.array_equal(o.row(new), g.row(new))
 
 
 def test_wide_row_paths_are_hit(gpu):

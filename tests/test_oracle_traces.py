@@ -36,7 +36,7 @@ def test_oracle_matches_trace(name):
         assert o.stats()["first_converged_round"] == TRACES[name]["first_converged"]
 
 
-@pytest.mark.parametrize("name", ["config1", "churn40", "partition", "stop_start", "rebase"])
+@pytest.mark.parametrize("name", ["config1", "churn40", "partition", "stop_start", "rebase", "identity_change"])
 def test_oracle_live_pin(name):
     """Full-state comparison with pyref, every round: rows, suspects, curious, peer_states (across the
     64-round stamp-window rebases in "rebase"), fingerprints, counters."""
@@ -58,7 +58,7 @@ def test_oracle_live_pin(name):
                 ps = o.peer_states(i)
                 assert ps == pm.peer_states(i), f"round {r} node {i} peer_states"
                 measured += sum(1 for e in ps if e[3] != 0xFFFFFFFF)
-                want = pyref.fingerprint(pm.peers[i].known, pm.identity) if pm.peers[i].running else 0
+                want = pyref.view_fingerprint(pm.peers[i].known) if pm.peers[i].running else 0
                 assert o.fingerprint(i) == want if pm.peers[i].running else True
             st = o.stats()
             assert {k: st[k] for k in scenarios.STAT_KEYS} == {k: pm.stats[k] for k in scenarios.STAT_KEYS}
