@@ -108,14 +108,16 @@ def pmc_summary(cfg_key: str, capacity: int, steps: int, warmup: int, failed_mod
 
 def committed_tail(cfg_key: str, mode: str):
     """The full quiescent tail of this workload (tools/converge.py, run to agreement or a cap of 2-4 N rounds
-    on an MI355X; profiles/*converge*.json): too long for the bench's minutes, so read from the record."""
+    on an MI355X; profiles/*converge*.json): too long for the bench's minutes, so read from the record —
+    only a record made with this very library build (lib_sha16), like pmc_summary."""
     best = None
+    sha = lib_sha16()
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*converge*.json"))):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if d.get("workload", "").startswith(cfg_key) and d.get("failed_mode") == mode:
+        if d.get("workload", "").startswith(cfg_key) and d.get("failed_mode") == mode and d.get("lib_sha16") == sha:
             best = {k: d[k] for k in ("converged_round", "tail_rounds_to_converge", "tail_rounds_run", "cap_rounds",
                                       "stopped_by") if k in d}
             best["source"] = os.path.relpath(p, ROOT)

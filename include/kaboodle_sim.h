@@ -88,7 +88,10 @@ typedef struct kb_config {
 } kb_config;
 enum { KB_VARIANT_SAME_WINDOW_BCAST = 1u,   /* Join/Failed delivered in the round they are sent, right after
                                                the tick (src/kaboodle.rs:770-778), not at the next round start */
-       KB_VARIANT_EXACT_LRU = 2u };         /* A3 orders by the exact instant (no stamp window, no ancient ties) */
+       KB_VARIANT_EXACT_LRU = 2u,           /* A3 orders by the exact instant (no stamp window, no ancient ties) */
+       KB_VARIANT_SPARSE_ROWS = 4u };       /* the same semantics on sparse rows: a shared base set, per-row
+                                               exceptions and an explicit list of the non-ancient stamps
+                                               (the configs[4] representation); no latency table */
 
 /* debug_flags: each forces the code path a mesh of >= 1M ids takes, so that path is
    parity-tested at sizes the oracle finishes in seconds. */

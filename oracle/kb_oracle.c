@@ -79,7 +79,12 @@ struct kbo_sim {
   kb_config cfg;
   uint32_t C;
   uint32_t k0, k1;
-  uint8_t* stamp;
+  uint8_t* stamp;              /* C x C dense stamp rows (NULL with KB_VARIANT_SPARSE_ROWS: sr below) */
+  struct srow* sr;             /* KB_VARIANT_SPARSE_ROWS: per-row exceptions + explicit stamps */
+  uint32_t* bbits;             /* sparse: the shared base set (the initial members), bitset */
+  uint32_t* bcnt;              /* sparse: bcnt[k] = |base ∩ [0, k)|, k = 0..C */
+  uint32_t* bpre;              /* sparse: bpre[k] = crc0 fold of base ∩ [0, k) (uniform identities), k = 0..C */
+  uint32_t* zpw;               /* sparse: Z^k, k = 0..C+1 */
   int32_t* tst;               /* C x C, KB_VARIANT_EXACT_LRU: the exact instant of every Known entry */
   uint16_t* lat;              /* C x C PeerInfo.latency in ms, LAT_NONE = None (track_latency only) */
   uint8_t* alive;
@@ -114,6 +119,7 @@ struct kbo_sim {
 };
 typedef struct kbo_sim kbo_sim;
 
+int kbo_sim_destroy(kbo_sim* s);
 static char g_err[256];
 static void seterr(const char* m) { snprintf(g_err, sizeof g_err, "%s", m); }
 const char* kbo_last_error(void) { return g_err; }
@@ -128,6 +134,109 @@ static inline uint8_t enc(int32_t t, int32_t r) {
   return (uint8_t)v;
 }
 static inline uint8_t* row(kbo_sim* s, uint32_t i) { return s->stamp + (size_t)i * s->C; }
+
+/* ---- sparse rows (KB_VARIANT_SPARSE_ROWS) -----------------------------------------------
+ * A view holds members = base Δ x (or x alone for a row that never adopted the base, e.g. a fresh joiner)
+ * and stamps: ANCIENT (2) for every member without an explicit entry, else the entry's byte (1 = suspect,
+ * > 2 = Known within the stamp window).  base is the initial member set, shared by every row.  The round
+ * touches rows through st_get / st_set and the sparse algorithms below (A3 from the rotated base order,
+ * KnownPeersRequest replies from the explicit list, the fingerprint from base prefix folds corrected at
+ * the exceptions); everything else materialises a row on demand. */
+struct srow {
+  uint32_t* x; uint32_t nx, capx;                  /* sorted ids where the row differs from its base */
+  uint32_t* lid; uint8_t* lb; uint32_t nl, capl;   /* sorted explicit stamps (members only) */
+  uint8_t based;                                   /* members = base Δ x (1) or x (0) */
+  uint32_t adopt_at;                               /* unbased: |x| at which adopting the base is tried next */
+};
+typedef struct srow srow;
+static inline int bbit(const kbo_sim* s, uint32_t j) { return (int)((s->bbits[j >> 5] >> (j & 31)) & 1u); }
+static uint32_t lbound(const uint32_t* v, uint32_t n, uint32_t key) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) { const uint32_t mid = lo + (hi - lo) / 2; if (v[mid] < key) lo = mid + 1; else hi = mid; }
+  return lo;
+}
+static inline int x_has(const srow* r, uint32_t j) { const uint32_t k = lbound(r->x, r->nx, j); return k < r->nx && r->x[k] == j; }
+static void x_toggle(srow* r, uint32_t j) {
+  const uint32_t k = lbound(r->x, r->nx, j);
+  if (k < r->nx && r->x[k] == j) { memmove(r->x + k, r->x + k + 1, (r->nx - k - 1) * 4u); r->nx--; return; }
+  if (r->nx == r->capx) { r->capx = r->capx ? 2 * r->capx : 16; r->x = (uint32_t*)realloc(r->x, r->capx * 4u); }
+  memmove(r->x + k + 1, r->x + k, (r->nx - k) * 4u);
+  r->x[k] = j; r->nx++;
+}
+static inline uint8_t l_get(const srow* r, uint32_t j) { const uint32_t k = lbound(r->lid, r->nl, j); return k < r->nl && r->lid[k] == j ? r->lb[k] : 0; }
+static void l_set(srow* r, uint32_t j, uint8_t b) {               /* b = 0 or ANCIENT: no explicit entry */
+  const uint32_t k = lbound(r->lid, r->nl, j);
+  const int has = k < r->nl && r->lid[k] == j;
+  if (b == ST_UNKNOWN || b == ST_ANCIENT) {
+    if (has) { memmove(r->lid + k, r->lid + k + 1, (r->nl - k - 1) * 4u); memmove(r->lb + k, r->lb + k + 1, r->nl - k - 1); r->nl--; }
+    return;
+  }
+  if (has) { r->lb[k] = b; return; }
+  if (r->nl == r->capl) {
+    r->capl = r->capl ? 2 * r->capl : 16;
+    r->lid = (uint32_t*)realloc(r->lid, r->capl * 4u); r->lb = (uint8_t*)realloc(r->lb, r->capl);
+  }
+  memmove(r->lid + k + 1, r->lid + k, (r->nl - k) * 4u); memmove(r->lb + k + 1, r->lb + k, r->nl - k);
+  r->lid[k] = j; r->lb[k] = b; r->nl++;
+}
+static inline int s_mem(const kbo_sim* s, uint32_t i, uint32_t j) {
+  const srow* r = &s->sr[i];
+  return (r->based ? bbit(s, j) : 0) ^ x_has(r, j);
+}
+/* the stamp byte of (i, j) in either layout (0 = not a member) */
+static inline uint8_t st_get(kbo_sim* s, uint32_t i, uint32_t j) {
+  if (!s->sr) return row(s, i)[j];
+  if (!s_mem(s, i, j)) return ST_UNKNOWN;
+  const uint8_t b = l_get(&s->sr[i], j);
+  return b ? b : ST_ANCIENT;
+}
+static void adopt_base(kbo_sim* s, uint32_t i);
+static inline void st_set(kbo_sim* s, uint32_t i, uint32_t j, uint8_t b) {
+  if (!s->sr) { row(s, i)[j] = b; return; }
+  srow* r = &s->sr[i];
+  if ((b != ST_UNKNOWN) != s_mem(s, i, j)) x_toggle(r, j);
+  l_set(r, j, b);
+  if (!r->based && r->nx > r->adopt_at) adopt_base(s, i);
+}
+/* the row's members as base Δ x once base describes it better (a joiner that has learned the mesh) */
+static void adopt_base(kbo_sim* s, uint32_t i) {
+  srow* r = &s->sr[i];
+  uint32_t* nx = (uint32_t*)malloc(sizeof(uint32_t) * (s->C ? s->C : 1));
+  uint32_t c = 0, k = 0;
+  for (uint32_t j = 0; j < s->C; ++j) {
+    const int in_x = k < r->nx && r->x[k] == j;
+    k += in_x;
+    if (bbit(s, j) != in_x) nx[c++] = j;                 /* member in exactly one of base, row */
+  }
+  if (c >= r->nx) { free(nx); r->adopt_at = 2 * r->adopt_at + 64; return; }
+  free(r->x);
+  r->x = nx; r->nx = c; r->capx = s->C; r->based = 1;
+}
+/* the row as dense bytes (inspection and the rare whole-row scans) */
+static void row_bytes(kbo_sim* s, uint32_t i, uint8_t* out) {
+  if (!s->sr) { memcpy(out, row(s, i), s->C); return; }
+  const srow* r = &s->sr[i];
+  for (uint32_t j = 0; j < s->C; ++j) out[j] = (r->based && bbit(s, j)) ? ST_ANCIENT : ST_UNKNOWN;
+  for (uint32_t k = 0; k < r->nx; ++k) out[r->x[k]] = out[r->x[k]] ? ST_UNKNOWN : ST_ANCIENT;
+  for (uint32_t k = 0; k < r->nl; ++k) out[r->lid[k]] = r->lb[k];
+}
+/* the row for inspection: the dense row itself, or a materialised copy (*tmp, freed by the caller) */
+static const uint8_t* row_view(kbo_sim* s, uint32_t i, uint8_t** tmp) {
+  *tmp = NULL;
+  if (!s->sr) return row(s, i);
+  *tmp = (uint8_t*)malloc(s->C ? s->C : 1);
+  row_bytes(s, i, *tmp);
+  return *tmp;
+}
+static void srow_free(srow* r) { free(r->x); free(r->lid); free(r->lb); memset(r, 0, sizeof *r); }
+static void srow_copy(srow* d, const srow* r) {
+  srow_free(d);
+  *d = *r;
+  d->capx = r->nx; d->capl = r->nl;
+  d->x = (uint32_t*)malloc(4u * (r->nx ? r->nx : 1)); memcpy(d->x, r->x, 4u * r->nx);
+  d->lid = (uint32_t*)malloc(4u * (r->nl ? r->nl : 1)); memcpy(d->lid, r->lid, 4u * r->nl);
+  d->lb = (uint8_t*)malloc(r->nl ? r->nl : 1); memcpy(d->lb, r->lb, r->nl);
+}
 static inline int active_faults(kbo_sim* s, int32_t r) { return s->cfg.fault_end_round < 0 || r < s->cfg.fault_end_round; }
 static inline o_u32x4 ph(kbo_sim* s, uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
   return o_philox(c0, c1, c2, c3, s->k0, s->k1);
@@ -174,8 +283,7 @@ static inline uint32_t mulz(const kbo_sim* s, uint32_t a) {
 /* generate_fingerprint (src/kaboodle.rs:71-83): CRC-32 over addr.to_string() || identity of every
  * entry in ascending address order (= ascending id).  Computed by folding the per-peer segment CRCs:
  * crc0(A||B) = crc0(A)*x^(8|B|) ^ crc0(B); final = crc0 ^ 0xFFFFFFFF*x^(8 len) ^ 0xFFFFFFFF. */
-static uint32_t fold_row(kbo_sim* s, uint32_t i) {
-  const uint8_t* rw = row(s, i);
+static uint32_t fold_bytes(kbo_sim* s, const uint8_t* rw) {
   uint32_t raw = 0; uint64_t len = 0;
   if (s->uniform) {
     uint64_t cnt = 0;
@@ -188,10 +296,36 @@ static uint32_t fold_row(kbo_sim* s, uint32_t i) {
   }
   return raw ^ o_multmodp(o_xpow8(len), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
 }
+/* sparse rows, uniform identities: the base's prefix folds between consecutive exceptions, one multiply
+ * per interval: raw(A ‖ base ∩ [a, b)) = (raw(A) ⊕ bpre[a])·Z^{bcnt[b] - bcnt[a]} ⊕ bpre[b]; an exception
+ * that is a member outside the base is appended (raw·Z ⊕ c_x), one inside the base is skipped. */
+static uint32_t fold_sparse(kbo_sim* s, uint32_t i) {
+  const srow* r = &s->sr[i];
+  uint32_t raw = 0, pos = 0;
+  uint64_t cnt = 0;
+  for (uint32_t k = 0; k < r->nx; ++k) {
+    const uint32_t x = r->x[k];
+    if (r->based) { raw = o_multmodp(s->zpw[s->bcnt[x] - s->bcnt[pos]], raw ^ s->bpre[pos]) ^ s->bpre[x]; cnt += s->bcnt[x] - s->bcnt[pos]; }
+    if (!r->based || !bbit(s, x)) { raw = mulz(s, raw) ^ s->cseg[x]; cnt++; }
+    pos = x + 1;
+  }
+  if (r->based) { raw = o_multmodp(s->zpw[s->bcnt[s->C] - s->bcnt[pos]], raw ^ s->bpre[pos]) ^ s->bpre[s->C]; cnt += s->bcnt[s->C] - s->bcnt[pos]; }
+  return raw ^ o_multmodp(o_xpow8(cnt * s->ulen), 0xFFFFFFFFu) ^ 0xFFFFFFFFu;
+}
+static uint32_t fold_row(kbo_sim* s, uint32_t i) {
+  if (!s->sr) return fold_bytes(s, row(s, i));
+  if (s->uniform) return fold_sparse(s, i);
+  uint8_t* rw = (uint8_t*)malloc(s->C);
+  row_bytes(s, i, rw);
+  const uint32_t f = fold_bytes(s, rw);
+  free(rw);
+  return f;
+}
 
 /* The literal reference definition, byte by byte (kept for the equivalence test). */
 uint32_t kbo_fingerprint_direct(kbo_sim* s, uint32_t i) {
-  const uint8_t* rw = row(s, i);
+  uint8_t* rw = (uint8_t*)malloc(s->C);
+  row_bytes(s, i, rw);
   uint32_t reg = 0xFFFFFFFFu;
   char a[32];
   for (uint32_t j = 0; j < s->C; ++j) {
@@ -200,6 +334,7 @@ uint32_t kbo_fingerprint_direct(kbo_sim* s, uint32_t i) {
     reg = o_crc_update(reg, (const uint8_t*)a, strlen(a));
     reg = o_crc_update(reg, s->ident + (size_t)j * MAXID, s->id_len[j]);
   }
+  free(rw);
   return reg ^ 0xFFFFFFFFu;
 }
 
@@ -234,24 +369,23 @@ static inline uint16_t lat_ewma(uint32_t sample, uint32_t prev) {   /* :808-816,
  * envelope prologue of a unicast delivered in wave lat_w (calculate_peer_latency, :412); -1: a Join
  * broadcast or a KnownPeers arm (latency kept, :294-296, or None for a new entry, :467) */
 static int map_insert_known(kbo_sim* s, uint32_t i, uint32_t p, int32_t t, int32_t r, int lat_w) {
-  uint8_t* b = row(s, i) + p;
-  int was = *b;
+  int was = st_get(s, i, p);
   uint16_t* lt = s->lat ? s->lat + (size_t)i * s->C + p : NULL;
   if (was == ST_SUSPECT) {
     osusp* q = susp_find(s, i, p);
     if (lt && lat_w >= 0 && q) *lt = lat_ewma(1000u * (uint32_t)(r - q->since) + (uint32_t)lat_w + 1u, *lt);
     if (q) q->kind = 0;
   }
-  *b = enc(t, r);
+  st_set(s, i, p, enc(t, r));
   if (s->tst) s->tst[(size_t)i * s->C + p] = t;
   if (was == ST_UNKNOWN) { if (lt) *lt = LAT_NONE; s->n[i]++; s->dirty[i] = 1; return 1; }
   return 0;
 }
 static int map_remove(kbo_sim* s, uint32_t i, uint32_t p) {
-  uint8_t* b = row(s, i) + p;
-  if (*b == ST_UNKNOWN) return 0;
-  if (*b == ST_SUSPECT) { osusp* q = susp_find(s, i, p); if (q) q->kind = 0; }
-  *b = ST_UNKNOWN;
+  const uint8_t b = st_get(s, i, p);
+  if (b == ST_UNKNOWN) return 0;
+  if (b == ST_SUSPECT) { osusp* q = susp_find(s, i, p); if (q) q->kind = 0; }
+  st_set(s, i, p, ST_UNKNOWN);
   s->n[i]--; s->dirty[i] = 1;
   return 1;
 }
@@ -264,7 +398,7 @@ static int set_suspect(kbo_sim* s, uint32_t i, uint32_t p, int kind, int32_t r) 
     q->peer = p;
   }
   q->kind = kind; q->since = r;
-  row(s, i)[p] = ST_SUSPECT;
+  st_set(s, i, p, ST_SUSPECT);
   return KB_OK;
 }
 
@@ -348,7 +482,8 @@ static void node_stop(kbo_sim* s, uint32_t i) {
  * the new KaboodleInner (fresh); the A3 sweep front starts after the new self. */
 static void node_restart(kbo_sim* s, uint32_t from, uint32_t to, int32_t r) {
   const size_t C = s->C;
-  memcpy(row(s, to), row(s, from), C);
+  if (s->sr) srow_copy(&s->sr[to], &s->sr[from]);
+  else memcpy(row(s, to), row(s, from), C);
   if (s->lat) memcpy(s->lat + (size_t)to * C, s->lat + (size_t)from * C, C * sizeof(uint16_t));
   if (s->tst) memcpy(s->tst + (size_t)to * C, s->tst + (size_t)from * C, C * sizeof(int32_t));
   memcpy(s->susp + (size_t)to * SLOTS, s->susp + (size_t)from * SLOTS, SLOTS * sizeof(osusp));
@@ -377,7 +512,12 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   s->cfg = *cfg; s->C = cfg->capacity;
   s->k0 = (uint32_t)cfg->seed; s->k1 = (uint32_t)(cfg->seed >> 32);
   size_t C = s->C;
-  s->stamp = (uint8_t*)calloc(C * C, 1);
+  const int sparse = (cfg->variant & KB_VARIANT_SPARSE_ROWS) != 0;
+  if (sparse && (cfg->track_latency || (cfg->variant & KB_VARIANT_EXACT_LRU))) {
+    seterr("sparse rows keep neither a latency table nor exact instants"); free(s); return KB_INVALID_ARGUMENT;
+  }
+  if (sparse) s->sr = (srow*)calloc(C, sizeof(srow));
+  else s->stamp = (uint8_t*)calloc(C * C, 1);
   s->alive = (uint8_t*)calloc(C, 1);
   s->start_round = (int32_t*)calloc(C, 4); s->n = (uint32_t*)calloc(C, 4); s->fp = (uint32_t*)calloc(C, 4);
   s->dirty = (uint8_t*)calloc(C, 1); s->last_bcast = (int32_t*)calloc(C, 4); s->a3cur = (uint32_t*)calloc(C, 4);
@@ -389,8 +529,8 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   s->moved = (uint8_t*)calloc(C, 1);
   s->cseg = (uint32_t*)calloc(C, 4); s->segmul = (uint32_t*)calloc(C, 4); s->seglen = (uint32_t*)calloc(C, 4);
   s->out = (ovec*)calloc(C, sizeof(ovec)); s->oseq = (uint32_t*)calloc(C, 4);
-  if (cfg->variant & ~(uint32_t)(KB_VARIANT_SAME_WINDOW_BCAST | KB_VARIANT_EXACT_LRU)) {
-    seterr("unknown variant"); free(s); return KB_INVALID_ARGUMENT;
+  if (cfg->variant & ~(uint32_t)(KB_VARIANT_SAME_WINDOW_BCAST | KB_VARIANT_EXACT_LRU | KB_VARIANT_SPARSE_ROWS)) {
+    seterr("unknown variant"); kbo_sim_destroy(s); return KB_INVALID_ARGUMENT;
   }
   if (cfg->variant & KB_VARIANT_EXACT_LRU) {
     s->tst = (int32_t*)malloc(C * C * sizeof(int32_t));
@@ -400,7 +540,9 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
     s->lat = (uint16_t*)malloc(C * C * sizeof(uint16_t));
     if (s->lat) memset(s->lat, 0xFF, C * C * sizeof(uint16_t));
   }
-  if (!s->stamp || !s->susp || !s->cur || (cfg->track_latency && !s->lat)) { seterr("out of host memory"); free(s); return KB_CAPACITY; }
+  if ((!s->stamp && !s->sr) || !s->susp || !s->cur || (cfg->track_latency && !s->lat)) {
+    seterr("out of host memory"); kbo_sim_destroy(s); return KB_CAPACITY;
+  }
   for (uint32_t i = 0; i < s->C; ++i) {
     s->id_len[i] = (uint8_t)cfg->id_len;
     default_identity(i, cfg->id_len, s->ident + (size_t)i * MAXID);
@@ -410,12 +552,32 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   }
   s->uniform = 1; s->ulen = ADDR_LEN + cfg->id_len; build_mulz(s);
   s->round = 0; s->next_free = cfg->initial_nodes;
+  if (sparse) {
+    /* the base: the initial members of a converged start (empty otherwise), with its prefix counts and
+     * prefix folds; the initial rows adopt it, every other row starts empty */
+    const uint32_t nb = cfg->init_mode == KB_INIT_CONVERGED ? cfg->initial_nodes : 0;
+    s->bbits = (uint32_t*)calloc(C / 32 + 1, 4); s->bcnt = (uint32_t*)malloc(4 * (C + 1));
+    s->bpre = (uint32_t*)malloc(4 * (C + 1)); s->zpw = (uint32_t*)malloc(4 * (C + 2));
+    if (!s->bbits || !s->bcnt || !s->bpre || !s->zpw) { seterr("out of host memory"); kbo_sim_destroy(s); return KB_CAPACITY; }
+    for (uint32_t j = 0; j < nb; ++j) s->bbits[j >> 5] |= 1u << (j & 31);
+    uint32_t raw = 0, c = 0;
+    for (uint32_t j = 0; j <= s->C; ++j) {
+      s->bcnt[j] = c; s->bpre[j] = raw;
+      if (j < s->C && bbit(s, j)) { raw = mulz(s, raw) ^ s->cseg[j]; c++; }
+    }
+    s->zpw[0] = 0x80000000u;
+    const uint32_t Z = o_xpow8(s->ulen);
+    for (size_t k = 1; k < C + 2; ++k) s->zpw[k] = o_multmodp(Z, s->zpw[k - 1]);
+    for (uint32_t i = 0; i < s->C; ++i) { s->sr[i].based = i < nb || nb == 0; s->sr[i].adopt_at = nb / 2 + 64; }
+  }
 #pragma omp parallel for schedule(static)
   for (uint32_t i = 0; i < cfg->initial_nodes; ++i) {   /* touches row i and per-id slots of i only */
     node_start(s, i, 0);
     if (cfg->init_mode == KB_INIT_CONVERGED) {
-      uint8_t* rw = row(s, i);
-      for (uint32_t j = 0; j < cfg->initial_nodes; ++j) if (j != i) rw[j] = ST_ANCIENT;
+      if (!sparse) {                        /* sparse: the base already holds them, ancient */
+        uint8_t* rw = row(s, i);
+        for (uint32_t j = 0; j < cfg->initial_nodes; ++j) if (j != i) rw[j] = ST_ANCIENT;
+      }
       s->n[i] = cfg->initial_nodes;
       s->last_bcast[i] = -1000;             /* running for a while: no Join at round 0 */
     }
@@ -427,7 +589,9 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
 
 int kbo_sim_destroy(kbo_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
-  for (uint32_t i = 0; i < s->C; ++i) free(s->out[i].v);
+  if (s->out) for (uint32_t i = 0; i < s->C; ++i) free(s->out[i].v);
+  if (s->sr) for (uint32_t i = 0; i < s->C; ++i) srow_free(&s->sr[i]);
+  free(s->sr); free(s->bbits); free(s->bcnt); free(s->bpre); free(s->zpw);
   free(s->probe_q); free(s->probes); free(s->presp); free(s->stamp); free(s->tst); free(s->lat); free(s->alive); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
   free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len); free(s->pend_ident); free(s->pend_len); free(s->moved);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
@@ -496,11 +660,21 @@ static uint32_t prp_walk(uint32_t x, uint32_t n, const uint32_t key[4]) {
  * as a uniform random subset of the largest size that fits: the first `cap` images of a keyed
  * pseudo-random permutation of the member ranks (prp_walk). */
 static void join_response(kbo_sim* s, uint32_t i, uint32_t joiner, int32_t r) {
-  const uint8_t* rw = row(s, i);
   uint32_t n = s->n[i];
   uint32_t* members = (uint32_t*)malloc(sizeof(uint32_t) * (n ? n : 1));
   uint32_t m = 0;
-  for (uint32_t j = 0; j < s->C; ++j) if (rw[j]) members[m++] = j;
+  if (s->sr) {                                     /* base Δ x, merged in id order */
+    const srow* rr = &s->sr[i];
+    uint32_t k = 0;
+    for (uint32_t j = 0; j < s->C; ++j) {
+      const int in_x = k < rr->nx && rr->x[k] == j;
+      k += in_x;
+      if (((rr->based && bbit(s, j)) != in_x) && m < n) members[m++] = j;
+    }
+  } else {
+    const uint8_t* rw = row(s, i);
+    for (uint32_t j = 0; j < s->C; ++j) if (rw[j]) members[m++] = j;
+  }
   uint32_t cap = kp_cap_uniform(s);
   uint32_t* pay;
   uint32_t plen;
@@ -529,7 +703,7 @@ static void phase_broadcasts(kbo_sim* s, uint32_t i, int32_t r) {
     if (b->sender == i) continue;                     /* own broadcasts are not delivered to self */
     if (bcast_lost(s, i, b, r, 0, k)) { lost++; continue; }
     if (b->peer == i) continue;                       /* Failed(self) ignored            :269-273 */
-    if (s->cfg.failed_mode == KB_FAILED_SIM_SENDER && row(s, i)[b->sender] != ST_UNKNOWN)
+    if (s->cfg.failed_mode == KB_FAILED_SIM_SENDER && st_get(s, i, b->sender) != ST_UNKNOWN)
       removed += (uint64_t)map_remove(s, i, b->peer); /* sender is a mesh member         :275-279 */
   }
   /* Join{addr} (src/kaboodle.rs:284-304) */
@@ -579,8 +753,65 @@ static inline uint32_t rot_key(uint32_t j, uint32_t base, uint32_t C) {  /* rota
   return (j + C - base - 1) % C;
 }
 
+/* the candidates of handle_suspected_peers' indirect pings: Known && != self, ascending id (:571-577) */
+static uint32_t a2_candidates(kbo_sim* s, uint32_t i, uint32_t* cand) {
+  uint32_t c = 0;
+  if (!s->sr) {
+    const uint8_t* rw = row(s, i);
+    for (uint32_t j = 0; j < s->C; ++j) if (rw[j] >= ST_ANCIENT && j != i) cand[c++] = j;
+    return c;
+  }
+  const srow* rr = &s->sr[i];
+  uint32_t k = 0, q = 0;
+  for (uint32_t j = 0; j < s->C; ++j) {
+    const int in_x = k < rr->nx && rr->x[k] == j;
+    k += in_x;
+    if ((rr->based && bbit(s, j)) == in_x) continue;             /* not a member */
+    while (q < rr->nl && rr->lid[q] < j) ++q;
+    if (j != i && !(q < rr->nl && rr->lid[q] == j && rr->lb[q] == ST_SUSPECT)) cand[c++] = j;
+  }
+  return c;
+}
+/* A3's five smallest (stamp, rotated id) keys over Known && != self, ascending */
+static inline void top5_add(uint32_t* best, uint32_t* kh5, uint32_t* kl5, int* nb, uint32_t j, uint32_t kh, uint32_t kl) {
+  if (*nb == NUM_CANDIDATES && (kh > kh5[*nb - 1] || (kh == kh5[*nb - 1] && kl > kl5[*nb - 1]))) return;
+  int pos = *nb < NUM_CANDIDATES ? *nb : NUM_CANDIDATES - 1;
+  while (pos > 0 && (kh5[pos - 1] > kh || (kh5[pos - 1] == kh && kl5[pos - 1] > kl))) {
+    kh5[pos] = kh5[pos - 1]; kl5[pos] = kl5[pos - 1]; best[pos] = best[pos - 1]; --pos;
+  }
+  kh5[pos] = kh; kl5[pos] = kl; best[pos] = j;
+  if (*nb < NUM_CANDIDATES) (*nb)++;
+}
+static int a3_candidates(kbo_sim* s, uint32_t i, uint32_t* best) {
+  uint32_t kh5[NUM_CANDIDATES], kl5[NUM_CANDIDATES];
+  int nb = 0;
+  if (!s->sr) {
+    const uint8_t* rw = row(s, i);
+    for (uint32_t j = 0; j < s->C; ++j) {
+      uint8_t b = rw[j];
+      if (b < ST_ANCIENT || j == i) continue;
+      uint32_t kh = s->tst ? ((uint32_t)s->tst[(size_t)i * s->C + j] ^ 0x80000000u) : b;   /* order-preserving */
+      top5_add(best, kh5, kl5, &nb, j, kh, rot_key(j, s->a3cur[i], s->C));
+    }
+    return nb;
+  }
+  /* sparse: every member without an explicit stamp is ancient, the smallest key; those met first in
+   * rotated order from the sweep front are the oldest, so the scan stops after five of them.  With fewer
+   * than five ancient members, the explicit Known stamps fill in by (stamp, rotated id). */
+  const srow* rr = &s->sr[i];
+  const uint32_t C = s->C, p0 = s->a3cur[i] + 1 == C ? 0 : s->a3cur[i] + 1;
+  for (uint32_t k = 0; k < C && nb < NUM_CANDIDATES; ++k) {
+    const uint32_t j = p0 + k >= C ? p0 + k - C : p0 + k;
+    if (j == i || !s_mem(s, i, j) || l_get(rr, j)) continue;
+    top5_add(best, kh5, kl5, &nb, j, ST_ANCIENT, k);
+  }
+  if (nb < NUM_CANDIDATES)
+    for (uint32_t q = 0; q < rr->nl; ++q)
+      if (rr->lb[q] >= ST_ANCIENT && rr->lid[q] != i) top5_add(best, kh5, kl5, &nb, rr->lid[q], rr->lb[q], rot_key(rr->lid[q], s->a3cur[i], C));
+  return nb;
+}
+
 static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
-  uint8_t* rw = row(s, i);
   bc->nfail = 0; bc->join = 0;
   /* A1 maybe_broadcast_join (:228-251) */
   if (s->last_bcast[i] == INT32_MIN || (r - s->last_bcast[i] >= REBROADCAST && s->n[i] <= 1)) {
@@ -606,9 +837,8 @@ static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
         uint32_t k = m < NUM_INDIRECT ? m : NUM_INDIRECT;
         if (k == 0) { removed[nrem++] = e->peer; continue; }
         if (!cand) {
-          cand = (uint32_t*)malloc(sizeof(uint32_t) * m);
-          uint32_t c = 0;
-          for (uint32_t j = 0; j < s->C; ++j) if (rw[j] >= ST_ANCIENT && j != i) cand[c++] = j;
+          cand = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+          (void)a2_candidates(s, i, cand);
         }
         o_u32x4 w = ph(s, i, (uint32_t)r, (uint32_t)P_INDIRECT << 24, e->peer);
         uint32_t pick[3];
@@ -642,20 +872,8 @@ static int tick(kbo_sim* s, uint32_t i, int32_t r, otick_bc* bc) {
   /* A3 ping_random_peer (:655-703): oldest 5 by (stamp, id rotated to start at the node's sweep front),
      one uniformly; the front moves to the oldest candidate */
   {
-    uint32_t best[NUM_CANDIDATES]; uint32_t bkey_hi[NUM_CANDIDATES], bkey_lo[NUM_CANDIDATES]; int nb = 0;
-    for (uint32_t j = 0; j < s->C; ++j) {
-      uint8_t b = rw[j];
-      if (b < ST_ANCIENT || j == i) continue;
-      uint32_t kh = s->tst ? ((uint32_t)s->tst[(size_t)i * s->C + j] ^ 0x80000000u) : b,   /* order-preserving */
-                kl = rot_key(j, s->a3cur[i], s->C);
-      if (nb == NUM_CANDIDATES && (kh > bkey_hi[nb - 1] || (kh == bkey_hi[nb - 1] && kl > bkey_lo[nb - 1]))) continue;
-      int pos = nb < NUM_CANDIDATES ? nb : NUM_CANDIDATES - 1;
-      while (pos > 0 && (bkey_hi[pos - 1] > kh || (bkey_hi[pos - 1] == kh && bkey_lo[pos - 1] > kl))) {
-        bkey_hi[pos] = bkey_hi[pos - 1]; bkey_lo[pos] = bkey_lo[pos - 1]; best[pos] = best[pos - 1]; --pos;
-      }
-      bkey_hi[pos] = kh; bkey_lo[pos] = kl; best[pos] = j;
-      if (nb < NUM_CANDIDATES) nb++;
-    }
+    uint32_t best[NUM_CANDIDATES];
+    const int nb = a3_candidates(s, i, best);
     if (nb > 0) {
       uint32_t u = ph(s, i, (uint32_t)r, (uint32_t)P_PING << 24, 0).v[0];
       uint32_t t = best[o_mulhi(u, (uint32_t)nb)];
@@ -694,22 +912,32 @@ static void handle_message(kbo_sim* s, uint32_t i, const omsg* m, int32_t r, uin
       break;
     }
     case K_KP: {                                   /* :448-472 */
-      uint8_t* rw = row(s, i);
       for (uint32_t k = 0; k < m->pay_len; ++k) {
         uint32_t p = m->pay[k];
-        if (rw[p] == ST_UNKNOWN) map_insert_known(s, i, p, r - SHARE_AGE, r, -1);
+        if (st_get(s, i, p) == ST_UNKNOWN) map_insert_known(s, i, p, r - SHARE_AGE, r, -1);
       }
       break;
     }
     case K_KPR: {                                  /* :473-512 */
-      const uint8_t* rw = row(s, i);
       uint8_t fresh = enc(r - (SHARE_AGE - 1), r);
       uint32_t cnt = 0, cap = 64;
       uint32_t* pay = (uint32_t*)malloc(sizeof(uint32_t) * cap);
-      for (uint32_t j = 0; j < s->C; ++j) {
-        if (rw[j] >= fresh && j != i && j != from) {
-          if (cnt == cap) { cap *= 2; pay = (uint32_t*)realloc(pay, sizeof(uint32_t) * cap); }
-          pay[cnt++] = j;
+      if (s->sr) {                                 /* sparse: fresh stamps are explicit (fresh > ancient) */
+        const srow* rr = &s->sr[i];
+        for (uint32_t q = 0; q < rr->nl; ++q) {
+          const uint32_t j = rr->lid[q];
+          if (rr->lb[q] >= fresh && j != i && j != from) {
+            if (cnt == cap) { cap *= 2; pay = (uint32_t*)realloc(pay, sizeof(uint32_t) * cap); }
+            pay[cnt++] = j;
+          }
+        }
+      } else {
+        const uint8_t* rw = row(s, i);
+        for (uint32_t j = 0; j < s->C; ++j) {
+          if (rw[j] >= fresh && j != i && j != from) {
+            if (cnt == cap) { cap *= 2; pay = (uint32_t*)realloc(pay, sizeof(uint32_t) * cap); }
+            pay[cnt++] = j;
+          }
         }
       }
       if (kp_size(s, i, pay, cnt) > BUFSZ) {        /* truncated at the receiver -> undeliverable (Q3) */
@@ -825,7 +1053,20 @@ static int step_round(kbo_sim* s) {
   int32_t r = s->round;
   uint32_t C = s->C;
   /* 0. stamp window: every EPOCH rounds the base advances; known stamps shift down, saturating */
-  if (r > 0 && r % EPOCH == 0) {
+  if (r > 0 && r % EPOCH == 0 && s->sr) {
+#pragma omp parallel for schedule(dynamic, 64)
+    for (uint32_t i = 0; i < C; ++i) {            /* explicit stamps that saturate become implicit */
+      srow* rr = &s->sr[i];
+      uint32_t o = 0;
+      for (uint32_t q = 0; q < rr->nl; ++q) {
+        uint8_t b = rr->lb[q];
+        if (b > ST_ANCIENT) b = (uint8_t)(b - EPOCH > ST_ANCIENT ? b - EPOCH : ST_ANCIENT);
+        if (b == ST_ANCIENT) continue;
+        rr->lid[o] = rr->lid[q]; rr->lb[o] = b; o++;
+      }
+      rr->nl = o;
+    }
+  } else if (r > 0 && r % EPOCH == 0) {
     size_t tot = (size_t)C * C;
 #pragma omp parallel for
     for (size_t k = 0; k < tot; ++k) {
@@ -994,7 +1235,7 @@ int kbo_sim_ping_addrs(kbo_sim* s, uint32_t node, const uint32_t* peers, size_t 
   if (!s->alive[node]) { seterr("Cannot ping while we are not started"); return KB_INVALID_OPERATION; }
   for (size_t k = 0; k < n; ++k) {
     if (peers[k] >= s->C) return KB_INVALID_ARGUMENT;
-    if (row(s, node)[peers[k]] != ST_UNKNOWN) continue;
+    if (st_get(s, node, peers[k]) != ST_UNKNOWN) continue;
     if (s->paq_n[node] == PAQ) { seterr("ping_addrs queue full"); return KB_CAPACITY; }
     s->paq[(size_t)node * PAQ + s->paq_n[node]++] = peers[k];
   }
@@ -1093,9 +1334,11 @@ int kbo_sim_true_fingerprint(kbo_sim* s, uint32_t* fp) {
 }
 int kbo_sim_peers(kbo_sim* s, uint32_t node, uint32_t* peers, size_t cap, size_t* n) {
   if (check(s, node) || !n) return KB_INVALID_ARGUMENT;
-  const uint8_t* rw = row(s, node);
+  uint8_t* tmp;
+  const uint8_t* rw = row_view(s, node, &tmp);
   size_t c = 0;
   for (uint32_t j = 0; j < s->C; ++j) if (rw[j]) { if (peers && c < cap) peers[c] = j; c++; }
+  free(tmp);
   *n = c;
   return (peers && cap < c) ? KB_CAPACITY : KB_OK;
 }
@@ -1120,7 +1363,8 @@ int kbo_sim_events(kbo_sim* s, uint32_t node, uint32_t* discovered, size_t cap_d
   size_t k = 0;
   while (k < s->nwatch && s->wnode[k] != node) ++k;
   if (k == s->nwatch) { seterr("node is not watched (kbo_sim_watch)"); return KB_INVALID_OPERATION; }
-  const uint8_t* rw = row(s, node);
+  uint8_t* tmp;
+  const uint8_t* rw = row_view(s, node, &tmp);
   uint8_t* snap = s->wsnap[k];
   size_t a = 0, r = 0, known = 0;
   for (uint32_t j = 0; j < s->C; ++j) {
@@ -1134,6 +1378,7 @@ int kbo_sim_events(kbo_sim* s, uint32_t node, uint32_t* discovered, size_t cap_d
   *fp_changed = known > 0 && *fp != s->wfp[k];
   const int fit = (!a || (discovered && cap_d >= a)) && (!r || (departed && cap_p >= r));
   if (!fit) {
+    free(tmp);
     if (discovered || departed) { seterr("event buffer too small"); return KB_CAPACITY; }
     return KB_OK;
   }
@@ -1145,11 +1390,13 @@ int kbo_sim_events(kbo_sim* s, uint32_t node, uint32_t* discovered, size_t cap_d
     snap[j] = (uint8_t)now;
   }
   if (*fp_changed) s->wfp[k] = *fp;
+  free(tmp);
   return KB_OK;
 }
 int kbo_sim_peer_states(kbo_sim* s, uint32_t node, kb_peer_state* out, size_t cap, size_t* n) {
   if (check(s, node) || !n) return KB_INVALID_ARGUMENT;
-  const uint8_t* rw = row(s, node);
+  uint8_t* tmp;
+  const uint8_t* rw = row_view(s, node, &tmp);
   size_t c = 0;
   /* the stamps hold the encoding of the last simulated round (the window is rebased at the START of
    * a round, step_round above), so their base is epoch_base(round - 1), not epoch_base(round) */
@@ -1174,6 +1421,7 @@ int kbo_sim_peer_states(kbo_sim* s, uint32_t node, kb_peer_state* out, size_t ca
     }
     c++;
   }
+  free(tmp);
   *n = c;
   return (out && cap < c) ? KB_CAPACITY : KB_OK;
 }
@@ -1189,7 +1437,7 @@ int kbo_sim_stats(kbo_sim* s, kb_stats* out) {
 }
 int kbo_sim_dump_row(kbo_sim* s, uint32_t node, uint8_t* rw, size_t cap) {
   if (check(s, node) || !rw || cap < s->C) return KB_INVALID_ARGUMENT;
-  memcpy(rw, row(s, node), s->C);
+  row_bytes(s, node, rw);
   return KB_OK;
 }
 int kbo_sim_dump_scalars(kbo_sim* s, int32_t* out, size_t cap) {
@@ -1245,6 +1493,19 @@ uint32_t kbo_fingerprint_of_set(const uint32_t* ids, size_t n, const uint8_t* id
   }
   free(v);
   return n ? reg ^ 0xFFFFFFFFu : 0;
+}
+/* KB_VARIANT_SPARSE_ROWS footprint (test infrastructure): out = [rows that adopted the base,
+ * exceptions, explicit stamps, entries of the largest row, bytes (4 per exception, 5 per stamp), rows] */
+int kbo_sparse_footprint(kbo_sim* s, uint64_t* out, size_t cap) {
+  if (!s || !s->sr || !out || cap < 6) return KB_INVALID_ARGUMENT;
+  uint64_t based = 0, nx = 0, nl = 0, mx = 0;
+  for (uint32_t i = 0; i < s->C; ++i) {
+    const srow* r = &s->sr[i];
+    based += r->based; nx += r->nx; nl += r->nl;
+    if (r->nx + r->nl > mx) mx = r->nx + r->nl;
+  }
+  out[0] = based; out[1] = nx; out[2] = nl; out[3] = mx; out[4] = 4 * nx + 5 * nl; out[5] = s->C;
+  return KB_OK;
 }
 uint32_t kbo_crc32(const uint8_t* p, size_t n) { o_crc_init(); return o_crc32(p, n); }
 void kbo_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t* out4) {

@@ -109,6 +109,9 @@ static int scenarios() {
       {160, 128, KB_INIT_CONVERGED, 20, 30, 12, 0, 4, 0, 1, 0, 140},
       {96, 80, KB_INIT_CONVERGED, 30, 10, 20, 0, 0, 0, 0, 1, 20},
       {96, 80, KB_INIT_CONVERGED, 30, 10, 20, 0, 0, 0, 0, 2, 20},
+      {256, 256, KB_INIT_CONVERGED, 50, 0, 0, 1, 0, 2, 0, 4, 30},     // sparse rows: partition + heal
+      {160, 128, KB_INIT_CONVERGED, 20, 30, 12, 0, 4, 0, 0, 4, 140},  // sparse rows: churn, rebases
+      {300, 300, KB_INIT_JOIN, 20, 0, 0, 0, 5, 0, 0, 4, 20},          // sparse rows: empty base
   };
   int k = 0;
   for (const Sc& c : list) {

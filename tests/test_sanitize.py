@@ -4,8 +4,9 @@ the HIP library's wire decoder (kaboodle_amd/csrc/kb_wire.h, host code fed by br
 both with -fsanitize=address,undefined and no recovery: any heap overflow, use after free, leak, signed
 overflow or null memcpy aborts the run.
 
-- the oracle through the whole kbo_ ABI on eight small scenarios (joins, loss, churn, partition and heal,
-  stop / restart / set_identity, probes, event drains, latency, both failed modes, both measurement variants);
+- the oracle through the whole kbo_ ABI on eleven small scenarios (joins, loss, churn, partition and heal,
+  stop / restart / set_identity, probes, event drains, latency, both failed modes, every variant: same-window
+  broadcasts, exact LRU, sparse rows);
 - kb_wire_decode on 200,000 random and mutated datagrams (seeded), valid encodings round-tripping;
 - kb_wire_decode on datagrams hypothesis generates (structured: valid headers with random tails, and raw
   bytes), each decoded from an exactly sized heap buffer on every channel."""
@@ -39,7 +40,7 @@ def _run(harness, *args, stdin=None):
 
 
 def test_oracle_scenarios_sanitized(harness):
-    assert "8 run, 0 failures" in _run(harness, "scenarios")
+    assert "11 run, 0 failures" in _run(harness, "scenarios")
 
 
 def test_wire_decode_fuzz_sanitized(harness):

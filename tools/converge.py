@@ -21,6 +21,13 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def lib_sha16() -> str:
+    """the library build this record was made with (bench.py attaches a tail record only when it matches)"""
+    import hashlib
+    import kaboodle_amd
+    return hashlib.sha256(open(kaboodle_amd.LIB_PATH, "rb").read()).hexdigest()[:16]
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", choices=("sim", "sock"), default="sim")
@@ -92,7 +99,7 @@ def main() -> int:
            "converged_round": conv, "tail_rounds_to_converge": None if conv is None else conv - F + 1,
            "tail_rounds_run": traj[-1]["round"] - F + 1, "cap_rounds": cap,
            "stopped_by": "converged" if conv is not None else ("cap" if traj[-1]["round"] >= F + cap - 1 else "budget"),
-           "wall_s": round(time.time() - t0, 1), "trajectory": traj}
+           "wall_s": round(time.time() - t0, 1), "lib_sha16": lib_sha16(), "trajectory": traj}
     txt = json.dumps(out)
     print(json.dumps({k: v for k, v in out.items() if k != "trajectory"}), flush=True)
     if a.out:
