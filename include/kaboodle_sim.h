@@ -101,8 +101,10 @@ enum {
   KB_DBG_KP_HBM = 4u,        /* KnownPeers groups on the HBM bitset, one workgroup per destination      */
   KB_DBG_KP_BIG_SMALL = 8u,  /* every KnownPeers group takes the BIG (1024-thread) kernel                */
   KB_DBG_PROC_UNSORTED = 16u,/* inboxes > 64 taken by k_proc's selection path (inboxes > SORT_MAX)       */
-  KB_DBG_WAVE_GRAPH = 32u    /* the unsharded receive window captured once as a HIP graph and replayed
+  KB_DBG_WAVE_GRAPH = 32u,   /* the unsharded receive window captured once as a HIP graph and replayed
                                 every round (also env KB_WAVE_GRAPH=1)                  */
+  KB_DBG_RESP_WAVE_HBM = 64u /* Join responses by wave with the rows read in place (the path of rows too
+                                wide for a wave's LDS copy, > 110K ids)                                */
 };
 
 /* Per-peer state as reported by peer_states() (PeerState, src/structs.rs:27-41). */
@@ -258,7 +260,8 @@ int  kb_sim_dump_suspects(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, 
 /* OR of the kernel-variant bits that did work since creation (PATH_* in kaboodle_amd/csrc/kb_common.h:
    1 broadcast phase on the HBM bitset, 2/4 Join responses from HBM scratch (sampled / complete),
    8 KnownPeers BIG group on the HBM bitset, 16 k_proc unsorted selection path, 32 Failed-list prep
-   from HBM, 64 Join responses by wave, 128 KnownPeers BIG group in LDS).  Test surface.           */
+   from HBM, 64 Join responses by wave, 128 KnownPeers BIG group in LDS, 256 Join responses by wave
+   from the rows in place).  Test surface.                                                          */
 int  kb_sim_debug_paths(kb_sim* sim, uint32_t* mask);
 /* Development counters since creation: [A3 rows scanned, rows scanned past their first 1024 ids,
    1024-id stamp chunks read].  Test surface.                                                        */

@@ -17,6 +17,7 @@ KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL = 0, 1
 KB_DBG_PHASEB_HBM, KB_DBG_RESP_HBM, KB_DBG_KP_HBM, KB_DBG_KP_BIG_SMALL, KB_DBG_PROC_UNSORTED = 1, 2, 4, 8, 16
 KB_DBG_ALL = 31                  # every wide-row variant
 KB_DBG_WAVE_GRAPH = 32           # the receive window as a replayed HIP graph
+KB_DBG_RESP_WAVE_HBM = 64        # Join responses by wave, rows read in place (rows > 110K ids)
 KB_VARIANT_SAME_WINDOW_BCAST, KB_VARIANT_EXACT_LRU = 1, 2   # oracle-only
 KB_LATENCY_NONE = 0xFFFFFFFF
 KT_ROWPASS, KT_ROUND, KT_FOLD, KT_RESP, KT_PROC = 0, 1, 2, 3, 4   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds

@@ -41,7 +41,8 @@ enum CtrIdx {
 };
 // kernel-variant coverage bits (kb_sim_debug_paths): the wide-row paths a >= 1M-id mesh takes
 enum : uint32_t { PATH_PHASEB_HBM = 1, PATH_RESP_SCRATCH_SAMPLED = 2, PATH_RESP_SCRATCH_FULL = 4, PATH_KP_BIG_HBM = 8,
-                  PATH_PROC_UNSORTED = 16, PATH_BFAIL_PREP_HBM = 32, PATH_RESP_WAVE = 64, PATH_KP_BIG_LDS = 128 };
+                  PATH_PROC_UNSORTED = 16, PATH_BFAIL_PREP_HBM = 32, PATH_RESP_WAVE = 64, PATH_KP_BIG_LDS = 128,
+                  PATH_RESP_WAVE_HBM = 256 };
 constexpr int NSEG = 64;          // fingerprint checkpoints per row
 constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
 constexpr int ZB = 9 * 1024;      // byte tables for Z^0..Z^8 (4 lookups per multiply)

@@ -894,32 +894,37 @@ __host__ __device__ inline uint32_t rwave_words(uint32_t NW, uint32_t NB) { retu
 __device__ inline bool resp_by_wave(const Dev& d, uint32_t i, uint32_t nnew, bool on) {
   return on && d.uniform && nnew <= RW_JCAP && d.n[i] - nnew > d.capj;
 }
+// Rows too wide for a wave's LDS copy (SG: above ≈ 110K ids; configs[3]'s 1M-id rows) keep only the head
+// (block prefix, joiners, suffix minima) in LDS and read the selects' 32-byte blocks from the row's bitset
+// itself: nothing writes a row while the Join responses are built, and a responder's row stays in L2 across
+// its responses.  (The workgroup path instead copied each row to HBM scratch first.)
+template <bool SG>
 __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint32_t* nodes, const uint32_t* nnodes_p,
                                                    OutBuf ob, int32_t r) {
   extern __shared__ __attribute__((aligned(16))) uint32_t rw_lds[];
   const uint32_t NW = d.NWR, NB = d.W / 256;
-  const uint32_t wv = threadIdx.x >> 6, l = lane();
-  uint32_t* BP = rw_lds + (size_t)wv * rwave_words(NW, NB);  // block prefix of the row's bitset    [NB + 1]
+  const uint32_t wv = threadIdx.x >> 6, l = lane(), nwv = blockDim.x >> 6;
+  uint32_t* BP = rw_lds + (size_t)wv * (SG ? rwave_head(NB) : rwave_words(NW, NB));   // block prefix [NB + 1]
   uint32_t* J = BP + NB + 1;                                    // this receiver's new joiners       [RW_JCAP]
   uint32_t* JM = J + RW_JCAP;                                   // suffix minima of J                [RW_JCAP + 1]
-  uint32_t* S = BP + rwave_head(NB);                            // the row bitset                    [NW]
+  uint32_t* S = BP + rwave_head(NB);                            // the row bitset (LDS copy)         [NW]
   const uint32_t nnodes = *nnodes_p;
-  for (uint32_t it = blockIdx.x * 4 + wv; it < nnodes; it += gridDim.x * 4) {
+  for (uint32_t it = blockIdx.x * nwv + wv; it < nnodes; it += gridDim.x * nwv) {
     const uint32_t i = nodes[it];
     const unsigned long long* nm = pb.newmask + (size_t)i * pb.JW;
     const unsigned long long* rm = pb.respmask + (size_t)i * pb.JW;
     uint32_t nnew = 0;
     for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
     if (!resp_by_wave(d, i, nnew, true)) continue;          // wave-uniform: k_resp_node serves it
-    if (l == 0) path_hit(d, PATH_RESP_WAVE);
+    if (l == 0) path_hit(d, SG ? PATH_RESP_WAVE_HBM : PATH_RESP_WAVE);
     const bool tdbg = (d.dev & 512) != 0;                   // phase timing (KB_DEV=512, KB_DEBUG_WAVES)
     uint64_t tp0 = tdbg ? wall_clock64() : 0, tp1 = 0, tp2 = 0;
     const uint32_t* B = bits_of(d, i);                      // row membership after the Join group
     const uint4* B4 = reinterpret_cast<const uint4*>(B);
     const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
     uint32_t bc = 0, last = 0;
-    uint4* S4 = reinterpret_cast<uint4*>(S);
-    stage16(S4, B4, NW / 4, l, 64);                         // the row into LDS, every load in flight
+    const uint4* S4 = reinterpret_cast<const uint4*>(SG ? B : S);
+    if (!SG) stage16(reinterpret_cast<uint4*>(S), B4, NW / 4, l, 64);   // the row into LDS, every load in flight
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) {
       const uint4 q0 = S4[2 * k], q1 = S4[2 * k + 1];
       const uint32_t c = __popc(q0.x) + __popc(q0.y) + __popc(q0.z) + __popc(q0.w) + __popc(q1.x) + __popc(q1.y) +
@@ -972,7 +977,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
         const uint32_t nk = nB - (nnew - upto), cap = d.capj;
         uint32_t* pay = ob.pay + poff;
         const Prp P = prp_make(nk, philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1));
-        sampled_fill(pay, l, 64, cap, P, S, BP, NB, ratio, J, JM, upto, nnew);
+        sampled_fill(pay, l, 64, cap, P, SG ? B : S, BP, NB, ratio, J, JM, upto, nnew);
         if (l == 0) {
           Msg m; m.dest = a; m.sender = i; m.seq = q; m.kind = K_KP; m.a = cap; m.fp = 0; m.n = 0; m.off = poff;
           ob.msgs[ob.off[i] + q] = m;
@@ -984,7 +989,8 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     }
     // algorithmic bytes: the row bitset, its Join masks and joiner ids read; the responses' ids and
     // records written
-    if (l == 0) slot_add(d, S_RESPB, 4ull * NW + 16ull * pb.JW + 4ull * pb.nj + (4ull * d.capj + 32ull) * q);
+    if (l == 0) slot_add(d, S_RESPB, 4ull * NW + 16ull * pb.JW + 4ull * pb.nj + (4ull * d.capj + 32ull) * q +
+                                     (SG ? 32ull * d.capj * q : 0ull));   // SG: each select's block read from the row
     if (tdbg && l == 0) {
       __builtin_amdgcn_s_waitcnt(0);
       const uint64_t tp3 = wall_clock64();

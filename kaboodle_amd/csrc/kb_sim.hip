@@ -1224,13 +1224,23 @@ static int step_round(kb_sim* s) {
         scratch = s->resp_scratch;
         lds = 0;
       }
-      // a wave per responder where its LDS slice fits (4 responders per 64 KB workgroup), else a workgroup
+      // a wave per responder where its LDS slice fits (4 responders per 64 KB workgroup); wider rows keep
+      // only the slice's head in LDS and select from the row itself (up to 4 waves per workgroup, as the
+      // head fits: 3 at 1M-id rows); else (or forced) a workgroup with HBM scratch
       const size_t wlds = 16ull * rwave_words(d.NWR, s->W / 256);
-      const bool wave_on = wlds <= 65536 && !(d.dbg & KB_DBG_RESP_HBM);
+      const size_t hlds = 4ull * rwave_head(s->W / 256);
+      const bool full_on = wlds <= 65536 && !(d.dbg & (KB_DBG_RESP_HBM | KB_DBG_RESP_WAVE_HBM));
+      const uint32_t hwaves = (uint32_t)std::min<size_t>(4, 65536 / hlds);
+      const bool head_on = !full_on && hwaves >= 1 && !(d.dbg & KB_DBG_RESP_HBM);
+      const bool wave_on = full_on || head_on;
       if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
-      if (wave_on) {                                   // timed by events on its own dispatch packet
-        klaunch(s, KI_RESP_WAVE, k_resp_wave, dim3(std::min<uint32_t>((resp_nodes + 3) / 4, 4096)), dim3(256), (uint32_t)wlds, d,
+      if (full_on) {                                   // timed by events on its own dispatch packet
+        klaunch(s, KI_RESP_WAVE, k_resp_wave<false>, dim3(std::min<uint32_t>((resp_nodes + 3) / 4, 4096)), dim3(256), (uint32_t)wlds, d,
                 pb, (const uint32_t*)s->resp_nodes, (const uint32_t*)(s->scan_tot + 4), o0, r);
+      } else if (head_on) {
+        klaunch(s, KI_RESP_WAVE, k_resp_wave<true>, dim3(std::min<uint32_t>((resp_nodes + hwaves - 1) / hwaves, 4096)),
+                dim3(64 * hwaves), (uint32_t)(hwaves * hlds), d, pb, (const uint32_t*)s->resp_nodes,
+                (const uint32_t*)(s->scan_tot + 4), o0, r);
       }
       klaunch(s, KI_RESP_NODE, k_resp_node, dim3(grid), dim3(256), (uint32_t)lds, d, pb, (const uint32_t*)s->resp_nodes,
               (const uint32_t*)(s->scan_tot + 4), o0, r, scratch, wave_on);

@@ -785,13 +785,28 @@ static inline void top5_add(uint32_t* best, uint32_t* kh5, uint32_t* kl5, int* n
 static int a3_candidates(kbo_sim* s, uint32_t i, uint32_t* best) {
   uint32_t kh5[NUM_CANDIDATES], kl5[NUM_CANDIDATES];
   int nb = 0;
-  if (!s->sr) {
+  if (s->tst) {                                    /* KB_VARIANT_EXACT_LRU: the exact instants */
     const uint8_t* rw = row(s, i);
     for (uint32_t j = 0; j < s->C; ++j) {
       uint8_t b = rw[j];
       if (b < ST_ANCIENT || j == i) continue;
-      uint32_t kh = s->tst ? ((uint32_t)s->tst[(size_t)i * s->C + j] ^ 0x80000000u) : b;   /* order-preserving */
+      const uint32_t kh = (uint32_t)s->tst[(size_t)i * s->C + j] ^ 0x80000000u;   /* order-preserving */
       top5_add(best, kh5, kl5, &nb, j, kh, rot_key(j, s->a3cur[i], s->C));
+    }
+    return nb;
+  }
+  if (!s->sr) {
+    /* rotated order from the sweep front; ANCIENT is the smallest stamp, so once five ancient members have
+     * been met nothing later in that order can rank among the five */
+    const uint8_t* rw = row(s, i);
+    const uint32_t C = s->C, p0 = s->a3cur[i] + 1 == C ? 0 : s->a3cur[i] + 1;
+    int anc = 0;
+    for (uint32_t k = 0; k < C; ++k) {
+      const uint32_t j = p0 + k >= C ? p0 + k - C : p0 + k;
+      const uint8_t b = rw[j];
+      if (b < ST_ANCIENT || j == i) continue;
+      top5_add(best, kh5, kl5, &nb, j, b, k);
+      if (b == ST_ANCIENT && ++anc == NUM_CANDIDATES) break;
     }
     return nb;
   }

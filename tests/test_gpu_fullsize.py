@@ -78,7 +78,7 @@ def wide():
 
 @pytest.mark.parametrize("upto", [2, 4])
 def test_wide_rows_140k(wide, upto):
-    """W = 147,456 > RESP_LDS_W: Join responses of non-wave responders from HBM scratch."""
+    """W = 147,456: Join responses by wave, the rows read in place (k_resp_wave<true>)."""
     wide.advance(upto, nrows=12)
     if upto == 4:
         assert wide.g.stats()["join_responses"] > 0
@@ -96,7 +96,7 @@ def test_wide_rows_140k_sharded(wide):
         assert np.array_equal(a.scalars(), b.scalars())
         for i in np.random.default_rng(3).choice(cfg.capacity, 16, replace=False):
             assert np.array_equal(a.row(int(i)), b.row(int(i))), f"node {i}"
-    assert wide.g.debug_paths() & (2 | 4), "no Join response took the scratch path"
+    assert wide.g.debug_paths() & (2 | 4 | 256), "no Join response took a wide-row path"
 
 
 @pytest.fixture(scope="module")

@@ -10,7 +10,7 @@ import pytest
 
 import parity
 import scenarios
-from kaboodle_amd._ffi import KB_DBG_ALL, KB_DBG_WAVE_GRAPH, KB_INIT_CONVERGED, KB_INVALID_OPERATION, KbError, Sim, SimConfig
+from kaboodle_amd._ffi import KB_DBG_ALL, KB_DBG_RESP_WAVE_HBM, KB_DBG_WAVE_GRAPH, KB_INIT_CONVERGED, KB_INVALID_OPERATION, KbError, Sim, SimConfig
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -38,6 +38,19 @@ def test_parity_wide_row_paths(gpu, name, case, rounds):
     k_proc's unsorted selection path), forced by kb_config.debug_flags at these sizes."""
     ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_ALL), rounds)
     assert ok, f"{name} (debug_flags={KB_DBG_ALL}): {msg}"
+
+
+@pytest.mark.parametrize("name", ["config2_join_1k", "churn_loss_512", "probes"])
+def test_parity_resp_wave_rows_in_place(gpu, name):
+    """Join responses by wave with the rows read in place (the path of rows too wide for a wave's LDS
+    copy, configs[3]'s 1M-id rows), forced by KB_DBG_RESP_WAVE_HBM at these sizes."""
+    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}[name]
+    g = Sim(gpu, parity.with_cfg(case, debug_flags=KB_DBG_RESP_WAVE_HBM)["cfg"])
+    ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_RESP_WAVE_HBM), rounds, gpu=g)
+    assert ok, f"{name} (rows in place): {msg}"
+    if name == "config2_join_1k":
+        assert g.debug_paths() & 256 and not g.debug_paths() & 64
+    g.close()
 
 
 @pytest.mark.parametrize("name", ["churn_loss_512", "partition_heal", "identity_change", "hot_inbox"])
