@@ -407,7 +407,10 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
 }
 
 template <bool LDSB>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 8))) void k_rowpass(Dev d, PhaseB pb, RowOut ro, int32_t r, uint32_t lf, uint32_t lj) {
+#ifndef KB_RP_WPE
+#define KB_RP_WPE 4           // minimum waves per SIMD the row pass is compiled for (register budget 512 / KB_RP_WPE)
+#endif
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KB_RP_WPE, 8))) void k_rowpass(Dev d, PhaseB pb, RowOut ro, int32_t r, uint32_t lf, uint32_t lj) {
   extern __shared__ uint32_t pb_dyn[];
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wv = threadIdx.x >> 6;

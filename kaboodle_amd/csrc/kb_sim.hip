@@ -1137,7 +1137,10 @@ static int step_round(kb_sim* s) {
     uint32_t lf = s->nf <= PB_FMAX, lj = s->nj <= PB_JMAX;
     uint32_t listw = (lf ? 2 * s->nf : 0) + (lj ? s->nj : 0);
     if (listw > budget / 2 || pb_hbm) { lf = lj = 0; listw = 0; }
-    const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR && !pb_hbm;
+    // the LDS variant stages each row's whole bitset for the Failed group's membership tests; without a
+    // Failed list (quiet rounds: A3 and a few Joins only) the row is read where A3 and the Joins touch it
+    // (372K peers, no broadcasts: 3.41 -> 0.54 ms, profiles/r04e_rowpass_variants.json)
+    const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR && !pb_hbm && s->nf > 0;
     const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / d.NWR) : RP_WAVES;
     const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
     int occ = 0;                                       // resident workgroups per CU (LDS, registers)

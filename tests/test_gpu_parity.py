@@ -40,17 +40,26 @@ def test_parity_wide_row_paths(gpu, name, case, rounds):
     assert ok, f"{name} (debug_flags={KB_DBG_ALL}): {msg}"
 
 
-@pytest.mark.parametrize("name", ["config2_join_1k", "churn_loss_512", "probes"])
+TRUNC_CASES = {
+    # views of > 567 ids: every Join response is a sampled (truncated) one, served by wave
+    "trunc_1200": ({"cfg": SimConfig(capacity=1300, initial_nodes=1200, init_mode=KB_INIT_CONVERGED, churn=0.01, seed=23)}, 6),
+    "trunc_loss_1800": ({"cfg": SimConfig(capacity=2000, initial_nodes=1800, init_mode=KB_INIT_CONVERGED, churn=0.005,
+                                          loss=0.02, seed=5, id_len=3)}, 8),
+}
+
+
+@pytest.mark.parametrize("name", sorted(TRUNC_CASES))
 def test_parity_resp_wave_rows_in_place(gpu, name):
     """Join responses by wave with the rows read in place (the path of rows too wide for a wave's LDS
-    copy, configs[3]'s 1M-id rows), forced by KB_DBG_RESP_WAVE_HBM at these sizes."""
-    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}[name]
-    g = Sim(gpu, parity.with_cfg(case, debug_flags=KB_DBG_RESP_WAVE_HBM)["cfg"])
-    ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_RESP_WAVE_HBM), rounds, gpu=g)
-    assert ok, f"{name} (rows in place): {msg}"
-    if name == "config2_join_1k":
-        assert g.debug_paths() & 256 and not g.debug_paths() & 64
-    g.close()
+    copy, configs[3]'s 1M-id rows), forced by KB_DBG_RESP_WAVE_HBM at these sizes; and the same cases on
+    the default (LDS copy) wave path."""
+    case, rounds = TRUNC_CASES[name]
+    for flags, want in ((KB_DBG_RESP_WAVE_HBM, 256), (0, 64)):
+        g = Sim(gpu, parity.with_cfg(case, debug_flags=flags)["cfg"])
+        ok, msg, st = parity.run_case(parity.with_cfg(case, debug_flags=flags), rounds, gpu=g)
+        assert ok, f"{name} (debug_flags={flags}): {msg}"
+        assert st["join_responses"] > 0 and g.debug_paths() & want and not g.debug_paths() & (320 ^ want)
+        g.close()
 
 
 @pytest.mark.parametrize("name", ["churn_loss_512", "partition_heal", "identity_change", "hot_inbox"])
