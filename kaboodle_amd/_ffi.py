@@ -138,7 +138,6 @@ _SIGS = {
     "sim_step": (C.c_int, [C.c_void_p, C.c_uint32]),
     "sim_start_node": (C.c_int, [C.c_void_p, C.c_uint32]),
     "sim_stop_node": (C.c_int, [C.c_void_p, C.c_uint32]),
-    "sim_restart_node": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     "sim_is_running": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_int)]),
     "sim_ping_addrs": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32), C.c_size_t]),
     "sim_set_identity": (C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p, C.c_size_t]),
@@ -167,6 +166,7 @@ _SIGS = {
     "last_error": (C.c_char_p, []),
 }
 _OPTIONAL = {
+    "sim_restart_node": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     # sharding (HIP library only; the oracle is the unsharded mesh every shard layout must reproduce)
     "rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8), C.c_size_t]),
     "sim_create_rank": (C.c_int, [C.POINTER(KbConfig), C.c_int32, C.c_int32, C.POINTER(C.c_uint8),
