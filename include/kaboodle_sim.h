@@ -258,7 +258,7 @@ int  kb_sim_dump_scalars(kb_sim* sim, int32_t* out, size_t cap);
 /* Canonical suspect table: sorted (peer, kind, since) triples for `node`; n = triples written.      */
 int  kb_sim_dump_suspects(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, size_t* n);
 /* OR of the kernel-variant bits that did work since creation (PATH_* in kaboodle_amd/csrc/kb_common.h:
-   1 broadcast phase on the HBM bitset, 2/4 Join responses from HBM scratch (sampled / complete),
+   1 broadcast phase on the HBM bitset (a round with a Failed list), 2/4 Join responses from HBM scratch (sampled / complete),
    8 KnownPeers BIG group on the HBM bitset, 16 k_proc unsorted selection path, 32 Failed-list prep
    from HBM, 64 Join responses by wave, 128 KnownPeers BIG group in LDS, 256 Join responses by wave
    from the rows in place).  Test surface.                                                          */

@@ -656,7 +656,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KB_RP_WPE, 
   if (l == 0) {
     s_cnt[wv][0] = w_lost; s_cnt[wv][1] = w_removed; s_cnt[wv][2] = w_resp; s_cnt[wv][3] = w_bytes;
     s_cnt[wv][4] = a3c.x; s_cnt[wv][5] = a3c.y; s_cnt[wv][6] = a3c.z;
-    if (!LDSB && w_nodes) path_hit(d, PATH_PHASEB_HBM);
+    if (!LDSB && w_nodes && pb.nf) path_hit(d, PATH_PHASEB_HBM);   // the Failed group on the HBM bitset
   }
   __syncthreads();
   if (threadIdx.x < 7) {

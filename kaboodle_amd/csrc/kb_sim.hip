@@ -965,7 +965,8 @@ static int launch_waves(kb_sim* s, int32_t rk) {
        // then the small ones (a wave per destination), which also set up nb.cap / nb.cnt
       const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
       const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
-      klaunch(s, KI_KP, k_kp, dim3(ks * groups + (R + 1023) / 1024), dim3(1024), (uint32_t)kp_lds_bytes(d.NWR), d, ib, s->wc, r,
+      const uint32_t small = std::max<uint32_t>((R + 1023) / 1024, s->ncu);
+      klaunch(s, KI_KP, k_kp, dim3(ks * groups + small), dim3(1024), (uint32_t)kp_lds_bytes(d.NWR), d, ib, s->wc, r,
               nb, ks * groups);
     }
     // inbox sorts + the KPR oversize probe, and the fast handlers
@@ -974,7 +975,7 @@ static int launch_waves(kb_sim* s, int32_t rk) {
     // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
     // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
     // on the late waves with few nodes.
-    klaunch(s, KI_PROC, k_proc, dim3(std::min<uint32_t>(4096, 2 * s->ncu)), dim3(256), 0, d, ib, nb, s->wc, r, s->slow);
+    klaunch(s, KI_PROC, k_proc, dim3(std::min<uint32_t>(4096, (KB_PROC_WPE > 2 ? KB_PROC_WPE : 2) * s->ncu)), dim3(256), 0, d, ib, nb, s->wc, r, s->slow);
     if (s->debug_waves) {
       uint32_t dbg[13], slow = 0;
       HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost, st));

@@ -584,7 +584,9 @@ __device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d
 
 // The groups under KP_BIG ids (KnownPeersRequest replies, small Join lists): a wave per destination,
 // in place on the row's bitset, the same arms-then-prologues order as the BIG groups.  (The body of
-// k_kp's last nblk workgroups.)
+// k_kp's last nblk workgroups: at least one per CU, since a round of the converged start's first
+// SHARE_AGE rounds delivers ~24K replies of a few hundred ids at 64K peers in one wave.)
+constexpr int KPS_UNROLL = 4;
 __device__ __attribute__((always_inline)) inline void kp_small_body(const Dev& d, const OutBuf& ib, const WaveCtl& wc, int32_t r,
                                                                    const OutBuf& nb, uint32_t bid, uint32_t nblk) {
   __shared__ uint32_t s_list[1024], s_nl;
@@ -611,12 +613,38 @@ __device__ __attribute__((always_inline)) inline void kp_small_body(const Dev& d
       uint8_t* rw = row_of(d, i);
       unsigned long long segs = 0;
       uint32_t added = 0;
-      for (uint32_t q = 0; q < nk; ++q) {                  // arms
-        const Msg m = ib.msgs[wc.kin[k0 + q]];
-        for (uint32_t e = l; e < m.a; e += 64) {
-          const uint32_t p = ib.pay[m.off + e], bit = 1u << (p & 31);
-          if (__hip_atomic_load(&B[p >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit) continue;
-          if (!(atomicOr(&B[p >> 5], bit) & bit)) { rw[p] = old; segs |= seg_bit(d, p); added++; }
+      // arms: KPS_UNROLL x 64 ids per step, their loads in flight together (all ids, then all member
+      // words, then the atomics of the absent ones): a KnownPeersRequest reply of a few hundred ids
+      // costs two HBM round trips, not two per 64 ids.  The records of up to 64 messages are fetched at
+      // once (lane k holds message q0 + k).
+      for (uint32_t q0 = 0; q0 < nk; q0 += 64) {
+        uint32_t moff = 0, mlen = 0;
+        if (q0 + l < nk) { const Msg m = ib.msgs[wc.kin[k0 + q0 + l]]; moff = m.off; mlen = m.a; }
+        const uint32_t qn = nk - q0 < 64 ? nk - q0 : 64u;
+        for (uint32_t j = 0; j < qn; ++j) {
+          const uint32_t off = bcast(moff, (int)j), len = bcast(mlen, (int)j);
+          for (uint32_t e0 = 0; e0 < len; e0 += 64 * KPS_UNROLL) {
+            uint32_t pv[KPS_UNROLL], wv_[KPS_UNROLL], ob_[KPS_UNROLL];
+#pragma unroll
+            for (int u = 0; u < KPS_UNROLL; ++u) {
+              const uint32_t e = e0 + 64u * u + l;
+              pv[u] = e < len ? ib.pay[off + e] : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int u = 0; u < KPS_UNROLL; ++u)
+              wv_[u] = pv[u] != 0xFFFFFFFFu ? __hip_atomic_load(&B[pv[u] >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                            : 0xFFFFFFFFu;
+#pragma unroll
+            for (int u = 0; u < KPS_UNROLL; ++u) {
+              const uint32_t bit = 1u << (pv[u] & 31);
+              ob_[u] = (wv_[u] & bit) ? bit : atomicOr(&B[pv[u] >> 5], bit);
+            }
+#pragma unroll
+            for (int u = 0; u < KPS_UNROLL; ++u) {
+              const uint32_t p = pv[u];
+              if (!(ob_[u] & (1u << (p & 31)))) { rw[p] = old; segs |= seg_bit(d, p); added++; }
+            }
+          }
         }
       }
       wave_mem_sync();
@@ -887,7 +915,11 @@ __global__ __launch_bounds__(1024) void k_sortfast(Dev d, OutBuf ib, OutBuf ob, 
   else fast_body(d, ib, ob, wc, r, slow, blockIdx.x - nsort);
 }
 
-__global__ __launch_bounds__(256) void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32_t* list) {
+#ifndef KB_PROC_WPE
+#define KB_PROC_WPE 1         // minimum waves per SIMD k_proc is compiled for (A/B knob; 1 = the compiler's choice)
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KB_PROC_WPE)))
+void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32_t* list) {
   const int32_t r = round_of(d, r_arg);
   __shared__ uint32_t ztab[ZT * 128];
   __shared__ Susp s_susp[4][SLOTS];
