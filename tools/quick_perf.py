@@ -8,7 +8,8 @@ R = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 MODE = KB_FAILED_SOCKET_FAITHFUL if (len(sys.argv) > 3 and sys.argv[3] == "sock") else KB_FAILED_SIM_SENDER
 # the bench's sizing (bench.rank_config): capacity = peers + churn reserve for the run
 cfg = SimConfig(capacity=N + max(4096, int(N * 0.001 * (R + 10) * 1.5)), initial_nodes=N, init_mode=KB_INIT_CONVERGED,
-                loss=0.01, churn=0.001, seed=1, failed_mode=MODE, track_latency=int("lat" in sys.argv[4:]))
+                loss=0.01, churn=0.001, seed=1, failed_mode=MODE, track_latency=int("lat" in sys.argv[4:]),
+                debug_flags=int(os.environ.get("KB_QP_DBG", "0"), 0))   # KB_QP_DBG: force kernel variants (A/B)
 t = time.time(); m = kaboodle_amd.Mesh(cfg); print("create", round(time.time() - t, 2), flush=True)
 m.step(2)
 m.reset_kernel_time()
