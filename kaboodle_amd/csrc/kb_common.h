@@ -37,6 +37,7 @@ enum CtrIdx {
   C_ROUND,                        // the round being simulated (k_log_mark): graph-replayed kernels read it here
   C_PATHS,                        // OR of the PATH_* bits of the kernel variants that did work (test surface)
   C_DBG_SLOW_LONG, C_DBG_SLOW_NONMEM, C_DBG_SLOW_DIRTY, C_DBG_SLOW_KPR, C_DBG_SLOW_OTHER,   // KB_DEV & 256: why k_proc
+  C_RESTN,                        // responders k_resp_wave left to k_resp_node (their list: the wave lists' slow buffer)
   NCTR
 };
 // kernel-variant coverage bits (kb_sim_debug_paths): the wide-row paths a >= 1M-id mesh takes

@@ -406,35 +406,39 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
   return wave_sum(nbytes);
 }
 
-template <bool LDSB>
+// LDSB: the row's bitset staged in LDS; LL: both broadcast lists staged in LDS (every list read is then an
+// LDS read: a runtime choice between LDS and HBM made the compiler read the Failed entries through flat
+// pointers, whose wait covered the HBM counter too and cost the loop one L2 round trip per 64 entries)
+template <bool LDSB, bool LL>
 #ifndef KB_RP_WPE
 #define KB_RP_WPE 4           // minimum waves per SIMD the row pass is compiled for (register budget 512 / KB_RP_WPE)
 #endif
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KB_RP_WPE, 8))) void k_rowpass(Dev d, PhaseB pb, RowOut ro, int32_t r, uint32_t lf, uint32_t lj) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KB_RP_WPE, 8))) void k_rowpass(Dev d, PhaseB pb, RowOut ro, int32_t r) {
   extern __shared__ uint32_t pb_dyn[];
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t l = lane();
-  uint32_t* FL = pb_dyn + (LDSB ? (size_t)wpb * d.NWR : 0);   // [2 * nf] when lf
-  uint32_t* JL = FL + (lf ? 2 * pb.nf : 0);                    // [nj] when lj
-  if (lf) for (uint32_t e = threadIdx.x; e < pb.nf; e += blockDim.x) {
-    const BCast b = pb.bfail[e];
-    FL[2 * e] = b.sender | (b.bseq << 23) | ((uint32_t)pb.dep[e] << 31);
-    FL[2 * e + 1] = b.peer;
+  uint2* FL = reinterpret_cast<uint2*>(pb_dyn + (LDSB ? (size_t)wpb * d.NWR : 0));   // [nf] when LL
+  uint32_t* JL = reinterpret_cast<uint32_t*>(FL + (LL ? pb.nf : 0));                // [nj] when LL
+  if (LL) {
+    for (uint32_t e = threadIdx.x; e < pb.nf; e += blockDim.x) {
+      const BCast b = pb.bfail[e];
+      FL[e] = make_uint2(b.sender | (b.bseq << 23) | ((uint32_t)pb.dep[e] << 31), b.peer);
+    }
+    for (uint32_t e = threadIdx.x; e < pb.nj; e += blockDim.x) JL[e] = pb.bjoin[e].sender | (pb.bjoin[e].bseq << 23);
   }
-  if (lj) for (uint32_t e = threadIdx.x; e < pb.nj; e += blockDim.x) JL[e] = pb.bjoin[e].sender | (pb.bjoin[e].bseq << 23);
   __syncthreads();
   auto fail_at = [&](uint32_t e, uint32_t& dep) __attribute__((always_inline)) -> BCast {
-    if (lf) {
-      const uint32_t x = FL[2 * e];
-      dep = x >> 31;
-      return BCast{x & 0x7FFFFFu, FL[2 * e + 1], (x >> 23) & 0xFFu, 0};
+    if (LL) {
+      const uint2 x = FL[e];
+      dep = x.x >> 31;
+      return BCast{x.x & 0x7FFFFFu, x.y, (x.x >> 23) & 0xFFu, 0};
     }
     dep = pb.dep[e];
     return pb.bfail[e];
   };
   auto join_at = [&](uint32_t e) __attribute__((always_inline)) -> BCast {
-    if (lj) { const uint32_t x = JL[e]; return BCast{x & 0x7FFFFFu, x & 0x7FFFFFu, x >> 23, 0}; }
+    if (LL) { const uint32_t x = JL[e]; return BCast{x & 0x7FFFFFu, x & 0x7FFFFFu, x >> 23, 0}; }
     return pb.bjoin[e];
   };
   const bool honour = d.failed_mode == KB_FAILED_SIM_SENDER;
@@ -903,7 +907,7 @@ __device__ inline bool resp_by_wave(const Dev& d, uint32_t i, uint32_t nnew, boo
 // its responses.  (The workgroup path instead copied each row to HBM scratch first.)
 template <bool SG>
 __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint32_t* nodes, const uint32_t* nnodes_p,
-                                                   OutBuf ob, int32_t r) {
+                                                   OutBuf ob, int32_t r, uint32_t* rest) {
   extern __shared__ __attribute__((aligned(16))) uint32_t rw_lds[];
   const uint32_t NW = d.NWR, NB = d.W / 256;
   const uint32_t wv = threadIdx.x >> 6, l = lane(), nwv = blockDim.x >> 6;
@@ -912,22 +916,44 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
   uint32_t* JM = J + RW_JCAP;                                   // suffix minima of J                [RW_JCAP + 1]
   uint32_t* S = BP + rwave_head(NB);                            // the row bitset (LDS copy)         [NW]
   const uint32_t nnodes = *nnodes_p;
-  for (uint32_t it = blockIdx.x * nwv + wv; it < nnodes; it += gridDim.x * nwv) {
-    const uint32_t i = nodes[it];
+  // A responder's HBM reads (its Join masks, header words, row bitset) are issued together, with the next
+  // responder's id: one memory round trip per responder instead of one per dependent use.  With at most 64
+  // mask words and 128 Join entries (every round of a large mesh) lane l holds mask word l and the ids of
+  // Join entries l and l + 64, which are the same for every responder and read once.
+  const bool small_lists = pb.JW <= 64 && pb.nj <= 128;
+  const uint32_t js0 = small_lists && l < pb.nj ? pb.bjoin[l].sender : 0u;
+  const uint32_t js1 = small_lists && l + 64 < pb.nj ? pb.bjoin[l + 64].sender : 0u;
+  const uint32_t stride = gridDim.x * nwv;
+  uint32_t it = blockIdx.x * nwv + wv;
+  uint32_t inext = it < nnodes ? nodes[it] : 0u;
+  for (; it < nnodes; it += stride) {
+    const uint32_t i = inext;
     const unsigned long long* nm = pb.newmask + (size_t)i * pb.JW;
     const unsigned long long* rm = pb.respmask + (size_t)i * pb.JW;
+    const unsigned long long nmv = small_lists && l < pb.JW ? nm[l] : 0ull;
+    const unsigned long long rmv = small_lists && l < pb.JW ? rm[l] : 0ull;
+    const uint32_t n_i = d.n[i], nbase_i = pb.nbase[i], poff_i = ob.poff[i], ooff_i = ob.off[i];
+    inext = it + stride < nnodes ? nodes[it + stride] : 0u;
+    const uint32_t* B = bits_of(d, i);                      // row membership after the Join group
+    const uint4* B4 = reinterpret_cast<const uint4*>(B);
+    // the row into LDS, every load in flight, before the wave-path test: it fails for a few responders at
+    // most (each then costs one wasted copy) and the copy's wait covers the loads above
+    if (!SG) stage16(reinterpret_cast<uint4*>(S), B4, NW / 4, l, 64);
     uint32_t nnew = 0;
-    for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
-    if (!resp_by_wave(d, i, nnew, true)) continue;          // wave-uniform: k_resp_node serves it
+    if (small_lists) nnew = wave_sum((uint32_t)__popcll(nmv));
+    else for (uint32_t wj = 0; wj < pb.JW; ++wj) nnew += __popcll(nm[wj]);
+    if (!(d.uniform && nnew <= RW_JCAP && n_i - nnew > d.capj)) {   // resp_by_wave: k_resp_node serves it
+      if (l == 0) rest[atomicAdd(&d.ctr[C_RESTN], 1u)] = i;
+      wait_lds();
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
     if (l == 0) path_hit(d, SG ? PATH_RESP_WAVE_HBM : PATH_RESP_WAVE);
     const bool tdbg = (d.dev & 512) != 0;                   // phase timing (KB_DEV=512, KB_DEBUG_WAVES)
     uint64_t tp0 = tdbg ? wall_clock64() : 0, tp1 = 0, tp2 = 0;
-    const uint32_t* B = bits_of(d, i);                      // row membership after the Join group
-    const uint4* B4 = reinterpret_cast<const uint4*>(B);
     const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
     uint32_t bc = 0, last = 0;
     const uint4* S4 = reinterpret_cast<const uint4*>(SG ? B : S);
-    if (!SG) stage16(reinterpret_cast<uint4*>(S), B4, NW / 4, l, 64);   // the row into LDS, every load in flight
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) {
       const uint4 q0 = S4[2 * k], q1 = S4[2 * k + 1];
       const uint32_t c = __popc(q0.x) + __popc(q0.y) + __popc(q0.z) + __popc(q0.w) + __popc(q1.x) + __popc(q1.y) +
@@ -942,11 +968,18 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) { const uint32_t c = BP[k]; BP[k] = ex; ex += c; }
     if (l == 0) BP[NB] = nB;
     if (tdbg) { wait_lds(); tp1 = wall_clock64(); }
-    for (uint32_t e = l; e < pb.nj; e += 64) {              // new joiners in list order
-      if (!newbit(nm, e)) continue;
-      uint32_t pos = __popcll(nm[e >> 6] & ((1ull << (e & 63)) - 1ull));
-      for (uint32_t w2 = 0; w2 < (e >> 6); ++w2) pos += __popcll(nm[w2]);
-      J[pos] = pb.bjoin[e].sender;
+    if (small_lists) {                                      // new joiners in list order: entries l and l + 64
+      const unsigned long long w0 = ((unsigned long long)bcast((uint32_t)(nmv >> 32), 0) << 32) | bcast((uint32_t)nmv, 0);
+      const unsigned long long w1 = ((unsigned long long)bcast((uint32_t)(nmv >> 32), 1) << 32) | bcast((uint32_t)nmv, 1);
+      if (l < pb.nj && ((w0 >> l) & 1ull)) J[__popcll(w0 & ((1ull << l) - 1ull))] = js0;
+      if (l + 64 < pb.nj && ((w1 >> l) & 1ull)) J[__popcll(w0) + __popcll(w1 & ((1ull << l) - 1ull))] = js1;
+    } else {
+      for (uint32_t e = l; e < pb.nj; e += 64) {
+        if (!newbit(nm, e)) continue;
+        uint32_t pos = __popcll(nm[e >> 6] & ((1ull << (e & 63)) - 1ull));
+        for (uint32_t w2 = 0; w2 < (e >> 6); ++w2) pos += __popcll(nm[w2]);
+        J[pos] = pb.bjoin[e].sender;
+      }
     }
     wait_lds();
     __builtin_amdgcn_wave_barrier();
@@ -965,25 +998,30 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     }
     wait_lds();
     __builtin_amdgcn_wave_barrier();
-    uint32_t poff = ob.poff[i], q = 0, ins_before = 0;
+    uint32_t poff = poff_i, q = 0, ins_before = 0;
     if (tdbg) tp2 = wall_clock64();
     for (uint32_t wj = 0; wj < pb.JW; ++wj) {
-      unsigned long long rmw = rm[wj];
-      const unsigned long long nmw = nm[wj];
+      unsigned long long rmw, nmw;
+      if (small_lists) {
+        rmw = ((unsigned long long)bcast((uint32_t)(rmv >> 32), (int)wj) << 32) | bcast((uint32_t)rmv, (int)wj);
+        nmw = ((unsigned long long)bcast((uint32_t)(nmv >> 32), (int)wj) << 32) | bcast((uint32_t)nmv, (int)wj);
+      } else {
+        rmw = rm[wj]; nmw = nm[wj];
+      }
       while (rmw) {
         const uint32_t bit = (uint32_t)(__ffsll((long long)rmw) - 1);
         const uint32_t K = wj * 64 + bit;
         rmw &= rmw - 1;
         const uint32_t upto = ins_before + __popcll(nmw & ((2ull << bit) - 1ull));   // new joiners <= K
-        const uint32_t expect = pb.nbase[i] + upto;
-        const uint32_t a = pb.bjoin[K].sender;
+        const uint32_t expect = nbase_i + upto;
+        const uint32_t a = small_lists ? (K < 64 ? bcast(js0, (int)K) : bcast(js1, (int)(K - 64))) : pb.bjoin[K].sender;
         const uint32_t nk = nB - (nnew - upto), cap = d.capj;
         uint32_t* pay = ob.pay + poff;
         const Prp P = prp_make(nk, philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1));
         sampled_fill(pay, l, 64, cap, P, SG ? B : S, BP, NB, ratio, J, JM, upto, nnew);
         if (l == 0) {
           Msg m; m.dest = a; m.sender = i; m.seq = q; m.kind = K_KP; m.a = cap; m.fp = 0; m.n = 0; m.off = poff;
-          ob.msgs[ob.off[i] + q] = m;
+          ob.msgs[ooff_i + q] = m;
           if (nk != expect) set_err(d, DERR_RESP);
         }
         poff += cap; q++;

@@ -153,7 +153,7 @@ __global__ void k_set_cap(Dev d, const uint32_t* nresp, uint32_t* cap, uint32_t*
                           uint32_t seq) {
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (i < d.hi) { cap[i] = nresp[i] + TICK_MAX; cnt[i] = nresp[i]; }
-  if (blockIdx.x == 0 && threadIdx.x == 0) pin_publish(hpin, tot, 5, seq);
+  if (blockIdx.x == 0 && threadIdx.x == 0) { d.ctr[C_RESTN] = 0; pin_publish(hpin, tot, 5, seq); }
 }
 // device values -> the host's mapped pinned buffer, then the sequence number it polls for (sharded
 // hand-offs of all-gathered counts)
@@ -442,7 +442,13 @@ static void prof_resolve(kb_sim* s, size_t n) {
   for (size_t k = 0; k < n; ++k) {
     const kb_sim::KRec& q = s->krec[k];
     float ms = 0;
-    if (hipEventElapsedTime(&ms, q.a, q.b) == hipSuccess) {
+    hipError_t e = hipEventElapsedTime(&ms, q.a, q.b);
+    if (e == hipErrorNotReady) {                      // still pending (an earlier round's tail): wait for it
+      (void)hipGetLastError();                        // rather than drop the record and recycle live events
+      (void)hipEventSynchronize(q.b);
+      e = hipEventElapsedTime(&ms, q.a, q.b);
+    }
+    if (e == hipSuccess) {
       if (q.kid == NKI) { s->round_ms += ms; s->round_launches++; }          // the whole round
       else {
         s->k_ms[q.kid] += ms; s->k_n[q.kid]++;
@@ -970,8 +976,8 @@ static int launch_waves(kb_sim* s, int32_t rk) {
               nb, ks * groups);
     }
     // inbox sorts + the KPR oversize probe, and the fast handlers
-    klaunch(s, KI_SORTFAST, k_sortfast, dim3(SORT_GROUPS + (R + 1023) / 1024), dim3(1024), 0, d, ib, nb, s->wc, r, s->slow,
-            SORT_GROUPS);
+    klaunch(s, KI_SORTFAST, k_sortfast, dim3(SORT_GROUPS + (R + SORTFAST_T - 1) / SORTFAST_T), dim3(SORTFAST_T), 0, d, ib, nb,
+            s->wc, r, s->slow, SORT_GROUPS);
     // persistent: as many workgroups as stay resident (204 VGPRs: 2 waves/SIMD, 2 workgroups per CU).
     // A larger grid only queues workgroups that read the node count and exit, which set a ~40 us floor
     // on the late waves with few nodes.
@@ -1135,9 +1141,9 @@ static int step_round(kb_sim* s) {
     // once per workgroup when they fit.  Its events are taken by its own dispatch packet
     // (hipExtLaunchKernel), so they time the kernel itself.
     const uint32_t budget = RP_LDS_BYTES / 4;          // dynamic LDS words per workgroup
-    uint32_t lf = s->nf <= PB_FMAX, lj = s->nj <= PB_JMAX;
-    uint32_t listw = (lf ? 2 * s->nf : 0) + (lj ? s->nj : 0);
-    if (listw > budget / 2 || pb_hbm) { lf = lj = 0; listw = 0; }
+    bool ll = s->nf <= PB_FMAX && s->nj <= PB_JMAX;   // both broadcast lists staged in LDS
+    uint32_t listw = ll ? 2 * s->nf + s->nj : 0;
+    if (listw > budget / 2 || pb_hbm) { ll = false; listw = 0; }
     // the LDS variant stages each row's whole bitset for the Failed group's membership tests; without a
     // Failed list (quiet rounds: A3 and a few Joins only) the row is read where A3 and the Joins touch it
     // (372K peers, no broadcasts: 3.41 -> 0.54 ms, profiles/r04e_rowpass_variants.json)
@@ -1145,12 +1151,12 @@ static int step_round(kb_sim* s) {
     const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / d.NWR) : RP_WAVES;
     const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
     int occ = 0;                                       // resident workgroups per CU (LDS, registers)
-    const uint64_t okey = ((uint64_t)ldsb << 63) | ((uint64_t)wpb << 40) | (uint64_t)lds;   // queried once per shape
+    const void* rpk = ldsb ? (ll ? reinterpret_cast<const void*>(&k_rowpass<true, true>) : reinterpret_cast<const void*>(&k_rowpass<true, false>))
+                           : (ll ? reinterpret_cast<const void*>(&k_rowpass<false, true>) : reinterpret_cast<const void*>(&k_rowpass<false, false>));
+    const uint64_t okey = ((uint64_t)ldsb << 63) | ((uint64_t)ll << 62) | ((uint64_t)wpb << 40) | (uint64_t)lds;   // queried once per shape
     if (okey == s->occ_key) occ = s->occ_val;
     else {
-      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ldsb ? reinterpret_cast<const void*>(&k_rowpass<true>)
-                                                                     : reinterpret_cast<const void*>(&k_rowpass<false>),
-                                                         (int)(64 * wpb), lds);
+      (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, rpk, (int)(64 * wpb), lds);
       s->occ_key = okey; s->occ_val = occ;
     }
     const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(8, (uint32_t)occ));
@@ -1160,8 +1166,10 @@ static int step_round(kb_sim* s) {
               lds, per_cu, (size_t)s->lds_per_cu, blocks);
     const bool rp_prof = s->debug_waves && (d.dev & 2048);
     if (rp_prof) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_TNODE, 0, 4 * (C_DBG_MSGS - C_DBG_TNODE), st));
-    if (ldsb) klaunch(s, KI_ROWPASS, k_rowpass<true>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r, lf, lj);
-    else klaunch(s, KI_ROWPASS, k_rowpass<false>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r, lf, lj);
+    if (ldsb && ll) klaunch(s, KI_ROWPASS, k_rowpass<true, true>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r);
+    else if (ldsb) klaunch(s, KI_ROWPASS, k_rowpass<true, false>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r);
+    else if (ll) klaunch(s, KI_ROWPASS, k_rowpass<false, true>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r);
+    else klaunch(s, KI_ROWPASS, k_rowpass<false, false>, dim3(blocks), dim3(64 * wpb), (uint32_t)lds, d, pb, s->ro, r);
     if (rp_prof) {                                     // KB_DEV=2048: the row pass's phases, summed over its waves
       uint32_t t[13];
       HIPCHK(hipMemcpy(t, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost));
@@ -1240,14 +1248,17 @@ static int step_round(kb_sim* s) {
       if (s->debug_waves) HIPCHK(hipMemsetAsync(d.ctr + C_DBG_INS, 0, 52, st));
       if (full_on) {                                   // timed by events on its own dispatch packet
         klaunch(s, KI_RESP_WAVE, k_resp_wave<false>, dim3(std::min<uint32_t>((resp_nodes + 3) / 4, 4096)), dim3(256), (uint32_t)wlds, d,
-                pb, (const uint32_t*)s->resp_nodes, (const uint32_t*)(s->scan_tot + 4), o0, r);
+                pb, (const uint32_t*)s->resp_nodes, (const uint32_t*)(s->scan_tot + 4), o0, r, s->slow);
       } else if (head_on) {
         klaunch(s, KI_RESP_WAVE, k_resp_wave<true>, dim3(std::min<uint32_t>((resp_nodes + hwaves - 1) / hwaves, 4096)),
                 dim3(64 * hwaves), (uint32_t)(hwaves * hlds), d, pb, (const uint32_t*)s->resp_nodes,
-                (const uint32_t*)(s->scan_tot + 4), o0, r);
+                (const uint32_t*)(s->scan_tot + 4), o0, r, s->slow);
       }
-      klaunch(s, KI_RESP_NODE, k_resp_node, dim3(grid), dim3(256), (uint32_t)lds, d, pb, (const uint32_t*)s->resp_nodes,
-              (const uint32_t*)(s->scan_tot + 4), o0, r, scratch, wave_on);
+      // the workgroup path serves what the wave path left: its list (in the wave lists' slow buffer, free
+      // until the tick) when the wave path ran, else every responder
+      klaunch(s, KI_RESP_NODE, k_resp_node, dim3(grid), dim3(256), (uint32_t)lds, d, pb,
+              (const uint32_t*)(wave_on ? s->slow : s->resp_nodes), (const uint32_t*)(wave_on ? d.ctr + C_RESTN : s->scan_tot + 4),
+              o0, r, scratch, wave_on);
       if (s->debug_waves && (d.dev & 512)) {
         uint32_t dbg[13];
         HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost, st));

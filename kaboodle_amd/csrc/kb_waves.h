@@ -704,9 +704,9 @@ __device__ __attribute__((always_inline)) inline void sort_body(const Dev& d, co
   __shared__ uint32_t v[SORT_MAX];
   __shared__ uint32_t s_list[1024], s_nl;
   const uint32_t nact = d.ctr[C_ACTIVE];
-  // the active list 1024 entries per workgroup at a time, interleaved over the workgroups: its long
+  // the active list blockDim entries per workgroup at a time, interleaved over the workgroups: its long
   // inboxes are listed in LDS by all threads at once
-  for (uint32_t c0 = 0; c0 < nact; c0 += nblk * 1024) {
+  for (uint32_t c0 = 0; c0 < nact; c0 += nblk * blockDim.x) {
   const uint32_t it = c0 + threadIdx.x * nblk + bid;
   if (threadIdx.x == 0) s_nl = 0;
   __syncthreads();
@@ -908,13 +908,19 @@ __device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, co
 // launch.  They touch disjoint nodes: the sorts take inboxes > 64 entries, the fast lane <= FAST_MAX; a
 // node with a KnownPeersRequest is fast only once the probe has proven its replies oversize (kpr_big = r,
 // written by the probe after its last read of that row), else it goes to k_proc, which reads the proof.
-__global__ __launch_bounds__(1024) void k_sortfast(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, uint32_t* slow,
+// 256-thread workgroups: the fast lane's nodes are then spread over every CU (with 1024-thread workgroups the
+// (R + 1023) / 1024 fast workgroups, one per CU at this kernel's occupancy, left most CUs idle)
+constexpr uint32_t SORTFAST_T = 256;
+__global__ __launch_bounds__(SORTFAST_T) void k_sortfast(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, uint32_t* slow,
                                                    uint32_t nsort) {
   const int32_t r = round_of(d, r_arg);
   if (blockIdx.x < nsort) sort_body(d, wc, r, blockIdx.x, nsort);
   else fast_body(d, ib, ob, wc, r, slow, blockIdx.x - nsort);
 }
 
+#ifndef KB_PROC_MANY
+#define KB_PROC_MANY 1        // batches of >= 8 prologue insertions fold one per lane (0: the whole wave on each)
+#endif
 #ifndef KB_PROC_WPE
 #define KB_PROC_WPE 1         // minimum waves per SIMD k_proc is compiled for (A/B knob; 1 = the compiler's choice)
 #endif
@@ -1084,7 +1090,7 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
             const uint64_t tb = tdbg ? wall_clock64() : 0;
             t_base += tb - ta;
             const uint8_t* hb = reinterpret_cast<const uint8_t*>(bw);
-            if (__popcll(insm) >= 8) {              // many: one insertion per lane
+            if (KB_PROC_MANY && __popcll(insm) >= 8) {   // many: one insertion per lane
               if (ins) {
                 const uint32_t x = lm.sender, k = seg_of(d, x), hend = (k + 1) * (d.SEGW / 8);
                 uint32_t praw = 0, pcnt = 0;
