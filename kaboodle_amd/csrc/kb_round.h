@@ -774,18 +774,22 @@ __device__ __attribute__((always_inline)) inline uint32_t bm_block(const uint32_
 // rem-th member of the 256-id block whose eight words are q0, q1
 __device__ __attribute__((always_inline)) inline uint32_t block_pick(const uint4& q0, const uint4& q1, uint32_t blk,
                                                                      uint32_t rem) {
-  const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-  uint32_t wi = 7, x = w[7];
-  bool found = false;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t c = __popc(w[k]);
-    if (!found) {
-      if (rem < c) { found = true; wi = k; x = w[k]; }
-      else rem -= c;
-    }
-  }
-  return (blk * 8 + wi) * 32 + select_in_word(x, rem);
+  // (rem < the block's count, as every caller guarantees) the word by a three-level search over pair and
+  // quad counts: a few selects instead of a chain of eight compares
+  const uint32_t p0 = __popc(q0.x), p1 = __popc(q0.y), p2 = __popc(q0.z), p3 = __popc(q0.w);
+  const uint32_t p4 = __popc(q1.x), p5 = __popc(q1.y), p6 = __popc(q1.z);
+  const uint32_t s01 = p0 + p1, s45 = p4 + p5, s03 = s01 + p2 + p3;
+  const bool h1 = rem >= s03;
+  rem -= h1 ? s03 : 0u;
+  const uint32_t sa = h1 ? s45 : s01;
+  const bool h2 = rem >= sa;
+  rem -= h2 ? sa : 0u;
+  const uint32_t pa = h1 ? (h2 ? p6 : p4) : (h2 ? p2 : p0);
+  const bool h3 = rem >= pa;
+  rem -= h3 ? pa : 0u;
+  const uint32_t wi = (h1 ? 4u : 0u) + (h2 ? 2u : 0u) + (h3 ? 1u : 0u);
+  const uint32_t xa = h1 ? (h2 ? (h3 ? q1.w : q1.z) : (h3 ? q1.y : q1.x)) : (h2 ? (h3 ? q0.w : q0.z) : (h3 ? q0.y : q0.x));
+  return (blk * 8 + wi) * 32 + select_in_word(xa, rem);
 }
 // b-th member (0-based) of bitset S with 256-id block prefix SP[0..nblk] (SP[nblk] = total > b); the
 // word and bit come from one 32-byte read of the block.
@@ -814,15 +818,29 @@ __device__ __attribute__((always_inline)) inline void sampled_fill(uint32_t* pay
   uint32_t y[RESP_KMAX];
 #pragma unroll
   for (int q = 0; q < RESP_KMAX; ++q) y[q] = 0;
-  uint32_t m = 0, x = k_first;
-  while (__ballot(m < mcount)) {
-    if (m < mcount) {
-      x = prp_pass(x, P);
-      if (x < P.n) {
+  if (4ull * P.n >= 3ull * ((uint64_t)(P.ma + 1) << P.c)) {
+    // n fills at least 3/4 of the Feistel domain (a large mesh: n just under a power of two), so a pass
+    // rarely lands outside [0, n): each key walks on its own, unrolled, with no run-time indexing of y
+    // (whose selects had cost more than the pass itself)
 #pragma unroll
-        for (int q = 0; q < RESP_KMAX; ++q) if ((uint32_t)q == m) y[q] = x;
-        ++m;
-        x = k_first + stride * m;
+    for (int q = 0; q < RESP_KMAX; ++q) {
+      const bool act = (uint32_t)q < mcount;
+      if (!__ballot(act)) break;
+      uint32_t x = prp_pass(k_first + stride * q, P);
+      while (__ballot(act && x >= P.n)) { if (act && x >= P.n) x = prp_pass(x, P); }
+      y[q] = x;
+    }
+  } else {
+    uint32_t m = 0, x = k_first;
+    while (__ballot(m < mcount)) {
+      if (m < mcount) {
+        x = prp_pass(x, P);
+        if (x < P.n) {
+#pragma unroll
+          for (int q = 0; q < RESP_KMAX; ++q) if ((uint32_t)q == m) y[q] = x;
+          ++m;
+          x = k_first + stride * m;
+        }
       }
     }
   }

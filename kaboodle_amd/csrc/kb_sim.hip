@@ -1222,7 +1222,8 @@ static int step_round(kb_sim* s) {
       if (rc) return rc;
     }
     if (resp_nodes) {
-      const uint32_t grid = std::min<uint32_t>(resp_nodes, 4096);
+      const uint32_t grid = std::min<uint32_t>(resp_nodes, 4096);   // (the workgroup path: 2 per CU when it serves only
+                                                                   // the few responders the wave path lists)
       const size_t words = resp_words(d.NWR, s->W / 256);
       uint32_t* scratch = nullptr;
       size_t lds = 4 * words;
@@ -1256,7 +1257,7 @@ static int step_round(kb_sim* s) {
       }
       // the workgroup path serves what the wave path left: its list (in the wave lists' slow buffer, free
       // until the tick) when the wave path ran, else every responder
-      klaunch(s, KI_RESP_NODE, k_resp_node, dim3(grid), dim3(256), (uint32_t)lds, d, pb,
+      klaunch(s, KI_RESP_NODE, k_resp_node, dim3(wave_on ? std::min<uint32_t>(grid, 2 * s->ncu) : grid), dim3(256), (uint32_t)lds, d, pb,
               (const uint32_t*)(wave_on ? s->slow : s->resp_nodes), (const uint32_t*)(wave_on ? d.ctr + C_RESTN : s->scan_tot + 4),
               o0, r, scratch, wave_on);
       if (s->debug_waves && (d.dev & 512)) {
