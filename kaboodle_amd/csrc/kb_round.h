@@ -259,13 +259,16 @@ __global__ void k_bfail_prep(const BCast* bf, uint32_t nf, uint32_t* gid, uint8_
   gid[q] = g; dep[q] = dp;
 }
 
-// Same facts for lists up to 2048 entries: one workgroup, LDS hash of peer -> first index naming it.
+// Same facts for lists up to BFAIL_LDS_MAX entries: one workgroup, LDS hash of peer -> first index naming it
+// (128 KB of LDS; wide meshes' Failed lists run to thousands: ≈ 7 000 at 372K peers, where the quadratic
+// per-entry scan above took 0.8 ms a round).
+constexpr uint32_t BFAIL_LDS_MAX = 8192;
 __global__ __launch_bounds__(1024) void k_bfail_prep_lds(const BCast* bf, uint32_t nf, uint32_t* gid, uint8_t* dep) {
-  constexpr uint32_t HS = 4096, EMPTY = 0xFFFFFFFFu;
+  constexpr uint32_t HS = 2 * BFAIL_LDS_MAX, EMPTY = 0xFFFFFFFFu;
   __shared__ uint32_t hk[HS], hv[HS];
   for (uint32_t t = threadIdx.x; t < HS; t += blockDim.x) { hk[t] = EMPTY; hv[t] = EMPTY; }
   __syncthreads();
-  auto slot0 = [](uint32_t x) { return (x * 0x9E3779B1u) >> 20; };   // 12 bits
+  auto slot0 = [](uint32_t x) { return (x * 0x9E3779B1u) >> 18; };   // 14 bits
   for (uint32_t e = threadIdx.x; e < nf; e += blockDim.x) {
     const uint32_t key = bf[e].peer;
     uint32_t h = slot0(key);

@@ -1126,7 +1126,7 @@ static int step_round(kb_sim* s) {
   if (lat_fail) klaunch(s, KI_LAT_MARK, k_lat_mark, dim3((s->nf + 255) / 256), dim3(256), 0, (const BCast*)s->bfail, s->nf, s->fnamed);
   const bool have_b = s->nf + s->nj > 0;
   const bool pb_hbm = (d.dbg & KB_DBG_PHASEB_HBM) != 0;
-  if (s->nf > 2048 || (pb_hbm && s->nf)) klaunch(s, KI_BFAIL_PREP, k_bfail_prep, dim3((s->nf + 255) / 256), dim3(256), 0, (const BCast*)s->bfail, s->nf, s->bf_gid, s->bf_dep, d.ctr + C_PATHS);
+  if (s->nf > BFAIL_LDS_MAX || (pb_hbm && s->nf)) klaunch(s, KI_BFAIL_PREP, k_bfail_prep, dim3((s->nf + 255) / 256), dim3(256), 0, (const BCast*)s->bfail, s->nf, s->bf_gid, s->bf_dep, d.ctr + C_PATHS);
   else if (s->nf) klaunch(s, KI_BFAIL_PREP, k_bfail_prep_lds, dim3(1), dim3(1024), 0, (const BCast*)s->bfail, s->nf, s->bf_gid, s->bf_dep);
   if (s->debug_waves && s->nf) {                     // KB_DEBUG_WAVES: broadcast list shape
     std::vector<uint8_t> dep(s->nf);
@@ -1146,7 +1146,10 @@ static int step_round(kb_sim* s) {
     if (listw > budget / 2 || pb_hbm) { ll = false; listw = 0; }
     // the LDS variant stages each row's whole bitset for the Failed group's membership tests; without a
     // Failed list (quiet rounds: A3 and a few Joins only) the row is read where A3 and the Joins touch it
-    // (372K peers, no broadcasts: 3.41 -> 0.54 ms, profiles/r04e_rowpass_variants.json)
+    // (372K peers, no broadcasts: 3.41 -> 0.54 ms, profiles/r04e_rowpass_variants.json).  (Rows too wide for
+    // more than 1-3 staged bitsets per workgroup still stage: the in-place variant with 8 waves per workgroup
+    // and the lists in LDS measured 17.4 -> 21.5 ms at 262K peers and 44.7 -> 41.8 ms at 372K in rounds with
+    // Failed lists, its random membership reads missing L2, profiles/r04s_nsweep.json)
     const bool ldsb = s->W <= PB_LDS_W && budget - listw >= d.NWR && !pb_hbm && s->nf > 0;
     const uint32_t wpb = ldsb ? std::min<uint32_t>(RP_WAVES, (budget - listw) / d.NWR) : RP_WAVES;
     const size_t lds = 4ull * ((ldsb ? (size_t)wpb * d.NWR : 0) + listw);
