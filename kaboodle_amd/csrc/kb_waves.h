@@ -834,12 +834,19 @@ __device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, co
         for (int j = CSLOTS - 1; j >= 0; --j) if (cf[j] && cp[j] == p) e = j;
         return e;
       };
+      // one copy of the handlers, always on entry 0, the register arrays shifted down after each message
+      // (unrolled over FAST_MAX, the handlers had made k_sortfast ≈ 50 KB of code, beyond the instruction
+      // cache that its waves share with the sorting workgroups)
+#pragma unroll 1
+      for (uint32_t k = 0; k < icnt; ++k) {
+        const uint32_t s = ms[0], kind = mk[0], ma_k = ma[0], mf_k = mf[0], mn_k = mn[0];
+        const uint8_t sb_k = sb[0];
 #pragma unroll
-      for (uint32_t k = 0; k < FAST_MAX; ++k) {
-        if (k >= icnt) break;
-        const uint32_t s = ms[k], kind = mk[k], ma_k = ma[k];
+        for (uint32_t q = 0; q + 1 < FAST_MAX; ++q) {
+          ms[q] = ms[q + 1]; mk[q] = mk[q + 1]; ma[q] = ma[q + 1]; mf[q] = mf[q + 1]; mn[q] = mn[q + 1]; sb[q] = sb[q + 1];
+        }
         if (s != last_sender) {                        // prologue: insert(sender, Known(now))
-          const uint8_t b = sb[k];
+          const uint8_t b = sb_k;
           if (b == ST_SUSPECT)
             for (int j = 0; j < SLOTS; ++j) if (sl[j].kind && sl[j].peer == s) { lat_sample(d, i, s, sl[j].since, r); sl[j].kind = 0; }
           if (b != now) { rw[s] = now; d.flog[(size_t)i * LOGCAP + (fn & (LOGCAP - 1))] = log_entry(s, r); fn++; }
@@ -869,13 +876,13 @@ __device__ __attribute__((always_inline)) inline void fast_body(const Dev& d, co
 #pragma unroll
             for (int q = 0; q < NOBS; ++q) ob4[q] = cu[e].obs[q];
 #pragma unroll
-            for (uint32_t q = 0; q < (uint32_t)NOBS; ++q) if (q < nobs) emit(ob4[q], K_ACK, ma_k, mf[k], mn[k]);
+            for (uint32_t q = 0; q < (uint32_t)NOBS; ++q) if (q < nobs) emit(ob4[q], K_ACK, ma_k, mf_k, mn_k);
             cu[e].used = 0;
           }
-          if (fp != mf[k] && !(n > mn[k])) emit(ma_k, K_KPR, 0, fp, n);
+          if (fp != mf_k && !(n > mn_k)) emit(ma_k, K_KPR, 0, fp, n);
         } else if (kind == K_KPR) {                  // :473-512, reply lost as oversize (Q3), then :507
           over++;
-          if (fp != mf[k] && !(n > mn[k])) emit(s, K_KPR, 0, fp, n);
+          if (fp != mf_k && !(n > mn_k)) emit(s, K_KPR, 0, fp, n);
         }
       }
       ob.cnt[i] = oseq;
@@ -918,6 +925,9 @@ __global__ __launch_bounds__(SORTFAST_T) void k_sortfast(Dev d, OutBuf ib, OutBu
   else fast_body(d, ib, ob, wc, r, slow, blockIdx.x - nsort);
 }
 
+#ifndef KB_KPR_BATCH
+#define KB_KPR_BATCH 4        // KPR reply scan: 64-entry log batches in flight per step
+#endif
 #ifndef KB_PROC_MANY
 #define KB_PROC_MANY 1        // batches of >= 8 prologue insertions fold one per lane (0: the whole wave on each)
 #endif
@@ -1052,8 +1062,9 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
       }
       return fp;
     };
-    auto maybe_sync = [&](uint32_t peer, uint32_t their_fp, uint32_t their_n) __attribute__((always_inline)) {   // :707-740
-      const uint32_t f = fp_now();
+    // (f: the fingerprint, taken once per message before its handler: fp_now's refold path is large, and
+    // one inlined copy per call site had made k_proc ≈ 85 KB of code, more than the instruction cache)
+    auto maybe_sync = [&](uint32_t f, uint32_t peer, uint32_t their_fp, uint32_t their_n) __attribute__((always_inline)) {   // :707-740
       if (f == their_fp || n > their_n) return;
       emit(peer, K_KPR, 0, f, n, 0);
     };
@@ -1179,10 +1190,12 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
         last_sender = s;
         __builtin_amdgcn_wave_barrier();
       }
+      // every handler but PingRequest's needs the fingerprint after the prologue, and none changes the
+      // membership before it reads it: one call site
+      const uint32_t f_cur = m.kind != K_PINGREQ ? fp_now() : 0u;
       switch (m.kind) {
         case K_PING: {                                               // :513-532
-          const uint32_t f = fp_now();
-          emit(s, K_ACK, i, f, n, 0);
+          emit(s, K_ACK, i, f_cur, n, 0);
           break;
         }
         case K_PINGREQ: {                                            // :533-545
@@ -1220,7 +1233,7 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
             wait_lds();
             __builtin_amdgcn_wave_barrier();
           }
-          maybe_sync(m.a, m.fp, m.n);
+          maybe_sync(f_cur, m.a, m.fp, m.n);
           break;
         }
         case K_KPR: {                                                // :473-512
@@ -1233,8 +1246,8 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
           const uint32_t poff = ob.poff[i] + pay_used;
           uint32_t total = 0;
           uint64_t size = 8 + (d.seglen[i] - ADDR_LEN) + 4 + 8;
-          bool over = d.uniform && kbig == r;
-          if (over) { w_over++; maybe_sync(s, m.fp, m.n); break; }
+          bool over = (d.uniform && kbig == r) || (d.dev & 4096);   // dev 4096: every reply oversize (timing experiments)
+          if (over) { w_over++; maybe_sync(f_cur, s, m.fp, m.n); break; }
           auto take = [&](bool ok, uint32_t j) __attribute__((always_inline)) {
             const unsigned long long okm = __ballot(ok);
             const uint32_t pos = total + __popcll(okm & ((1ull << l) - 1ull));
@@ -1253,7 +1266,7 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
           dbg_kpr++;
           // KPR_BATCH x 64 entries per step: all their log, member-bit and stamp loads in flight at once,
           // then taken in log order (the early exit stays between steps)
-          constexpr int KPR_BATCH = 4;
+          constexpr int KPR_BATCH = KB_KPR_BATCH;
           for (uint32_t k0 = complete ? ws : fn - LOGCAP; k0 < fn && !over; k0 += 64 * KPR_BATCH) {
             uint32_t ev[KPR_BATCH], wv4[KPR_BATCH], bv[KPR_BATCH];
 #pragma unroll
@@ -1299,7 +1312,7 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
           over = d.uniform ? total > d.capk : size > (uint64_t)BUFSZ;
           if (over) w_over++;
           else { emit(s, K_KP, total, 0, 0, poff); pay_used += total; w_bytes += 4ull * total; }
-          maybe_sync(s, m.fp, m.n);
+          maybe_sync(f_cur, s, m.fp, m.n);
           break;
         }
         default: break;
