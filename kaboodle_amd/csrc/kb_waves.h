@@ -380,6 +380,9 @@ constexpr int KP_UNROLL = 10;            // 640 ids per wave step: a whole Join 
 #define KB_KP_COLS 2
 #endif
 constexpr uint32_t KP_COLS = KB_KP_COLS; // BIG groups in LDS: workgroups per destination, one per column part (A/B: 2 beats 4 and 1)
+// a part must hold whole checkpoint segments: its workgroup refolds the segments it changed from its own
+// LDS slice (3 parts of 64 segments straddle: an A/B build with 3 faulted)
+static_assert(NSEG % KB_KP_COLS == 0, "KP_COLS must divide the 64 checkpoint segments");
 __host__ __device__ constexpr size_t kp_lds_bytes(uint32_t nwr) {
   return 4ull * (nwr <= KP_LDS_WORDS ? nwr : 4);
 }
