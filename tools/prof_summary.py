@@ -116,7 +116,8 @@ def pmc(d, fields):
     out = dict(meta)
     import hashlib
     lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "kaboodle_amd", "libkaboodle_sim.so")
-    out["lib_sha16"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]   # the build the counters measured
+    out["lib_sha16"] = (hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]   # the build the counters measured
+                        if os.path.exists(lib) else None)
     out["kernels"] = dict(sorted(kern.items(), key=lambda kv: -kv[1]["hbm_bytes_per_round"]))
     out["correction"] = ("FETCH_SIZE(KB)*1024, x2 only for " + ", ".join(sorted(STREAM16)) +
                          " (gfx950 half-count of 16 B/lane streaming reads; other kernels raw) + WRITE_SIZE(KB)*1024")
