@@ -588,7 +588,11 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   const uint32_t R = s->R;
   const uint32_t groups = (R + 63) / 64;
   uint32_t S = 1;
-  while (S < 64 && groups * S < 8192) S <<= 1;        // enough sweep waves to fill the chip
+#ifndef KB_FOLD_WAVES
+#define KB_FOLD_WAVES 16384                            // fold waves wanted: column splits double up to it (64K:
+                                                       // 16 splits, 0.44 -> 0.42 ms against 8 and 32, profiles/r04fs_ab_fold_splits.txt)
+#endif
+  while (S < 64 && groups * S < KB_FOLD_WAVES) S <<= 1;   // enough sweep waves to fill the chip
   s->S = S;
   Dev& d = s->d;
   d.lo = s->lo; d.hi = s->hi;

@@ -230,7 +230,10 @@ __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
 // log2(FP_LANES) combine levels across them in address order.  Spreading the 64-multiply chain over
 // several lanes gives the SIMDs that many times the waves to hide its latency with.  Runs after
 // k_fold; k_tick_post then finds the row clean.
-constexpr uint32_t FP_LANES = 8;
+#ifndef KB_FP_LANES
+#define KB_FP_LANES 8
+#endif
+constexpr uint32_t FP_LANES = KB_FP_LANES;   // (A/B knob)
 __global__ __launch_bounds__(256) void k_fp_rows(Dev d) {
   constexpr uint32_t PER = NSEG / FP_LANES;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
