@@ -125,7 +125,11 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
 // kernel writes a row while the inboxes are built (a row read while a prologue moves a stamp to
 // Known(now) and logs it could count that peer twice), and the proof is in place before the fast
 // handlers of k_sortfast decide.  The KnownPeers prologues of k_kp in between only add fresh entries.
-constexpr uint32_t PROBE_GROUPS = 512;     // workgroups of the scatter launch that run the probe
+#ifndef KB_PROBE_GROUPS
+#define KB_PROBE_GROUPS 1024
+#endif
+constexpr uint32_t PROBE_GROUPS = KB_PROBE_GROUPS;   // workgroups of the scatter launch that run the probe (1024: 3.00
+                                                     // -> 2.93 ms against 512; 2048 and 4096 the same, profiles/r04kn*)
 __device__ __attribute__((always_inline)) inline void kpr_probe(const Dev& d, const WaveCtl& wc, int32_t r, uint32_t bid,
                                                                uint32_t nblk) {
   const uint32_t nact = d.ctr[C_ACTIVE];
@@ -700,7 +704,10 @@ __global__ __launch_bounds__(1024) void k_kp(Dev d, OutBuf ib, WaveCtl wc, int32
 // index, one workgroup per node, bitonic in LDS (up to SORT_MAX entries; longer ones keep the
 // selection path of k_proc)
 constexpr uint32_t SORT_MAX = 8192;
-constexpr uint32_t SORT_GROUPS = 256;      // k_sortfast workgroups that sort inboxes and run the KPR probe
+#ifndef KB_SORT_GROUPS
+#define KB_SORT_GROUPS 256
+#endif
+constexpr uint32_t SORT_GROUPS = KB_SORT_GROUPS;   // k_sortfast workgroups that sort long inboxes (A/B knob)
 __device__ inline uint32_t sort_max(const Dev& d) { return (d.dbg & KB_DBG_PROC_UNSORTED) ? 64u : SORT_MAX; }
 __device__ __attribute__((always_inline)) inline void sort_body(const Dev& d, const WaveCtl& wc, int32_t r, uint32_t bid,
                                                                uint32_t nblk) {
