@@ -593,7 +593,10 @@ __device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d
 // in place on the row's bitset, the same arms-then-prologues order as the BIG groups.  (The body of
 // k_kp's last nblk workgroups: at least one per CU, since a round of the converged start's first
 // SHARE_AGE rounds delivers ~24K replies of a few hundred ids at 64K peers in one wave.)
-constexpr int KPS_UNROLL = 4;
+#ifndef KB_KPS_UNROLL
+#define KB_KPS_UNROLL 4
+#endif
+constexpr int KPS_UNROLL = KB_KPS_UNROLL;   // (A/B knob)
 __device__ __attribute__((always_inline)) inline void kp_small_body(const Dev& d, const OutBuf& ib, const WaveCtl& wc, int32_t r,
                                                                    const OutBuf& nb, uint32_t bid, uint32_t nblk) {
   __shared__ uint32_t s_list[1024], s_nl;
