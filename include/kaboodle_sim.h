@@ -83,8 +83,13 @@ typedef struct kb_config {
   uint32_t variant;          /* KB_VARIANT_*: 0 = round semantics v1.  Nonzero selects an alternative
                                 reading of a declared deviation, implemented by the
                                 CPU oracle only, to measure what the declaration changes; the HIP
-                                library refuses it (KB_INVALID_ARGUMENT)                            */
-  uint32_t reserved[3];
+                                library refuses it (KB_INVALID_ARGUMENT) — except
+                                KB_VARIANT_SPARSE_ROWS alone, the same semantics on the configs[4]
+                                layout, which the HIP library runs (unsharded)          */
+  uint32_t sparse_row_cap;   /* KB_VARIANT_SPARSE_ROWS on the GPU: entries per row (exceptions and
+                                explicit stamps); 0 = min(capacity, 4096).  Exceeding it is
+                                KB_CAPACITY, never a truncation (ignored by the oracle)              */
+  uint32_t reserved[2];
 } kb_config;
 enum { KB_VARIANT_SAME_WINDOW_BCAST = 1u,   /* Join/Failed delivered in the round they are sent, right after
                                                the tick (src/kaboodle.rs:770-778), not at the next round start */
@@ -268,6 +273,11 @@ int  kb_sim_debug_paths(kb_sim* sim, uint32_t* mask);
 int  kb_sim_debug_counters(kb_sim* sim, uint64_t* out, size_t cap);
 /* Canonical curious table: for each entry sorted by peer: peer, nobs, obs[0..3] (6 x int32).       */
 int  kb_sim_dump_curious(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, size_t* n);
+/* KB_VARIANT_SPARSE_ROWS handles: the layout's footprint, out[0..5] = rows that adopted the base,
+   exceptions, explicit stamps, entries of the largest row, bytes of the entries, rows (the oracle's
+   kbo_sparse_footprint; here 4 bytes per entry, exception and stamp packed together).  Other handles:
+   KB_INVALID_OPERATION.  Test surface.                                                             */
+int  kb_sim_sparse_footprint(kb_sim* sim, uint64_t* out, size_t cap);
 
 /* ---- pure helpers ------------------------------------------------------------------------------- */
 /* Canonical simulated address of an id: "10.100.100.<100 + id/50000>:<10000 + id%50000>".          */

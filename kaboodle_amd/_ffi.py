@@ -19,6 +19,7 @@ KB_DBG_ALL = 31                  # every wide-row variant
 KB_DBG_WAVE_GRAPH = 32           # the receive window as a replayed HIP graph
 KB_DBG_RESP_WAVE_HBM = 64        # Join responses by wave, rows read in place (rows > 110K ids)
 KB_VARIANT_SAME_WINDOW_BCAST, KB_VARIANT_EXACT_LRU = 1, 2   # oracle-only
+KB_VARIANT_SPARSE_ROWS = 4       # the configs[4] layout: oracle and the HIP library (unsharded)
 KB_LATENCY_NONE = 0xFFFFFFFF
 KT_ROWPASS, KT_ROUND, KT_FOLD, KT_RESP, KT_PROC = 0, 1, 2, 3, 4   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
 KB_WAVE_SLOTS = 9
@@ -33,7 +34,7 @@ class KbConfig(C.Structure):
         ("failed_mode", C.c_uint32), ("id_len", C.c_uint32), ("partition_groups", C.c_uint32),
         ("partition_start", C.c_int32), ("partition_end", C.c_int32), ("device", C.c_int32),
         ("debug_flags", C.c_uint32), ("track_latency", C.c_uint32), ("variant", C.c_uint32),
-        ("reserved", C.c_uint32 * 3),
+        ("sparse_row_cap", C.c_uint32), ("reserved", C.c_uint32 * 2),
     ]
 
 
@@ -114,7 +115,9 @@ class SimConfig:
     device: int = -1
     debug_flags: int = 0         # KB_DBG_*: force the wide-row kernel variants (test surface)
     track_latency: int = 0       # 1: keep the ping-latency EWMA reported by peer_states
-    variant: int = 0             # KB_VARIANT_*: oracle-only alternative semantics (deviation measurements)
+    variant: int = 0             # KB_VARIANT_*: oracle-only alternative semantics (deviation measurements), or
+                                 # KB_VARIANT_SPARSE_ROWS (the configs[4] layout, also on the GPU)
+    sparse_row_cap: int = 0      # KB_VARIANT_SPARSE_ROWS on the GPU: entries per row (0: min(capacity, 4096))
 
     def to_c(self) -> KbConfig:
         c = KbConfig()
@@ -129,6 +132,7 @@ class SimConfig:
             self.partition_groups, self.partition_start, self.partition_end)
         c.device = self.device
         c.debug_flags, c.track_latency, c.variant = self.debug_flags, self.track_latency, self.variant
+        c.sparse_row_cap = self.sparse_row_cap
         return c
 
 
@@ -181,6 +185,7 @@ _OPTIONAL = {
     "sim_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "sim_kernel_breakdown": (C.c_int, [C.c_void_p, C.POINTER(KbKernelTime), C.c_size_t, C.POINTER(C.c_size_t)]),
     "sim_host_syncs": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "sim_sparse_footprint": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_size_t]),
 }
 
 
@@ -448,6 +453,14 @@ class Sim:
         self.lib.call("sim_kernel_breakdown", self.h, arr, n.value, C.byref(n))
         return {a.name.decode(): {"ms": a.ms, "launches": a.launches, "bytes": a.bytes if a.has_bytes else None,
                                   "wave_ms": list(a.wave_ms)} for a in arr[: n.value]}
+
+    def sparse_footprint(self) -> dict:
+        """KB_VARIANT_SPARSE_ROWS: rows that adopted the base, exceptions, explicit stamps, entries of the largest
+        row, bytes of the entries, rows (kb_sim_sparse_footprint)."""
+        out = (C.c_uint64 * 6)()
+        self.lib.call("sim_sparse_footprint", self.h, out, 6)
+        keys = ("rows_based", "exceptions", "stamps", "max_row_entries", "bytes", "rows")
+        return dict(zip(keys, (int(v) for v in out)))
 
     def host_syncs(self) -> int:
         """Host waits on the device since creation (stream synchronisations, pinned hand-offs)."""

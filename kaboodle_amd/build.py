@@ -19,7 +19,7 @@ def needs_build() -> bool:
     if not os.path.exists(OUT):
         return True
     t = os.path.getmtime(OUT)
-    deps = [SRC] + [os.path.join(HERE, "csrc", f) for f in ("kb_device.h", "kb_common.h", "kb_round.h", "kb_tick.h", "kb_waves.h", "kb_xfer.h", "kb_wire.h")] + [
+    deps = [SRC] + [os.path.join(HERE, "csrc", f) for f in ("kb_device.h", "kb_common.h", "kb_round.h", "kb_tick.h", "kb_waves.h", "kb_xfer.h", "kb_wire.h", "kb_sparse.h", "kb_sparse_host.h")] + [
             os.path.join(os.path.dirname(HERE), "include", "kaboodle_sim.h")]
     return any(os.path.getmtime(p) > t for p in deps)
 

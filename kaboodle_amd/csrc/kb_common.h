@@ -73,6 +73,7 @@ struct Dev {
   unsigned long long* sdirty;
   uint8_t* dirty;
   uint8_t* alive;
+  uint8_t* idset;                 // [C] an identity was set on this never-bound address: not a fresh id
   uint32_t* abits;                // running set bitset [W/32]
   int32_t* start_round;
   uint32_t* n;

@@ -104,16 +104,20 @@ __global__ void k_churn_leave(Dev d, int32_t r) {
   const unsigned long long t = block_sum(left);
   if (threadIdx.x == 0 && t) atomicAdd(&d.ctr[C_LEAVES], (uint32_t)t);
 }
+// churn joins take fresh ids in order: an id some instance bound (started through the API, a restart's new
+// address) or given an identity is skipped.  The round's few dozen joins run in one thread.
 __global__ void k_churn_join(Dev d, int32_t r) {
+  if (threadIdx.x || blockIdx.x) return;
   const uint32_t leaves = d.ctr[C_LEAVES];
-  const uint32_t nf = d.ctr[C_NEXTFREE];
-  const uint32_t joins = leaves < d.C - nf ? leaves : d.C - nf;
-  for (uint32_t k = threadIdx.x; k < joins; k += blockDim.x) node_start(d, nf + k, r);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    d.ctr[C_NEXTFREE] = nf + joins; d.ctr[C_LEAVES] = 0;
-    if (d.lo == 0) { d.stats[S_CLEAVE] += leaves; d.stats[S_CJOIN] += joins; }   // replicated: counted once
+  uint32_t nf = d.ctr[C_NEXTFREE], joins = 0;
+  for (uint32_t k = 0; k < leaves; ++k) {
+    while (nf < d.C && (d.start_round[nf] != NONE_ROUND || d.idset[nf])) nf++;
+    if (nf >= d.C) break;
+    node_start(d, nf++, r);
+    joins++;
   }
+  d.ctr[C_NEXTFREE] = nf; d.ctr[C_LEAVES] = 0;
+  if (d.lo == 0) { d.stats[S_CLEAVE] += leaves; d.stats[S_CJOIN] += joins; }   // replicated: counted once
 }
 
 // ---- running set bitset + count, and its fingerprint (what a converged node reports) -----------

@@ -36,6 +36,7 @@
 #include "kb_tick.h"
 #include "kb_waves.h"
 #include "kb_xfer.h"
+#include "kb_sparse.h"
 
 using namespace kb;
 
@@ -234,9 +235,12 @@ static thread_local std::string g_err;
 static void seterr(const std::string& s) { g_err = s; }
 #define HIPCHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { seterr(std::string(#x) + ": " + hipGetErrorString(e_)); return KB_IO_ERROR; } } while (0)
 
+// zeroed device memory, the zeroing complete on return (hipMemset runs on the null stream, which does not order
+// with the simulator's non-blocking stream: a buffer regrown mid-round could be zeroed after a kernel wrote it)
 template <class T> static hipError_t dalloc(T** p, size_t n) {
   hipError_t e = hipMalloc((void**)p, sizeof(T) * (n ? n : 1));
   if (e == hipSuccess) e = hipMemset(*p, 0, sizeof(T) * (n ? n : 1));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
   return e;
 }
 
@@ -310,8 +314,10 @@ __global__ __launch_bounds__(256) void k_lat_column(Dev d, uint32_t node, uint16
   if (j < d.C) out[j] = *lat_at(d, node, j);
 }
 
+namespace kb { struct SpSim; }
 struct kb_sim {
   kb_config cfg;
+  SpSim* sp = nullptr;                 // KB_VARIANT_SPARSE_ROWS: the sparse-row engine answers every call
   Dev d;
   int device;
   hipStream_t st;
@@ -327,6 +333,7 @@ struct kb_sim {
   std::vector<uint8_t> h_pend; std::vector<int16_t> h_pendlen;   // identity set on a stopped instance that ran:
                                                                  // its next address takes it (-1: none)
   std::vector<uint8_t> h_moved;                                  // the instance bound here restarted elsewhere
+  std::vector<uint8_t> h_idset;                                  // identity set on a never-bound address (d.idset)
   std::vector<Event> events;
   uint32_t* rpack = nullptr; uint32_t* rpack_in = nullptr;       // a restart's packed row (send / receive)
   // discovery: Probes queued for the next round, those delivered this round, responses not yet drained
@@ -530,6 +537,8 @@ static int upload_segments(kb_sim* s) {
   return KB_OK;
 }
 
+#include "kb_sparse_host.h"
+
 static void free_all(kb_sim* s) {
   for (void* p : s->allocs) (void)hipFree(p);
   s->allocs.clear();
@@ -557,7 +566,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (!cfg || !out || cfg->abi_version != KB_ABI_VERSION) { seterr("bad config"); delete xf; return KB_INVALID_ARGUMENT; }
   if (cfg->capacity == 0 || cfg->capacity > 7800000u || cfg->initial_nodes > cfg->capacity || cfg->id_len > MAXID ||
       cfg->max_waves == 0 || cfg->max_waves > 64) { seterr("config out of range"); delete xf; return KB_INVALID_ARGUMENT; }
-  if (cfg->variant) { seterr("semantic variants are measurement-only (CPU oracle)"); delete xf; return KB_INVALID_ARGUMENT; }
+  if (cfg->variant) { seterr(cfg->variant == KB_VARIANT_SPARSE_ROWS ? "sparse rows run unsharded (kb_sim_create)" : "semantic variants other than KB_VARIANT_SPARSE_ROWS are measurement-only (CPU oracle)"); delete xf; return KB_INVALID_ARGUMENT; }
   const uint32_t C = cfg->capacity;
   const uint32_t rows_per = (C + (uint32_t)world - 1) / (uint32_t)world;
   if (world < 1 || world > (int)XMAX || rank < 0 || rank >= world || (uint64_t)(world - 1) * rows_per >= C) {
@@ -614,12 +623,13 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (cfg->debug_flags & KB_DBG_WAVE_GRAPH) s->graph_on = true;
   s->h_ident.assign((size_t)C * MAXID, 0); s->h_idlen.assign(C, (uint8_t)Lid);
   s->h_pend.assign((size_t)C * MAXID, 0); s->h_pendlen.assign(C, (int16_t)-1); s->h_moved.assign(C, 0);
+  s->h_idset.assign(C, 0);
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &s->h_ident[(size_t)j * MAXID]);
   hipError_t e = hipSuccess;
 #define A(ptr, n) if (e == hipSuccess) e = talloc(s, &(ptr), (n))     // per-id / global tables
 #define AR(ptr, n) if (e == hipSuccess) e = ralloc(s, &(ptr), (n))   // row tables: n entries per local row
   AR(d.stamp, W); AR(d.bits, d.NWR); AR(d.segp, NSEG); AR(d.sdirty, 1);
-  AR(d.dirty, 1); A(d.alive, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
+  AR(d.dirty, 1); A(d.alive, C); A(d.idset, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
   AR(d.last_bcast, 1); AR(d.a3cur, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
   AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
   A(d.ztab, 17 * 128); A(d.zbtab, ZB);
@@ -684,7 +694,20 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   return KB_OK;
 }
 
-extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) { return create_shard(cfg, 0, 1, nullptr, out); }
+extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
+  if (cfg && out && cfg->abi_version == KB_ABI_VERSION && (cfg->variant & KB_VARIANT_SPARSE_ROWS)) {
+    if (cfg->capacity == 0 || cfg->capacity > 7800000u || cfg->initial_nodes > cfg->capacity || cfg->id_len > MAXID ||
+        cfg->max_waves == 0 || cfg->max_waves > 64) { seterr("config out of range"); return KB_INVALID_ARGUMENT; }
+    SpSim* sp = nullptr;
+    const int rc = sp_create(cfg, &sp);
+    if (rc) return rc;
+    kb_sim* s = new kb_sim();
+    s->cfg = *cfg; s->C = cfg->capacity; s->sp = sp; s->device = sp->device; s->world = 1; s->R = s->C; s->hi = s->C;
+    *out = s;
+    return KB_OK;
+  }
+  return create_shard(cfg, 0, 1, nullptr, out);
+}
 
 extern "C" int kb_rccl_unique_id(uint8_t* out, size_t cap) {
   if (!out || cap < sizeof(ncclUniqueId)) { seterr("unique id buffer too small"); return KB_INVALID_ARGUMENT; }
@@ -726,6 +749,7 @@ extern "C" int kb_sim_create_local(const kb_config* cfg, int32_t shards, kb_sim*
 
 extern "C" int kb_sim_destroy(kb_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
+  if (s->sp) { sp_destroy(s->sp); delete s; return KB_OK; }
   if (!s->shards.empty()) {
     for (kb_sim* t : s->shards) destroy_shard(t);
     delete s->hub;
@@ -737,6 +761,7 @@ extern "C" int kb_sim_destroy(kb_sim* s) {
 }
 
 extern "C" int kb_sim_shard_info(kb_sim* s, int32_t* rank, int32_t* world, uint32_t* lo, uint32_t* hi) {
+  if (s && s->sp && rank && world && lo && hi) { *rank = 0; *world = 1; *lo = 0; *hi = s->C; return KB_OK; }
   if (!s || !rank || !world || !lo || !hi) return KB_INVALID_ARGUMENT;
   if (!s->shards.empty()) { *rank = 0; *world = s->world; *lo = 0; *hi = s->C; return KB_OK; }
   *rank = s->rank; *world = s->world; *lo = s->lo; *hi = s->hi;
@@ -1021,7 +1046,11 @@ static int launch_waves(kb_sim* s, int32_t rk) {
 // A restart's map: the old address's row packed on the shard holding it, moved (sharded: an all-to-all-v
 // in which only that shard sends, to the shard holding the new row) and unpacked; the event observer
 // moves with it (src/lib.rs:104: the map and its observer belong to the Kaboodle, not to its socket).
-static int move_row(kb_sim* s, uint32_t from, uint32_t to) {
+// *snap_after: an observer attached to the new address before this round (after start() returned) and the
+// instance had none: its snapshot is taken from the row once the restart has applied (the caller), so the
+// channel reports only later changes, not the whole inherited map
+static int move_row(kb_sim* s, uint32_t from, uint32_t to, bool* snap_after) {
+  *snap_after = false;
   const RowPack LP = row_pack_layout(s->W, s->d.NWR, s->d.lat != nullptr);
   if (!s->rpack) HIPCHK(hipMalloc(&s->rpack, 4ull * LP.words));
   if (s->xf && !s->rpack_in) HIPCHK(hipMalloc(&s->rpack_in, 4ull * LP.words));
@@ -1053,9 +1082,16 @@ static int move_row(kb_sim* s, uint32_t from, uint32_t to) {
   HIPCHK(hipMemcpyAsync(hdr, src, sizeof hdr, hipMemcpyDeviceToHost, s->st));
   HIPCHK(sync_st(s));
   uint32_t* snap = nullptr;
-  if (hdr[RP_WATCHED]) {
-    HIPCHK(talloc(s, &snap, (size_t)s->d.NWR));
-    s->watch_node.push_back(to); s->watch_fp.push_back(hdr[RP_WFP]); s->watch_snap.push_back(snap);
+  size_t kt = 0;
+  while (kt < s->watch_node.size() && s->watch_node[kt] != to) ++kt;
+  if (hdr[RP_WATCHED]) {                           // the instance's observer replaces one attached to the new address
+    if (kt < s->watch_node.size()) { snap = s->watch_snap[kt]; s->watch_fp[kt] = hdr[RP_WFP]; }
+    else {
+      HIPCHK(talloc(s, &snap, (size_t)s->d.NWR));
+      s->watch_node.push_back(to); s->watch_fp.push_back(hdr[RP_WFP]); s->watch_snap.push_back(snap);
+    }
+  } else if (kt < s->watch_node.size()) {
+    *snap_after = true;
   }
   k_row_unpack<<<g, 256, 0, s->st>>>(s->d, to, src, LP, snap);
   return KB_OK;
@@ -1092,8 +1128,20 @@ static int step_round(kb_sim* s) {
       const bool rs = k < s->events.size() && s->events[k].kind == EV_RESTART;
       if (k == s->events.size() || rs) {
         if (k > k0) klaunch(s, KI_EVENTS, k_events, dim3(1), dim3(1), 0, d, s->d_events + k0, (uint32_t)(k - k0), r);
-        if (rs) { const int rc = move_row(s, s->events[k].src, s->events[k].node); if (rc) return rc; }
         k0 = k;
+        if (rs) {
+          bool snap_after = false;
+          const uint32_t to = s->events[k].node;
+          const int rc = move_row(s, s->events[k].src, to, &snap_after);
+          if (rc) return rc;
+          if (snap_after) {                                // the restart itself, then the observer's starting point
+            klaunch(s, KI_EVENTS, k_events, dim3(1), dim3(1), 0, d, s->d_events + k, 1u, r);
+            size_t kt = 0;
+            while (s->watch_node[kt] != to) ++kt;
+            k_events_commit<<<(d.NWR + 255) / 256, 256, 0, st>>>(d.bits + (size_t)to * d.NWR, s->watch_snap[kt], d.NWR);
+            k0 = k + 1;
+          }
+        }
       }
     }
     HIPCHK(sync_st(s));
@@ -1102,7 +1150,7 @@ static int step_round(kb_sim* s) {
   const bool faults_on = s->cfg.fault_end_round < 0 || r < s->cfg.fault_end_round;
   if (faults_on && s->cfg.churn_threshold) {
     klaunch(s, KI_CHURN_LEAVE, k_churn_leave, dim3(gall), dim3(tb), 0, d, r);
-    klaunch(s, KI_CHURN_JOIN, k_churn_join, dim3(1), dim3(1024), 0, d, r);
+    klaunch(s, KI_CHURN_JOIN, k_churn_join, dim3(1), dim3(64), 0, d, r);
   }
   klaunch(s, KI_ALIVE_BITS, k_alive_bits, dim3((d.NWR + tb - 1) / tb), dim3(tb), 0, d);
   klaunch(s, KI_TRUEFP_PART, k_truefp_part, dim3(TRUEFP_G), dim3(256), 0, d, d.tfpart);
@@ -1393,6 +1441,7 @@ static int group_step(kb_sim* g, uint32_t rounds) {
 }
 
 extern "C" int kb_sim_step(kb_sim* s, uint32_t rounds) {
+  if (s && s->sp) return sp_step(s->sp, rounds);
   if (!s) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return group_step(s, rounds);
   (void)hipSetDevice(s->device);
@@ -1455,6 +1504,7 @@ static int ever_bound(kb_sim* s, uint32_t node, int* ever) {
   return KB_OK;
 }
 extern "C" int kb_sim_start_node(kb_sim* s, uint32_t node) {
+  if (s && s->sp) return chk(s, node) ? KB_INVALID_ARGUMENT : sp_start_node(s->sp, node);
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
   kb_sim* h = is_group(s) ? s->shards[0] : s;        // lifecycle facts are replicated on every shard
   int run = 0, ever = 0;
@@ -1465,6 +1515,7 @@ extern "C" int kb_sim_start_node(kb_sim* s, uint32_t node) {
   return KB_OK;
 }
 extern "C" int kb_sim_stop_node(kb_sim* s, uint32_t node) {
+  if (s && s->sp) return chk(s, node) ? KB_INVALID_ARGUMENT : sp_stop_node(s->sp, node);
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_stop_node(t, node); });
   s->events.push_back(Event{node, EV_STOP, node, 0});
@@ -1489,6 +1540,7 @@ static int restart_apply(kb_sim* s, uint32_t node, uint32_t to) {
   return KB_OK;
 }
 extern "C" int kb_sim_restart_node(kb_sim* s, uint32_t node, uint32_t* new_node) {
+  if (s && s->sp) return (chk(s, node) || !new_node) ? KB_INVALID_ARGUMENT : sp_restart_node(s->sp, node, new_node);
   if (chk(s, node) || !new_node) return KB_INVALID_ARGUMENT;
   kb_sim* h = is_group(s) ? s->shards[0] : s;
   if (h->h_moved[node]) { seterr("the instance bound here restarted at a fresh address"); return KB_INVALID_OPERATION; }
@@ -1503,12 +1555,19 @@ extern "C" int kb_sim_restart_node(kb_sim* s, uint32_t node, uint32_t* new_node)
   }
   uint32_t nf = 0;
   HIPCHK(hipMemcpy(&nf, h->d.ctr + C_NEXTFREE, 4, hipMemcpyDeviceToHost));
+  for (; nf < s->C; ++nf) {                          // the next fresh id: never bound, no identity set
+    int ev = 0;
+    const int rc = ever_bound(h, nf, &ev);
+    if (rc) return rc;
+    if (!ev && !h->h_idset[nf]) break;
+  }
   if (nf >= s->C) { seterr("no fresh address left for the restart (capacity)"); return KB_CAPACITY; }
   *new_node = nf;
   GROUP_ALL([&](kb_sim* t) { (void)hipSetDevice(t->device); return restart_apply(t, node, nf); });
   return restart_apply(s, node, nf);
 }
 extern "C" int kb_sim_is_running(kb_sim* s, uint32_t node, int* running) {
+  if (s && s->sp) return (chk(s, node) || !running) ? KB_INVALID_ARGUMENT : sp_is_running(s->sp, node, running);
   if (chk(s, node) || !running) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_is_running(s->shards[0], node, running);
   uint8_t a = 0;
@@ -1517,6 +1576,7 @@ extern "C" int kb_sim_is_running(kb_sim* s, uint32_t node, int* running) {
   return KB_OK;
 }
 extern "C" int kb_sim_ping_addrs(kb_sim* s, uint32_t node, const uint32_t* peers, size_t n) {
+  if (s && s->sp) return (chk(s, node) || (n && !peers)) ? KB_INVALID_ARGUMENT : sp_ping_addrs(s->sp, node, peers, n);
   if (chk(s, node) || (n && !peers)) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_ping_addrs(t, node, peers, n); });
   for (size_t k = 0; k < n; ++k) if (peers[k] >= s->C) return KB_INVALID_ARGUMENT;
@@ -1539,6 +1599,7 @@ extern "C" int kb_sim_ping_addrs(kb_sim* s, uint32_t node, const uint32_t* peers
   return KB_OK;
 }
 extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* identity, size_t len) {
+  if (s && s->sp) return (chk(s, node) || len > MAXID || (len && !identity)) ? KB_INVALID_ARGUMENT : sp_set_identity(s->sp, node, identity, len);
   if (chk(s, node) || len > MAXID || (len && !identity)) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_set_identity(t, node, identity, len); });
   if (s->h_moved[node]) { seterr("the instance bound here restarted at a fresh address"); return KB_INVALID_OPERATION; }
@@ -1553,6 +1614,8 @@ extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* iden
   }
   memcpy(&s->h_ident[(size_t)node * MAXID], identity, len);
   s->h_idlen[node] = (uint8_t)len;
+  s->h_idset[node] = 1;                            // no longer a fresh id for churn joins and restarts
+  { const uint8_t one = 1; HIPCHK(hipMemcpy(s->d.idset + node, &one, 1, hipMemcpyHostToDevice)); }
   int rc = upload_segments(s);
   if (rc) return rc;
   s->buf_gen++;                                    // a captured receive window holds the old Dev (uniform, L)
@@ -1561,6 +1624,7 @@ extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* iden
   return KB_OK;
 }
 extern "C" int kb_sim_identity(kb_sim* s, uint32_t node, uint8_t* buf, size_t cap, size_t* len) {
+  if (s && s->sp) return (chk(s, node) || !len) ? KB_INVALID_ARGUMENT : sp_identity(s->sp, node, buf, cap, len);
   if (chk(s, node) || !len) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_identity(s->shards[0], node, buf, cap, len);   // replicated per id
   *len = s->h_idlen[node];
@@ -1571,12 +1635,14 @@ extern "C" int kb_sim_identity(kb_sim* s, uint32_t node, uint8_t* buf, size_t ca
 }
 // ---- discovery (src/discovery.rs:30-89, src/kaboodle.rs:305-331) ----------------------------------
 extern "C" int kb_sim_probe(kb_sim* s, const kb_wire_addr* prober) {
+  if (s && s->sp) { if (!prober) return KB_INVALID_ARGUMENT; s->sp->probe_q.push_back(*prober); return KB_OK; }
   if (!s || !prober) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_probe(t, prober); });
   s->probe_q.push_back(*prober);
   return KB_OK;
 }
 extern "C" int kb_sim_probe_responses(kb_sim* s, kb_probe_response* out, size_t cap, size_t* n) {
+  if (s && s->sp) return n ? sp_probe_responses(s->sp, out, cap, n) : KB_INVALID_ARGUMENT;
   if (!s || !n) return KB_INVALID_ARGUMENT;
   if (is_group(s)) {                                 // every shard's responders, merged in canonical order
     std::vector<kb_probe_response> all;
@@ -1600,6 +1666,7 @@ extern "C" int kb_sim_probe_responses(kb_sim* s, kb_probe_response* out, size_t 
 }
 // the last round's Join / Failed broadcasts (whole mesh; sender order, a node's Join before its Failed)
 extern "C" int kb_sim_broadcasts(kb_sim* s, kb_broadcast* out, size_t cap, size_t* n) {
+  if (s && s->sp) return n ? sp_broadcasts(s->sp, out, cap, n) : KB_INVALID_ARGUMENT;
   if (!s || !n) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_broadcasts(s->shards[0], out, cap, n);   // every shard holds the lists
   std::vector<BCast> j(s->nj), f(s->nf);
@@ -1621,6 +1688,7 @@ extern "C" int kb_sim_broadcasts(kb_sim* s, kb_broadcast* out, size_t cap, size_
   return (out && cap < c) ? KB_CAPACITY : KB_OK;
 }
 extern "C" int kb_sim_fingerprint(kb_sim* s, uint32_t node, uint32_t* fp) {
+  if (s && s->sp) return (chk(s, node) || !fp) ? KB_INVALID_ARGUMENT : sp_fingerprint(s->sp, node, fp);
   if (chk(s, node) || !fp) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_fingerprint(t, node, fp); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -1631,6 +1699,7 @@ extern "C" int kb_sim_fingerprint(kb_sim* s, uint32_t node, uint32_t* fp) {
 }
 // all ids; 0 for non-running ids and (sharded ranks) for rows held by other shards
 extern "C" int kb_sim_fingerprints(kb_sim* s, uint32_t* fps, size_t cap) {
+  if (s && s->sp) return (!fps || cap < s->C) ? KB_INVALID_ARGUMENT : sp_fingerprints(s->sp, fps);
   if (!s || !fps || cap < s->C) return KB_INVALID_ARGUMENT;
   if (is_group(s)) {
     std::vector<uint32_t> part(s->C);
@@ -1652,6 +1721,7 @@ extern "C" int kb_sim_fingerprints(kb_sim* s, uint32_t* fps, size_t cap) {
   return KB_OK;
 }
 extern "C" int kb_sim_true_fingerprint(kb_sim* s, uint32_t* fp) {
+  if (s && s->sp) return fp ? sp_true_fingerprint(s->sp, fp) : KB_INVALID_ARGUMENT;
   if (!s || !fp) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_true_fingerprint(s->shards[0], fp);
   k_alive_bits<<<(s->d.NWR + 255) / 256, 256, 0, s->st>>>(s->d);
@@ -1663,6 +1733,13 @@ extern "C" int kb_sim_true_fingerprint(kb_sim* s, uint32_t* fp) {
   return KB_OK;
 }
 extern "C" int kb_sim_dump_row(kb_sim* s, uint32_t node, uint8_t* rw, size_t cap) {
+  if (s && s->sp) {
+    if (chk(s, node) || !rw || cap < s->C) return KB_INVALID_ARGUMENT;
+    std::vector<uint8_t> v;
+    const int rc = sp_read_row(s->sp, node, v);
+    if (!rc) memcpy(rw, v.data(), s->C);
+    return rc;
+  }
   if (chk(s, node) || !rw || cap < s->C) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_row(t, node, rw, cap); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -1673,6 +1750,16 @@ extern "C" int kb_sim_dump_row(kb_sim* s, uint32_t node, uint8_t* rw, size_t cap
   return KB_OK;
 }
 extern "C" int kb_sim_peers(kb_sim* s, uint32_t node, uint32_t* peers, size_t cap, size_t* n) {
+  if (s && s->sp) {
+    if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
+    std::vector<uint8_t> rw;
+    const int rc = sp_read_row(s->sp, node, rw);
+    if (rc) return rc;
+    size_t c = 0;
+    for (uint32_t j = 0; j < s->C; ++j) if (rw[j]) { if (peers && c < cap) peers[c] = j; c++; }
+    *n = c;
+    return (peers && cap < c) ? KB_CAPACITY : KB_OK;
+  }
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_peers(t, node, peers, cap, n); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -1685,6 +1772,7 @@ extern "C" int kb_sim_peers(kb_sim* s, uint32_t node, uint32_t* peers, size_t ca
   return (peers && cap < c) ? KB_CAPACITY : KB_OK;
 }
 extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, size_t cap, size_t* n) {
+  if (s && s->sp) return (chk(s, node) || !n) ? KB_INVALID_ARGUMENT : sp_peer_states(s->sp, node, out, cap, n);
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_peer_states(t, node, out, cap, n); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -1727,6 +1815,7 @@ extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, 
   return (out && cap < c) ? KB_CAPACITY : KB_OK;
 }
 extern "C" int kb_sim_watch(kb_sim* s, uint32_t node) {
+  if (s && s->sp) return chk(s, node) ? KB_INVALID_ARGUMENT : sp_watch(s->sp, node);
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_watch(t, node); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -1741,6 +1830,10 @@ extern "C" int kb_sim_watch(kb_sim* s, uint32_t node) {
 }
 extern "C" int kb_sim_events(kb_sim* s, uint32_t node, uint32_t* discovered, size_t cap_d, size_t* n_d,
                              uint32_t* departed, size_t cap_p, size_t* n_p, uint32_t* fp, int* fp_changed) {
+  if (s && s->sp) {
+    if (chk(s, node) || !n_d || !n_p || !fp || !fp_changed) return KB_INVALID_ARGUMENT;
+    return sp_events(s->sp, node, discovered, cap_d, n_d, departed, cap_p, n_p, fp, fp_changed);
+  }
   if (chk(s, node) || !n_d || !n_p || !fp || !fp_changed) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) {
     return kb_sim_events(t, node, discovered, cap_d, n_d, departed, cap_p, n_p, fp, fp_changed); });
@@ -1789,6 +1882,7 @@ static int fold_stats(kb_sim* s) {
   return KB_OK;
 }
 extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
+  if (s && s->sp) return out ? sp_stats_out(s->sp, out) : KB_INVALID_ARGUMENT;
   if (!s || !out) return KB_INVALID_ARGUMENT;
   { const int rc = fold_stats(s); if (rc) return rc; }
   unsigned long long st[NSTAT];
@@ -1835,6 +1929,7 @@ extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
 }
 // per id: alive, n, last_bcast, start_round; n and last_bcast only for the rows this handle holds
 extern "C" int kb_sim_dump_scalars(kb_sim* s, int32_t* out, size_t cap) {
+  if (s && s->sp) return (!out || cap < 4ull * s->C) ? KB_INVALID_ARGUMENT : sp_dump_scalars(s->sp, out);
   if (!s || !out || cap < 4ull * s->C) return KB_INVALID_ARGUMENT;
   if (is_group(s)) {
     std::vector<int32_t> part(4ull * s->C);
@@ -1861,6 +1956,7 @@ extern "C" int kb_sim_dump_scalars(kb_sim* s, int32_t* out, size_t cap) {
   return KB_OK;
 }
 extern "C" int kb_sim_dump_suspects(kb_sim* s, uint32_t node, int32_t* out, size_t cap, size_t* n) {
+  if (s && s->sp) return (chk(s, node) || !n) ? KB_INVALID_ARGUMENT : sp_dump_suspects(s->sp, node, out, cap, n);
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_suspects(t, node, out, cap, n); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -1874,6 +1970,7 @@ extern "C" int kb_sim_dump_suspects(kb_sim* s, uint32_t node, int32_t* out, size
   return KB_OK;
 }
 extern "C" int kb_sim_dump_curious(kb_sim* s, uint32_t node, int32_t* out, size_t cap, size_t* n) {
+  if (s && s->sp) return (chk(s, node) || !n) ? KB_INVALID_ARGUMENT : sp_dump_curious(s->sp, node, out, cap, n);
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_curious(t, node, out, cap, n); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -1915,6 +2012,7 @@ static void prof_flush(kb_sim* s) {
   prof_resolve(s, s->krec.size());
 }
 extern "C" int kb_sim_kernel_time(kb_sim* s, int kind, double* ms, uint64_t* launches) {
+  if (s && s->sp) return (!ms || !launches) ? KB_INVALID_ARGUMENT : sp_kernel_time(s->sp, kind, ms, launches);
   if (!s || !ms || !launches) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_kernel_time(s->shards[0], kind, ms, launches);
   prof_flush(s);
@@ -1931,6 +2029,7 @@ static uint64_t stat_counter(kb_sim* s, int idx) {
   return v;
 }
 extern "C" int kb_sim_reset_kernel_time(kb_sim* s) {
+  if (s && s->sp) return sp_reset_kernel_time(s->sp);
   if (!s) return KB_INVALID_ARGUMENT;
   GROUP_ALL(kb_sim_reset_kernel_time);
   prof_flush(s);
@@ -1945,6 +2044,7 @@ extern "C" int kb_sim_reset_kernel_time(kb_sim* s) {
 // algorithmic bytes a kernel moved since the last reset, counted in-kernel; this handle's
 // rows: shard 0's for a group, like kb_sim_kernel_time
 extern "C" int kb_sim_kernel_bytes(kb_sim* s, int kind, uint64_t* bytes) {
+  if (s && s->sp) { if (!bytes) return KB_INVALID_ARGUMENT; *bytes = 0; return KB_INVALID_ARGUMENT; }
   if (!s || !bytes) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_kernel_bytes(s->shards[0], kind, bytes);
   const int k = kt_kid(kind), b = k < 0 ? -1 : kbytes_stat(k);
@@ -1953,6 +2053,7 @@ extern "C" int kb_sim_kernel_bytes(kb_sim* s, int kind, uint64_t* bytes) {
   return KB_OK;
 }
 extern "C" int kb_sim_set_profiling(kb_sim* s, int level) {
+  if (s && s->sp) { if (level < 0 || level > 2) return KB_INVALID_ARGUMENT; s->sp->prof_level = level; return KB_OK; }
   if (!s || level < 0 || level > 2) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_set_profiling(t, level); });
   s->prof_level = level;
@@ -1961,6 +2062,7 @@ extern "C" int kb_sim_set_profiling(kb_sim* s, int level) {
 // every kernel the rounds launched since the last reset: HIP-event time (sum and per delivery wave),
 // launches, algorithmic bytes where counted in-kernel; kernels never launched are omitted
 extern "C" int kb_sim_kernel_breakdown(kb_sim* s, kb_kernel_time* out, size_t cap, size_t* n) {
+  if (s && s->sp) return n ? sp_kernel_breakdown(s->sp, out, cap, n) : KB_INVALID_ARGUMENT;
   if (!s || !n) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_kernel_breakdown(s->shards[0], out, cap, n);
   prof_flush(s);
@@ -1985,6 +2087,7 @@ extern "C" int kb_sim_kernel_breakdown(kb_sim* s, kb_kernel_time* out, size_t ca
 // host waits on the device since creation (stream synchronisations and pinned hand-offs); for a
 // group, the largest over its shards
 extern "C" int kb_sim_host_syncs(kb_sim* s, uint64_t* n) {
+  if (s && s->sp) { if (!n) return KB_INVALID_ARGUMENT; *n = s->sp->host_syncs; return KB_OK; }
   if (!s || !n) return KB_INVALID_ARGUMENT;
   if (is_group(s)) {
     uint64_t m = 0;
@@ -1997,6 +2100,7 @@ extern "C" int kb_sim_host_syncs(kb_sim* s, uint64_t* n) {
 }
 // OR of the PATH_* bits (kb_common.h) of the kernel variants that did work since creation
 extern "C" int kb_sim_debug_paths(kb_sim* s, uint32_t* mask) {
+  if (s && s->sp) { if (!mask) return KB_INVALID_ARGUMENT; *mask = 0; return KB_OK; }
   if (!s || !mask) return KB_INVALID_ARGUMENT;
   if (is_group(s)) {
     uint32_t m = 0;
@@ -2009,6 +2113,7 @@ extern "C" int kb_sim_debug_paths(kb_sim* s, uint32_t* mask) {
 }
 // development counters (test surface): [A3 rows scanned, rows scanned past their first chunk, chunks read]
 extern "C" int kb_sim_debug_counters(kb_sim* s, uint64_t* out, size_t cap) {
+  if (s && s->sp) { if (!out || cap < 3) return KB_INVALID_ARGUMENT; out[0] = out[1] = out[2] = 0; return KB_OK; }
   if (!s || !out || cap < 3) return KB_INVALID_ARGUMENT;
   kb_sim* h = is_group(s) ? s->shards[0] : s;
   { const int rc = fold_stats(h); if (rc) return rc; }
@@ -2016,4 +2121,9 @@ extern "C" int kb_sim_debug_counters(kb_sim* s, uint64_t* out, size_t cap) {
   HIPCHK(hipMemcpy(v, h->d.stats + S_A3ROWS, sizeof v, hipMemcpyDeviceToHost));
   for (int k = 0; k < 3; ++k) out[k] = v[k];
   return KB_OK;
+}
+extern "C" int kb_sim_sparse_footprint(kb_sim* s, uint64_t* out, size_t cap) {
+  if (!s || !out) return KB_INVALID_ARGUMENT;
+  if (!s->sp) { seterr("not a KB_VARIANT_SPARSE_ROWS handle"); return KB_INVALID_OPERATION; }
+  return sp_footprint(s->sp, out, cap);
 }

@@ -100,6 +100,7 @@ struct kbo_sim {
   uint8_t* ident; uint8_t* id_len;
   uint8_t* pend_ident; int16_t* pend_len;   /* identity set on a stopped instance, taken by its next address (-1: none) */
   uint8_t* moved;                           /* the instance bound here restarted at a fresh address */
+  uint8_t* idset;                           /* an identity was set on this never-bound address (not fresh) */
   uint32_t* cseg; uint32_t* segmul;   /* crc0(addr||identity), x^(8*seglen) */
   uint32_t* seglen;
   uint32_t mulz_tab[4][256]; int uniform; uint32_t ulen;
@@ -120,6 +121,7 @@ struct kbo_sim {
 typedef struct kbo_sim kbo_sim;
 
 int kbo_sim_destroy(kbo_sim* s);
+static int fresh_id(const kbo_sim* s, uint32_t id);
 static char g_err[256];
 static void seterr(const char* m) { snprintf(g_err, sizeof g_err, "%s", m); }
 const char* kbo_last_error(void) { return g_err; }
@@ -489,8 +491,26 @@ static void node_restart(kbo_sim* s, uint32_t from, uint32_t to, int32_t r) {
   memcpy(s->susp + (size_t)to * SLOTS, s->susp + (size_t)from * SLOTS, SLOTS * sizeof(osusp));
   s->n[to] = s->n[from];
   s->dirty[to] = 1;
-  for (size_t k = 0; k < s->nwatch; ++k) if (s->wnode[k] == from) s->wnode[k] = to;   /* the map's observer */
   node_start(s, to, r);
+  /* the map's observer follows the instance.  An observer already attached to the new address (subscribed
+   * after start() returned, before this round) either gives way to the instance's own, or, when the instance
+   * had none, starts from the map as the restart left it (a channel reports only later changes) */
+  size_t kf = s->nwatch, kt = s->nwatch;
+  for (size_t k = 0; k < s->nwatch; ++k) { if (s->wnode[k] == from) kf = k; if (s->wnode[k] == to) kt = k; }
+  if (kf < s->nwatch) {
+    if (kt < s->nwatch) {
+      free(s->wsnap[kt]);
+      s->wnode[kt] = s->wnode[s->nwatch - 1]; s->wsnap[kt] = s->wsnap[s->nwatch - 1]; s->wfp[kt] = s->wfp[s->nwatch - 1];
+      if (kf == s->nwatch - 1) kf = kt;
+      s->nwatch--;
+    }
+    s->wnode[kf] = to;
+  } else if (kt < s->nwatch) {
+    uint8_t* tmp;
+    const uint8_t* rw = row_view(s, to, &tmp);
+    for (uint32_t j = 0; j < s->C; ++j) s->wsnap[kt][j] = rw[j] != 0;
+    free(tmp);
+  }
 }
 
 /* ---- creation ----------------------------------------------------------------------------------- */
@@ -527,6 +547,7 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   s->pend_ident = (uint8_t*)calloc(C * MAXID, 1); s->pend_len = (int16_t*)malloc(C * sizeof(int16_t));
   if (s->pend_len) for (size_t k = 0; k < C; ++k) s->pend_len[k] = -1;
   s->moved = (uint8_t*)calloc(C, 1);
+  s->idset = (uint8_t*)calloc(C, 1);
   s->cseg = (uint32_t*)calloc(C, 4); s->segmul = (uint32_t*)calloc(C, 4); s->seglen = (uint32_t*)calloc(C, 4);
   s->out = (ovec*)calloc(C, sizeof(ovec)); s->oseq = (uint32_t*)calloc(C, 4);
   if (cfg->variant & ~(uint32_t)(KB_VARIANT_SAME_WINDOW_BCAST | KB_VARIANT_EXACT_LRU | KB_VARIANT_SPARSE_ROWS)) {
@@ -593,7 +614,7 @@ int kbo_sim_destroy(kbo_sim* s) {
   if (s->sr) for (uint32_t i = 0; i < s->C; ++i) srow_free(&s->sr[i]);
   free(s->sr); free(s->bbits); free(s->bcnt); free(s->bpre); free(s->zpw);
   free(s->probe_q); free(s->probes); free(s->presp); free(s->stamp); free(s->tst); free(s->lat); free(s->alive); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
-  free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len); free(s->pend_ident); free(s->pend_len); free(s->moved);
+  free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len); free(s->pend_ident); free(s->pend_len); free(s->moved); free(s->idset);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
   for (size_t k = 0; k < s->nwatch; ++k) free(s->wsnap[k]);
   free(s->wnode); free(s->wsnap); free(s->wfp);
@@ -1104,7 +1125,11 @@ static int step_round(kbo_sim* s) {
       if (ph(s, i, (uint32_t)r, (uint32_t)P_CHURN << 24, 0).v[0] < s->cfg.churn_threshold) { node_stop(s, i); leaves++; }
     }
     s->st.churn_leaves += leaves;
-    for (uint32_t k = 0; k < leaves && s->next_free < C; ++k) { node_start(s, s->next_free++, r); s->st.churn_joins++; }
+    for (uint32_t k = 0; k < leaves; ++k) {       /* fresh ids: an address some instance bound is skipped */
+      while (s->next_free < C && !fresh_id(s, s->next_free)) s->next_free++;
+      if (s->next_free >= C) break;
+      node_start(s, s->next_free++, r); s->st.churn_joins++;
+    }
   }
   /* the Probes queued since the last round travel with this round's broadcasts */
   free(s->probes);
@@ -1196,6 +1221,9 @@ static int ever_bound(const kbo_sim* s, uint32_t node) {
   for (uint32_t k = 0; k < s->nev; ++k) if (s->ev[k].node == node && s->ev[k].kind != EV_STOP) return 1;
   return 0;
 }
+/* a fresh address: never bound by an instance (ran, or a start is queued) and given no identity; churn joins
+ * and restarts take the next one in id order, so they never land on an address the API already used */
+static int fresh_id(const kbo_sim* s, uint32_t id) { return !ever_bound(s, id) && !s->idset[id]; }
 /* the first start of an instance at address `node` (src/lib.rs:136-156); a no-op while running.  A stopped
  * instance restarts at a fresh address: kbo_sim_restart_node. */
 int kbo_sim_start_node(kbo_sim* s, uint32_t node) {
@@ -1222,8 +1250,10 @@ int kbo_sim_restart_node(kbo_sim* s, uint32_t node, uint32_t* out) {
   if (s->moved[node]) { seterr("the instance bound here restarted at a fresh address"); return KB_INVALID_OPERATION; }
   if (api_running(s, node)) { *out = node; return KB_OK; }
   if (!ever_bound(s, node)) { push_ev(s, EV_START, node, node); *out = node; return KB_OK; }
-  if (s->next_free >= s->C) { seterr("no fresh address left for the restart (capacity)"); return KB_CAPACITY; }
-  const uint32_t to = s->next_free++;
+  uint32_t to = s->next_free;
+  while (to < s->C && !fresh_id(s, to)) to++;
+  if (to >= s->C) { seterr("no fresh address left for the restart (capacity)"); return KB_CAPACITY; }
+  s->next_free = to + 1;
   const int pl = s->pend_len[node];
   const uint8_t* src = pl >= 0 ? s->pend_ident + (size_t)node * MAXID : s->ident + (size_t)node * MAXID;
   const uint32_t len = pl >= 0 ? (uint32_t)pl : s->id_len[node];
@@ -1278,6 +1308,7 @@ int kbo_sim_set_identity(kbo_sim* s, uint32_t node, const uint8_t* identity, siz
   }
   memcpy(s->ident + (size_t)node * MAXID, identity, len);
   s->id_len[node] = (uint8_t)len;
+  s->idset[node] = 1;
   compute_seg(s, node);
   s->uniform = 1;
   for (uint32_t j = 0; j < s->C; ++j) if (s->id_len[j] != s->cfg.id_len) { s->uniform = 0; break; }
@@ -1521,6 +1552,11 @@ int kbo_sparse_footprint(kbo_sim* s, uint64_t* out, size_t cap) {
   }
   out[0] = based; out[1] = nx; out[2] = nl; out[3] = mx; out[4] = 4 * nx + 5 * nl; out[5] = s->C;
   return KB_OK;
+}
+int kbo_sim_sparse_footprint(kbo_sim* s, uint64_t* out, size_t cap) {
+  if (!s || !out) return KB_INVALID_ARGUMENT;
+  if (!s->sr) { seterr("not a KB_VARIANT_SPARSE_ROWS handle"); return KB_INVALID_OPERATION; }
+  return kbo_sparse_footprint(s, out, cap);
 }
 uint32_t kbo_crc32(const uint8_t* p, size_t n) { o_crc_init(); return o_crc32(p, n); }
 void kbo_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1, uint32_t* out4) {

@@ -269,6 +269,13 @@ def standard_cases() -> list[tuple[str, dict, int]]:
     cases.append(("probe_tiny", {"cfg": SimConfig(capacity=4, initial_nodes=2, seed=2),
                                  "events": {0: [("probe", 0, ("192.0.2.1", 9000))], 2: [("probe", 0, ("192.0.2.1", 9000))],
                                             3: [("start", 3, None)], 5: [("probe", 0, ("192.0.2.2", 9001))]}}, 8))
+    # fresh ids: churn joins and restarts skip an address the API already bound (49, started) or
+    # gave an identity (51), so no two instances ever share an address
+    cases.append(("fresh_ids", {"cfg": SimConfig(capacity=64, initial_nodes=48, init_mode=KB_INIT_CONVERGED, loss=0.02,
+                                                 churn=0.02, fault_end_round=24, seed=12),
+                                "events": {1: [("start", 49, None), ("ident", 51, b"x")], 3: [("stop", 7, None)],
+                                           5: [("restart", 7, None)], 6: [("stop", 20, None)], 9: [("restart", 20, None)]}},
+                  28))
     # stamps from before round 0 (early joiners' KnownPeers inserts) crossing three window rebases
     cases.append(("old_stamps", {"cfg": SimConfig(capacity=160, initial_nodes=128, init_mode=KB_INIT_CONVERGED, loss=0.02,
                                                   churn=0.03, fault_end_round=12, seed=31)}, 200))

@@ -126,6 +126,7 @@ class PyMesh:
         self.id_len = id_len
         self.identity = [default_identity(i, id_len) for i in range(capacity)]   # what each address announces
         self.pending = {}        # identity set on a stopped instance, taken by its next address
+        self.idset = set()       # never-bound addresses given an identity (not fresh)
         self.peers = [Peer(i) for i in range(capacity)]
         self.round = 0
         self.next_free = initial_nodes
@@ -189,6 +190,10 @@ class PyMesh:
     def _ever(self, i):
         return self.peers[i].ever or any(ev[1] == i and ev[0] != "stop" for ev in self.events)
 
+    def _fresh(self, i):
+        """an address no instance has bound and no identity was set on: what churn joins and restarts take"""
+        return not self._ever(i) and i not in self.idset
+
     def set_identity(self, i, ident: bytes):
         """Kaboodle::set_identity (src/lib.rs:323-336) on a stopped instance: the identity it will announce
         from its next start on (a never-bound address takes it at once)."""
@@ -197,6 +202,7 @@ class PyMesh:
             self.pending[i] = ident
         else:
             self.identity[i] = ident
+            self.idset.add(i)
 
     def start_node(self, i):
         assert self._api_running(i) or not self._ever(i)
@@ -214,7 +220,10 @@ class PyMesh:
             self.events.append(("start", i, i))
             return i
         new = self.next_free
-        self.next_free += 1
+        while new < self.C and not self._fresh(new):
+            new += 1
+        assert new < self.C, "no fresh address left"
+        self.next_free = new + 1
         self.identity[new] = self.pending.pop(i, self.identity[i])
         self.events.append(("restart", new, i))
         return new
@@ -250,6 +259,8 @@ class PyMesh:
                 self._stop(i)
             self.stats["churn_leaves"] += len(leaves)
             for _ in leaves:
+                while self.next_free < self.C and not self._fresh(self.next_free):
+                    self.next_free += 1
                 if self.next_free < self.C:
                     self._start(self.next_free, r)
                     self.next_free += 1

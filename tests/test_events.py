@@ -154,3 +154,52 @@ def test_gpu_events_rccl_rank_world1():
     ok, msg, n = parity.run_events_case(case, rounds, [0, 300, 600], gpu=g)
     assert ok, msg
     assert n > 0
+
+
+def _handoff(impls):
+    """Observers across a restart: node 5 is watched and restarts at a fresh address; an observer
+    also attached to that new address before the round gives way to the instance's own (one batch stream, no
+    duplicate).  Node 6 is not watched; an observer attached to its new address after start() returned starts
+    from the inherited map, so its batches carry only later changes, not the whole map."""
+    cfg = impls[0][1]
+    sims = [Sim(lib, c) for lib, c in impls]
+    for s in sims:
+        s.watch(5)
+    out = []
+    for r in range(14):
+        for s in sims:
+            if r == 2:
+                s.stop_node(5)
+                s.stop_node(6)
+            if r == 4:
+                a, b = s.restart_node(5), s.restart_node(6)
+                assert (a, b) == (cfg.initial_nodes, cfg.initial_nodes + 1)
+                s.watch(a)
+                s.watch(b)
+            s.step(1)
+        if r >= 4:
+            ev = [(s.events(cfg.initial_nodes), s.events(cfg.initial_nodes + 1)) for s in sims]
+            out.append(ev)
+            if r == 4:                             # the new address's first batch: what changed since start()
+                (_, (d6, p6, _, _)) = ev[0]
+                assert len(d6) <= 2 and p6 == [], (d6, p6)
+            assert all(e == ev[0] for e in ev), f"round {r}: {ev}"
+    for s in sims:
+        with pytest.raises(KbError):               # the old address has no observer left
+            s.events(5)
+        s.close()
+    return out
+
+
+def test_oracle_observer_handoff_on_restart():
+    cfg = SimConfig(capacity=48, initial_nodes=40, init_mode=KB_INIT_CONVERGED, loss=0.02, seed=3)
+    _handoff([(parity.oracle_lib(), cfg)])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 4], ids=["dense", "sparse"])
+def test_gpu_observer_handoff_on_restart(variant):
+    import kaboodle_amd
+    kaboodle_amd.require_gpu()
+    cfg = SimConfig(capacity=48, initial_nodes=40, init_mode=KB_INIT_CONVERGED, loss=0.02, seed=3, variant=variant)
+    _handoff([(parity.oracle_lib(), cfg), (parity.gpu_lib(), cfg)])
