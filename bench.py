@@ -171,14 +171,14 @@ def cpu_baseline(cfg, budget_s: float, nodes: int, budget_1t: float) -> dict:
     lib.lib.kbo_num_threads.restype = C.c_int
     cores = int(lib.lib.kbo_num_threads())
 
-    def sample(o, budget, cap):
+    def sample(o, budget, cap, least=1):
         t0 = time.perf_counter()
         rounds, alive_sum = 0, 0
         while True:
             o.step(1)
             rounds += 1
             alive_sum += o.stats()["alive"]
-            if time.perf_counter() - t0 >= budget or rounds >= cap:
+            if (time.perf_counter() - t0 >= budget and rounds >= least) or rounds >= cap:
                 return rounds, alive_sum, time.perf_counter() - t0
 
     with Sim(lib, cfg) as o:
@@ -187,7 +187,7 @@ def cpu_baseline(cfg, budget_s: float, nodes: int, budget_1t: float) -> dict:
         one = None
         if budget_1t > 0:
             lib.lib.kbo_set_num_threads(1)
-            r1, a1, dt1 = sample(o, budget_1t, 50)
+            r1, a1, dt1 = sample(o, budget_1t, 50, least=3)   # at least 3 rounds (~17 s each at 64K)
             lib.lib.kbo_set_num_threads(cores)
             one = {"value": a1 / dt1, "unit": "peer-rounds/s", "cores": 1,
                    "sample": f"the next {r1} rounds of the same run on one thread ({dt1:.1f} s)"}

@@ -104,6 +104,9 @@ struct Dev {
   uint16_t* lat;                  // [W][local rows] PeerInfo.latency in ms, PEER-major (LAT_NONE = None); null
                                   // unless track_latency
   int32_t wave;                   // delivery wave of the launch (latency clock)
+  int32_t* tst;                   // KB_VARIANT_EXACT_LRU: [local rows][W] the instant of every Known entry whose
+                                  // stamp byte has saturated to ANCIENT (a fresher byte encodes its instant
+                                  // itself); null otherwise
 };
 
 // freshness log (the KnownPeersRequest reply set, :503-508, without scanning the row): an entry is

@@ -6,8 +6,12 @@
 namespace kb {
 
 // ---- stamp window: every 64 rounds known stamps shift down, saturating at "ancient"
-__global__ void k_rebase(Dev d) {
+// (KB_VARIANT_EXACT_LRU: a byte that saturates hands its instant, decoded with the epoch it was written in, to
+// the tst table; every stamp write is Known(now) or Known(r - 10), so a byte above ANCIENT encodes its instant)
+__global__ void k_rebase(Dev d, int32_t r) {
   const size_t total = (size_t)(d.hi - d.lo) * d.W / 16;     // the local rows
+  const uint32_t wpr = d.W / 16;
+  const int32_t E = epoch_base(r - 1);                      // the epoch the bytes were written in
   uint4* p = reinterpret_cast<uint4*>(d.stamp + (size_t)d.lo * d.W);
   for (size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (size_t)gridDim.x * blockDim.x) {
     const uint4 v = p[k];
@@ -19,13 +23,67 @@ __global__ void k_rebase(Dev d) {
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         uint32_t b = (x >> (8 * t)) & 0xFF;
-        if (b > ST_ANCIENT) { b = b > ST_ANCIENT + EPOCH ? b - EPOCH : ST_ANCIENT; any = true; }   // unsigned: no b - EPOCH < 0
+        if (b > ST_ANCIENT) {
+          if (d.tst && b <= ST_ANCIENT + EPOCH) {
+            const size_t i = d.lo + k / wpr, j = (k % wpr) * 16 + q * 4 + t;
+            d.tst[i * d.W + j] = (int32_t)b - EOFF + E;
+          }
+          b = b > ST_ANCIENT + EPOCH ? b - EPOCH : ST_ANCIENT; any = true;   // unsigned: no b - EPOCH < 0
+        }
         y |= b << (8 * t);
       }
       w[q] = y;
     }
     if (any) p[k] = make_uint4(w[0], w[1], w[2], w[3]);
   }
+}
+
+// KB_VARIANT_EXACT_LRU: ping_random_peer's oldest five by the exact instant of the last contact
+// (src/kaboodle.rs:662-675 sorts by Instant), ties broken by the rotated address from the sweep front, over the
+// whole row; written as the row pass's keys (rank << 24 | rotated id) for k_tick_post.  A wave per row, 16 ids per
+// lane per step: stamp bytes, member bits, and the saturated entries' instants.
+__device__ inline unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const unsigned long long t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
+  return v;
+}
+__global__ __launch_bounds__(256) void k_a3_exact(Dev d, uint32_t* part, int32_t r) {
+  const uint32_t i = d.lo + blockIdx.x * 4 + (threadIdx.x >> 6), l = lane();
+  if (i >= d.hi || !d.alive[i]) return;
+  const uint32_t C = d.C, cur = d.a3cur[i];
+  const int32_t E = epoch_base(r);
+  unsigned long long top[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
+  const uint8_t* srow = row_of(d, i);
+  const uint32_t* brow = bits_of(d, i);
+  const int32_t* trow = d.tst + (size_t)i * d.W;
+  for (uint32_t base = 0; base < d.W; base += 1024) {
+    const uint32_t j0 = base + 16 * l;
+    const uint32_t bw = (brow[j0 >> 5] >> (j0 & 31)) & 0xFFFFu;
+    if (!bw) continue;
+    const uint4 sv = *reinterpret_cast<const uint4*>(srow + j0);
+    const uint32_t s4[4] = {sv.x, sv.y, sv.z, sv.w};
+    for (uint32_t t = 0; t < 16; ++t) {
+      if (!((bw >> t) & 1u)) continue;
+      const uint32_t j = j0 + t;
+      if (j >= C || j == i) continue;
+      const uint32_t b = (s4[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+      if (b < ST_ANCIENT) continue;                                 // WaitingFor*: not a candidate
+      const int32_t inst = b > ST_ANCIENT ? (int32_t)b - EOFF + E : trow[j];
+      const uint32_t rot = j > cur ? j - cur - 1 : j + C - cur - 1;
+      unsigned long long key = ((unsigned long long)((uint32_t)inst ^ 0x80000000u) << 32) | rot;
+      if (key >= top[4]) continue;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) { if (key < top[q]) { const unsigned long long x = top[q]; top[q] = key; key = x; } }
+    }
+  }
+  uint32_t out[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {                        // keys are distinct (rotated ids): one lane pops each minimum
+    const unsigned long long m = wave_min_u64(top[0]);
+    out[k] = m == ~0ull ? 0xFFFFFFFFu : ((uint32_t)k << 24) | (uint32_t)(m & 0xFFFFFFu);
+    if (m != ~0ull && top[0] == m) { top[0] = top[1]; top[1] = top[2]; top[2] = top[3]; top[3] = top[4]; top[4] = ~0ull; }
+  }
+  if (l < 10) part[(size_t)i * 10 + l] = l < 5 ? (l == 0 ? out[0] : l == 1 ? out[1] : l == 2 ? out[2] : l == 3 ? out[3] : out[4]) : 0xFFFFFFFFu;
 }
 
 // ---- lifecycle: API start/stop in call order, then churn (src/lib.rs:136-183) ------------------
@@ -47,13 +105,14 @@ __global__ void k_events(Dev d, const Event* ev, uint32_t nev, int32_t r) {
 // packed into one u32 buffer (every row table of the node: stamps, member bits, checkpoints, suspect slots,
 // freshness log, latency column, plus the event observer's snapshot), moved to the shard holding the new
 // row (an all-to-all-v with one non-empty pair; unsharded: in place) and unpacked there.
-struct RowPack { uint32_t hdr, fstart, susp, segp, flog, bits, snap, stamp, lat, words; };
+struct RowPack { uint32_t hdr, fstart, susp, segp, flog, bits, snap, stamp, lat, tst, words; };
 enum { RP_N, RP_FP, RP_DIRTY, RP_FLOGN, RP_WATCHED, RP_WFP, RP_SD0, RP_SD1, RP_HDR = 16 };
-__host__ __device__ inline RowPack row_pack_layout(uint32_t W, uint32_t NWR, bool lat) {
+__host__ __device__ inline RowPack row_pack_layout(uint32_t W, uint32_t NWR, bool lat, bool tst) {
   RowPack L;
   L.hdr = 0; L.fstart = RP_HDR; L.susp = L.fstart + 16; L.segp = L.susp + SLOTS * 4; L.flog = L.segp + 2 * NSEG;
   L.bits = L.flog + LOGCAP; L.snap = L.bits + NWR; L.stamp = L.snap + NWR; L.lat = L.stamp + W / 4;
-  L.words = L.lat + (lat ? W / 2 : 0);
+  L.tst = L.lat + (lat ? W / 2 : 0);
+  L.words = L.tst + (tst ? W : 0);
   return L;
 }
 __global__ __launch_bounds__(256) void k_row_pack(Dev d, uint32_t i, uint32_t* __restrict__ out, RowPack L,
@@ -74,6 +133,8 @@ __global__ __launch_bounds__(256) void k_row_pack(Dev d, uint32_t i, uint32_t* _
   for (uint32_t k = t; k < d.W / 4; k += T) out[L.stamp + k] = st[k];
   if (d.lat)
     for (uint32_t k = t; k < d.W / 2; k += T) out[L.lat + k] = (uint32_t)*lat_at(d, i, 2 * k) | ((uint32_t)*lat_at(d, i, 2 * k + 1) << 16);
+  if (d.tst)
+    for (uint32_t k = t; k < d.W; k += T) out[L.tst + k] = (uint32_t)d.tst[(size_t)i * d.W + k];
 }
 __global__ __launch_bounds__(256) void k_row_unpack(Dev d, uint32_t i, const uint32_t* __restrict__ in, RowPack L,
                                                     uint32_t* __restrict__ snap) {
@@ -95,6 +156,8 @@ __global__ __launch_bounds__(256) void k_row_unpack(Dev d, uint32_t i, const uin
       const uint32_t v = in[L.lat + k];
       *lat_at(d, i, 2 * k) = (uint16_t)v; *lat_at(d, i, 2 * k + 1) = (uint16_t)(v >> 16);
     }
+  if (d.tst)
+    for (uint32_t k = t; k < d.W; k += T) d.tst[(size_t)i * d.W + k] = (int32_t)in[L.tst + k];
 }
 __global__ void k_churn_leave(Dev d, int32_t r) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

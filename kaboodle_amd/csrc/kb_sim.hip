@@ -47,14 +47,14 @@ enum KId : int {
   KI_LAT_MARK, KI_BFAIL_PREP, KI_ROWPASS, KI_LAT_SWEEP, KI_SCAN_TILES, KI_SCAN_APPLY, KI_SET_CAP, KI_RESP_WAVE,
   KI_RESP_NODE, KI_TICK_SCAN, KI_TICK_PRE, KI_FOLD, KI_FP_ROWS, KI_TICK_POST, KI_BCAST_WRITE, KI_ROUTE, KI_ROUTE_X,
   KI_XBOUND, KI_PACK, KI_ROUTE_RECV, KI_SCATTER, KI_SCATTER_FLAT, KI_KP, KI_SORTFAST, KI_PROC, KI_ROUND_END,
-  KI_PROBE, NKI
+  KI_PROBE, KI_A3_EXACT, NKI
 };
 static const char* const KNAME[NKI] = {
   "k_rebase", "k_events", "k_churn_leave", "k_churn_join", "k_alive_bits", "k_truefp_part", "k_truefp_fin",
   "k_log_mark", "k_lat_mark", "k_bfail_prep", "k_rowpass", "k_lat_sweep", "k_scan_tiles", "k_scan_apply",
   "k_set_cap", "k_resp_wave", "k_resp_node", "k_tick_scan", "k_tick_pre", "k_fold", "k_fp_rows", "k_tick_post",
   "k_bcast_write", "k_route", "k_route_x", "k_xbound", "k_pack", "k_route_recv", "k_scatter", "k_scatter_flat",
-  "k_kp", "k_sortfast", "k_proc", "k_round_end", "k_probe"};
+  "k_kp", "k_sortfast", "k_proc", "k_round_end", "k_probe", "k_a3_exact"};
 // the in-kernel algorithmic byte counter of a kernel (StatIdx), or -1
 static int kbytes_stat(int kid) {
   switch (kid) {
@@ -499,11 +499,13 @@ static int upload_segments(kb_sim* s) {
   const uint32_t C = s->C;
   std::vector<uint32_t> cseg(C), segmul(C), seglen(C);
   bool uniform = true;
+  uint32_t xp[ADDR_LEN + MAXID + 1];                 // x^(8 len) per segment length
+  for (uint32_t l = 0; l <= ADDR_LEN + MAXID; ++l) xp[l] = h_xpow8(l);
   for (uint32_t j = 0; j < C; ++j) {
     char a[32]; kb_format_addr(j, a, sizeof a);
     uint32_t reg = h_crc_update(0, (const uint8_t*)a, ADDR_LEN);
     reg = h_crc_update(reg, &s->h_ident[(size_t)j * MAXID], s->h_idlen[j]);
-    cseg[j] = reg; seglen[j] = ADDR_LEN + s->h_idlen[j]; segmul[j] = h_xpow8(seglen[j]);
+    cseg[j] = reg; seglen[j] = ADDR_LEN + s->h_idlen[j]; segmul[j] = xp[seglen[j]];
     if (s->h_idlen[j] != s->cfg.id_len) uniform = false;
   }
   s->d.uniform = uniform ? 1 : 0;
@@ -566,7 +568,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (!cfg || !out || cfg->abi_version != KB_ABI_VERSION) { seterr("bad config"); delete xf; return KB_INVALID_ARGUMENT; }
   if (cfg->capacity == 0 || cfg->capacity > 7800000u || cfg->initial_nodes > cfg->capacity || cfg->id_len > MAXID ||
       cfg->max_waves == 0 || cfg->max_waves > 64) { seterr("config out of range"); delete xf; return KB_INVALID_ARGUMENT; }
-  if (cfg->variant) { seterr(cfg->variant == KB_VARIANT_SPARSE_ROWS ? "sparse rows run unsharded (kb_sim_create)" : "semantic variants other than KB_VARIANT_SPARSE_ROWS are measurement-only (CPU oracle)"); delete xf; return KB_INVALID_ARGUMENT; }
+  if (cfg->variant && cfg->variant != KB_VARIANT_EXACT_LRU) { seterr(cfg->variant == KB_VARIANT_SPARSE_ROWS ? "sparse rows run unsharded (kb_sim_create)" : "semantic variants other than KB_VARIANT_SPARSE_ROWS are measurement-only (CPU oracle)"); delete xf; return KB_INVALID_ARGUMENT; }
   const uint32_t C = cfg->capacity;
   const uint32_t rows_per = (C + (uint32_t)world - 1) / (uint32_t)world;
   if (world < 1 || world > (int)XMAX || rank < 0 || rank >= world || (uint64_t)(world - 1) * rows_per >= C) {
@@ -635,6 +637,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   A(d.ztab, 17 * 128); A(d.zbtab, ZB);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.sacc, (size_t)NACC * NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
+  if (cfg->variant == KB_VARIANT_EXACT_LRU) AR(d.tst, W);   // exact A3 instants
   if (cfg->track_latency) { A(d.lat, (size_t)W * lat_stride(R)); A(s->lat_col, C); A(s->fnamed, d.NWR); }   // peer-major
   s->msg_cap = std::max<uint32_t>(8u * R + (uint32_t)TICK_MAX * R, 1u << 16);
   s->pay_cap = std::max<uint32_t>((d.capk + 1) * R, 1u << 24);
@@ -669,6 +672,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); destroy_shard(s); return KB_CAPACITY; }
   (void)hipMemset(L(s, d.kpr_big), 0xFF, 4ull * R);          // no round yet
   if (d.lat) { (void)hipMemset(d.lat, 0xFF, 2ull * lat_stride(R) * W); (void)hipMemset(s->fnamed, 0, 4ull * d.NWR); }   // all None
+  if (d.tst) (void)hipMemsetD32(d.tst + (size_t)s->lo * W, INT32_MIN / 2, (size_t)R * W);   // a converged start: ancient, all tied
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
   if (hipHostMalloc((void**)&s->h_pin, 4 * PIN_WORDS, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
@@ -1051,7 +1055,7 @@ static int launch_waves(kb_sim* s, int32_t rk) {
 // channel reports only later changes, not the whole inherited map
 static int move_row(kb_sim* s, uint32_t from, uint32_t to, bool* snap_after) {
   *snap_after = false;
-  const RowPack LP = row_pack_layout(s->W, s->d.NWR, s->d.lat != nullptr);
+  const RowPack LP = row_pack_layout(s->W, s->d.NWR, s->d.lat != nullptr, s->d.tst != nullptr);
   if (!s->rpack) HIPCHK(hipMalloc(&s->rpack, 4ull * LP.words));
   if (s->xf && !s->rpack_in) HIPCHK(hipMalloc(&s->rpack_in, 4ull * LP.words));
   const bool have = from >= s->lo && from < s->hi, take = to >= s->lo && to < s->hi;
@@ -1112,7 +1116,7 @@ static int step_round(kb_sim* s) {
   }
   (void)hipEventRecord(er[0], st);
   // 0. stamp window
-  if (r > 0 && r % EPOCH == 0) klaunch(s, KI_REBASE, k_rebase, dim3(8192), dim3(256), 0, d);
+  if (r > 0 && r % EPOCH == 0) klaunch(s, KI_REBASE, k_rebase, dim3(8192), dim3(256), 0, d, r);
   // 1. lifecycle (every shard applies the same events and churn draws to the replicated per-id state)
   if (!s->events.empty()) {
     if (s->events.size() > s->events_cap) {
@@ -1333,6 +1337,7 @@ static int step_round(kb_sim* s) {
   // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded
   if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
   if (d.uniform) klaunch(s, KI_FP_ROWS, k_fp_rows, dim3((FP_LANES * R + tb - 1) / tb), dim3(tb), 0, d);
+  if (d.tst) klaunch(s, KI_A3_EXACT, k_a3_exact, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);   // exact A3 order
   klaunch(s, KI_TICK_POST, k_tick_post, dim3(gnode), dim3(tb), 0, d, s->ro, o0, r);
   {
     ScanArgs a = scan_args(s, R, s->scan_tot);

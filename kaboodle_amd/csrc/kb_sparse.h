@@ -479,6 +479,7 @@ __global__ __launch_bounds__(64) void k_sp_truefp_fin(SpDev d, const uint2* part
 // ---- broadcast phase: round r-1's Failed, Join and Probe deliveries (src/kaboodle.rs:256-331) -----------
 struct SpBc {
   const BCast* bfail; uint32_t nf;
+  uint32_t fcounted;                             // the Failed group was counted by k_sp_bfail_sf (socket_faithful)
   const BCast* bjoin; uint32_t nj; uint32_t JW;
   uint32_t* jnew; uint32_t* jresp;               // [C][JW] bits: the entry inserted its joiner / got a response
   uint32_t* jr_n; uint32_t* jr_pay;              // per node: responses, their payload ids
@@ -499,12 +500,15 @@ __global__ __launch_bounds__(256) void k_sp_bcast(SpDev d, SpBc bc, int32_t r) {
   uint32_t nresp = 0, pay = 0;
   if (i < d.C && d.alive[i] && d.start_round[i] < r) {
     const bool fl = sp_faults(d, r) && d.loss_thr;
+    // partition groups: the receiver's once, each entry's precomputed by k_sp_bcast_write (BCast.pad)
+    const bool pact = d.pgroups > 1 && r >= d.pstart && r < d.pend;
+    const uint32_t rg = pact ? (uint32_t)((uint64_t)i * d.pgroups / d.C) : 0u;
     U4 w = U4{0, 0, 0, 0};
     uint32_t wk = SP_NONE;
-    for (uint32_t k = 0; k < bc.nf; ++k) {                   // Failed(p) :268-283
+    for (uint32_t k = 0; k < (bc.fcounted ? 0u : bc.nf); ++k) {   // Failed(p) :268-283
       const BCast b = bc.bfail[k];
       if (b.sender == i) continue;
-      bool ls = sp_part(d, r, b.sender, i);
+      bool ls = pact && b.pad != rg;
       if (!ls && fl) {
         if ((k >> 2) != wk) { wk = k >> 2; w = philox(i, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | wk, 0, d.k0, d.k1); }
         ls = sp_word(w, k & 3u) < d.loss_thr;
@@ -517,7 +521,7 @@ __global__ __launch_bounds__(256) void k_sp_bcast(SpDev d, SpBc bc, int32_t r) {
     for (uint32_t k = 0; k < bc.nj; ++k) {                   // Join{addr} :284-304
       const BCast b = bc.bjoin[k];
       if (b.sender == i) continue;
-      bool ls = sp_part(d, r, b.sender, i);
+      bool ls = pact && b.pad != rg;
       if (!ls && fl) {
         if ((k >> 2) != wk) { wk = k >> 2; w = philox(i, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | (1u << 23) | wk, 0, d.k0, d.k1); }
         ls = sp_word(w, k & 3u) < d.loss_thr;
@@ -545,6 +549,54 @@ __global__ __launch_bounds__(256) void k_sp_bcast(SpDev d, SpBc bc, int32_t r) {
   if (i < d.C) { bc.jr_n[i] = nresp; bc.jr_pay[i] = pay; }
   const int idx[5] = {S_BDROP, S_RMFAILED, S_PROBERESP, S_LOSS, S_JRESP};
   const unsigned long long v[5] = {lost, removed, presp, plost, jresp};
+  sp_stats(d, idx, v);
+}
+
+// The Failed group in socket_faithful mode: a Failed broadcast is never honoured there, so its
+// only effect on a receiver is whether the delivery was lost (drop_bcast): entries from the receiver itself are
+// skipped, partition-blocked ones are lost, the rest lost iff word e mod 4 of philox(recv, r, BLOSS | e/4, 0) is
+// below the threshold (the draws of k_sp_bcast and the oracle, src/kaboodle.rs:268-283).  Every receiver
+// evaluates ~N/10 entries a round, N x N/40 Philox calls at 4M peers: the kernel is bound by them.  The list
+// arrives packed (sender << 8 | partition group, four entries per 16 bytes, 0xFFFFFFFF padding) and is staged
+// through LDS, one broadcast 16-byte read per four entries; a group of four whose entries are all blocked or
+// the receiver's own takes no draw.
+constexpr uint32_t SP_FK_LDS = 1024;              // 16-byte groups (4096 entries) staged per pass
+__global__ __launch_bounds__(256) void k_sp_bfail_sf(SpDev d, const uint4* __restrict__ fkey, uint32_t nf, int32_t r) {
+  __shared__ uint4 sk[SP_FK_LDS];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = i < d.C && d.alive[i] && d.start_round[i] < r;
+  const bool fl = sp_faults(d, r) && d.loss_thr;
+  const bool pact = d.pgroups > 1 && r >= d.pstart && r < d.pend;
+  const uint32_t rg = pact ? (uint32_t)((uint64_t)i * d.pgroups / d.C) : 0u;
+  const uint32_t ng = (nf + 3) / 4, thr = d.loss_thr;
+  unsigned long long lost = 0;
+  for (uint32_t g0 = 0; g0 < ng; g0 += SP_FK_LDS) {
+    const uint32_t gn = min(SP_FK_LDS, ng - g0);
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < gn; t += blockDim.x) sk[t] = fkey[g0 + t];
+    __syncthreads();
+    if (!act) continue;
+    uint32_t lg = 0;
+    for (uint32_t g = 0; g < gn; ++g) {
+      const uint4 k4 = sk[g];
+      const uint32_t kk[4] = {k4.x, k4.y, k4.z, k4.w};
+      uint32_t draw = 0;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const uint32_t k = kk[t];
+        if (k == 0xFFFFFFFFu || (k >> 8) == i) continue;
+        if (pact && (k & 255u) != rg) lg++;
+        else draw |= 1u << t;
+      }
+      if (fl && draw) {
+        const U4 w = philox(i, (uint32_t)r, ((uint32_t)P_BLOSS << 24) | (g0 + g), 0, d.k0, d.k1);
+        lg += ((draw & 1u) && w.x < thr) + ((draw & 2u) && w.y < thr) + ((draw & 4u) && w.z < thr) + ((draw & 8u) && w.w < thr);
+      }
+    }
+    lost += lg;
+  }
+  const int idx[1] = {S_BDROP};
+  const unsigned long long v[1] = {lost};
   sp_stats(d, idx, v);
 }
 
@@ -759,13 +811,18 @@ __global__ __launch_bounds__(256) void k_sp_tick(SpDev d, SpOut o0, const uint32
     if (tr) atomicAdd(&s[1], tr);
   }
 }
-__global__ void k_sp_bcast_write(SpDev d, SpTickOut bo, const uint32_t* joff, const uint32_t* foff, BCast* bjoin, BCast* bfail) {
+__global__ void k_sp_bcast_write(SpDev d, SpTickOut bo, const uint32_t* joff, const uint32_t* foff, BCast* bjoin, BCast* bfail,
+                                 uint32_t* fkey) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.C) return;
   uint32_t bseq = 0;
-  if (bo.bj[i]) bjoin[joff[i]] = BCast{i, i, bseq++, 0};
+  const uint32_t g = d.pgroups > 1 ? (uint32_t)((uint64_t)i * d.pgroups / d.C) : 0u;   // the sender's partition group
+  if (bo.bj[i]) bjoin[joff[i]] = BCast{i, i, bseq++, g};
   const uint32_t nf = bo.bnf[i];
-  for (uint32_t q = 0; q < nf; ++q) bfail[foff[i] + q] = BCast{i, bo.bfp[(size_t)i * SLOTS + q], bseq++, 0};
+  for (uint32_t q = 0; q < nf; ++q) {
+    bfail[foff[i] + q] = BCast{i, bo.bfp[(size_t)i * SLOTS + q], bseq++, g};
+    fkey[foff[i] + q] = (i << 8) | (g & 255u);     // k_sp_bfail_sf's packed entry (partition groups <= 255)
+  }
 }
 
 // ---- receive window (src/kaboodle.rs:394-548) -----------------------------------------------------

@@ -12,12 +12,12 @@ namespace kb {
 
 enum SpKId : int {
   SPK_REBASE, SPK_EVENTS, SPK_CHURN, SPK_BCAST, SPK_BOUND0, SPK_JRESP, SPK_TRUEFP, SPK_TICK, SPK_BCAST_WRITE, SPK_SCAN,
-  SPK_COMPACT, SPK_ROUTE, SPK_PAYBOUND, SPK_SCATTER, SPK_HANDLE, SPK_WINDOW, SPK_ROUND_END, SPK_N
+  SPK_COMPACT, SPK_ROUTE, SPK_PAYBOUND, SPK_SCATTER, SPK_HANDLE, SPK_WINDOW, SPK_ROUND_END, SPK_BFAIL_SF, SPK_N
 };
 static const char* const SPK_NAME[SPK_N] = {
   "k_sp_rebase", "k_sp_events", "k_sp_churn", "k_sp_bcast", "k_sp_bound0", "k_sp_jresp", "k_sp_truefp", "k_sp_tick",
   "k_sp_bcast_write", "k_sp_scan", "k_sp_compact", "k_sp_route", "k_sp_paybound", "k_sp_scatter", "k_sp_handle",
-  "k_sp_window", "k_sp_round_end"};
+  "k_sp_window", "k_sp_round_end", "k_sp_bfail_sf"};
 
 struct SpSim {
   kb_config cfg;
@@ -36,6 +36,7 @@ struct SpSim {
   std::vector<kb_probe_response> presp;
   uint2* d_presp = nullptr; uint32_t* d_presp_n = nullptr; size_t presp_cap = 0;
   BCast* bjoin = nullptr; BCast* bfail = nullptr;
+  uint32_t* fkey = nullptr;                         // the Failed list packed for k_sp_bfail_sf (padded to 4)
   uint32_t nj = 0, nf = 0;
   uint64_t bj_total = 0, bf_total = 0;
   uint32_t* jnew = nullptr; uint32_t* jresp = nullptr; size_t jw_cap = 0;
@@ -140,11 +141,13 @@ static int sp_upload_segments(SpSim* S) {
   const uint32_t C = S->C;
   std::vector<uint32_t> cseg(C), segmul(C), seglen(C);
   bool uniform = true;
+  uint32_t xp[ADDR_LEN + MAXID + 1];                 // x^(8 len) per segment length
+  for (uint32_t l = 0; l <= ADDR_LEN + MAXID; ++l) xp[l] = h_xpow8(l);
   for (uint32_t j = 0; j < C; ++j) {
     char a[32]; kb_format_addr(j, a, sizeof a);
     uint32_t reg = h_crc_update(0, (const uint8_t*)a, ADDR_LEN);
     reg = h_crc_update(reg, &S->h_ident[(size_t)j * MAXID], S->h_idlen[j]);
-    cseg[j] = reg; seglen[j] = ADDR_LEN + S->h_idlen[j]; segmul[j] = h_xpow8(seglen[j]);
+    cseg[j] = reg; seglen[j] = ADDR_LEN + S->h_idlen[j]; segmul[j] = xp[seglen[j]];
     if (S->h_idlen[j] != S->cfg.id_len) uniform = false;
   }
   S->d.uniform = uniform ? 1 : 0;
@@ -205,7 +208,7 @@ static int sp_create(const kb_config* cfg, SpSim** out) {
   SA(d.cseg, C); SA(d.segmul, C); SA(d.seglen, C); SA(d.bbits, C / 32 + 1); SA(d.bcnt, (size_t)C + 1);
   SA(d.bpre, (size_t)C + 1); SA(d.zpow, (size_t)C + 2); SA(d.stats, NSTAT); SA(d.sacc, (size_t)SP_ACC * NSTAT);
   SA(d.ctr, NCTR); SA(d.tacc, 2 * SP_ACC);
-  SA(S->bjoin, C); SA(S->bfail, (size_t)C * SLOTS); SA(S->jr_n, C); SA(S->jr_pay, C);
+  SA(S->bjoin, C); SA(S->bfail, (size_t)C * SLOTS); SA(S->fkey, (size_t)C * SLOTS + 4); SA(S->jr_n, C); SA(S->jr_pay, C);
   SA(S->bo.bj, C); SA(S->bo.bnf, C); SA(S->bo.bfp, (size_t)C * SLOTS); SA(S->joff, C); SA(S->foff, C);
   SA(S->icnt, C); SA(S->icur, C); SA(S->ebound, C); SA(S->kprc, C); SA(S->pb, C);
   SA(S->ioff, C); SA(S->eoff, C); SA(S->poff, C); SA(S->en, C); SA(S->ooff, C);
@@ -340,6 +343,11 @@ static int sp_step_round(SpSim* S) {
   }
   bc.jnew = S->jnew; bc.jresp = S->jresp; bc.jr_n = S->jr_n; bc.jr_pay = S->jr_pay;
   bc.np = np; bc.presp = S->d_presp; bc.presp_n = S->d_presp_n; bc.presp_cap = (uint32_t)std::min<size_t>(S->presp_cap, 0xFFFFFFFFu);
+  if (S->nf && S->cfg.failed_mode == KB_FAILED_SOCKET_FAITHFUL && S->cfg.partition_groups <= 255) {
+    HIPCHK(hipMemsetAsync(S->fkey + S->nf, 0xFF, 12, st));   // pad the last group of four
+    sp_launch(S, SPK_BFAIL_SF, k_sp_bfail_sf, g, tb, d, (const uint4*)S->fkey, S->nf, r);
+    bc.fcounted = 1;
+  }
   sp_launch(S, SPK_BCAST, k_sp_bcast, g, tb, d, bc, r);
   // wave-0 regions: Join responses first, then the tick's emissions
   sp_launch(S, SPK_BOUND0, k_sp_bound0, g, tb, d, (const uint32_t*)S->jr_n, S->ebound);
@@ -366,7 +374,8 @@ static int sp_step_round(SpSim* S) {
     uint32_t* out[3] = {S->joff, S->foff, S->ooff};
     sp_scan(S, 3, in, out, 2);
   }
-  sp_launch(S, SPK_BCAST_WRITE, k_sp_bcast_write, g, tb, d, S->bo, (const uint32_t*)S->joff, (const uint32_t*)S->foff, S->bjoin, S->bfail);
+  sp_launch(S, SPK_BCAST_WRITE, k_sp_bcast_write, g, tb, d, S->bo, (const uint32_t*)S->joff, (const uint32_t*)S->foff, S->bjoin, S->bfail,
+            S->fkey);
   HIPCHK(hipMemcpyAsync(tot + 2, S->scan_tot + 2, 12, hipMemcpyDeviceToHost, st));
   HIPCHK(sp_sync(S));
   const uint32_t nj_next = tot[2], nf_next = tot[3];

@@ -10,7 +10,8 @@ import pytest
 
 import parity
 import scenarios
-from kaboodle_amd._ffi import KB_DBG_ALL, KB_DBG_RESP_WAVE_HBM, KB_DBG_WAVE_GRAPH, KB_INIT_CONVERGED, KB_INVALID_OPERATION, KbError, Sim, SimConfig
+from kaboodle_amd._ffi import (KB_DBG_ALL, KB_DBG_RESP_WAVE_HBM, KB_DBG_WAVE_GRAPH, KB_INIT_CONVERGED, KB_INVALID_OPERATION,
+                               KB_VARIANT_EXACT_LRU, KbError, Sim, SimConfig)
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -38,6 +39,24 @@ def test_parity_wide_row_paths(gpu, name, case, rounds):
     k_proc's unsorted selection path), forced by kb_config.debug_flags at these sizes."""
     ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_ALL), rounds)
     assert ok, f"{name} (debug_flags={KB_DBG_ALL}): {msg}"
+
+
+@pytest.mark.parametrize("name,case,rounds", parity.standard_cases(), ids=[c[0] for c in parity.standard_cases()])
+def test_parity_exact_lru(gpu, name, case, rounds):
+    """A3 ordered by the exact instant of the last contact (KB_VARIANT_EXACT_LRU: src/kaboodle.rs:662-675 sorts
+    by Instant) instead of the 1-byte stamp window: the instants of entries that saturate at a rebase are kept in
+    a table, fresher ones are decoded from their bytes (rebase_window and old_stamps cross two and three
+    rebases).  Complete state every round, latency on."""
+    ok, msg, _ = parity.run_case(parity.with_cfg(case, variant=KB_VARIANT_EXACT_LRU, track_latency=1), rounds)
+    assert ok, f"{name} (exact LRU): {msg}"
+
+
+@pytest.mark.parametrize("name", ["stop_start", "rebase_window", "fresh_ids"])
+def test_parity_exact_lru_sharded(gpu, name):
+    """The exact instants move with a restart's map and stay row-local when sharded (x3)."""
+    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}[name]
+    ok, msg, _ = parity.run_case(parity.with_cfg(case, variant=KB_VARIANT_EXACT_LRU), rounds, shards=3)
+    assert ok, f"{name} (exact LRU, x3): {msg}"
 
 
 TRUNC_CASES = {

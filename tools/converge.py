@@ -36,16 +36,21 @@ def main() -> int:
     ap.add_argument("--cap-factor", type=float, default=2.0)
     ap.add_argument("--every", type=int, default=256)
     ap.add_argument("--budget-s", type=float, default=1e9, help="stop early after this many seconds")
+    ap.add_argument("--lru", choices=("window", "exact"), default="window",
+                    help="A3's order: the 1-byte stamp window with the sweep front (declared), or the exact instants "
+                         "(KB_VARIANT_EXACT_LRU, src/kaboodle.rs:662-675)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     import numpy as np
     import kaboodle_amd
-    from kaboodle_amd._ffi import KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL, KB_INIT_CONVERGED, SimConfig
+    from kaboodle_amd._ffi import (KB_FAILED_SIM_SENDER, KB_FAILED_SOCKET_FAITHFUL, KB_INIT_CONVERGED, KB_VARIANT_EXACT_LRU,
+                                   SimConfig)
     kaboodle_amd.require_gpu()
     n, F = a.nodes, a.faults
     cfg = SimConfig(capacity=n + max(4096, int(n * 0.001 * (F + 8) * 1.5)), initial_nodes=n,
                     init_mode=KB_INIT_CONVERGED, loss=0.01, churn=0.001, fault_end_round=F, seed=1,
-                    failed_mode=KB_FAILED_SOCKET_FAITHFUL if a.mode == "sock" else KB_FAILED_SIM_SENDER)
+                    failed_mode=KB_FAILED_SOCKET_FAITHFUL if a.mode == "sock" else KB_FAILED_SIM_SENDER,
+                    variant=KB_VARIANT_EXACT_LRU if a.lru == "exact" else 0)
     cap = int(a.cap_factor * n)
     t0 = time.time()
     traj = []
@@ -96,6 +101,7 @@ def main() -> int:
                 traj.append({"round": r - 1, "node": i, "extra": extra, "missing": missing})
     out = {"workload": f"configs[2]: {n} peers, converged start, 1% loss, 0.1%/round churn, faults until round {F}",
            "failed_mode": "socket_faithful" if a.mode == "sock" else "sim_sender", "fault_end_round": F,
+           "a3_order": a.lru,
            "converged_round": conv, "tail_rounds_to_converge": None if conv is None else conv - F + 1,
            "tail_rounds_run": traj[-1]["round"] - F + 1, "cap_rounds": cap,
            "stopped_by": "converged" if conv is not None else ("cap" if traj[-1]["round"] >= F + cap - 1 else "budget"),

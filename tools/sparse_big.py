@@ -1,0 +1,121 @@
+"""configs[4] on one MI355X: the partition + heal scenario (converged start, 5 % loss, two halves cut
+off for rounds 3-11, healed at round 12 by every 256th peer pinging the other half, socket_faithful) on the GPU's
+sparse rows (KB_VARIANT_SPARSE_ROWS) at 4,194,304 peers, with per-round time, agreement, the layout's footprint,
+the kernel breakdown and the property checks of tests/test_gpu_sparse_big.py on sampled rows.
+
+    python tools/sparse_big.py --nodes 4194304 --rounds 24 --out profiles/r05_sparse_4m.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def scenario(n: int, every: int = 256, seed: int = 9, row_cap: int = 2048, rounds_part=(3, 12)):
+    from kaboodle_amd._ffi import KB_FAILED_SOCKET_FAITHFUL, KB_INIT_CONVERGED, KB_VARIANT_SPARSE_ROWS, SimConfig
+    a, b = rounds_part
+    cfg = SimConfig(capacity=n, initial_nodes=n, init_mode=KB_INIT_CONVERGED, loss=0.05, partition_groups=2,
+                    partition_start=a, partition_end=b, seed=seed, failed_mode=KB_FAILED_SOCKET_FAITHFUL,
+                    variant=KB_VARIANT_SPARSE_ROWS, sparse_row_cap=row_cap)
+    return {"cfg": cfg, "events": {b: [("ping", i, [(i + n // 2) % n]) for i in range(0, n, every)]}}
+
+
+def fp_of_peers(sim, lib, i: int) -> tuple[int, int]:
+    """(the row's fingerprint, generate_fingerprint of its peers() list computed from scratch)"""
+    import ctypes as C
+    ids = np.asarray(sim.peers(i), dtype=np.uint32)
+    f = lib.lib.kb_fingerprint_of_set
+    f.restype = C.c_uint32
+    f.argtypes = [C.POINTER(C.c_uint32), C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p]
+    want = f(ids.ctypes.data_as(C.POINTER(C.c_uint32)), len(ids), None, 0, None)   # empty identities (id_len 0)
+    return sim.fingerprint(i), int(want)
+
+
+def check_invariants(st: dict, n: int, rounds: int) -> list[str]:
+    out = []
+    if st["alive"] != n:
+        out.append(f"alive {st['alive']} != {n}")
+    if st["alive_rounds"] != n * rounds:
+        out.append(f"alive_rounds {st['alive_rounds']} != {n * rounds}")
+    if st["bcast_failed"] != st["removed_timeout"]:
+        out.append(f"every A2 removal is one Failed broadcast: {st['bcast_failed']} != {st['removed_timeout']}")
+    if st["removed_failed"] or st["drop_dead"] or st["churn_joins"] or st["bcast_join"]:
+        out.append("socket_faithful, no churn: no Failed honoured, no dead receivers, no joins")
+    return out
+
+
+def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: int = 9, verbose: bool = True) -> dict:
+    import parity
+    from kaboodle_amd._ffi import Sim
+    lib = parity.gpu_lib()
+    case = scenario(n, every, seed, row_cap)
+    t0 = time.time()
+    g = Sim(lib, case["cfg"])
+    t_create = time.time() - t0
+    g.set_profiling(1)
+    rng = np.random.default_rng(seed)
+    traj, prev = [], g.stats()
+    fails = []
+    for r in range(rounds):
+        parity.apply_events((g,), case, r)
+        t = time.time()
+        g.step(1)
+        dt = time.time() - t
+        st = g.stats()
+        rec = {"round": r, "ms": round(dt * 1e3, 1), "agree": st["agree"],
+               "failed_bcasts": st["bcast_failed"] - prev["bcast_failed"],
+               "drop_bcast": st["drop_bcast"] - prev["drop_bcast"], "drop_partition": st["drop_partition"] - prev["drop_partition"],
+               "sent": sum(st[k] - prev[k] for k in ("sent_ping", "sent_ping_req", "sent_ack", "sent_known_peers", "sent_kpr")),
+               "kpr": st["sent_kpr"] - prev["sent_kpr"], "oversize": st["drop_oversize"] - prev["drop_oversize"]}
+        if r % 4 == 3 or r == rounds - 1:
+            fp = g.sparse_footprint()
+            rec.update({"exceptions_per_row": round(fp["exceptions"] / n, 3), "stamps_per_row": round(fp["stamps"] / n, 2),
+                        "max_row_entries": fp["max_row_entries"], "bytes_per_row": round(fp["bytes"] / n, 1)})
+            for i in rng.choice(n, check_rows, replace=False):
+                got, want = fp_of_peers(g, lib, int(i))
+                if got != want:
+                    fails.append(f"round {r} row {i}: fingerprint {got:#x} != generate_fingerprint(peers()) {want:#x}")
+        prev = st
+        traj.append(rec)
+        if verbose:
+            print(json.dumps(rec), flush=True)
+    st = g.stats()
+    fails += check_invariants(st, n, rounds)
+    kb = g.kernel_breakdown()
+    round_ms, nr = g.kernel_time(1)
+    g.close()
+    return {"nodes": n, "rounds": rounds, "row_cap": row_cap, "create_s": round(t_create, 1), "trajectory": traj,
+            "kernels_ms_per_round": {k: round(v["ms"] / rounds, 3) for k, v in sorted(kb.items(), key=lambda x: -x[1]["ms"])},
+            "gpu_round_ms_mean": round(round_ms / max(nr, 1), 2), "final_stats": st, "failures": fails}
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nodes", type=int, default=4 * 1024 * 1024)
+    ap.add_argument("--rounds", type=int, default=24)
+    ap.add_argument("--every", type=int, default=256)
+    ap.add_argument("--row-cap", type=int, default=2048)
+    ap.add_argument("--check-rows", type=int, default=4)
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    res = run(a.nodes, a.rounds, a.every, a.row_cap, a.check_rows)
+    res["scenario"] = ("configs[4]: converged start, 5% loss, 2-way partition rounds 3-11, heal at 12 (every "
+                       f"{a.every}th peer pings across), socket_faithful, sparse rows on one MI355X")
+    print(json.dumps({k: v for k, v in res.items() if k != "trajectory"}), flush=True)
+    if a.out:
+        os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+        json.dump(res, open(a.out, "w"), indent=1)
+    return 1 if res["failures"] else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
