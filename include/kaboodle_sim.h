@@ -82,10 +82,11 @@ typedef struct kb_config {
                                 (src/kaboodle.rs:789-817); 0: latency reported as none (no table)    */
   uint32_t variant;          /* KB_VARIANT_*: 0 = round semantics v1.  Nonzero selects an alternative
                                 reading of a declared deviation, implemented by the
-                                CPU oracle only, to measure what the declaration changes; the HIP
-                                library refuses it (KB_INVALID_ARGUMENT) — except
-                                KB_VARIANT_SPARSE_ROWS alone, the same semantics on the configs[4]
-                                layout, which the HIP library runs (unsharded)          */
+                                CPU oracle, to measure what the declaration changes.  The HIP
+                                library runs KB_VARIANT_EXACT_LRU alone (A3 by exact instants) and
+                                KB_VARIANT_SPARSE_ROWS alone (the same semantics on the configs[4]
+                                layout, unsharded) and refuses the rest
+                                (KB_INVALID_ARGUMENT)                                                */
   uint32_t sparse_row_cap;   /* KB_VARIANT_SPARSE_ROWS on the GPU: entries per row (exceptions and
                                 explicit stamps); 0 = min(capacity, 4096).  Exceeding it is
                                 KB_CAPACITY, never a truncation (ignored by the oracle)              */
@@ -141,7 +142,8 @@ typedef struct kb_stats {
   uint64_t sent_kp_ids;           /* peer entries carried by the KnownPeers messages sent               */
   uint64_t alive_rounds;          /* sum over the simulated rounds of the peers running in that round  */
   uint64_t probe_responses;       /* ProbeResponses sent (maybe_respond_to_probe), lost ones included   */
-  uint64_t reserved[5];
+  uint64_t exported;              /* records routed to external peers (kb_sim_exported)                 */
+  uint64_t reserved[4];
 } kb_stats;
 
 typedef struct kb_sim kb_sim;
@@ -233,6 +235,32 @@ int  kb_sim_probe_responses(kb_sim* sim, kb_probe_response* out, size_t cap, siz
 typedef struct kb_broadcast { uint32_t kind, sender, peer, pad; } kb_broadcast;
 int  kb_sim_broadcasts(kb_sim* sim, kb_broadcast* out, size_t cap, size_t* n);
 
+/* ---- external peers: real instances attached through a bridge ----------------------
+ * kb_sim_set_external marks an address no instance has bound as an EXTERNAL peer: a real Kaboodle instance
+ * outside the mesh that simulated peers reach at that id (the bridge maps it to the real socket address).
+ * It never runs in the mesh (no row, no tick, not in the running set or the agreement) and churn joins and
+ * restarts skip it.  Every unicast record a simulated peer addresses to it and a delivery wave routes
+ * (src/kaboodle.rs:197-226) is EXPORTED instead of delivered: the real network carries it from there.
+ * kb_sim_exported drains them in (round, wave, sender, seq) order, KnownPeers ids into `ids` (pay_off /
+ * pay_len; ascending within a record: the reference sends a HashMap, src/structs.rs:110, whose order
+ * carries nothing).  kb_sim_inject queues a record from an external peer to a simulated one — what the bridge decoded
+ * from a real socket (:394-403) — delivered in wave 0 of the next round as that peer's emissions, in call
+ * order (seq), under the round's delivery rules (stopped receiver, partition, the Philox loss keyed on
+ * (sender, round, wave, seq)); kind = KB_WIRE_PING .. KB_WIRE_KNOWN_PEERS_REQUEST, a = PingRequest / Ack
+ * peer, fp / n = Ack / KnownPeersRequest fields, ids[pay_len] = a KnownPeers list (ids of the mesh).  At most
+ * 33 records per external peer per round (KB_CAPACITY).  kind = KB_WIRE_JOIN injects the external peer's Join
+ * broadcast (maybe_broadcast_join, src/kaboodle.rs:228-251; dest, a and ids unused): it joins the next
+ * round's Join list at its sender place and reaches every running simulated peer under the broadcast rules
+ * (:284-304: insert, maybe answer with KnownPeers — exported); one per external peer per round.  Handles of kb_sim_create_rank: every rank makes
+ * these calls alike; each rank drains the exports of its own senders.                                   */
+typedef struct kb_unicast {
+  int32_t  round;                      /* kb_sim_exported: the round and wave that routed it               */
+  uint32_t wave, sender, dest, seq, kind, a, fp, n, pay_off, pay_len, pad;
+} kb_unicast;
+int  kb_sim_set_external(kb_sim* sim, uint32_t node);
+int  kb_sim_inject(kb_sim* sim, const kb_unicast* msg, const uint32_t* ids);
+int  kb_sim_exported(kb_sim* sim, kb_unicast* out, size_t cap, size_t* n, uint32_t* ids, size_t cap_ids, size_t* n_ids);
+
 /* ---- sharding across GPUs --------------------------------------------------------
  * A mesh of C ids can be split into `world` (1..8) contiguous row shards: shard k holds the observer
  * state of ids [k*S, min(C, (k+1)*S)), S = ceil(C/world).  The reference's UDP transport between
@@ -250,6 +278,10 @@ int  kb_sim_broadcasts(kb_sim* sim, kb_broadcast* out, size_t cap, size_t* n);
  *   step), exchanged by device copies — the whole ABI then behaves as for an unsharded mesh.       */
 #define KB_UNIQUE_ID_BYTES 128
 int  kb_rccl_unique_id(uint8_t* out, size_t cap);
+/* A unique id for ranks in separate processes that share ONE device (RCCL refuses two ranks on one GPU): given to
+   kb_sim_create_rank it selects a test transport over IPC-mapped device windows and a shared-memory rendezvous
+   (DESIGN.md §6), with the same collective discipline as RCCL.  Window: env KB_IPC_WINDOW_MB (default 256). */
+int  kb_ipc_unique_id(uint8_t* out, size_t cap);
 int  kb_sim_create_rank(const kb_config* cfg, int32_t rank, int32_t world, const uint8_t* unique_id,
                         kb_sim** out);
 int  kb_sim_create_local(const kb_config* cfg, int32_t shards, kb_sim** out);

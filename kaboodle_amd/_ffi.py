@@ -55,7 +55,7 @@ class KbStats(C.Structure):
         ("removed_timeout", C.c_uint64), ("removed_failed", C.c_uint64), ("join_responses", C.c_uint64),
         ("curious_overflow", C.c_uint64), ("churn_leaves", C.c_uint64), ("churn_joins", C.c_uint64),
         ("sent_kp_ids", C.c_uint64), ("alive_rounds", C.c_uint64), ("probe_responses", C.c_uint64),
-        ("reserved", C.c_uint64 * 5),
+        ("exported", C.c_uint64), ("reserved", C.c_uint64 * 4),
     ]
 
     def as_dict(self) -> dict:
@@ -74,6 +74,12 @@ class KbWireAddrC(C.Structure):
 class KbProbeResponse(C.Structure):
     _fields_ = [("responder", C.c_uint32), ("probe", C.c_uint32), ("round", C.c_int32), ("prober", KbWireAddrC),
                 ("identity_len", C.c_uint32), ("identity", C.c_uint8 * 32)]
+
+
+class KbUnicast(C.Structure):
+    _fields_ = [("round", C.c_int32), ("wave", C.c_uint32), ("sender", C.c_uint32), ("dest", C.c_uint32),
+                ("seq", C.c_uint32), ("kind", C.c_uint32), ("a", C.c_uint32), ("fp", C.c_uint32), ("n", C.c_uint32),
+                ("pay_off", C.c_uint32), ("pay_len", C.c_uint32), ("pad", C.c_uint32)]
 
 
 class KbBroadcast(C.Structure):
@@ -166,6 +172,10 @@ _SIGS = {
     "sim_probe": (C.c_int, [C.c_void_p, C.POINTER(KbWireAddrC)]),
     "sim_probe_responses": (C.c_int, [C.c_void_p, C.POINTER(KbProbeResponse), C.c_size_t, C.POINTER(C.c_size_t)]),
     "sim_broadcasts": (C.c_int, [C.c_void_p, C.POINTER(KbBroadcast), C.c_size_t, C.POINTER(C.c_size_t)]),
+    "sim_set_external": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "sim_inject": (C.c_int, [C.c_void_p, C.POINTER(KbUnicast), C.POINTER(C.c_uint32)]),
+    "sim_exported": (C.c_int, [C.c_void_p, C.POINTER(KbUnicast), C.c_size_t, C.POINTER(C.c_size_t),
+                               C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t)]),
     "format_addr": (C.c_int, [C.c_uint32, C.c_char_p, C.c_size_t]),
     "last_error": (C.c_char_p, []),
 }
@@ -173,6 +183,7 @@ _OPTIONAL = {
     "sim_restart_node": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     # sharding (HIP library only; the oracle is the unsharded mesh every shard layout must reproduce)
     "rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8), C.c_size_t]),
+    "ipc_unique_id": (C.c_int, [C.POINTER(C.c_uint8), C.c_size_t]),
     "sim_create_rank": (C.c_int, [C.POINTER(KbConfig), C.c_int32, C.c_int32, C.POINTER(C.c_uint8),
                                   C.POINTER(C.c_void_p)]),
     "sim_create_local": (C.c_int, [C.POINTER(KbConfig), C.c_int32, C.POINTER(C.c_void_p)]),
@@ -222,6 +233,13 @@ def rccl_unique_id(lib: SimLib) -> bytes:
     """A fresh RCCL unique id (rank 0 makes it; the host broadcasts it to the other ranks)."""
     buf = (C.c_uint8 * KB_UNIQUE_ID_BYTES)()
     lib.call("rccl_unique_id", buf, KB_UNIQUE_ID_BYTES)
+    return bytes(buf)
+
+
+def ipc_unique_id(lib: SimLib) -> bytes:
+    """A unique id for ranks in separate processes sharing one device (the IPC test transport)."""
+    buf = (C.c_uint8 * KB_UNIQUE_ID_BYTES)()
+    lib.call("ipc_unique_id", buf, KB_UNIQUE_ID_BYTES)
     return bytes(buf)
 
 
@@ -378,6 +396,29 @@ class Sim:
         arr = (KbBroadcast * max(n.value, 1))()
         self.lib.call("sim_broadcasts", self.h, arr, n.value, C.byref(n))
         return [("Join" if a.kind == 16 else "Failed", a.sender, a.peer) for a in arr[: n.value]]
+
+    # -- external peers: real instances attached through a bridge --
+    def set_external(self, node: int) -> None:
+        """Mark a never-bound address as an external peer (kb_sim_set_external)."""
+        self.lib.call("sim_set_external", self.h, node)
+
+    def inject(self, sender: int, dest: int, kind: int, a: int = 0, fp: int = 0, n: int = 0, ids=()) -> None:
+        """Queue a record from external peer `sender` to `dest` for the next round's wave 0 (kb_sim_inject);
+        kind = wire kind 0..4 (Ping, PingRequest, Ack, KnownPeers, KnownPeersRequest), or 16: the external peer's
+        Join broadcast, delivered in the next round's broadcast phase (dest unused)."""
+        m = KbUnicast(sender=sender, dest=dest, kind=kind, a=a, fp=fp, n=n, pay_len=len(ids))
+        arr = (C.c_uint32 * max(1, len(ids)))(*ids)
+        self.lib.call("sim_inject", self.h, C.byref(m), arr)
+
+    def exported(self):
+        """Drain the records routed to external peers: [(round, wave, sender, dest, seq, kind, a, fp, n, ids)]."""
+        n, ni = C.c_size_t(), C.c_size_t()
+        self.lib.call("sim_exported", self.h, None, 0, C.byref(n), None, 0, C.byref(ni))
+        arr = (KbUnicast * max(n.value, 1))()
+        ids = (C.c_uint32 * max(ni.value, 1))()
+        self.lib.call("sim_exported", self.h, arr, n.value, C.byref(n), ids, ni.value, C.byref(ni))
+        return [(u.round, u.wave, u.sender, u.dest, u.seq, u.kind, u.a, u.fp, u.n, list(ids[u.pay_off:u.pay_off + u.pay_len]))
+                for u in arr[: n.value]]
 
     def stats(self) -> dict:
         st = KbStats()

@@ -58,8 +58,7 @@ class Bridge:
             if broadcast_port is None:
                 broadcast_port = DEFAULT_BROADCAST_PORT
             self.bin, self.bout, self.baddr = create_broadcast_sockets(interface, broadcast_port)
-            fam = socket.AF_INET6 if interface.is_ipv6 else socket.AF_INET
-            self.usock = socket.socket(fam, socket.SOCK_DGRAM)
+            self.usock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)   # IPv4 only (refused above otherwise)
             self.usock.bind((interface.ip, 0))
         self.stats = {"probes_in": 0, "external_join": 0, "external_failed": 0, "undecodable": 0,
                       "probe_responses_out": 0, "broadcasts_out": 0}

@@ -25,6 +25,7 @@ enum StatIdx {
   S_RESPB,                        // bytes k_resp_wave moved (bench; not a kb_stats field)
   S_PROCB,                        // bytes k_proc moved (bench; not a kb_stats field)
   S_PROBERESP,                    // ProbeResponses sent (kb_stats.probe_responses)
+  S_EXPORT,                       // records routed to external peers (kb_stats.exported)
   NSTAT
 };
 enum CtrIdx {
@@ -38,6 +39,7 @@ enum CtrIdx {
   C_PATHS,                        // OR of the PATH_* bits of the kernel variants that did work (test surface)
   C_DBG_SLOW_LONG, C_DBG_SLOW_NONMEM, C_DBG_SLOW_DIRTY, C_DBG_SLOW_KPR, C_DBG_SLOW_OTHER,   // KB_DEV & 256: why k_proc
   C_RESTN,                        // responders k_resp_wave left to k_resp_node (their list: the wave lists' slow buffer)
+  C_XREC, C_XPAY,                 // exported records / KnownPeers ids this round (external peers)
   NCTR
 };
 // kernel-variant coverage bits (kb_sim_debug_paths): the wide-row paths a >= 1M-id mesh takes
@@ -104,10 +106,30 @@ struct Dev {
   uint16_t* lat;                  // [W][local rows] PeerInfo.latency in ms, PEER-major (LAT_NONE = None); null
                                   // unless track_latency
   int32_t wave;                   // delivery wave of the launch (latency clock)
+  uint8_t* ext;                   // [C] external peers: records to them are exported
+  struct XRec* xrec;              // exported records of the round (layout of kb_unicast), xrec_cap of them
+  uint32_t* xids;                 // their KnownPeers ids, xids_cap of them
+  uint32_t xrec_cap, xids_cap;
   int32_t* tst;                   // KB_VARIANT_EXACT_LRU: [local rows][W] the instant of every Known entry whose
                                   // stamp byte has saturated to ANCIENT (a fresher byte encodes its instant
                                   // itself); null otherwise
+  int32_t* tlb;                   // with tst: [local rows][W / 1024] a lower bound of the saturated instants of
+                                  // each 1024-id block (exact after k_a3_exact scans the block; INT32_MAX = none)
 };
+
+// a record routed to an external peer, as kb_unicast (include/kaboodle_sim.h)
+struct XRec { int32_t round; uint32_t wave, sender, dest, seq, kind, a, fp, n, pay_off, pay_len, pad; };
+constexpr uint32_t DERR_EXPORT = 11;
+// export one routed record (and its KnownPeers ids, read from `pay`) for the host to drain after the round
+__device__ inline void export_rec(uint32_t* ctr, XRec* xrec, uint32_t xrec_cap, uint32_t* xids, uint32_t xids_cap,
+                                  const Msg& m, const uint32_t* pay, int32_t r, uint32_t w) {
+  const uint32_t k = atomicAdd(&ctr[C_XREC], 1u);
+  const uint32_t np = m.kind == K_KP ? m.a : 0u;
+  const uint32_t po = np ? atomicAdd(&ctr[C_XPAY], np) : 0u;
+  if (k >= xrec_cap || po + np > xids_cap) { atomicCAS(&ctr[C_ERR], 0u, DERR_EXPORT); return; }
+  for (uint32_t q = 0; q < np; ++q) xids[po + q] = pay[m.off + q];
+  xrec[k] = XRec{r, w, m.sender, m.dest, m.seq, m.kind, m.kind == K_KP ? 0u : m.a, m.fp, m.n, po, np, 0u};
+}
 
 // freshness log (the KnownPeersRequest reply set, :503-508, without scanning the row): an entry is
 // appended exactly when a stamp byte changes to Known(now); a (peer, t) entry is live iff the peer

@@ -27,6 +27,7 @@ __global__ void k_rebase(Dev d, int32_t r) {
           if (d.tst && b <= ST_ANCIENT + EPOCH) {
             const size_t i = d.lo + k / wpr, j = (k % wpr) * 16 + q * 4 + t;
             d.tst[i * d.W + j] = (int32_t)b - EOFF + E;
+            atomicMin(d.tlb + i * (d.W >> 10) + (j >> 10), (int32_t)b - EOFF + E);   // the block's bound covers it
           }
           b = b > ST_ANCIENT + EPOCH ? b - EPOCH : ST_ANCIENT; any = true;   // unsigned: no b - EPOCH < 0
         }
@@ -41,40 +42,104 @@ __global__ void k_rebase(Dev d, int32_t r) {
 // KB_VARIANT_EXACT_LRU: ping_random_peer's oldest five by the exact instant of the last contact
 // (src/kaboodle.rs:662-675 sorts by Instant), ties broken by the rotated address from the sweep front, over the
 // whole row; written as the row pass's keys (rank << 24 | rotated id) for k_tick_post.  A wave per row, 16 ids per
-// lane per step: stamp bytes, member bits, and the saturated entries' instants.
+// lane per 1024-id block: stamp bytes, member bits, and the saturated entries' instants.
+//   A saturated instant is older than every instant a byte still encodes (it was written an epoch earlier), so the
+// five oldest are the saturated ones whenever a row holds five.  Those are found block by block in the order of a
+// lower bound, tlb (instant) with the block's smallest rotated id: a block is scanned only while its bound is below
+// the fifth key found so far, and the scan makes its tlb exact.  k_rebase lowers tlb for every entry it saturates;
+// a refresh leaves it low (still a bound).  Only a row with fewer than five saturated candidates reads its live bytes.
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) { const unsigned long long t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
   return v;
 }
+__device__ inline unsigned long long wave_fifth(const unsigned long long top[5]) {   // the wave's 5th smallest key
+  unsigned long long t0 = top[0], t1 = top[1], t2 = top[2], t3 = top[3], t4 = top[4], m = ~0ull;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    m = wave_min_u64(t0);
+    if (m != ~0ull && t0 == m) { t0 = t1; t1 = t2; t2 = t3; t3 = t4; t4 = ~0ull; }
+  }
+  return m;
+}
+template <bool SAT, bool LIVE>
+__device__ inline int32_t a3x_block(const Dev& d, uint32_t i, uint32_t b, uint32_t cur, int32_t E, const uint8_t* srow,
+                                    const uint32_t* brow, const int32_t* trow, unsigned long long top[5]) {
+  const uint32_t C = d.C, j0 = (b << 10) + 16 * lane();
+  const uint32_t bw = (brow[j0 >> 5] >> (j0 & 31)) & 0xFFFFu;
+  int32_t smin = INT32_MAX;                                          // the block's saturated minimum (SAT)
+  if (!bw) return smin;
+  const uint4 sv = *reinterpret_cast<const uint4*>(srow + j0);
+  const uint32_t s4[4] = {sv.x, sv.y, sv.z, sv.w};
+  for (uint32_t t = 0; t < 16; ++t) {
+    if (!((bw >> t) & 1u)) continue;
+    const uint32_t j = j0 + t;
+    if (j >= C || j == i) continue;
+    const uint32_t sb = (s4[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+    if (sb < ST_ANCIENT) continue;                                   // WaitingFor*: not a candidate
+    int32_t inst;
+    if (sb == ST_ANCIENT) {
+      if (!SAT) continue;
+      inst = trow[j];
+      smin = inst < smin ? inst : smin;
+    } else {
+      if (!LIVE) continue;
+      inst = (int32_t)sb - EOFF + E;
+    }
+    const uint32_t rot = j > cur ? j - cur - 1 : j + C - cur - 1;
+    unsigned long long key = ((unsigned long long)((uint32_t)inst ^ 0x80000000u) << 32) | rot;
+    if (key >= top[4]) continue;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) { if (key < top[q]) { const unsigned long long x = top[q]; top[q] = key; key = x; } }
+  }
+  return smin;
+}
+constexpr uint32_t A3X_KPL = 8;                                     // bounds per lane: rows up to 512K ids
 __global__ __launch_bounds__(256) void k_a3_exact(Dev d, uint32_t* part, int32_t r) {
   const uint32_t i = d.lo + blockIdx.x * 4 + (threadIdx.x >> 6), l = lane();
   if (i >= d.hi || !d.alive[i]) return;
-  const uint32_t C = d.C, cur = d.a3cur[i];
+  const uint32_t C = d.C, cur = d.a3cur[i], NB = d.W >> 10;
   const int32_t E = epoch_base(r);
   unsigned long long top[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
   const uint8_t* srow = row_of(d, i);
   const uint32_t* brow = bits_of(d, i);
   const int32_t* trow = d.tst + (size_t)i * d.W;
-  for (uint32_t base = 0; base < d.W; base += 1024) {
-    const uint32_t j0 = base + 16 * l;
-    const uint32_t bw = (brow[j0 >> 5] >> (j0 & 31)) & 0xFFFFu;
-    if (!bw) continue;
-    const uint4 sv = *reinterpret_cast<const uint4*>(srow + j0);
-    const uint32_t s4[4] = {sv.x, sv.y, sv.z, sv.w};
-    for (uint32_t t = 0; t < 16; ++t) {
-      if (!((bw >> t) & 1u)) continue;
-      const uint32_t j = j0 + t;
-      if (j >= C || j == i) continue;
-      const uint32_t b = (s4[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-      if (b < ST_ANCIENT) continue;                                 // WaitingFor*: not a candidate
-      const int32_t inst = b > ST_ANCIENT ? (int32_t)b - EOFF + E : trow[j];
-      const uint32_t rot = j > cur ? j - cur - 1 : j + C - cur - 1;
-      unsigned long long key = ((unsigned long long)((uint32_t)inst ^ 0x80000000u) << 32) | rot;
-      if (key >= top[4]) continue;
+  if (NB > 64 * A3X_KPL) {                                           // wider rows: one pass over everything
+    for (uint32_t b = 0; b < NB; ++b) a3x_block<true, true>(d, i, b, cur, E, srow, brow, trow, top);
+  } else {
+    int32_t* lbrow = d.tlb + (size_t)i * NB;
+    const uint32_t p = cur + 1 == C ? 0 : cur + 1;                   // the sweep front: rotated id 0
+    int32_t lbk[A3X_KPL];
+    unsigned long long rkey[A3X_KPL];                                // the block's smallest rotated id
 #pragma unroll
-      for (int q = 0; q < 5; ++q) { if (key < top[q]) { const unsigned long long x = top[q]; top[q] = key; key = x; } }
+    for (uint32_t k = 0; k < A3X_KPL; ++k) {
+      const uint32_t b = l + 64 * k, lo = b << 10, hi = lo + 1023 < C - 1 ? lo + 1023 : C - 1;
+      lbk[k] = (b < NB && lo < C) ? lbrow[b] : INT32_MAX;            // INT32_MAX: nothing saturated (or no ids)
+      rkey[k] = (p >= lo && p <= hi) ? 0 : (lo > p ? lo - p : lo + C - p);
     }
+    for (;;) {
+      unsigned long long lm = ~0ull;
+      uint32_t bm = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < A3X_KPL; ++k) {
+        if (lbk[k] == INT32_MAX) continue;
+        const unsigned long long key = ((unsigned long long)((uint32_t)lbk[k] ^ 0x80000000u) << 32) | rkey[k];
+        if (key < lm) { lm = key; bm = l + 64 * k; }
+      }
+      const unsigned long long m = wave_min_u64(lm);                // keys are distinct: rotated ids differ
+      if (m == ~0ull || m >= wave_fifth(top)) break;
+      const uint32_t b = __shfl(bm, (int)__builtin_ctzll(__ballot(lm == m)), 64);
+      int32_t smin = a3x_block<true, false>(d, i, b, cur, E, srow, brow, trow, top);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) { const int32_t t = __shfl_xor(smin, o, 64); smin = t < smin ? t : smin; }
+      if (l == 0) lbrow[b] = smin;                                   // exact now
+      if (l == (b & 63)) {
+#pragma unroll
+        for (uint32_t k = 0; k < A3X_KPL; ++k) if (k == (b >> 6)) lbk[k] = INT32_MAX;   // scanned
+      }
+    }
+    if (wave_fifth(top) == ~0ull)                                    // fewer than five saturated: the live bytes
+      for (uint32_t b = 0; b < NB; ++b) a3x_block<false, true>(d, i, b, cur, E, srow, brow, trow, top);
   }
   uint32_t out[5];
 #pragma unroll
@@ -156,8 +221,10 @@ __global__ __launch_bounds__(256) void k_row_unpack(Dev d, uint32_t i, const uin
       const uint32_t v = in[L.lat + k];
       *lat_at(d, i, 2 * k) = (uint16_t)v; *lat_at(d, i, 2 * k + 1) = (uint16_t)(v >> 16);
     }
-  if (d.tst)
+  if (d.tst) {
     for (uint32_t k = t; k < d.W; k += T) d.tst[(size_t)i * d.W + k] = (int32_t)in[L.tst + k];
+    for (uint32_t k = t; k < d.W >> 10; k += T) d.tlb[(size_t)i * (d.W >> 10) + k] = INT32_MIN;   // rescan the moved row
+  }
 }
 __global__ void k_churn_leave(Dev d, int32_t r) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;

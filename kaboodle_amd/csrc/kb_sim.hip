@@ -244,6 +244,26 @@ template <class T> static hipError_t dalloc(T** p, size_t n) {
   return e;
 }
 
+// the Join broadcasts of external peers (kb_sim_inject) merged into the round's Join list in sender
+// order, as the tick's Joins would be (one per sender, bseq 0; pad = the sender's partition group when the list
+// carries it, pgroups > 1)
+static int merge_ext_joins(hipStream_t st, BCast* list, uint32_t* n, std::vector<uint32_t>& joins, uint32_t pgroups, uint32_t C) {
+  if (joins.empty()) return KB_OK;
+  std::vector<BCast> v(*n);
+  if (*n) HIPCHK(hipMemcpyAsync(v.data(), list, sizeof(BCast) * *n, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  for (const uint32_t x : joins) {
+    const uint32_t g = pgroups > 1 ? (uint32_t)((uint64_t)x * pgroups / C) : 0u;
+    const auto at = std::upper_bound(v.begin(), v.end(), x, [](uint32_t a, const BCast& b) { return a < b.sender; });
+    v.insert(at, BCast{x, x, 0, g});
+  }
+  HIPCHK(hipMemcpyAsync(list, v.data(), sizeof(BCast) * v.size(), hipMemcpyHostToDevice, st));
+  HIPCHK(hipStreamSynchronize(st));
+  *n = (uint32_t)v.size();
+  joins.clear();
+  return KB_OK;
+}
+
 static uint32_t h_crc_table[256];
 static void h_crc_init() {
   for (uint32_t i = 0; i < 256; ++i) { uint32_t c = i; for (int k = 0; k < 8; ++k) c = (c & 1) ? (c >> 1) ^ CRC_POLY : c >> 1; h_crc_table[i] = c; }
@@ -334,6 +354,13 @@ struct kb_sim {
                                                                  // its next address takes it (-1: none)
   std::vector<uint8_t> h_moved;                                  // the instance bound here restarted elsewhere
   std::vector<uint8_t> h_idset;                                  // identity set on a never-bound address (d.idset)
+  std::vector<uint8_t> h_ext;                                    // external peers (d.ext)
+  // external peers: records injected for the next round's wave 0, records exported not drained
+  size_t n_ext = 0;
+  std::vector<XRec> inj; std::vector<uint32_t> inj_ids;
+  std::vector<uint32_t> inj_join;                    // external peers' Join broadcasts for the next round
+  XRec* d_inj = nullptr; uint32_t* d_inj_ids = nullptr; size_t d_inj_cap = 0, d_inj_ids_cap = 0;
+  std::vector<kb_unicast> xq; std::vector<uint32_t> xq_ids;
   std::vector<Event> events;
   uint32_t* rpack = nullptr; uint32_t* rpack_in = nullptr;       // a restart's packed row (send / receive)
   // discovery: Probes queued for the next round, those delivered this round, responses not yet drained
@@ -545,7 +572,7 @@ static void free_all(kb_sim* s) {
   for (void* p : s->allocs) (void)hipFree(p);
   s->allocs.clear();
   void* dyn[] = {s->newmask_base, s->respmask_base, s->resp_scratch, s->d_events, s->rmsg, s->rpay, s->rstatus,
-                 s->rinbox, s->rkp, s->d_presp, s->d_presp_n, s->rpack, s->rpack_in};
+                 s->rinbox, s->rkp, s->d_presp, s->d_presp_n, s->rpack, s->rpack_in, s->d_inj, s->d_inj_ids};
   for (void* p : dyn) if (p) (void)hipFree(p);
 }
 static void destroy_shard(kb_sim* s) {
@@ -631,13 +658,13 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
 #define A(ptr, n) if (e == hipSuccess) e = talloc(s, &(ptr), (n))     // per-id / global tables
 #define AR(ptr, n) if (e == hipSuccess) e = ralloc(s, &(ptr), (n))   // row tables: n entries per local row
   AR(d.stamp, W); AR(d.bits, d.NWR); AR(d.segp, NSEG); AR(d.sdirty, 1);
-  AR(d.dirty, 1); A(d.alive, C); A(d.idset, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
+  AR(d.dirty, 1); A(d.alive, C); A(d.idset, C); A(d.ext, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
   AR(d.last_bcast, 1); AR(d.a3cur, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
   AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
   A(d.ztab, 17 * 128); A(d.zbtab, ZB);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.sacc, (size_t)NACC * NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
-  if (cfg->variant == KB_VARIANT_EXACT_LRU) AR(d.tst, W);   // exact A3 instants
+  if (cfg->variant == KB_VARIANT_EXACT_LRU) { AR(d.tst, W); AR(d.tlb, W / 1024); }   // exact A3 instants
   if (cfg->track_latency) { A(d.lat, (size_t)W * lat_stride(R)); A(s->lat_col, C); A(s->fnamed, d.NWR); }   // peer-major
   s->msg_cap = std::max<uint32_t>(8u * R + (uint32_t)TICK_MAX * R, 1u << 16);
   s->pay_cap = std::max<uint32_t>((d.capk + 1) * R, 1u << 24);
@@ -672,7 +699,10 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); destroy_shard(s); return KB_CAPACITY; }
   (void)hipMemset(L(s, d.kpr_big), 0xFF, 4ull * R);          // no round yet
   if (d.lat) { (void)hipMemset(d.lat, 0xFF, 2ull * lat_stride(R) * W); (void)hipMemset(s->fnamed, 0, 4ull * d.NWR); }   // all None
-  if (d.tst) (void)hipMemsetD32(d.tst + (size_t)s->lo * W, INT32_MIN / 2, (size_t)R * W);   // a converged start: ancient, all tied
+  if (d.tst) {
+    (void)hipMemsetD32(d.tst + (size_t)s->lo * W, INT32_MIN / 2, (size_t)R * W);   // a converged start: ancient, all tied
+    (void)hipMemsetD32(d.tlb + (size_t)s->lo * (W / 1024), INT32_MIN, (size_t)R * (W / 1024));   // bounds: scan every block once
+  }
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
   if (hipHostMalloc((void**)&s->h_pin, 4 * PIN_WORDS, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
@@ -722,11 +752,32 @@ extern "C" int kb_rccl_unique_id(uint8_t* out, size_t cap) {
   return KB_OK;
 }
 
+// a unique id for ranks that share ONE device (the IpcXfer test transport, kb_xfer.h): the magic prefix, then the
+// name of the shared-memory segment rank 0 creates
+extern "C" int kb_ipc_unique_id(uint8_t* out, size_t cap) {
+  if (!out || cap < KB_UNIQUE_ID_BYTES) { seterr("unique id buffer too small"); return KB_INVALID_ARGUMENT; }
+  memset(out, 0, KB_UNIQUE_ID_BYTES);
+  memcpy(out, IPC_MAGIC, sizeof IPC_MAGIC);
+  uint64_t rnd = 0;
+  FILE* f = fopen("/dev/urandom", "rb");
+  if (f) { if (fread(&rnd, sizeof rnd, 1, f) != 1) rnd = 0; fclose(f); }
+  snprintf(reinterpret_cast<char*>(out) + sizeof IPC_MAGIC, KB_UNIQUE_ID_BYTES - sizeof IPC_MAGIC, "/kbipc-%d-%016llx",
+           (int)getpid(), (unsigned long long)rnd);
+  return KB_OK;
+}
+
 extern "C" int kb_sim_create_rank(const kb_config* cfg, int32_t rank, int32_t world, const uint8_t* unique_id, kb_sim** out) {
   if (!cfg || !unique_id || !out || world < 1 || world > (int)XMAX || rank < 0 || rank >= world) {
     seterr("bad rank/world"); return KB_INVALID_ARGUMENT;
   }
   if (hipSetDevice(cfg->device >= 0 ? cfg->device : 0) != hipSuccess) { seterr("hipSetDevice failed"); return KB_NO_DEVICE; }
+  if (memcmp(unique_id, IPC_MAGIC, sizeof IPC_MAGIC) == 0) {          // ranks sharing one device (test transport)
+    const char* wm = getenv("KB_IPC_WINDOW_MB");
+    const size_t mb = wm ? (size_t)atoll(wm) : 256;
+    IpcXfer* x = new IpcXfer();
+    if (!x->init(rank, world, unique_id, mb << 20)) { seterr(x->error()); delete x; return KB_IO_ERROR; }
+    return create_shard(cfg, rank, world, x, out);
+  }
   RcclXfer* x = new RcclXfer();
   if (!x->init(rank, world, unique_id)) { seterr(x->error()); delete x; return KB_IO_ERROR; }
   return create_shard(cfg, rank, world, x, out);
@@ -798,8 +849,9 @@ static int err_status(uint32_t e) {
   if (e) {
     const char* what[] = {"", "suspect slots exhausted", "outbox region overflow", "payload pool overflow",
                           "truncated Join response too large", "inbox overflow", "Join response member count mismatch",
-                          "freshness log", "fingerprint count mismatch", "wave-0 outbox exceeds preallocated capacity"};
-    seterr(std::string("device capacity error: ") + (e < 10 ? what[e] : "?"));
+                          "freshness log", "fingerprint count mismatch", "wave-0 outbox exceeds preallocated capacity",
+                          "?", "export buffer overflow"};
+    seterr(std::string("device capacity error: ") + (e < 12 ? what[e] : "?"));
     return KB_CAPACITY;
   }
   return KB_OK;
@@ -1160,7 +1212,8 @@ static int step_round(kb_sim* s) {
   klaunch(s, KI_TRUEFP_PART, k_truefp_part, dim3(TRUEFP_G), dim3(256), 0, d, d.tfpart);
   klaunch(s, KI_TRUEFP_FIN, k_truefp_fin, dim3(1), dim3(64), 0, d, d.tfpart);
   klaunch(s, KI_LOG_MARK, k_log_mark, dim3(gnode), dim3(tb), 0, d, r);
-  // 2. broadcasts of round r-1
+  // 2. broadcasts of round r-1 (with the external peers' Joins)
+  if (!s->inj_join.empty()) { const int rc = merge_ext_joins(st, s->bjoin, &s->nj, s->inj_join, 0, C); if (rc) return rc; }
   OutBuf& o0 = s->ob[0];
   PhaseB pb;
   pb.bfail = s->bfail; pb.nf = s->nf; pb.bjoin = s->bjoin; pb.nj = s->nj; pb.JW = (s->nj + 63) / 64;
@@ -1264,6 +1317,27 @@ static int step_round(kb_sim* s) {
     HIPCHK(hipMemsetAsync(s->d_presp_n, 0, 4, st));
     klaunch(s, KI_PROBE, k_probe, dim3(gnode), dim3(tb), 0, d, np, r, s->d_presp, s->d_presp_n, (uint32_t)s->presp_cap);
   }
+  // records from external peers (kb_sim_inject): room for their KnownPeers ids in their wave-0 payload regions
+  const uint32_t ninj = (uint32_t)s->inj.size();
+  bool inj_pay = false;
+  if (ninj) {
+    if (ninj > s->d_inj_cap) {
+      if (s->d_inj) (void)hipFree(s->d_inj);
+      s->d_inj_cap = 2 * ninj;
+      HIPCHK(hipMalloc(&s->d_inj, sizeof(XRec) * s->d_inj_cap));
+    }
+    if (s->inj_ids.size() > s->d_inj_ids_cap || !s->d_inj_ids) {
+      if (s->d_inj_ids) (void)hipFree(s->d_inj_ids);
+      s->d_inj_ids_cap = 2 * s->inj_ids.size() + 16;
+      HIPCHK(hipMalloc(&s->d_inj_ids, 4 * s->d_inj_ids_cap));
+    }
+    HIPCHK(hipMemcpyAsync(s->d_inj, s->inj.data(), sizeof(XRec) * ninj, hipMemcpyHostToDevice, st));
+    if (!s->inj_ids.empty()) {
+      HIPCHK(hipMemcpyAsync(s->d_inj_ids, s->inj_ids.data(), 4 * s->inj_ids.size(), hipMemcpyHostToDevice, st));
+      inj_pay = true;
+    }
+    klaunch(s, KI_EVENTS, k_inject_prep, dim3(1), dim3(64), 0, d, (const XRec*)s->d_inj, ninj, s->paysum);
+  }
   {  // wave-0 outbox regions: responses first, then the tick's messages
     ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 3;
@@ -1273,7 +1347,7 @@ static int step_round(kb_sim* s) {
     a.list = s->resp_nodes; a.list_base = s->lo;
     launch_scan(s, a);
   }
-  const bool need_tot = have_b && s->nj;
+  const bool need_tot = (have_b && s->nj) || inj_pay;
   klaunch(s, KI_SET_CAP, k_set_cap, dim3(gnode), dim3(tb), 0, d, s->nresp, o0.cap, o0.cnt, s->scan_tot, s->d_pin, need_tot ? ++s->pin_seq : 0u);
   if (need_tot) {
     const uint32_t* tot = s->h_pin;                 // written by k_set_cap through the host mapping
@@ -1339,6 +1413,10 @@ static int step_round(kb_sim* s) {
   if (d.uniform) klaunch(s, KI_FP_ROWS, k_fp_rows, dim3((FP_LANES * R + tb - 1) / tb), dim3(tb), 0, d);
   if (d.tst) klaunch(s, KI_A3_EXACT, k_a3_exact, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);   // exact A3 order
   klaunch(s, KI_TICK_POST, k_tick_post, dim3(gnode), dim3(tb), 0, d, s->ro, o0, r);
+  if (ninj) {                                          // the external peers' wave-0 emissions, after the tick's
+    klaunch(s, KI_EVENTS, k_inject, dim3(1), dim3(64), 0, d, o0, (const XRec*)s->d_inj, ninj, (const uint32_t*)s->d_inj_ids);
+    s->inj.clear(); s->inj_ids.clear();
+  }
   {
     ScanArgs a = scan_args(s, R, s->scan_tot);
     a.narr = 2;
@@ -1393,6 +1471,26 @@ static int step_round(kb_sim* s) {
     s->nj = s->h_pin[0]; s->nf = s->h_pin[1]; err = s->h_pin[2];
   }
   s->bj_total += s->nj; s->bf_total += s->nf;
+  if (s->n_ext) {                                      // the round's records to external peers, to the host queue
+    uint32_t c[2];
+    HIPCHK(hipMemcpy(c, d.ctr + C_XREC, 8, hipMemcpyDeviceToHost));
+    const uint32_t nrec = std::min(c[0], d.xrec_cap), nid = std::min(c[1], d.xids_cap);
+    std::vector<XRec> v(nrec);
+    const size_t base = s->xq_ids.size();
+    s->xq_ids.resize(base + nid);
+    if (nrec) HIPCHK(hipMemcpy(v.data(), d.xrec, sizeof(XRec) * nrec, hipMemcpyDeviceToHost));
+    if (nid) HIPCHK(hipMemcpy(s->xq_ids.data() + base, d.xids, 4ull * nid, hipMemcpyDeviceToHost));
+    std::sort(v.begin(), v.end(), [](const XRec& a, const XRec& b) {
+      return a.wave != b.wave ? a.wave < b.wave : a.sender != b.sender ? a.sender < b.sender : a.seq < b.seq; });
+    for (const XRec& x : v) {
+      kb_unicast u;
+      memcpy(&u, &x, sizeof u);
+      u.pay_off = (uint32_t)(base + x.pay_off);
+      s->xq.push_back(u);
+    }
+    const uint32_t z[2] = {0, 0};
+    HIPCHK(hipMemcpy(d.ctr + C_XREC, z, 8, hipMemcpyHostToDevice));
+  }
   if (np) {                                          // the round's ProbeResponses, (responder, probe) order
     uint32_t k = 0;
     HIPCHK(hipMemcpy(&k, s->d_presp_n, 4, hipMemcpyDeviceToHost));
@@ -1669,6 +1767,90 @@ extern "C" int kb_sim_probe_responses(kb_sim* s, kb_probe_response* out, size_t 
   s->presp.clear();
   return KB_OK;
 }
+// ---- external peers ------------------------------------------------------------------------
+static_assert(sizeof(XRec) == sizeof(kb_unicast), "XRec mirrors kb_unicast");
+extern "C" int kb_sim_set_external(kb_sim* s, uint32_t node) {
+  if (s && s->sp) return chk(s, node) ? KB_INVALID_ARGUMENT : sp_set_external(s->sp, node);
+  if (chk(s, node)) return KB_INVALID_ARGUMENT;
+  kb_sim* h = is_group(s) ? s->shards[0] : s;
+  if (h->h_ext.empty()) h->h_ext.assign(s->C, 0);
+  if (h->h_ext[node]) return KB_OK;
+  int ever = 0;
+  { const int rc = ever_bound(h, node, &ever); if (rc) return rc; }
+  if (ever) { seterr("an external peer takes an address no instance has bound"); return KB_INVALID_OPERATION; }
+  auto one = [&](kb_sim* t) -> int {
+    (void)hipSetDevice(t->device);
+    if (t->h_ext.empty()) t->h_ext.assign(t->C, 0);
+    t->h_ext[node] = 1; t->n_ext++;
+    t->h_idset[node] = 1;                            // not a fresh id: churn joins and restarts skip it
+    const uint8_t o = 1;
+    HIPCHK(hipMemcpy(t->d.ext + node, &o, 1, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(t->d.idset + node, &o, 1, hipMemcpyHostToDevice));
+    if (!t->d.xrec) {
+      t->d.xrec_cap = 1u << 16; t->d.xids_cap = 1u << 22;
+      HIPCHK(talloc(t, &t->d.xrec, t->d.xrec_cap)); HIPCHK(talloc(t, &t->d.xids, t->d.xids_cap));
+      t->buf_gen++;                                  // a captured receive window holds the old Dev
+    }
+    return KB_OK;
+  };
+  if (is_group(s)) { for (kb_sim* t : s->shards) { const int rc = one(t); if (rc) return rc; } return KB_OK; }
+  return one(s);
+}
+extern "C" int kb_sim_inject(kb_sim* s, const kb_unicast* m, const uint32_t* ids) {
+  if (s && s->sp) return sp_inject(s->sp, m, ids);
+  if (!s || !m || m->sender >= s->C || m->dest >= s->C || (m->kind > K_KPR && m->kind != KB_WIRE_JOIN) || (m->pay_len && !ids))
+    return KB_INVALID_ARGUMENT;
+  kb_sim* h = is_group(s) ? s->shards[0] : s;
+  if (h->h_ext.empty() || !h->h_ext[m->sender]) { seterr("kb_sim_inject: the sender is not an external peer"); return KB_INVALID_OPERATION; }
+  if (m->kind == KB_WIRE_JOIN) {                       // a Join broadcast: the next round's Join list
+    if (std::find(h->inj_join.begin(), h->inj_join.end(), m->sender) != h->inj_join.end()) {
+      seterr("kb_sim_inject: one Join per external peer per round"); return KB_CAPACITY;
+    }
+    if (is_group(s)) { for (kb_sim* t : s->shards) t->inj_join.push_back(m->sender); }
+    else s->inj_join.push_back(m->sender);
+    return KB_OK;
+  }
+  if ((m->kind == K_PINGREQ || m->kind == K_ACK) && m->a >= s->C) return KB_INVALID_ARGUMENT;
+  for (uint32_t k = 0; k < m->pay_len; ++k) if (ids[k] >= s->C) return KB_INVALID_ARGUMENT;
+  uint32_t per = 0, rel = 0;
+  for (const XRec& x : h->inj) if (x.sender == m->sender) { per++; if (x.kind == K_KP) rel += x.pay_len; }
+  if (per >= (uint32_t)TICK_MAX) { seterr("kb_sim_inject: 33 records per external peer per round"); return KB_CAPACITY; }
+  auto one = [&](kb_sim* t) -> int {
+    XRec x{0, 0, m->sender, m->dest, 0, m->kind, m->kind == K_KP ? 0u : m->a, m->fp, m->n, (uint32_t)t->inj_ids.size(),
+           m->kind == K_KP ? m->pay_len : 0u, rel};
+    if (m->kind == K_KP) t->inj_ids.insert(t->inj_ids.end(), ids, ids + m->pay_len);
+    t->inj.push_back(x);
+    return KB_OK;
+  };
+  if (is_group(s)) { for (kb_sim* t : s->shards) one(t); return KB_OK; }
+  return one(s);
+}
+extern "C" int kb_sim_exported(kb_sim* s, kb_unicast* out, size_t cap, size_t* n, uint32_t* ids, size_t cap_ids, size_t* n_ids) {
+  if (s && s->sp) return (!n || !n_ids) ? KB_INVALID_ARGUMENT : sp_exported(s->sp, out, cap, n, ids, cap_ids, n_ids);
+  if (!s || !n || !n_ids) return KB_INVALID_ARGUMENT;
+  std::vector<kb_unicast> all;
+  std::vector<uint32_t> all_ids;
+  const std::vector<kb_sim*> hs = is_group(s) ? s->shards : std::vector<kb_sim*>{s};
+  for (kb_sim* t : hs)
+    for (const kb_unicast& u : t->xq) {
+      kb_unicast v = u;
+      v.pay_off = (uint32_t)all_ids.size();
+      all_ids.insert(all_ids.end(), t->xq_ids.begin() + u.pay_off, t->xq_ids.begin() + u.pay_off + u.pay_len);
+      std::sort(all_ids.begin() + v.pay_off, all_ids.end());   // a KnownPeers map has no order: ascending ids
+      all.push_back(v);
+    }
+  std::stable_sort(all.begin(), all.end(), [](const kb_unicast& a, const kb_unicast& b) {
+    return a.round != b.round ? a.round < b.round : a.wave != b.wave ? a.wave < b.wave : a.sender != b.sender ? a.sender < b.sender
+                                                                                       : a.seq < b.seq; });
+  *n = all.size(); *n_ids = all_ids.size();
+  if (!out && !ids) return KB_OK;
+  if (cap < all.size() || (!all_ids.empty() && (!ids || cap_ids < all_ids.size()))) { seterr("export buffer too small"); return KB_CAPACITY; }
+  if (!all.empty()) memcpy(out, all.data(), all.size() * sizeof(kb_unicast));
+  if (!all_ids.empty()) memcpy(ids, all_ids.data(), 4 * all_ids.size());
+  for (kb_sim* t : hs) { t->xq.clear(); t->xq_ids.clear(); }
+  return KB_OK;
+}
+
 // the last round's Join / Failed broadcasts (whole mesh; sender order, a node's Join before its Failed)
 extern "C" int kb_sim_broadcasts(kb_sim* s, kb_broadcast* out, size_t cap, size_t* n) {
   if (s && s->sp) return n ? sp_broadcasts(s->sp, out, cap, n) : KB_INVALID_ARGUMENT;
@@ -1930,6 +2112,7 @@ extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
   out->sent_kp_ids = st[S_KPIDS];
   out->alive_rounds = st[S_ALIVER];
   out->probe_responses = st[S_PROBERESP];
+  out->exported = st[S_EXPORT];
   return KB_OK;
 }
 // per id: alive, n, last_bcast, start_round; n and last_bcast only for the rows this handle holds

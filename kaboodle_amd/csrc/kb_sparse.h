@@ -57,6 +57,8 @@ struct SpDev {
   Susp* susp; Cur* cur; uint32_t* paq; uint32_t* paq_n;
   uint8_t* alive; int32_t* start_round;
   uint8_t* idset;                                 // [C] an identity was set on this never-bound address (not fresh)
+  uint8_t* ext;                                   // [C] external peers: records to them are exported
+  XRec* xrec; uint32_t* xids; uint32_t xrec_cap, xids_cap;
   uint32_t* cseg; uint32_t* segmul; uint32_t* seglen;
   uint32_t* bbits;                                // [C/32 + 1] base bitset
   uint32_t* bcnt;                                 // [C + 1] |base ∩ [0, k)|
@@ -828,6 +830,7 @@ __global__ void k_sp_bcast_write(SpDev d, SpTickOut bo, const uint32_t* joff, co
 // ---- receive window (src/kaboodle.rs:394-548) -----------------------------------------------------
 struct SpRoute {
   const Msg* msgs; uint32_t M; uint8_t* status;
+  const uint32_t* pay;                                // the records' KnownPeers ids (exports copy them)
   uint32_t* icnt; uint32_t* ebound; uint32_t* kprc;   // per destination: delivered, reply bound, KPRs
 };
 __device__ inline void sp_count_sent(const Msg& m, unsigned long long (&s)[6]) {
@@ -837,12 +840,15 @@ __device__ inline void sp_count_sent(const Msg& m, unsigned long long (&s)[6]) {
 // delivery of one record: dead receiver, partition, Philox loss keyed on (sender, round, wave, seq)
 __global__ __launch_bounds__(256) void k_sp_route(SpDev d, SpRoute rt, int32_t r, uint32_t w) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long s[6] = {0, 0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0;
+  unsigned long long s[6] = {0, 0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, xp = 0;
   if (k < rt.M) {
     const Msg m = rt.msgs[k];
     sp_count_sent(m, s);
     uint8_t st = 0;
-    if (!d.alive[m.dest]) dead++;
+    if (!d.alive[m.dest]) {
+      if (d.ext[m.dest]) { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, rt.pay, r, w); xp++; }
+      else dead++;
+    }
     else if (sp_part(d, r, m.sender, m.dest)) part++;
     else if (sp_faults(d, r) && d.loss_thr &&
              philox(m.sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m.seq, d.k0, d.k1).x < d.loss_thr) loss++;
@@ -855,9 +861,25 @@ __global__ __launch_bounds__(256) void k_sp_route(SpDev d, SpRoute rt, int32_t r
     }
     rt.status[k] = st;
   }
-  const int idx[9] = {S_PING, S_PINGREQ, S_ACK, S_KP, S_KPR, S_KPIDS, S_DEAD, S_PART, S_LOSS};
-  const unsigned long long v[9] = {s[0], s[1], s[2], s[3], s[4], s[5], dead, part, loss};
+  const int idx[10] = {S_PING, S_PINGREQ, S_ACK, S_KP, S_KPR, S_KPIDS, S_DEAD, S_PART, S_LOSS, S_EXPORT};
+  const unsigned long long v[10] = {s[0], s[1], s[2], s[3], s[4], s[5], dead, part, loss, xp};
   sp_stats(d, idx, v);
+}
+// records from external peers (kb_sim_inject): room in their wave-0 regions, then the records after the tick
+__global__ void k_sp_inject_prep(SpDev d, const XRec* inj, uint32_t n, uint32_t* ecap, uint32_t* pcap) {
+  if (threadIdx.x || blockIdx.x) return;
+  for (uint32_t k = 0; k < n; ++k) { ecap[inj[k].sender] += 1; if (inj[k].kind == K_KP) pcap[inj[k].sender] += inj[k].pay_len; }
+}
+__global__ void k_sp_inject(SpDev d, SpOut o, const XRec* inj, uint32_t n, const uint32_t* ids) {
+  if (threadIdx.x || blockIdx.x) return;
+  for (uint32_t k = 0; k < n; ++k) {
+    const XRec x = inj[k];
+    uint32_t seq = o.en[x.sender];
+    const uint32_t off = o.poff[x.sender] + x.pad;
+    if (x.kind == K_KP) for (uint32_t q = 0; q < x.pay_len; ++q) o.pay[off + q] = ids[x.pay_off + q];
+    sp_emit(d, o, x.sender, seq, x.dest, x.kind, x.kind == K_KP ? x.pay_len : x.a, x.fp, x.n, x.kind == K_KP ? off : 0u);
+    o.en[x.sender] = seq;
+  }
 }
 // records never routed (emitted in the last wave): counted as sent and as missing the receive window
 __global__ __launch_bounds__(256) void k_sp_window(SpDev d, const Msg* msgs, uint32_t M) {

@@ -63,15 +63,21 @@ struct SpSim {
   uint64_t k_n[SPK_N] = {};
   double round_ms = 0; uint64_t round_n = 0;
   uint64_t host_syncs = 0;
-  uint64_t moved_bytes0 = 0;
+  // external peers
+  std::vector<uint8_t> h_ext;
+  size_t n_ext = 0;
+  std::vector<XRec> inj; std::vector<uint32_t> inj_ids;
+  std::vector<uint32_t> inj_join;                    // external peers' Join broadcasts for the next round
+  XRec* d_inj = nullptr; uint32_t* d_inj_ids = nullptr; size_t d_inj_cap = 0, d_inj_ids_cap = 0;
+  std::vector<kb_unicast> xq; std::vector<uint32_t> xq_ids;
 };
 
 static int sp_err_status(uint32_t e) {
   if (!e) return KB_OK;
   const char* what[] = {"", "suspect slots exhausted", "outbox region overflow", "payload pool overflow", "?", "inbox overflow",
                         "Join response member count mismatch", "?", "indirect-ping candidate out of range", "?",
-                        "a row's entry list exceeded kb_config.sparse_row_cap"};
-  seterr(std::string("device capacity error: ") + (e <= 10 ? what[e] : "?"));
+                        "a row's entry list exceeded kb_config.sparse_row_cap", "export buffer overflow"};
+  seterr(std::string("device capacity error: ") + (e <= 11 ? what[e] : "?"));
   return KB_CAPACITY;
 }
 // zeroed device memory.  The zeroing is complete on return: hipMemset runs on the null stream, which does not
@@ -204,7 +210,7 @@ static int sp_create(const kb_config* cfg, SpSim** out) {
 #define SA(ptr, n) if (e == hipSuccess) e = sp_alloc(S, &(ptr), (n))
   SA(d.ent, (size_t)C * d.ECAP); SA(d.ne, C); SA(d.based, C); SA(d.n, C); SA(d.fp, C); SA(d.dirty, C);
   SA(d.last_bcast, C); SA(d.a3cur, C); SA(d.susp, (size_t)C * SLOTS); SA(d.cur, (size_t)C * CSLOTS);
-  SA(d.paq, (size_t)C * PAQ); SA(d.paq_n, C); SA(d.alive, C); SA(d.start_round, C); SA(d.idset, C);
+  SA(d.paq, (size_t)C * PAQ); SA(d.paq_n, C); SA(d.alive, C); SA(d.start_round, C); SA(d.idset, C); SA(d.ext, C);
   SA(d.cseg, C); SA(d.segmul, C); SA(d.seglen, C); SA(d.bbits, C / 32 + 1); SA(d.bcnt, (size_t)C + 1);
   SA(d.bpre, (size_t)C + 1); SA(d.zpow, (size_t)C + 2); SA(d.stats, NSTAT); SA(d.sacc, (size_t)SP_ACC * NSTAT);
   SA(d.ctr, NCTR); SA(d.tacc, 2 * SP_ACC);
@@ -310,7 +316,11 @@ static int sp_step_round(SpSim* S) {
     sp_launch(S, SPK_CHURN, k_sp_churn_leave, g, tb, d, r);
     sp_launch(S, SPK_CHURN, k_sp_churn_join, 1, 1, d, r);
   }
-  // 2. broadcasts of round r-1 (Failed, Join), and the Probes queued since the last round
+  // 2. broadcasts of round r-1 (Failed, Join with the external peers' Joins), and the Probes queued since the last round
+  if (!S->inj_join.empty()) {
+    const int rc = merge_ext_joins(S->st, S->bjoin, &S->nj, S->inj_join, S->cfg.partition_groups, C);
+    if (rc) return rc;
+  }
   S->probes.swap(S->probe_q);
   S->probe_q.clear();
   const uint32_t np = (uint32_t)S->probes.size();
@@ -349,8 +359,16 @@ static int sp_step_round(SpSim* S) {
     bc.fcounted = 1;
   }
   sp_launch(S, SPK_BCAST, k_sp_bcast, g, tb, d, bc, r);
-  // wave-0 regions: Join responses first, then the tick's emissions
+  // wave-0 regions: Join responses first, then the tick's emissions; the external peers' injected records
   sp_launch(S, SPK_BOUND0, k_sp_bound0, g, tb, d, (const uint32_t*)S->jr_n, S->ebound);
+  const uint32_t ninj = (uint32_t)S->inj.size();
+  if (ninj) {
+    { size_t c = S->d_inj_cap; const int rc = sp_grow(S, &S->d_inj, &c, ninj); if (rc) return rc; S->d_inj_cap = c; }
+    { size_t c = S->d_inj_ids_cap; const int rc = sp_grow(S, &S->d_inj_ids, &c, S->inj_ids.size() + 1); if (rc) return rc; S->d_inj_ids_cap = c; }
+    HIPCHK(hipMemcpyAsync(S->d_inj, S->inj.data(), sizeof(XRec) * ninj, hipMemcpyHostToDevice, st));
+    if (!S->inj_ids.empty()) HIPCHK(hipMemcpyAsync(S->d_inj_ids, S->inj_ids.data(), 4 * S->inj_ids.size(), hipMemcpyHostToDevice, st));
+    sp_launch(S, SPK_EVENTS, k_sp_inject_prep, 1, 1, d, (const XRec*)S->d_inj, ninj, S->ebound, S->jr_pay);
+  }
   {
     const uint32_t* in[2] = {S->ebound, S->jr_pay};
     uint32_t* out[2] = {S->eoff, S->poff};
@@ -369,6 +387,10 @@ static int sp_step_round(SpSim* S) {
   sp_launch(S, SPK_TRUEFP, k_sp_truefp_part, SP_TFP / 256, 256, d, S->tfpart);
   sp_launch(S, SPK_TRUEFP, k_sp_truefp_fin, 1, 64, d, (const uint2*)S->tfpart, S->tfp);
   sp_launch(S, SPK_TICK, k_sp_tick, g, tb, d, o0, (const uint32_t*)S->jr_n, S->bo, (const uint32_t*)S->tfp, r);
+  if (ninj) {
+    sp_launch(S, SPK_EVENTS, k_sp_inject, 1, 1, d, o0, (const XRec*)S->d_inj, ninj, (const uint32_t*)S->d_inj_ids);
+    S->inj.clear(); S->inj_ids.clear();
+  }
   {
     const uint32_t* in[3] = {S->bo.bj, S->bo.bnf, S->en};
     uint32_t* out[3] = {S->joff, S->foff, S->ooff};
@@ -392,6 +414,7 @@ static int sp_step_round(SpSim* S) {
     { const int rc = sp_grow(S, &S->status, &S->status_cap, M); if (rc) return rc; }
     SpRoute rt;
     rt.msgs = S->out[cur]; rt.M = M; rt.status = S->status; rt.icnt = S->icnt; rt.ebound = S->ebound; rt.kprc = S->kprc;
+    rt.pay = S->pool[cur];
     const uint32_t gm = (M + 255) / 256;
     sp_launch(S, SPK_ROUTE, k_sp_route, gm, 256, d, rt, r, w);
     sp_launch(S, SPK_PAYBOUND, k_sp_paybound, g, tb, d, (const uint32_t*)S->kprc, (const uint32_t*)S->icnt, S->pb);
@@ -438,6 +461,26 @@ static int sp_step_round(SpSim* S) {
   if (S->prof_level > 0) sp_prof_resolve(S);
   S->nj = nj_next; S->nf = nf_next;
   S->bj_total += nj_next; S->bf_total += nf_next;
+  if (S->n_ext) {                                    // the round's records to external peers, to the host queue
+    uint32_t c[2];
+    HIPCHK(hipMemcpy(c, d.ctr + C_XREC, 8, hipMemcpyDeviceToHost));
+    const uint32_t nrec = std::min(c[0], d.xrec_cap), nid = std::min(c[1], d.xids_cap);
+    std::vector<XRec> v(nrec);
+    const size_t base = S->xq_ids.size();
+    S->xq_ids.resize(base + nid);
+    if (nrec) HIPCHK(hipMemcpy(v.data(), d.xrec, sizeof(XRec) * nrec, hipMemcpyDeviceToHost));
+    if (nid) HIPCHK(hipMemcpy(S->xq_ids.data() + base, d.xids, 4ull * nid, hipMemcpyDeviceToHost));
+    std::sort(v.begin(), v.end(), [](const XRec& a, const XRec& b) {
+      return a.wave != b.wave ? a.wave < b.wave : a.sender != b.sender ? a.sender < b.sender : a.seq < b.seq; });
+    for (const XRec& x : v) {
+      kb_unicast u;
+      memcpy(&u, &x, sizeof u);
+      u.pay_off = (uint32_t)(base + x.pay_off);
+      S->xq.push_back(u);
+    }
+    const uint32_t z[2] = {0, 0};
+    HIPCHK(hipMemcpy(d.ctr + C_XREC, z, 8, hipMemcpyHostToDevice));
+  }
   if (np) {                                          // the round's ProbeResponses, (responder, probe) order
     uint32_t k = 0;
     HIPCHK(hipMemcpy(&k, S->d_presp_n, 4, hipMemcpyDeviceToHost));
@@ -743,6 +786,7 @@ static int sp_stats_out(SpSim* S, kb_stats* out) {
   out->sent_kp_ids = st[S_KPIDS];
   out->alive_rounds = st[S_ALIVER];
   out->probe_responses = st[S_PROBERESP];
+  out->exported = st[S_EXPORT];
   return KB_OK;
 }
 static int sp_dump_scalars(SpSim* S, int32_t* out) {
@@ -815,6 +859,56 @@ static int sp_kernel_breakdown(SpSim* S, kb_kernel_time* out, size_t cap, size_t
   }
   *n = c;
   return (out && cap < c) ? KB_CAPACITY : KB_OK;
+}
+// external peers: the dense engine's rules (kb_sim.hip kb_sim_set_external / inject / exported)
+static int sp_set_external(SpSim* S, uint32_t node) {
+  if (S->h_ext.empty()) S->h_ext.assign(S->C, 0);
+  if (S->h_ext[node]) return KB_OK;
+  int ever = 0;
+  { const int rc = sp_ever_bound(S, node, &ever); if (rc) return rc; }
+  if (ever) { seterr("an external peer takes an address no instance has bound"); return KB_INVALID_OPERATION; }
+  S->h_ext[node] = 1; S->n_ext++; S->h_idset[node] = 1;
+  const uint8_t o = 1;
+  HIPCHK(hipMemcpy(S->d.ext + node, &o, 1, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(S->d.idset + node, &o, 1, hipMemcpyHostToDevice));
+  if (!S->d.xrec) {
+    S->d.xrec_cap = 1u << 16; S->d.xids_cap = 1u << 22;
+    HIPCHK(sp_alloc(S, &S->d.xrec, S->d.xrec_cap)); HIPCHK(sp_alloc(S, &S->d.xids, S->d.xids_cap));
+  }
+  return KB_OK;
+}
+static int sp_inject(SpSim* S, const kb_unicast* m, const uint32_t* ids) {
+  if (!m || m->sender >= S->C || m->dest >= S->C || (m->kind > K_KPR && m->kind != KB_WIRE_JOIN) || (m->pay_len && !ids))
+    return KB_INVALID_ARGUMENT;
+  if (S->h_ext.empty() || !S->h_ext[m->sender]) { seterr("kb_sim_inject: the sender is not an external peer"); return KB_INVALID_OPERATION; }
+  if (m->kind == KB_WIRE_JOIN) {                       // a Join broadcast: the next round's Join list
+    if (std::find(S->inj_join.begin(), S->inj_join.end(), m->sender) != S->inj_join.end()) {
+      seterr("kb_sim_inject: one Join per external peer per round"); return KB_CAPACITY;
+    }
+    S->inj_join.push_back(m->sender);
+    return KB_OK;
+  }
+  if ((m->kind == K_PINGREQ || m->kind == K_ACK) && m->a >= S->C) return KB_INVALID_ARGUMENT;
+  for (uint32_t k = 0; k < m->pay_len; ++k) if (ids[k] >= S->C) return KB_INVALID_ARGUMENT;
+  uint32_t per = 0, rel = 0;
+  for (const XRec& x : S->inj) if (x.sender == m->sender) { per++; if (x.kind == K_KP) rel += x.pay_len; }
+  if (per >= (uint32_t)TICK_MAX) { seterr("kb_sim_inject: 33 records per external peer per round"); return KB_CAPACITY; }
+  XRec x{0, 0, m->sender, m->dest, 0, m->kind, m->kind == K_KP ? 0u : m->a, m->fp, m->n, (uint32_t)S->inj_ids.size(),
+         m->kind == K_KP ? m->pay_len : 0u, rel};
+  if (m->kind == K_KP) S->inj_ids.insert(S->inj_ids.end(), ids, ids + m->pay_len);
+  S->inj.push_back(x);
+  return KB_OK;
+}
+static int sp_exported(SpSim* S, kb_unicast* out, size_t cap, size_t* n, uint32_t* ids, size_t cap_ids, size_t* n_ids) {
+  *n = S->xq.size(); *n_ids = S->xq_ids.size();
+  if (!out && !ids) return KB_OK;
+  if (cap < S->xq.size() || (!S->xq_ids.empty() && (!ids || cap_ids < S->xq_ids.size()))) { seterr("export buffer too small"); return KB_CAPACITY; }
+  if (!S->xq.empty()) memcpy(out, S->xq.data(), S->xq.size() * sizeof(kb_unicast));
+  for (const kb_unicast& u : S->xq)                    // a KnownPeers map has no order: ascending ids
+    std::sort(S->xq_ids.begin() + u.pay_off, S->xq_ids.begin() + u.pay_off + u.pay_len);
+  if (!S->xq_ids.empty()) memcpy(ids, S->xq_ids.data(), 4 * S->xq_ids.size());
+  S->xq.clear(); S->xq_ids.clear();
+  return KB_OK;
 }
 // the sparse layout's footprint (test surface): [rows based, exceptions, explicit stamps, entries of the
 // largest row, bytes (4 per entry), rows], the oracle's kbo_sparse_footprint in this layout

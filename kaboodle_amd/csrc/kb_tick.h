@@ -337,6 +337,29 @@ __global__ void k_bcast_write(Dev d, BcastSlots bs, const uint32_t* join_off, co
   for (uint32_t q = 0; q < nfl; ++q) bfail[fail_off[i] + q] = BCast{i, bs.fail[(size_t)i * SLOTS + q], bseq++, 0};
 }
 
+// ---- records from external peers (kb_sim_inject): their wave-0 emissions, in call order ------
+// inj[k].pad = the record's KnownPeers offset inside its sender's payload region (the host sums them per sender);
+// inj[k].pay_off = where its ids start in `ids`.  One thread: a handful of records per round.
+__global__ void k_inject_prep(Dev d, const XRec* inj, uint32_t n, uint32_t* paysum) {
+  if (threadIdx.x || blockIdx.x) return;
+  for (uint32_t k = 0; k < n; ++k)
+    if (local(d, inj[k].sender) && inj[k].kind == K_KP) paysum[inj[k].sender] += inj[k].pay_len;
+}
+__global__ void k_inject(Dev d, OutBuf ob, const XRec* inj, uint32_t n, const uint32_t* ids) {
+  if (threadIdx.x || blockIdx.x) return;
+  for (uint32_t k = 0; k < n; ++k) {
+    const XRec x = inj[k];
+    if (!local(d, x.sender)) continue;
+    const uint32_t slot = ob.cnt[x.sender];
+    if (slot >= ob.cap[x.sender]) { set_err(d, DERR_OUTBOX); continue; }
+    const uint32_t off = ob.poff[x.sender] + x.pad;
+    if (x.kind == K_KP) for (uint32_t q = 0; q < x.pay_len; ++q) ob.pay[off + q] = ids[x.pay_off + q];
+    ob.msgs[ob.off[x.sender] + slot] = Msg{x.dest, x.sender, slot, x.kind, x.kind == K_KP ? x.pay_len : x.a, x.fp, x.n,
+                                           x.kind == K_KP ? off : 0u};
+    ob.cnt[x.sender] = slot + 1;
+  }
+}
+
 // round results for the host, {Join broadcasts, Failed broadcasts, error}: into its mapped pinned buffer
 // (rres, seq != 0: the host waits for it), and into rr on the device (sharded: all-gathered first)
 __global__ void k_round_end(Dev d, int32_t r, const uint32_t* tot, uint32_t* rres, uint32_t seq, uint32_t* rr) {

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
   s_kd[threadIdx.x] = KAGG_EMPTY; s_kc[threadIdx.x] = 0; s_kp[threadIdx.x] = 0;   // blockDim == KAGG
   __syncthreads();
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0, kpids = 0;
+  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0, kpids = 0, xp = 0;
   const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
   s_ex[wv][l] = wave_excl(cnt);
   s_base[wv][l] = i < d.hi ? ob.off[i] : 0;
@@ -84,7 +84,10 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
     if (m.kind == K_KP) kpids += m.a;
     uint8_t st = 0;
     if (last) win++;
-    else if (!d.alive[m.dest]) dead++;
+    else if (!d.alive[m.dest]) {
+      if (d.ext[m.dest]) { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, ob.pay, r, w); xp++; }
+      else dead++;
+    }
     else if (part_blocks(d, r, m.sender, m.dest)) part++;
     else if (faults(d, r) && d.loss_thr &&
              philox(m.sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m.seq, d.k0, d.k1).x < d.loss_thr) loss++;
@@ -108,8 +111,9 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
     if (s_kp[threadIdx.x]) atomicAdd(&wc.kpay[x], s_kp[threadIdx.x]);
   }
   {
-    const int idx[10] = {S_PING, S_PING + 1, S_PING + 2, S_PING + 3, S_PING + 4, S_DEAD, S_PART, S_LOSS, S_WINDOW, S_KPIDS};
-    const unsigned long long v[10] = {ks[0], ks[1], ks[2], ks[3], ks[4], dead, part, loss, win, kpids};
+    const int idx[11] = {S_PING, S_PING + 1, S_PING + 2, S_PING + 3, S_PING + 4, S_DEAD, S_PART, S_LOSS, S_WINDOW, S_KPIDS,
+                         S_EXPORT};
+    const unsigned long long v[11] = {ks[0], ks[1], ks[2], ks[3], ks[4], dead, part, loss, win, kpids, xp};
     stat_add_n(d, idx, v);
   }
 }
@@ -237,7 +241,7 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
   const uint32_t wv = threadIdx.x >> 6, l = lane();
   const uint32_t i = d.lo + blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0, kpids = 0;
+  unsigned long long ks[5] = {0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, win = 0, kpids = 0, xp = 0;
   const uint32_t cnt = i < d.hi ? ob.cnt[i] : 0;
   s_ex[wv][l] = wave_excl(cnt);
   s_base[wv][l] = i < d.hi ? ob.off[i] : 0;
@@ -254,7 +258,10 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
     if (m.kind == K_KP) kpids += m.a;
     uint8_t st = 0;
     if (last) win++;
-    else if (!d.alive[m.dest]) dead++;
+    else if (!d.alive[m.dest]) {
+      if (d.ext[m.dest]) { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, ob.pay, r, w); xp++; }   // the sender's shard exports
+      else dead++;
+    }
     else if (part_blocks(d, r, m.sender, m.dest)) part++;
     else if (faults(d, r) && d.loss_thr &&
              philox(m.sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m.seq, d.k0, d.k1).x < d.loss_thr) loss++;
@@ -267,8 +274,9 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
     if (!last) x.ostatus[g] = st;
   }
   {
-    const int idx[10] = {S_PING, S_PING + 1, S_PING + 2, S_PING + 3, S_PING + 4, S_DEAD, S_PART, S_LOSS, S_WINDOW, S_KPIDS};
-    const unsigned long long v[10] = {ks[0], ks[1], ks[2], ks[3], ks[4], dead, part, loss, win, kpids};
+    const int idx[11] = {S_PING, S_PING + 1, S_PING + 2, S_PING + 3, S_PING + 4, S_DEAD, S_PART, S_LOSS, S_WINDOW, S_KPIDS,
+                         S_EXPORT};
+    const unsigned long long v[11] = {ks[0], ks[1], ks[2], ks[3], ks[4], dead, part, loss, win, kpids, xp};
     stat_add_n(d, idx, v);
   }
 }

@@ -101,6 +101,11 @@ struct kbo_sim {
   uint8_t* pend_ident; int16_t* pend_len;   /* identity set on a stopped instance, taken by its next address (-1: none) */
   uint8_t* moved;                           /* the instance bound here restarted at a fresh address */
   uint8_t* idset;                           /* an identity was set on this never-bound address (not fresh) */
+  uint8_t* ext;                             /* external peer: a real instance outside the mesh */
+  omsg* inj; size_t ninj, capinj;           /* records from external peers, delivered in the next round's wave 0 */
+  uint32_t* injj; size_t ninjj, capinjj;    /* external peers' Join broadcasts, merged into the next round's list */
+  kb_unicast* xp; size_t nxp, capxp;        /* records routed to external peers, not drained yet */
+  uint32_t* xids; size_t nxids, capxids;    /*   and the ids of their KnownPeers lists */
   uint32_t* cseg; uint32_t* segmul;   /* crc0(addr||identity), x^(8*seglen) */
   uint32_t* seglen;
   uint32_t mulz_tab[4][256]; int uniform; uint32_t ulen;
@@ -548,6 +553,7 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   if (s->pend_len) for (size_t k = 0; k < C; ++k) s->pend_len[k] = -1;
   s->moved = (uint8_t*)calloc(C, 1);
   s->idset = (uint8_t*)calloc(C, 1);
+  s->ext = (uint8_t*)calloc(C, 1);
   s->cseg = (uint32_t*)calloc(C, 4); s->segmul = (uint32_t*)calloc(C, 4); s->seglen = (uint32_t*)calloc(C, 4);
   s->out = (ovec*)calloc(C, sizeof(ovec)); s->oseq = (uint32_t*)calloc(C, 4);
   if (cfg->variant & ~(uint32_t)(KB_VARIANT_SAME_WINDOW_BCAST | KB_VARIANT_EXACT_LRU | KB_VARIANT_SPARSE_ROWS)) {
@@ -614,7 +620,9 @@ int kbo_sim_destroy(kbo_sim* s) {
   if (s->sr) for (uint32_t i = 0; i < s->C; ++i) srow_free(&s->sr[i]);
   free(s->sr); free(s->bbits); free(s->bcnt); free(s->bpre); free(s->zpw);
   free(s->probe_q); free(s->probes); free(s->presp); free(s->stamp); free(s->tst); free(s->lat); free(s->alive); free(s->start_round); free(s->n); free(s->fp); free(s->dirty);
-  free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len); free(s->pend_ident); free(s->pend_len); free(s->moved); free(s->idset);
+  free(s->last_bcast); free(s->a3cur); free(s->susp); free(s->cur); free(s->paq); free(s->paq_n); free(s->ident); free(s->id_len); free(s->pend_ident); free(s->pend_len); free(s->moved); free(s->idset); free(s->ext);
+  for (size_t k = 0; k < s->ninj; ++k) free(s->inj[k].pay);
+  free(s->inj); free(s->xp); free(s->xids); free(s->injj);
   free(s->cseg); free(s->segmul); free(s->seglen); free(s->out); free(s->oseq); free(s->bfail); free(s->bjoin);
   for (size_t k = 0; k < s->nwatch; ++k) free(s->wsnap[k]);
   free(s->wnode); free(s->wsnap); free(s->wfp);
@@ -714,6 +722,19 @@ static void join_response(kbo_sim* s, uint32_t i, uint32_t joiner, int32_t r) {
   emit(s, i, joiner, K_KP, plen, 0, 0, pay, plen);
 #pragma omp atomic
   s->st.join_responses++;
+}
+
+/* the Join broadcasts of external peers (kbo_sim_inject) enter the round's Join list at their sender's place, as
+ * a tick's Join would (bseq 0) */
+static void merge_ext_joins(kbo_sim* s) {
+  for (size_t q = 0; q < s->ninjj; ++q) {
+    const uint32_t x = s->injj[q];
+    bpush(&s->bjoin, &s->nbjoin, &s->capbjoin, x, x, 0);
+    for (size_t k = s->nbjoin - 1; k > 0 && s->bjoin[k - 1].sender > x; --k) {
+      const obcast t = s->bjoin[k - 1]; s->bjoin[k - 1] = s->bjoin[k]; s->bjoin[k] = t;
+    }
+  }
+  s->ninjj = 0;
 }
 
 static void phase_broadcasts(kbo_sim* s, uint32_t i, int32_t r) {
@@ -1038,6 +1059,24 @@ static int run_waves(kbo_sim* s, int32_t r) {
     for (uint32_t i = 0; i < C; ++i) { inb0[i].n = 0; inb1[i].n = 0; }
     for (size_t k = 0; k < M; ++k) {
       omsg* m = &all[k];
+      if (!s->alive[m->dest] && s->ext[m->dest]) {      /* to an external peer: leaves the simulated transport */
+        if (s->nxp == s->capxp) { s->capxp = s->capxp ? 2 * s->capxp : 64; s->xp = (kb_unicast*)realloc(s->xp, s->capxp * sizeof(kb_unicast)); }
+        kb_unicast* x = &s->xp[s->nxp++];
+        memset(x, 0, sizeof *x);
+        x->round = r; x->wave = w; x->sender = m->sender; x->dest = m->dest; x->seq = m->seq; x->kind = m->kind;
+        x->a = m->kind == K_KP ? 0 : m->a; x->fp = m->fp; x->n = m->n;
+        x->pay_off = (uint32_t)s->nxids; x->pay_len = m->kind == K_KP ? m->pay_len : 0;
+        if (x->pay_len) {
+          if (s->nxids + x->pay_len > s->capxids) {
+            while (s->nxids + x->pay_len > s->capxids) s->capxids = s->capxids ? 2 * s->capxids : 1024;
+            s->xids = (uint32_t*)realloc(s->xids, s->capxids * 4);
+          }
+          memcpy(s->xids + s->nxids, m->pay, 4u * x->pay_len);
+          s->nxids += x->pay_len;
+        }
+        s->st.exported++;
+        continue;
+      }
       if (!s->alive[m->dest]) { s->st.drop_dead++; continue; }
       if (partition_blocks(s, r, m->sender, m->dest)) { s->st.drop_partition++; continue; }
       if (active_faults(s, r) && s->cfg.loss_threshold &&
@@ -1139,6 +1178,7 @@ static int step_round(kbo_sim* s) {
   /* 2. broadcasts emitted during round r-1 (KB_VARIANT_SAME_WINDOW_BCAST: after this round's tick) */
   const int same_window = (s->cfg.variant & KB_VARIANT_SAME_WINDOW_BCAST) != 0;
   if (!same_window) {
+    merge_ext_joins(s);
 #pragma omp parallel for schedule(dynamic, 64)
     for (uint32_t i = 0; i < C; ++i)
       if (s->alive[i] && s->start_round[i] < r) phase_broadcasts(s, i, r);
@@ -1176,10 +1216,17 @@ static int step_round(kbo_sim* s) {
   }
   free(bc);
   if (same_window) {            /* the tick's broadcasts reach every running peer inside this window */
+    merge_ext_joins(s);
 #pragma omp parallel for schedule(dynamic, 64)
     for (uint32_t i = 0; i < C; ++i)
       if (s->alive[i]) phase_broadcasts(s, i, r);
   }
+  /* records from external peers (kbo_sim_inject): their wave-0 emissions, in call order */
+  for (size_t k = 0; k < s->ninj; ++k) {
+    const omsg* m = &s->inj[k];
+    emit(s, m->sender, m->dest, m->kind, m->a, m->fp, m->n, m->pay, m->pay_len);
+  }
+  s->ninj = 0;
   /* 4. receive window: unicast waves */
   err = run_waves(s, r);
   if (err) return err;
@@ -1551,6 +1598,60 @@ int kbo_sparse_footprint(kbo_sim* s, uint64_t* out, size_t cap) {
     if (r->nx + r->nl > mx) mx = r->nx + r->nl;
   }
   out[0] = based; out[1] = nx; out[2] = nl; out[3] = mx; out[4] = 4 * nx + 5 * nl; out[5] = s->C;
+  return KB_OK;
+}
+/* external peers: include/kaboodle_sim.h kb_sim_set_external / kb_sim_inject / kb_sim_exported */
+int kbo_sim_set_external(kbo_sim* s, uint32_t node) {
+  if (check(s, node)) return KB_INVALID_ARGUMENT;
+  if (s->ext[node]) return KB_OK;
+  if (ever_bound(s, node)) { seterr("an external peer takes an address no instance has bound"); return KB_INVALID_OPERATION; }
+  s->ext[node] = 1;
+  s->idset[node] = 1;                       /* not a fresh id: churn joins and restarts skip it */
+  return KB_OK;
+}
+int kbo_sim_inject(kbo_sim* s, const kb_unicast* m, const uint32_t* ids) {
+  if (!s || !m || m->sender >= s->C || m->dest >= s->C || (m->kind > K_KPR && m->kind != KB_WIRE_JOIN) || (m->pay_len && !ids))
+    return KB_INVALID_ARGUMENT;
+  if (!s->ext[m->sender]) { seterr("kb_sim_inject: the sender is not an external peer"); return KB_INVALID_OPERATION; }
+  if (m->kind == KB_WIRE_JOIN) {                       /* a Join broadcast: the next round's Join list */
+    for (size_t k = 0; k < s->ninjj; ++k)
+      if (s->injj[k] == m->sender) { seterr("kb_sim_inject: one Join per external peer per round"); return KB_CAPACITY; }
+    if (s->ninjj == s->capinjj) { s->capinjj = s->capinjj ? 2 * s->capinjj : 8; s->injj = (uint32_t*)realloc(s->injj, 4 * s->capinjj); }
+    s->injj[s->ninjj++] = m->sender;
+    return KB_OK;
+  }
+  if ((m->kind == K_PINGREQ || m->kind == K_ACK) && m->a >= s->C) return KB_INVALID_ARGUMENT;
+  for (uint32_t k = 0; k < m->pay_len; ++k) if (ids[k] >= s->C) return KB_INVALID_ARGUMENT;
+  size_t per = 0;
+  for (size_t k = 0; k < s->ninj; ++k) per += s->inj[k].sender == m->sender;
+  if (per >= (size_t)(3 * SLOTS + 1 + PAQ)) { seterr("kb_sim_inject: 33 records per external peer per round"); return KB_CAPACITY; }
+  if (s->ninj == s->capinj) { s->capinj = s->capinj ? 2 * s->capinj : 16; s->inj = (omsg*)realloc(s->inj, s->capinj * sizeof(omsg)); }
+  omsg* o = &s->inj[s->ninj++];
+  memset(o, 0, sizeof *o);
+  o->sender = m->sender; o->dest = m->dest; o->kind = m->kind; o->fp = m->fp; o->n = m->n;
+  if (m->kind == K_KP) {
+    o->pay_len = m->pay_len; o->a = m->pay_len;
+    o->pay = (uint32_t*)malloc(4u * (m->pay_len ? m->pay_len : 1));
+    if (m->pay_len) memcpy(o->pay, ids, 4u * m->pay_len);
+  } else {
+    o->a = m->a;
+  }
+  return KB_OK;
+}
+static int o_cmp_u32(const void* a, const void* b) {
+  const uint32_t x = *(const uint32_t*)a, y = *(const uint32_t*)b;
+  return x < y ? -1 : x > y;
+}
+int kbo_sim_exported(kbo_sim* s, kb_unicast* out, size_t cap, size_t* n, uint32_t* ids, size_t cap_ids, size_t* n_ids) {
+  if (!s || !n || !n_ids) return KB_INVALID_ARGUMENT;
+  *n = s->nxp; *n_ids = s->nxids;
+  if (!out && !ids) return KB_OK;
+  if (cap < s->nxp || (s->nxids && (!ids || cap_ids < s->nxids))) { seterr("export buffer too small"); return KB_CAPACITY; }
+  if (s->nxp) memcpy(out, s->xp, s->nxp * sizeof(kb_unicast));
+  for (size_t k = 0; k < s->nxp; ++k)                  /* a KnownPeers map has no order: ascending ids */
+    if (s->xp[k].pay_len > 1) qsort(s->xids + s->xp[k].pay_off, s->xp[k].pay_len, 4, o_cmp_u32);
+  if (s->nxids) memcpy(ids, s->xids, 4u * s->nxids);
+  s->nxp = 0; s->nxids = 0;
   return KB_OK;
 }
 int kbo_sim_sparse_footprint(kbo_sim* s, uint64_t* out, size_t cap) {

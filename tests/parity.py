@@ -220,6 +220,80 @@ def run_events_case(case: dict, rounds: int, watched, drain_every: int = 1, shar
     return True, "ok", n
 
 
+K_PING, K_PINGREQ, K_ACK, K_KP, K_KPR = range(5)
+K_JOIN = 16                              # KB_WIRE_JOIN: an external peer's Join broadcast
+
+
+def external_replies(exported, me_known, r: int, proactive_to=None):
+    """What a real instance at an external address sends back into the mesh for the records it received
+    (src/kaboodle.rs:394-548, a scripted stand-in for a real instance, DESIGN.md §9): Ping -> Ack{self, fp, n};
+    PingRequest(p) -> Ping p; KnownPeersRequest -> KnownPeers of the peers it knows; Ack / KnownPeers learn
+    their senders; every 10th round (from round 1) each external peer broadcasts Join, as maybe_broadcast_join
+    re-broadcasts (src/kaboodle.rs:228-251).  Returns [(sender, dest, kind, a, fp, n, ids)] in order, at most 33
+    unicast records per external peer."""
+    out = []
+    for (_, _, sender, dest, _, kind, a, fp, n, ids) in exported:
+        me_known.setdefault(dest, set()).add(sender)
+        if kind == K_PING:
+            out.append((dest, sender, K_ACK, dest, 0xC0FFEE00 + dest, len(me_known[dest]) + 1, []))
+        elif kind == K_PINGREQ:
+            out.append((dest, a, K_PING, 0, 0, 0, []))
+        elif kind == K_KPR:
+            out.append((dest, sender, K_KP, 0, 0, 0, sorted(me_known[dest] - {sender})[:40]))
+        elif kind == K_KP:
+            me_known[dest].update(ids)
+    if proactive_to is not None:
+        for x, targets in proactive_to.items():
+            t = targets[r % len(targets)]
+            out.append((x, t, K_PING, 0, 0, 0, []))
+            if r % 5 == 2:
+                out.append((x, t, K_KPR, 0, 0xBADF00D, 1, []))
+    per = {}
+    kept = []
+    for m in out:
+        per[m[0]] = per.get(m[0], 0) + 1
+        if per[m[0]] <= 33:
+            kept.append(m)
+    if proactive_to is not None and r % 10 == 1:
+        kept += [(x, 0, K_JOIN, 0, 0, 0, []) for x in proactive_to]
+    return kept
+
+
+def run_external_case(case: dict, rounds: int, externals, libs, shards: int = 0) -> tuple[bool, str, int]:
+    """The case with external peers (kb_sim_set_external) answered by external_replies: every implementation
+    gets the same injections (they depend only on the exports, which must be identical) and must keep the same
+    complete state every round.  Returns (ok, message, exported records compared)."""
+    cfg = case["cfg"]
+    sims = [Sim(libs[0], cfg)] + [Sim(lb, cfg, shards=shards) for lb in libs[1:]]
+    for sm in sims:
+        setup(sm, case)
+        for x in externals:
+            sm.set_external(x)
+    known = [dict() for _ in sims]
+    targets = {x: [(x * 7 + k * 13) % cfg.initial_nodes for k in range(5)] for x in externals}
+    nx = 0
+    for r in range(rounds):
+        apply_events(sims, case, r)
+        for sm in sims:
+            sm.step(1)
+        ex = [sm.exported() for sm in sims]
+        for e in ex[1:]:
+            if e != ex[0]:
+                return False, f"round {r}: exports differ: {ex[0][:3]} vs {e[:3]}", nx
+        nx += len(ex[0])
+        st = [state_of(sm) for sm in sims]
+        for k in range(1, len(sims)):
+            d = diff_states(st[0], st[k])
+            if d:
+                return False, f"round {r}: " + "; ".join(d[:6]), nx
+        for k, sm in enumerate(sims):
+            for m in external_replies(ex[k], known[k], r, targets):
+                sm.inject(*m[:6], ids=m[6])
+    for sm in sims:
+        sm.close()
+    return True, "ok", nx
+
+
 def standard_cases() -> list[tuple[str, dict, int]]:
     cases = []
     cases.append(("config1_2x2", {"cfg": SimConfig(capacity=4, initial_nodes=0),

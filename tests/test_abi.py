@@ -42,7 +42,7 @@ def test_oracle_exports_every_symbol():
     skip = {"kb_sim_kernel_time", "kb_sim_reset_kernel_time", "kb_sim_kernel_bytes",   # GPU timing surface
             "kb_sim_set_profiling", "kb_sim_kernel_breakdown", "kb_sim_host_syncs",
             "kb_sim_debug_paths", "kb_sim_debug_counters",                             # GPU kernel variants
-            "kb_rccl_unique_id", "kb_sim_create_rank", "kb_sim_create_local", "kb_sim_shard_info",  # sharding
+            "kb_rccl_unique_id", "kb_ipc_unique_id", "kb_sim_create_rank", "kb_sim_create_local", "kb_sim_shard_info",  # sharding
             "kb_wire_encode", "kb_wire_decode", "kb_wire_addr_of_id", "kb_wire_id_of_addr"}     # wire codec (host)
     missing = [n for n in declared() if n not in skip and not hasattr(lib, "kbo_" + n[3:])]
     assert not missing

@@ -59,6 +59,37 @@ def test_parity_exact_lru_sharded(gpu, name):
     assert ok, f"{name} (exact LRU, x3): {msg}"
 
 
+def test_parity_exact_lru_block_bounds(gpu):
+    """Rows of four 1024-id blocks over three rebases (k_a3_exact's bound-ordered block scan: the tied converged
+    start, bounds tightened by scans, lowered by k_rebase, reset by a restart's move).  Complete state every 4th
+    round and at the end."""
+    case = {"cfg": SimConfig(capacity=4000, initial_nodes=3400, init_mode=KB_INIT_CONVERGED, churn=0.0005, loss=0.01,
+                             seed=41, variant=KB_VARIANT_EXACT_LRU),
+            "events": {70: [("stop", 17, None)], 75: [("restart", 17, None)], 150: [("stop", 2900, None)],
+                       160: [("restart", 2900, None)]}}
+    ok, msg, _ = parity.run_case(case, 200, check_every=4, full_rows=True)
+    assert ok, f"exact LRU blocks: {msg}"
+
+
+EXT_CASES = ["converged_loss_256", "churn_loss_512", "partition_heal", "stop_start", "join_64"]
+
+
+@pytest.mark.parametrize("mode", ["dense", "x3", "sparse"])
+@pytest.mark.parametrize("name", EXT_CASES)
+def test_gpu_external_peers(gpu, name, mode):
+    """External peers: two addresses beyond the case's ids stand for real instances; the records
+    simulated peers address to them are exported (identically, every round) and a scripted real instance's
+    replies are injected into the next round's wave 0 (parity.external_replies): complete state every round,
+    unsharded, as 3 row shards (the sender's shard exports, the external's shard injects) and on sparse rows."""
+    from dataclasses import replace
+    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}[name]
+    c = case["cfg"]
+    cfg = replace(c, capacity=c.capacity + 4, variant=4 if mode == "sparse" else 0)
+    ok, msg, nx = parity.run_external_case({**case, "cfg": cfg}, rounds, [c.capacity + 1, c.capacity + 3],
+                                           [parity.oracle_lib(), gpu], shards=3 if mode == "x3" else 0)
+    assert ok and nx > 0, f"{name} ({mode}): {msg}"
+
+
 TRUNC_CASES = {
     # views of > 567 ids: every Join response is a sampled (truncated) one, served by wave
     "trunc_1200": ({"cfg": SimConfig(capacity=1300, initial_nodes=1200, init_mode=KB_INIT_CONVERGED, churn=0.01, seed=23)}, 6),

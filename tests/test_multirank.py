@@ -1,8 +1,10 @@
 """The N > 1 bench path on CPU: world_size-2 gloo process groups (127.0.0.1).  Each rank runs its
-replica of the workload (here through the CPU oracle, since there is no GPU in this container) and the
-whole-job numbers are reduced exactly as bench.py does on RCCL: max wall time, summed peer-rounds."""
+replica of the workload (here through the CPU oracle, since there is no GPU in this container), timed as
+bench.py times it (barrier, the steps, barrier), and the whole-job numbers are reduced exactly as bench.py does
+on RCCL: max wall time, summed peer-rounds.  The GPU exchange between rank processes is tests/test_gpu_multiproc.py."""
 import os
 import socket
+import time
 
 import pytest
 import torch.distributed as dist
@@ -32,13 +34,17 @@ def _worker(rank, world, port, out):
     with Sim(parity.oracle_lib(), cfg) as o:
         o.step(a.warmup)
         units = 0
-        for _ in range(a.steps):
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(a.steps * (1 + 2 * rank)):       # rank 1 does three times the work: the max must be its time
             o.step(1)
             units += o.stats()["alive"]
+        dist.barrier()
+        dt = time.perf_counter() - t0
+        mine = dt
         fps = o.fingerprints().tolist()
-    dt = 1.0 + rank                    # a stand-in wall time per rank, to check the reduction
     tot_dt, tot_units = bench.aggregate(dt, float(units), world)
-    out[rank] = (cfg.seed, units, tot_dt, tot_units, fps[:8])
+    out[rank] = (cfg.seed, units, tot_dt, tot_units, fps[:8], mine)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -48,10 +54,10 @@ def test_replicas_reduce_like_bench():
     mgr = mp.Manager()
     out = mgr.dict()
     mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
-    (s0, u0, dt0, tu0, fp0), (s1, u1, dt1, tu1, fp1) = out[0], out[1]
+    (s0, u0, dt0, tu0, fp0, m0), (s1, u1, dt1, tu1, fp1, m1) = out[0], out[1]
     assert s0 != s1                                     # distinct replicas
     assert fp0 != fp1
-    assert dt0 == dt1 == 2.0                            # max over ranks
+    assert dt0 == dt1 == max(m0, m1) > 0                # max over ranks of the measured times
     assert tu0 == tu1 == float(u0 + u1)                 # summed units
 
 
