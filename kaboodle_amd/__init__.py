@@ -24,6 +24,10 @@ def lib() -> SimLib:
     if _LIB is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"HIP library not built: {LIB_PATH} (run __graft_entry__.build())")
+        # torch's wheel carries its own HIP runtime.  Loaded first, it satisfies the library's libamdhip64
+        # dependency; loaded after the library, it maps a second runtime next to /opt/rocm's, and the one that
+        # initialises second finds no device (kb_sim_create: "no HIP device", tools/diag/hip_load_order.py).
+        import torch  # noqa: F401
         _LIB = SimLib(LIB_PATH, "kb_")
     return _LIB
 

@@ -1,10 +1,11 @@
 """The bridge between a simulated mesh and real instances (kaboodle_amd.bridge) and the networking.rs
 plumbing (kaboodle_amd.networking), on loopback sockets: a real discover_mesh_member's Probe datagram
-reaches the mesh, the ProbeResponse comes back to the prober's socket and decodes as discovery.rs decodes
-it; the mesh's Join broadcasts go out only when forwarding is asked for (by default they would fill real
-views with unreachable members, kaboodle_amd/bridge.py), as SwimBroadcast datagrams a real instance
-decodes.  The CPU oracle stands in for the mesh here; test_bridge_hip_mesh runs the same exchange against
-the HIP library on an MI355X."""
+reaches the mesh, the ProbeResponse comes back to the prober's socket from the responder's own socket and
+decodes as discovery.rs decodes it; the mesh's Join broadcasts go out only when forwarding is asked for, as
+SwimBroadcast datagrams a real instance decodes, carrying the simulated peer's socket address; and a real
+instance (tests/realpeer.py) joins the simulated mesh through the bridge and stays a member over 40 rounds of
+unicast traffic both ways.  The CPU oracle stands in for the mesh here; the gpu-marked tests run the same
+exchanges against the HIP library on an MI355X."""
 import os
 import socket
 import time
@@ -12,7 +13,7 @@ import time
 import pytest
 
 import parity
-from kaboodle_amd._ffi import Sim, SimConfig
+from kaboodle_amd._ffi import KB_INIT_CONVERGED, Sim, SimConfig
 
 pytestmark = pytest.mark.skipif(not os.path.exists(parity.GPU_SO), reason="wire codec lives in the HIP library")
 
@@ -49,9 +50,10 @@ def _exchange(mesh):
     assert br.stats["probes_in"] == 1
     dg, src = prober.recvfrom(1024)
     env = wire.receive(dg, "discovery")    # discovery.rs:81 reads it as a SwimEnvelope
-    assert src == uni.getsockname() and env["identity"] in (mesh.identity(0), mesh.identity(1))
+    assert src in (br.addr_for(0), br.addr_for(1))   # from the responder's own socket (src/kaboodle.rs:316-330)
+    assert env["identity"] == mesh.identity(br.node_for(src))
     assert br.stats["probe_responses_out"] == 2  # n = 2: both answer (o = 0)
-    # a real instance's Join is not a simulated peer: counted, dropped
+    # a real instance's Join with no external id to give it (no attach, no auto_attach pool): counted, dropped
     prober.sendto(wire.encode("Join", identity=b"real", peer=paddr), bin_.getsockname())
     time.sleep(0.05)
     br.run_round()
@@ -62,7 +64,7 @@ def _exchange(mesh):
     br.run_round()                         # round 3: node 2's Join
     dg, _src = listener.recvfrom(wire.INCOMING_BUFFER_SIZE)
     g = wire.receive(dg, "broadcast")
-    assert (g["kind"], wire.id_of(g["peer"]), g["identity"]) == ("Join", 2, mesh.identity(2))
+    assert (g["kind"], br.node_for(g["peer"]), g["identity"]) == ("Join", 2, mesh.identity(2))
     br.close()
     for s in (listener, prober):
         s.close()
@@ -80,6 +82,64 @@ def test_bridge_hip_mesh():
     kaboodle_amd.require_gpu()
     with kaboodle_amd.Mesh(SimConfig(capacity=8, initial_nodes=0, id_len=5, seed=3)) as m:
         _exchange(m)
+
+
+def _real_instance_joins(mesh, rounds: int = 40):
+    """A real instance (tests/realpeer.py, the reference's protocol loop on UDP sockets) joins a simulated mesh through
+    the bridge and stays a member: its Join broadcast reaches every simulated peer (kb_sim_inject KB_WIRE_JOIN), the
+    Join responses come back as KnownPeers from the responders' own sockets, its pings are acked by simulated peers
+    and the simulated peers' pings to it are exported, sent, acked and injected back, for `rounds` rounds."""
+    from kaboodle_amd import wire
+    from kaboodle_amd.bridge import Bridge
+    from realpeer import RealPeer
+    n_sim = 24
+    bin_ = _udp()
+    bin_.setblocking(False)
+    uni = _udp()
+    real = RealPeer(b"real-0", bin_.getsockname(), seed=7)
+    br = Bridge(mesh, sockets=(bin_, bin_, real.bin.getsockname(), uni), auto_attach=[30, 31], forward_broadcasts=True)
+    mesh.step(1)                                   # the converged mesh's first round, before the instance starts
+    t = 1000
+    real.tick(t)                                   # Kaboodle::start: the Join broadcast (:228-251)
+    st = br.run_round()
+    assert st["joins_in"] == 1 and br.ext_of == {real.addr: 30} and mesh.identity(30) == b"real-0"
+    assert all(30 in mesh.peers(i) for i in range(n_sim)), "the Join reached every simulated peer"
+    for _ in range(rounds):
+        t += 1000
+        real.tick(t)
+        time.sleep(0.002)
+        br.run_round()
+    sims = {br.addr_for(i) for i in range(n_sim)}
+    known = set(real.peers) - {real.addr}
+    assert len(known & sims) >= n_sim // 2, f"the real instance learnt {len(known & sims)} simulated peers"
+    assert not known - sims, "every address it knows is a simulated peer's socket"
+    assert all(30 in mesh.peers(i) for i in range(n_sim)), "the real instance stayed a member of every view"
+    acked = {src for (_t, d, k, src) in real.log if d == "in" and k == "Ack"}
+    pinged = {dst for (_t, d, k, dst) in real.log if d == "out" and k == "Ping"}
+    assert pinged and pinged <= acked | {dst for (tt, d, k, dst) in real.log if d == "out" and tt >= t - 2000}
+    assert any(k == "Ping" for (_t, d, k, _s) in real.log if d == "in"), "simulated peers pinged it"
+    assert br.stats["unicast_in"] > rounds and br.stats["unicast_out"] > rounds and br.stats["unknown_sender"] == 0
+    assert br.stats["unmapped_addr"] == 0 and br.stats["inject_refused"] == 0 and br.stats["undecodable"] == 0
+    assert mesh.stats()["exported"] == br.stats["unicast_out"]
+    real.close()
+    br.close()
+    return wire
+
+
+def test_real_instance_joins_through_bridge():
+    cfg = SimConfig(capacity=32, initial_nodes=24, init_mode=KB_INIT_CONVERGED, id_len=5, seed=11)
+    with Sim(parity.oracle_lib(), cfg) as o:
+        _real_instance_joins(o)
+
+
+@pytest.mark.gpu
+def test_real_instance_joins_hip_mesh():
+    """The same join through the bridge against the HIP library's mesh on an MI355X."""
+    import kaboodle_amd
+    kaboodle_amd.require_gpu()
+    cfg = SimConfig(capacity=32, initial_nodes=24, init_mode=KB_INIT_CONVERGED, id_len=5, seed=11)
+    with kaboodle_amd.Mesh(cfg) as m:
+        _real_instance_joins(m)
 
 
 def test_bridge_default_interface_and_ipv6(monkeypatch):
