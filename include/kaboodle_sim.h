@@ -90,8 +90,17 @@ typedef struct kb_config {
   uint32_t sparse_row_cap;   /* KB_VARIANT_SPARSE_ROWS on the GPU: entries per row (exceptions and
                                 explicit stamps); 0 = min(capacity, 4096).  Exceeding it is
                                 KB_CAPACITY, never a truncation (ignored by the oracle)              */
-  uint32_t reserved[2];
+  uint32_t stat_flags;       /* KB_STAT_*: counters a long run may skip (0: count everything)         */
+  uint32_t reserved[1];
 } kb_config;
+/* stat_flags */
+enum { KB_STAT_NO_SF_FAILED_DROPS = 1u };  /* socket_faithful: do not count the lost deliveries of Failed
+                                              broadcasts in drop_bcast.  In that mode Failed changes no state
+                                              (DESIGN.md §2.10), so the count is its whole cost: one Philox word
+                                              per (receiver, entry), O(N x entries) a round.  drop_bcast then
+                                              counts Join and Probe losses only; all other state and counters
+                                              are unchanged.  KB_VARIANT_SPARSE_ROWS and the oracle; the dense
+                                              engine refuses it (KB_INVALID_ARGUMENT)                        */
 enum { KB_VARIANT_SAME_WINDOW_BCAST = 1u,   /* Join/Failed delivered in the round they are sent, right after
                                                the tick (src/kaboodle.rs:770-778), not at the next round start */
        KB_VARIANT_EXACT_LRU = 2u,           /* A3 orders by the exact instant (no stamp window, no ancient ties) */

@@ -19,6 +19,7 @@ KB_DBG_ALL = 31                  # every wide-row variant
 KB_DBG_WAVE_GRAPH = 32           # the receive window as a replayed HIP graph
 KB_DBG_RESP_WAVE_HBM = 64        # Join responses by wave, rows read in place (rows > 110K ids)
 KB_VARIANT_SAME_WINDOW_BCAST, KB_VARIANT_EXACT_LRU = 1, 2   # oracle-only
+KB_STAT_NO_SF_FAILED_DROPS = 1
 KB_VARIANT_SPARSE_ROWS = 4       # the configs[4] layout: oracle and the HIP library (unsharded)
 KB_LATENCY_NONE = 0xFFFFFFFF
 KT_ROWPASS, KT_ROUND, KT_FOLD, KT_RESP, KT_PROC = 0, 1, 2, 3, 4   # kb_sim_kernel_time / kb_sim_kernel_bytes kinds
@@ -34,7 +35,7 @@ class KbConfig(C.Structure):
         ("failed_mode", C.c_uint32), ("id_len", C.c_uint32), ("partition_groups", C.c_uint32),
         ("partition_start", C.c_int32), ("partition_end", C.c_int32), ("device", C.c_int32),
         ("debug_flags", C.c_uint32), ("track_latency", C.c_uint32), ("variant", C.c_uint32),
-        ("sparse_row_cap", C.c_uint32), ("reserved", C.c_uint32 * 2),
+        ("sparse_row_cap", C.c_uint32), ("stat_flags", C.c_uint32), ("reserved", C.c_uint32 * 1),
     ]
 
 
@@ -124,6 +125,7 @@ class SimConfig:
     variant: int = 0             # KB_VARIANT_*: oracle-only alternative semantics (deviation measurements), or
                                  # KB_VARIANT_SPARSE_ROWS (the configs[4] layout, also on the GPU)
     sparse_row_cap: int = 0      # KB_VARIANT_SPARSE_ROWS on the GPU: entries per row (0: min(capacity, 4096))
+    stat_flags: int = 0          # KB_STAT_*: KB_STAT_NO_SF_FAILED_DROPS skips socket_faithful Failed drop counts
 
     def to_c(self) -> KbConfig:
         c = KbConfig()
@@ -138,7 +140,7 @@ class SimConfig:
             self.partition_groups, self.partition_start, self.partition_end)
         c.device = self.device
         c.debug_flags, c.track_latency, c.variant = self.debug_flags, self.track_latency, self.variant
-        c.sparse_row_cap = self.sparse_row_cap
+        c.sparse_row_cap, c.stat_flags = self.sparse_row_cap, self.stat_flags
         return c
 
 

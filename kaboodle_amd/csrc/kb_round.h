@@ -546,10 +546,8 @@ __device__ __attribute__((always_inline)) inline uint32_t a3_scan(const Dev& d, 
 // LDSB: the row's bitset staged in LDS; LL: both broadcast lists staged in LDS (every list read is then an
 // LDS read: a runtime choice between LDS and HBM made the compiler read the Failed entries through flat
 // pointers, whose wait covered the HBM counter too and cost the loop one L2 round trip per 64 entries)
+constexpr uint32_t KB_RP_WPE = 4;           // minimum waves per SIMD the row pass is compiled for (register budget 512 / KB_RP_WPE)
 template <bool LDSB, bool LL>
-#ifndef KB_RP_WPE
-#define KB_RP_WPE 4           // minimum waves per SIMD the row pass is compiled for (register budget 512 / KB_RP_WPE)
-#endif
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KB_RP_WPE, 8))) void k_rowpass(Dev d, PhaseB pb, RowOut ro, int32_t r) {
   extern __shared__ uint32_t pb_dyn[];
   const uint32_t wpb = blockDim.x >> 6;
@@ -940,10 +938,8 @@ __device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint
 // inserted after the response (J[upto..nnew), suffix minima JM), stepping over them (least fixed point
 // of e = #later joiners <= select(y + e)).  RESP_U keys per batch: their permutations, block searches and
 // 32-byte block reads are independent, so the loads of a batch are in flight together.
-#ifndef KB_RESP_U
-#define KB_RESP_U 4
-#endif
-constexpr int RESP_U = KB_RESP_U;   // (A/B knob)
+constexpr uint32_t KB_RESP_U = 4;
+constexpr int RESP_U = KB_RESP_U; 
 constexpr int RESP_KMAX = 9;          // keys per lane at stride >= 64: cap <= 567 (src/kaboodle.rs:43, :373-383)
 __device__ __attribute__((always_inline)) inline void sampled_fill(uint32_t* pay, uint32_t k_first, uint32_t stride,
                                                                    uint32_t cap, const Prp& P, const uint32_t* B,

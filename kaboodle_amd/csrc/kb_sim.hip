@@ -555,11 +555,32 @@ static int upload_segments(kb_sim* s) {
     HIPCHK(hipMemcpy(s->d.zfin, zf.data(), 4ull * (C + 2), hipMemcpyHostToDevice));
   }
   HIPCHK(hipMemcpy(s->d.ztab, ztab.data(), 4ull * ztab.size(), hipMemcpyHostToDevice));
-  std::vector<uint32_t> zb(ZB);
-  for (uint32_t c = 0; c < 9; ++c)
+  std::vector<uint32_t> zb(ZB10);
+  for (uint32_t c = 0; c < 11; ++c)
     for (uint32_t k = 0; k < 4; ++k)
       for (uint32_t v = 0; v < 256; ++v) zb[c * 1024 + k * 256 + v] = multmodp(zpow[c], v << (8 * k));
   HIPCHK(hipMemcpy(s->d.zbtab, zb.data(), 4ull * zb.size(), hipMemcpyHostToDevice));
+  // decimal blocks: ids 10q..10q+9 share their record but for the port's last digit, so with
+  // uniform records crc0(rec_{10q+t}) = A_q ⊕ e_t (crc0 is linear) and a block of k members in mask m folds to
+  // A_q·G(k) ⊕ E(m), G(k) = Σ_{u<k} Z^u: a table per (block, k) and one per mask instead of htab's 256 per 8 ids.
+  // Taken only when every id's record satisfies it (empty identities; default identities differ per id).
+  bool dec = uniform && C >= 10;
+  for (uint32_t j = 0; dec && j < C; ++j) dec = (cseg[j] ^ cseg[j - j % 10]) == (cseg[j % 10] ^ cseg[0]);
+  s->d.dec = dec && !(s->d.dev & 8192) ? 1u : 0u;    // KB_DEV=8192: the htab fold instead (A/B timing; same results)
+  if (dec) {
+    const uint32_t nq = (s->W + 9) / 10;
+    std::vector<uint32_t> G(11, 0), dt((size_t)nq * DEC_STRIDE, 0), et(1024, 0);
+    for (uint32_t k = 1; k <= 10; ++k) G[k] = G[k - 1] ^ zpow[k - 1];
+    for (uint32_t q = 0; q < nq && 10 * q < C; ++q)
+      for (uint32_t k = 1; k <= 10; ++k) dt[(size_t)q * DEC_STRIDE + k] = multmodp(G[k], cseg[10 * q]);
+    for (uint32_t m = 1; m < 1024; ++m) {
+      uint32_t raw = 0;
+      for (uint32_t t = 0; t < 10; ++t) if ((m >> t) & 1u) raw = multmodp(Z, raw) ^ (cseg[t] ^ cseg[0]);
+      et[m] = raw;
+    }
+    HIPCHK(hipMemcpy(s->d.dtab, dt.data(), 4ull * dt.size(), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(s->d.etab, et.data(), 4ull * et.size(), hipMemcpyHostToDevice));
+  }
   const size_t hn = (size_t)(s->W / 8) * 256;
   k_build_htab<<<(unsigned)((hn + 255) / 256), 256>>>(s->d);
   HIPCHK(hipDeviceSynchronize());
@@ -595,6 +616,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   if (!cfg || !out || cfg->abi_version != KB_ABI_VERSION) { seterr("bad config"); delete xf; return KB_INVALID_ARGUMENT; }
   if (cfg->capacity == 0 || cfg->capacity > 7800000u || cfg->initial_nodes > cfg->capacity || cfg->id_len > MAXID ||
       cfg->max_waves == 0 || cfg->max_waves > 64) { seterr("config out of range"); delete xf; return KB_INVALID_ARGUMENT; }
+  if (cfg->stat_flags) { seterr("kb_config.stat_flags: sparse rows and the oracle only"); delete xf; return KB_INVALID_ARGUMENT; }
   if (cfg->variant && cfg->variant != KB_VARIANT_EXACT_LRU) { seterr(cfg->variant == KB_VARIANT_SPARSE_ROWS ? "sparse rows run unsharded (kb_sim_create)" : "semantic variants other than KB_VARIANT_SPARSE_ROWS are measurement-only (CPU oracle)"); delete xf; return KB_INVALID_ARGUMENT; }
   const uint32_t C = cfg->capacity;
   const uint32_t rows_per = (C + (uint32_t)world - 1) / (uint32_t)world;
@@ -626,10 +648,8 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   const uint32_t R = s->R;
   const uint32_t groups = (R + 63) / 64;
   uint32_t S = 1;
-#ifndef KB_FOLD_WAVES
-#define KB_FOLD_WAVES 16384                            // fold waves wanted: column splits double up to it (64K:
+constexpr uint32_t KB_FOLD_WAVES = 16384;                            // fold waves wanted: column splits double up to it (64K:
                                                        // 16 splits, 0.44 -> 0.42 ms against 8 and 32, profiles/r04fs_ab_fold_splits.txt)
-#endif
   while (S < 64 && groups * S < KB_FOLD_WAVES) S <<= 1;   // enough sweep waves to fill the chip
   s->S = S;
   Dev& d = s->d;
@@ -661,7 +681,7 @@ static int create_shard(const kb_config* cfg, int rank, int world, Xfer* xf, kb_
   AR(d.dirty, 1); A(d.alive, C); A(d.idset, C); A(d.ext, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
   AR(d.last_bcast, 1); AR(d.a3cur, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
   AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
-  A(d.ztab, 17 * 128); A(d.zbtab, ZB);
+  A(d.ztab, 17 * 128); A(d.zbtab, ZB10); A(d.dtab, (size_t)((W + 9) / 10) * DEC_STRIDE); A(d.etab, 1024);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.sacc, (size_t)NACC * NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
   if (cfg->variant == KB_VARIANT_EXACT_LRU) { AR(d.tst, W); AR(d.tlb, W / 1024); }   // exact A3 instants
@@ -1056,9 +1076,7 @@ static int launch_waves(kb_sim* s, int32_t rk) {
        // then the small ones (a wave per destination), which also set up nb.cap / nb.cnt
       const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
       const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
-#ifndef KB_KPS_PER_CU
-#define KB_KPS_PER_CU 1
-#endif
+constexpr uint32_t KB_KPS_PER_CU = 1;
       const uint32_t small = std::max<uint32_t>((R + 1023) / 1024, KB_KPS_PER_CU * s->ncu);
       klaunch(s, KI_KP, k_kp, dim3(ks * groups + small), dim3(1024), (uint32_t)kp_lds_bytes(d.NWR), d, ib, s->wc, r,
               nb, ks * groups);
@@ -1409,7 +1427,10 @@ static int step_round(kb_sim* s) {
   klaunch(s, KI_TICK_SCAN, k_tick_scan, dim3(gnode), dim3(tb), 0, d, s->bs, r, s->slow);                       // A1; list the A2 nodes
   klaunch(s, KI_TICK_PRE, k_tick_pre, dim3(std::min<uint32_t>(gwave, 1024)), dim3(256), 0, d, o0, s->bs, r, s->slow);   // A2 per listed node
   // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded
-  if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
+  if (d.uniform) {
+    if (d.dec) klaunch(s, KI_FOLD, k_fold<true>, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
+    else klaunch(s, KI_FOLD, k_fold<false>, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
+  }
   if (d.uniform) klaunch(s, KI_FP_ROWS, k_fp_rows, dim3((FP_LANES * R + tb - 1) / tb), dim3(tb), 0, d);
   if (d.tst) klaunch(s, KI_A3_EXACT, k_a3_exact, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);   // exact A3 order
   klaunch(s, KI_TICK_POST, k_tick_post, dim3(gnode), dim3(tb), 0, d, s->ro, o0, r);

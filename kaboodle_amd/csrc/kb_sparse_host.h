@@ -181,6 +181,7 @@ static int sp_create(const kb_config* cfg, SpSim** out) {
   h_crc_init();
   if (cfg->variant != KB_VARIANT_SPARSE_ROWS) { seterr("the sparse rows take no other semantic variant"); return KB_INVALID_ARGUMENT; }
   if (cfg->track_latency) { seterr("sparse rows keep no latency table"); return KB_INVALID_ARGUMENT; }
+  if (cfg->stat_flags & ~(uint32_t)KB_STAT_NO_SF_FAILED_DROPS) { seterr("unknown kb_config.stat_flags"); return KB_INVALID_ARGUMENT; }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) { seterr("no HIP device"); return KB_NO_DEVICE; }
   SpSim* S = new SpSim();
@@ -353,7 +354,9 @@ static int sp_step_round(SpSim* S) {
   }
   bc.jnew = S->jnew; bc.jresp = S->jresp; bc.jr_n = S->jr_n; bc.jr_pay = S->jr_pay;
   bc.np = np; bc.presp = S->d_presp; bc.presp_n = S->d_presp_n; bc.presp_cap = (uint32_t)std::min<size_t>(S->presp_cap, 0xFFFFFFFFu);
-  if (S->nf && S->cfg.failed_mode == KB_FAILED_SOCKET_FAITHFUL && S->cfg.partition_groups <= 255) {
+  if (S->nf && S->cfg.failed_mode == KB_FAILED_SOCKET_FAITHFUL && (S->cfg.stat_flags & KB_STAT_NO_SF_FAILED_DROPS)) {
+    bc.fcounted = 1;                                   // no state effect, and their drops are not counted
+  } else if (S->nf && S->cfg.failed_mode == KB_FAILED_SOCKET_FAITHFUL && S->cfg.partition_groups <= 255) {
     HIPCHK(hipMemsetAsync(S->fkey + S->nf, 0xFF, 12, st));   // pad the last group of four
     sp_launch(S, SPK_BFAIL_SF, k_sp_bfail_sf, g, tb, d, (const uint4*)S->fkey, S->nf, r);
     bc.fcounted = 1;

@@ -129,9 +129,7 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
 // kernel writes a row while the inboxes are built (a row read while a prologue moves a stamp to
 // Known(now) and logs it could count that peer twice), and the proof is in place before the fast
 // handlers of k_sortfast decide.  The KnownPeers prologues of k_kp in between only add fresh entries.
-#ifndef KB_PROBE_GROUPS
-#define KB_PROBE_GROUPS 1024
-#endif
+constexpr uint32_t KB_PROBE_GROUPS = 1024;
 constexpr uint32_t PROBE_GROUPS = KB_PROBE_GROUPS;   // workgroups of the scatter launch that run the probe (1024: 3.00
                                                      // -> 2.93 ms against 512; 2048 and 4096 the same, profiles/r04kn*)
 __device__ __attribute__((always_inline)) inline void kpr_probe(const Dev& d, const WaveCtl& wc, int32_t r, uint32_t bid,
@@ -388,9 +386,7 @@ __global__ void k_scatter_flat(Dev d, OutBuf ib, WaveCtl wc, uint32_t n, int32_t
 constexpr uint32_t KP_BIG = 4096;          // payload ids from which a group takes the BIG kernel
 constexpr uint32_t KP_LDS_WORDS = 16384;   // BIG: rows up to 512K ids keep their bitset in LDS (64 KB)
 constexpr int KP_UNROLL = 10;            // 640 ids per wave step: a whole Join response (<= 567)
-#ifndef KB_KP_COLS
-#define KB_KP_COLS 2
-#endif
+constexpr uint32_t KB_KP_COLS = 2;
 constexpr uint32_t KP_COLS = KB_KP_COLS; // BIG groups in LDS: workgroups per destination, one per column part (A/B: 2 beats 4 and 1)
 // a part must hold whole checkpoint segments: its workgroup refolds the segments it changed from its own
 // LDS slice (3 parts of 64 segments straddle: an A/B build with 3 faulted)
@@ -601,10 +597,8 @@ __device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d
 // in place on the row's bitset, the same arms-then-prologues order as the BIG groups.  (The body of
 // k_kp's last nblk workgroups: at least one per CU, since a round of the converged start's first
 // SHARE_AGE rounds delivers ~24K replies of a few hundred ids at 64K peers in one wave.)
-#ifndef KB_KPS_UNROLL
-#define KB_KPS_UNROLL 4
-#endif
-constexpr int KPS_UNROLL = KB_KPS_UNROLL;   // (A/B knob)
+constexpr uint32_t KB_KPS_UNROLL = 4;
+constexpr int KPS_UNROLL = KB_KPS_UNROLL; 
 __device__ __attribute__((always_inline)) inline void kp_small_body(const Dev& d, const OutBuf& ib, const WaveCtl& wc, int32_t r,
                                                                    const OutBuf& nb, uint32_t bid, uint32_t nblk) {
   __shared__ uint32_t s_list[1024], s_nl;
@@ -715,10 +709,8 @@ __global__ __launch_bounds__(1024) void k_kp(Dev d, OutBuf ib, WaveCtl wc, int32
 // index, one workgroup per node, bitonic in LDS (up to SORT_MAX entries; longer ones keep the
 // selection path of k_proc)
 constexpr uint32_t SORT_MAX = 8192;
-#ifndef KB_SORT_GROUPS
-#define KB_SORT_GROUPS 256
-#endif
-constexpr uint32_t SORT_GROUPS = KB_SORT_GROUPS;   // k_sortfast workgroups that sort long inboxes (A/B knob)
+constexpr uint32_t KB_SORT_GROUPS = 256;
+constexpr uint32_t SORT_GROUPS = KB_SORT_GROUPS;   // k_sortfast workgroups that sort long inboxes
 __device__ inline uint32_t sort_max(const Dev& d) { return (d.dbg & KB_DBG_PROC_UNSORTED) ? 64u : SORT_MAX; }
 __device__ __attribute__((always_inline)) inline void sort_body(const Dev& d, const WaveCtl& wc, int32_t r, uint32_t bid,
                                                                uint32_t nblk) {
@@ -946,15 +938,9 @@ __global__ __launch_bounds__(SORTFAST_T) void k_sortfast(Dev d, OutBuf ib, OutBu
   else fast_body(d, ib, ob, wc, r, slow, blockIdx.x - nsort);
 }
 
-#ifndef KB_KPR_BATCH
-#define KB_KPR_BATCH 4        // KPR reply scan: 64-entry log batches in flight per step
-#endif
-#ifndef KB_PROC_MANY
-#define KB_PROC_MANY 1        // batches of >= 8 prologue insertions fold one per lane (0: the whole wave on each)
-#endif
-#ifndef KB_PROC_WPE
-#define KB_PROC_WPE 1         // minimum waves per SIMD k_proc is compiled for (A/B knob; 1 = the compiler's choice)
-#endif
+constexpr uint32_t KB_KPR_BATCH = 4;        // KPR reply scan: 64-entry log batches in flight per step
+constexpr uint32_t KB_PROC_MANY = 1;        // batches of >= 8 prologue insertions fold one per lane (0: the whole wave on each)
+constexpr uint32_t KB_PROC_WPE = 1;         // minimum waves per SIMD k_proc is compiled for (1 = the compiler's choice)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KB_PROC_WPE)))
 void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32_t* list) {
   const int32_t r = round_of(d, r_arg);

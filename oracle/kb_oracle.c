@@ -556,6 +556,7 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   s->ext = (uint8_t*)calloc(C, 1);
   s->cseg = (uint32_t*)calloc(C, 4); s->segmul = (uint32_t*)calloc(C, 4); s->seglen = (uint32_t*)calloc(C, 4);
   s->out = (ovec*)calloc(C, sizeof(ovec)); s->oseq = (uint32_t*)calloc(C, 4);
+  if (cfg->stat_flags & ~(uint32_t)KB_STAT_NO_SF_FAILED_DROPS) { seterr("unknown kb_config.stat_flags"); return KB_INVALID_ARGUMENT; }
   if (cfg->variant & ~(uint32_t)(KB_VARIANT_SAME_WINDOW_BCAST | KB_VARIANT_EXACT_LRU | KB_VARIANT_SPARSE_ROWS)) {
     seterr("unknown variant"); kbo_sim_destroy(s); return KB_INVALID_ARGUMENT;
   }
@@ -740,7 +741,10 @@ static void merge_ext_joins(kbo_sim* s) {
 static void phase_broadcasts(kbo_sim* s, uint32_t i, int32_t r) {
   uint64_t lost = 0, removed = 0;
   /* Failed(p) (src/kaboodle.rs:268-283) */
-  for (size_t k = 0; k < s->nbfail; ++k) {
+  /* socket_faithful Failed changes no state; KB_STAT_NO_SF_FAILED_DROPS skips counting its lost deliveries */
+  const size_t nbf = s->cfg.failed_mode == KB_FAILED_SOCKET_FAITHFUL && (s->cfg.stat_flags & KB_STAT_NO_SF_FAILED_DROPS)
+                         ? 0 : s->nbfail;
+  for (size_t k = 0; k < nbf; ++k) {
     const obcast* b = &s->bfail[k];
     if (b->sender == i) continue;                     /* own broadcasts are not delivered to self */
     if (bcast_lost(s, i, b, r, 0, k)) { lost++; continue; }

@@ -65,21 +65,23 @@ def test_sparse_truncated_join_responses(gpu, name):
     assert ok and st["join_responses"] > 0, f"{name}: {msg}"
 
 
-def partition_case(n: int, every: int, seed: int = 9) -> dict:
+def partition_case(n: int, every: int, seed: int = 9, stat_flags: int = 0) -> dict:
     """configs[4]'s scenario at n peers: converged start, 5 % loss, two halves cut off
     for rounds 3-11, healed at round 12 by every `every`-th peer pinging the other half (ping_addrs), in the
     deployment-faithful reading of Failed."""
     cfg = SimConfig(capacity=n, initial_nodes=n, init_mode=KB_INIT_CONVERGED, loss=0.05, partition_groups=2,
                     partition_start=3, partition_end=12, seed=seed, failed_mode=KB_FAILED_SOCKET_FAITHFUL,
-                    variant=KB_VARIANT_SPARSE_ROWS)
+                    variant=KB_VARIANT_SPARSE_ROWS, stat_flags=stat_flags)
     return {"cfg": cfg, "events": {12: [("ping", i, [(i + n // 2) % n]) for i in range(0, n, every)]}}
 
 
-@pytest.mark.parametrize("n,rounds,every", [(2048, 40, 64), (16384, 30, 256)])
-def test_sparse_partition_heal(gpu, n, rounds, every):
+@pytest.mark.parametrize("n,rounds,every,flags", [(2048, 40, 64, 0), (16384, 30, 256, 0), (2048, 40, 64, 1)],
+                         ids=["2048", "16384", "2048-no-sf-failed-drops"])
+def test_sparse_partition_heal(gpu, n, rounds, every, flags):
     """The partition + heal scenario against the oracle's sparse rows: counters, every fingerprint and per-node
-    scalar each round, sampled whole rows, suspect/curious tables and peer_states."""
-    case = partition_case(n, every)
+    scalar each round, sampled whole rows, suspect/curious tables and peer_states; and with
+    KB_STAT_NO_SF_FAILED_DROPS (the Failed lists' drops not counted) on both."""
+    case = partition_case(n, every, stat_flags=flags)
     o = Sim(parity.oracle_lib(omp=True), case["cfg"])
     g = Sim(gpu, case["cfg"])
     rng = np.random.default_rng(n)

@@ -80,3 +80,28 @@ def test_partition_heal_sparse_socket_faithful():
 def test_sparse_refuses_latency():
     with pytest.raises(Exception):
         Sim(parity.oracle_lib(), SimConfig(capacity=16, initial_nodes=16, variant=SPARSE, track_latency=1))
+
+
+def test_no_sf_failed_drops_changes_only_the_count():
+    """KB_STAT_NO_SF_FAILED_DROPS (kb_config.stat_flags): socket_faithful Failed broadcasts change no state, so
+    skipping the count of their lost deliveries leaves every state byte, fingerprint and counter but drop_bcast
+    as it was; drop_bcast keeps the Join / Probe losses only."""
+    from dataclasses import replace
+    from kaboodle_amd._ffi import KB_STAT_NO_SF_FAILED_DROPS, KB_VARIANT_SPARSE_ROWS
+    base = SimConfig(capacity=600, initial_nodes=512, init_mode=KB_INIT_CONVERGED, loss=0.05, churn=0.002,
+                     partition_groups=2, partition_start=3, partition_end=12, seed=4, failed_mode=KB_FAILED_SOCKET_FAITHFUL)
+    for variant in (0, KB_VARIANT_SPARSE_ROWS):
+        a = Sim(parity.oracle_lib(), replace(base, variant=variant))
+        b = Sim(parity.oracle_lib(), replace(base, variant=variant, stat_flags=KB_STAT_NO_SF_FAILED_DROPS))
+        fewer = 0
+        for r in range(30):
+            a.step(1)
+            b.step(1)
+            sa, sb = parity.state_of(a), parity.state_of(b)
+            da, db = sa["stats"].pop("drop_bcast"), sb["stats"].pop("drop_bcast")
+            assert not parity.diff_states(sa, sb), f"variant {variant} round {r}"
+            assert db <= da
+            fewer += db < da
+        assert fewer > 0 and b.stats()["bcast_failed"] > 0
+        a.close()
+        b.close()

@@ -4,6 +4,10 @@ sparse rows (KB_VARIANT_SPARSE_ROWS) at 4,194,304 peers, with per-round time, ag
 the kernel breakdown and the property checks of tests/test_gpu_sparse_big.py on sampled rows.
 
     python tools/sparse_big.py --nodes 4194304 --rounds 24 --out profiles/r05_sparse_4m.json
+
+Reconvergence after the heal: --fault-end R ends the loss at round R, --until-converged runs until every live
+view's fingerprint equals the true set's (or --rounds / --budget-s), --no-sf-failed-drops skips counting the
+Failed lists' lost deliveries (KB_STAT_NO_SF_FAILED_DROPS: no state changes, drop_bcast excludes them).
 """
 from __future__ import annotations
 
@@ -20,12 +24,14 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def scenario(n: int, every: int = 256, seed: int = 9, row_cap: int = 2048, rounds_part=(3, 12)):
+def scenario(n: int, every: int = 256, seed: int = 9, row_cap: int = 2048, rounds_part=(3, 12), fault_end: int = -1,
+             stat_flags: int = 0):
     from kaboodle_amd._ffi import KB_FAILED_SOCKET_FAITHFUL, KB_INIT_CONVERGED, KB_VARIANT_SPARSE_ROWS, SimConfig
     a, b = rounds_part
     cfg = SimConfig(capacity=n, initial_nodes=n, init_mode=KB_INIT_CONVERGED, loss=0.05, partition_groups=2,
                     partition_start=a, partition_end=b, seed=seed, failed_mode=KB_FAILED_SOCKET_FAITHFUL,
-                    variant=KB_VARIANT_SPARSE_ROWS, sparse_row_cap=row_cap)
+                    variant=KB_VARIANT_SPARSE_ROWS, sparse_row_cap=row_cap, fault_end_round=fault_end,
+                    stat_flags=stat_flags)
     return {"cfg": cfg, "events": {b: [("ping", i, [(i + n // 2) % n]) for i in range(0, n, every)]}}
 
 
@@ -53,11 +59,13 @@ def check_invariants(st: dict, n: int, rounds: int) -> list[str]:
     return out
 
 
-def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: int = 9, verbose: bool = True) -> dict:
+def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: int = 9, verbose: bool = True,
+        fault_end: int = -1, stat_flags: int = 0, until_converged: bool = False, budget_s: float = 0.0,
+        print_every: int = 1, fp_every: int = 4) -> dict:
     import parity
     from kaboodle_amd._ffi import Sim
     lib = parity.gpu_lib()
-    case = scenario(n, every, seed, row_cap)
+    case = scenario(n, every, seed, row_cap, fault_end=fault_end, stat_flags=stat_flags)
     t0 = time.time()
     g = Sim(lib, case["cfg"])
     t_create = time.time() - t0
@@ -65,6 +73,8 @@ def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: in
     rng = np.random.default_rng(seed)
     traj, prev = [], g.stats()
     fails = []
+    heal = case["cfg"].partition_end
+    converged_round, stopped_by, t_start = None, "rounds", time.time()
     for r in range(rounds):
         parity.apply_events((g,), case, r)
         t = time.time()
@@ -76,7 +86,13 @@ def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: in
                "drop_bcast": st["drop_bcast"] - prev["drop_bcast"], "drop_partition": st["drop_partition"] - prev["drop_partition"],
                "sent": sum(st[k] - prev[k] for k in ("sent_ping", "sent_ping_req", "sent_ack", "sent_known_peers", "sent_kpr")),
                "kpr": st["sent_kpr"] - prev["sent_kpr"], "oversize": st["drop_oversize"] - prev["drop_oversize"]}
-        if r % 4 == 3 or r == rounds - 1:
+        done = until_converged and r >= heal and st["agree"] == st["alive"]
+        if done:
+            converged_round, stopped_by = r, "converged"
+        if budget_s and time.time() - t_start > budget_s and not done:
+            stopped_by = "budget"
+        last = done or stopped_by == "budget" or r == rounds - 1
+        if r % fp_every == fp_every - 1 or last:
             fp = g.sparse_footprint()
             rec.update({"exceptions_per_row": round(fp["exceptions"] / n, 3), "stamps_per_row": round(fp["stamps"] / n, 2),
                         "max_row_entries": fp["max_row_entries"], "bytes_per_row": round(fp["bytes"] / n, 1)})
@@ -85,15 +101,21 @@ def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: in
                 if got != want:
                     fails.append(f"round {r} row {i}: fingerprint {got:#x} != generate_fingerprint(peers()) {want:#x}")
         prev = st
-        traj.append(rec)
-        if verbose:
-            print(json.dumps(rec), flush=True)
+        if r % print_every == 0 or last or r <= heal + 2:
+            traj.append(rec)
+            if verbose:
+                print(json.dumps(rec), flush=True)
+        if last:
+            break
+    rounds = r + 1
     st = g.stats()
     fails += check_invariants(st, n, rounds)
     kb = g.kernel_breakdown()
     round_ms, nr = g.kernel_time(1)
     g.close()
-    return {"nodes": n, "rounds": rounds, "row_cap": row_cap, "create_s": round(t_create, 1), "trajectory": traj,
+    return {"nodes": n, "rounds": rounds, "row_cap": row_cap, "create_s": round(t_create, 1), "fault_end_round": fault_end,
+            "stat_flags": stat_flags, "converged_round": converged_round, "stopped_by": stopped_by,
+            "wall_s": round(time.time() - t_start, 1), "trajectory": traj,
             "kernels_ms_per_round": {k: round(v["ms"] / rounds, 3) for k, v in sorted(kb.items(), key=lambda x: -x[1]["ms"])},
             "gpu_round_ms_mean": round(round_ms / max(nr, 1), 2), "final_stats": st, "failures": fails}
 
@@ -106,9 +128,19 @@ def main() -> int:
     ap.add_argument("--row-cap", type=int, default=2048)
     ap.add_argument("--check-rows", type=int, default=4)
     ap.add_argument("--out", default="")
+    ap.add_argument("--fault-end", type=int, default=-1, help="loss ends at this round (-1: never)")
+    ap.add_argument("--until-converged", action="store_true")
+    ap.add_argument("--budget-s", type=float, default=0.0)
+    ap.add_argument("--print-every", type=int, default=1)
+    ap.add_argument("--fp-every", type=int, default=4)
+    ap.add_argument("--no-sf-failed-drops", action="store_true")
     a = ap.parse_args()
-    res = run(a.nodes, a.rounds, a.every, a.row_cap, a.check_rows)
-    res["scenario"] = ("configs[4]: converged start, 5% loss, 2-way partition rounds 3-11, heal at 12 (every "
+    from kaboodle_amd._ffi import KB_STAT_NO_SF_FAILED_DROPS
+    res = run(a.nodes, a.rounds, a.every, a.row_cap, a.check_rows, fault_end=a.fault_end,
+              stat_flags=KB_STAT_NO_SF_FAILED_DROPS if a.no_sf_failed_drops else 0, until_converged=a.until_converged,
+              budget_s=a.budget_s, print_every=a.print_every, fp_every=a.fp_every)
+    res["scenario"] = ("configs[4]: converged start, 5% loss" + (f" until round {a.fault_end}" if a.fault_end >= 0 else "")
+                       + ", 2-way partition rounds 3-11, heal at 12 (every "
                        f"{a.every}th peer pings across), socket_faithful, sparse rows on one MI355X")
     print(json.dumps({k: v for k, v in res.items() if k != "trajectory"}), flush=True)
     if a.out:
