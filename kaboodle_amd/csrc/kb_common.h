@@ -49,8 +49,6 @@ enum : uint32_t { PATH_PHASEB_HBM = 1, PATH_RESP_SCRATCH_SAMPLED = 2, PATH_RESP_
 constexpr int NSEG = 64;          // fingerprint checkpoints per row
 constexpr int ZT = 9;             // LDS nibble tables for Z^0..Z^8
 constexpr int ZB = 9 * 1024;      // byte tables for Z^0..Z^8 (4 lookups per multiply)
-constexpr int ZB10 = 11 * 1024;   // byte tables for Z^0..Z^10 (the decimal-block fold)
-constexpr int DEC_STRIDE = 11;    // dtab entries per decimal block (popcount 0..10)
 
 // Row shards: a shard holds the rows of ids [lo, hi) — the observer state of those
 // peers.  Row-indexed tables are allocated for the local rows only and their pointers are biased by
@@ -94,10 +92,7 @@ struct Dev {
   uint32_t* zpow;                 // Z^k, Z = x^(8L), k in [0, C+1]
   uint32_t* zfin;                 // Z^k * 0xFFFFFFFF (the init term of a k-member fingerprint)
   uint32_t* ztab;                 // [17][8][16] nibble tables of multiplication by Z^c
-  uint32_t* zbtab;                // [11][4][256] byte tables of multiplication by Z^c
-  uint32_t dec;                   // the decimal-block tables hold (records of ids 10q..10q+9 differ in one byte)
-  uint32_t* dtab;                 // [ceil(W/10)][11] A_q·G(k): block q's base record crc0 times Σ_{u<k} Z^u
-  uint32_t* etab;                 // [1024] fold of the one-byte differences e_t of the members of a 10-bit mask
+  uint32_t* zbtab;                // [9][4][256] byte tables of multiplication by Z^c
   uint32_t* htab;                 // [(W/8)][256] crc0 of every member pattern of every 8-id half block
   unsigned long long* stats;
   unsigned long long* sacc;       // [NACC][NSTAT] per-workgroup partial counters, folded into stats on read

@@ -939,7 +939,7 @@ __device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint
 // of e = #later joiners <= select(y + e)).  RESP_U keys per batch: their permutations, block searches and
 // 32-byte block reads are independent, so the loads of a batch are in flight together.
 constexpr uint32_t KB_RESP_U = 4;
-constexpr int RESP_U = KB_RESP_U; 
+constexpr int RESP_U = KB_RESP_U;
 constexpr int RESP_KMAX = 9;          // keys per lane at stride >= 64: cap <= 567 (src/kaboodle.rs:43, :373-383)
 __device__ __attribute__((always_inline)) inline void sampled_fill(uint32_t* pay, uint32_t k_first, uint32_t stride,
                                                                    uint32_t cap, const Prp& P, const uint32_t* B,

@@ -555,32 +555,11 @@ static int upload_segments(kb_sim* s) {
     HIPCHK(hipMemcpy(s->d.zfin, zf.data(), 4ull * (C + 2), hipMemcpyHostToDevice));
   }
   HIPCHK(hipMemcpy(s->d.ztab, ztab.data(), 4ull * ztab.size(), hipMemcpyHostToDevice));
-  std::vector<uint32_t> zb(ZB10);
-  for (uint32_t c = 0; c < 11; ++c)
+  std::vector<uint32_t> zb(ZB);
+  for (uint32_t c = 0; c < 9; ++c)
     for (uint32_t k = 0; k < 4; ++k)
       for (uint32_t v = 0; v < 256; ++v) zb[c * 1024 + k * 256 + v] = multmodp(zpow[c], v << (8 * k));
   HIPCHK(hipMemcpy(s->d.zbtab, zb.data(), 4ull * zb.size(), hipMemcpyHostToDevice));
-  // decimal blocks: ids 10q..10q+9 share their record but for the port's last digit, so with
-  // uniform records crc0(rec_{10q+t}) = A_q ⊕ e_t (crc0 is linear) and a block of k members in mask m folds to
-  // A_q·G(k) ⊕ E(m), G(k) = Σ_{u<k} Z^u: a table per (block, k) and one per mask instead of htab's 256 per 8 ids.
-  // Taken only when every id's record satisfies it (empty identities; default identities differ per id).
-  bool dec = uniform && C >= 10;
-  for (uint32_t j = 0; dec && j < C; ++j) dec = (cseg[j] ^ cseg[j - j % 10]) == (cseg[j % 10] ^ cseg[0]);
-  s->d.dec = dec && !(s->d.dev & 8192) ? 1u : 0u;    // KB_DEV=8192: the htab fold instead (A/B timing; same results)
-  if (dec) {
-    const uint32_t nq = (s->W + 9) / 10;
-    std::vector<uint32_t> G(11, 0), dt((size_t)nq * DEC_STRIDE, 0), et(1024, 0);
-    for (uint32_t k = 1; k <= 10; ++k) G[k] = G[k - 1] ^ zpow[k - 1];
-    for (uint32_t q = 0; q < nq && 10 * q < C; ++q)
-      for (uint32_t k = 1; k <= 10; ++k) dt[(size_t)q * DEC_STRIDE + k] = multmodp(G[k], cseg[10 * q]);
-    for (uint32_t m = 1; m < 1024; ++m) {
-      uint32_t raw = 0;
-      for (uint32_t t = 0; t < 10; ++t) if ((m >> t) & 1u) raw = multmodp(Z, raw) ^ (cseg[t] ^ cseg[0]);
-      et[m] = raw;
-    }
-    HIPCHK(hipMemcpy(s->d.dtab, dt.data(), 4ull * dt.size(), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(s->d.etab, et.data(), 4ull * et.size(), hipMemcpyHostToDevice));
-  }
   const size_t hn = (size_t)(s->W / 8) * 256;
   k_build_htab<<<(unsigned)((hn + 255) / 256), 256>>>(s->d);
   HIPCHK(hipDeviceSynchronize());
@@ -681,7 +660,7 @@ constexpr uint32_t KB_FOLD_WAVES = 16384;                            // fold wav
   AR(d.dirty, 1); A(d.alive, C); A(d.idset, C); A(d.ext, C); A(d.abits, d.NWR); A(d.start_round, C); AR(d.n, 1); AR(d.fp, 1);
   AR(d.last_bcast, 1); AR(d.a3cur, 1); AR(d.susp, SLOTS); AR(d.cur, CSLOTS); AR(d.paq, PAQ);
   AR(d.paq_n, 1); A(d.cseg, C); A(d.segmul, C); A(d.seglen, C); A(d.zpow, (size_t)C + 2); A(d.zfin, (size_t)C + 2);
-  A(d.ztab, 17 * 128); A(d.zbtab, ZB10); A(d.dtab, (size_t)((W + 9) / 10) * DEC_STRIDE); A(d.etab, 1024);
+  A(d.ztab, 17 * 128); A(d.zbtab, ZB);
   A(d.htab, (size_t)(W / 8) * 256); A(d.stats, NSTAT); A(d.sacc, (size_t)NACC * NSTAT); A(d.ctr, NCTR); A(d.truefp, 1); A(d.tfpart, TRUEFP_G);
   AR(d.flog, LOGCAP); AR(d.flog_n, 1); AR(d.fstart, 16); AR(d.kpr_big, 1);
   if (cfg->variant == KB_VARIANT_EXACT_LRU) { AR(d.tst, W); AR(d.tlb, W / 1024); }   // exact A3 instants
@@ -1427,10 +1406,7 @@ static int step_round(kb_sim* s) {
   klaunch(s, KI_TICK_SCAN, k_tick_scan, dim3(gnode), dim3(tb), 0, d, s->bs, r, s->slow);                       // A1; list the A2 nodes
   klaunch(s, KI_TICK_PRE, k_tick_pre, dim3(std::min<uint32_t>(gwave, 1024)), dim3(256), 0, d, o0, s->bs, r, s->slow);   // A2 per listed node
   // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded
-  if (d.uniform) {
-    if (d.dec) klaunch(s, KI_FOLD, k_fold<true>, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
-    else klaunch(s, KI_FOLD, k_fold<false>, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
-  }
+  if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
   if (d.uniform) klaunch(s, KI_FP_ROWS, k_fp_rows, dim3((FP_LANES * R + tb - 1) / tb), dim3(tb), 0, d);
   if (d.tst) klaunch(s, KI_A3_EXACT, k_a3_exact, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);   // exact A3 order
   klaunch(s, KI_TICK_POST, k_tick_post, dim3(gnode), dim3(tb), 0, d, s->ro, o0, r);

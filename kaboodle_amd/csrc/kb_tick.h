@@ -173,51 +173,9 @@ __global__ __launch_bounds__(256) void k_tick_pre(Dev d, OutBuf ob, BcastSlots b
 // ================================================================================================
 struct FoldArgs { uint32_t S; };
 
-// Checkpoint of ids [c0, c1) of one row by decimal blocks (d.dec): per block of ids 10q..10q+9
-// with k members in mask m, raw = raw·Z^k ⊕ dtab[q][k] ⊕ etab[m].  The row's words are re-aligned to the
-// first block's start (one funnel shift per word; words outside the segment read as 0), so 16 blocks take
-// exactly 5 words at compile-time offsets.  zb: Z^0..Z^10 byte tables, et: etab, both in LDS.
-__device__ __attribute__((always_inline)) inline uint2 fold_dec(const Dev& d, const uint32_t* zb, const uint32_t* et,
-                                                               const uint32_t* bw, uint32_t c0, uint32_t c1) {
-  const uint32_t q0 = c0 / 10, qn = (c1 - 1) / 10 + 1 - q0;       // blocks meeting [c0, c1)
-  const uint32_t p = 10 * q0, o = p & 31;                           // stream bit 0 = id p
-  const uint32_t wlo = c0 >> 5, whi = c1 >> 5;                      // the segment's words
-  uint32_t wi = p >> 5;                                             // next raw word to read
-  auto word = [&](uint32_t k) __attribute__((always_inline)) -> uint32_t { return k >= wlo && k < whi ? bw[k] : 0u; };
-  uint32_t prev = word(wi++);
-  uint32_t raw = 0, cnt = 0;
-  const uint32_t* dq = d.dtab + (size_t)q0 * DEC_STRIDE;
-  for (uint32_t b0 = 0; b0 < qn; b0 += 16) {
-    uint32_t s5[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {                                   // 160 stream bits = blocks b0..b0+15
-      const uint32_t nx = word(wi++);
-      s5[k] = __builtin_amdgcn_alignbit(nx, prev, o);
-      prev = nx;
-    }
-#pragma unroll
-    for (int b = 0; b < 16; ++b) {
-      if (b0 + b >= qn) break;                                      // wave-uniform
-      const int bit = 10 * b, w = bit >> 5, sh = bit & 31;          // compile-time: 10b + 9 < 160
-      const uint32_t m = (sh <= 22 ? (s5[w] >> sh) : __builtin_amdgcn_alignbit(s5[(w + 1) % 5], s5[w], sh)) & 0x3FFu;
-      const uint32_t k = __popc(m);
-      raw = mulzb(zb, raw, k) ^ dq[(b0 + b) * DEC_STRIDE + k] ^ et[m];
-      cnt += k;
-    }
-  }
-  return make_uint2(raw, cnt);
-}
-
-template <bool DEC>
 __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
-  __shared__ uint32_t zb[DEC ? ZB10 + 1024 : ZB];
-  if (DEC) {
-    for (uint32_t k = threadIdx.x; k < ZB10; k += blockDim.x) zb[k] = d.zbtab[k];
-    for (uint32_t k = threadIdx.x; k < 1024; k += blockDim.x) zb[ZB10 + k] = d.etab[k];
-    __syncthreads();
-  } else {
-    load_zbtab(d, zb);
-  }
+  __shared__ uint32_t zb[ZB];
+  load_zbtab(d, zb);
   const uint32_t S = fa.S;
   const uint32_t s = blockIdx.x % S;
   const uint32_t g = (blockIdx.x / S) * 4 + (threadIdx.x >> 6);
@@ -238,11 +196,6 @@ __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
       const bool mine = (sd >> k) & 1ull;
       if (!__ballot(mine)) continue;                  // wave-uniform: no row of this wave changed here
       const uint32_t c0 = k * d.SEGW, c1 = c0 + d.SEGW;
-      if (DEC) {
-        const uint2 sp = fold_dec(d, zb, zb + ZB10, bw, c0, c1);
-        if (mine) { d.segp[(size_t)i * NSEG + k] = sp; folded |= 1ull << k; nbytes += d.SEGW / 8; }
-        continue;
-      }
       uint32_t raw = 0, cnt = 0;
       uint4 mb = *reinterpret_cast<const uint4*>(bw + (c0 >> 5));
       for (uint32_t col = c0; col < c1; col += 128) {
@@ -278,7 +231,7 @@ __global__ __launch_bounds__(256) void k_fold(Dev d, FoldArgs fa) {
 // several lanes gives the SIMDs that many times the waves to hide its latency with.  Runs after
 // k_fold; k_tick_post then finds the row clean.
 constexpr uint32_t KB_FP_LANES = 8;
-constexpr uint32_t FP_LANES = KB_FP_LANES; 
+constexpr uint32_t FP_LANES = KB_FP_LANES;
 __global__ __launch_bounds__(256) void k_fp_rows(Dev d) {
   constexpr uint32_t PER = NSEG / FP_LANES;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;

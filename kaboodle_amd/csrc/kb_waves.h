@@ -598,7 +598,7 @@ __device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d
 // k_kp's last nblk workgroups: at least one per CU, since a round of the converged start's first
 // SHARE_AGE rounds delivers ~24K replies of a few hundred ids at 64K peers in one wave.)
 constexpr uint32_t KB_KPS_UNROLL = 4;
-constexpr int KPS_UNROLL = KB_KPS_UNROLL; 
+constexpr int KPS_UNROLL = KB_KPS_UNROLL;
 __device__ __attribute__((always_inline)) inline void kp_small_body(const Dev& d, const OutBuf& ib, const WaveCtl& wc, int32_t r,
                                                                    const OutBuf& nb, uint32_t bid, uint32_t nblk) {
   __shared__ uint32_t s_list[1024], s_nl;
