@@ -106,10 +106,11 @@ def pmc_summary(cfg_key: str, capacity: int, steps: int, warmup: int, failed_mod
     return best, src
 
 
-def committed_tail(cfg_key: str, mode: str):
+def committed_tail(cfg_key: str, mode: str, a3_order: str = "window"):
     """The full quiescent tail of this workload (tools/converge.py, run to agreement or a cap of 2-4 N rounds
     on an MI355X; profiles/*converge*.json): too long for the bench's minutes, so read from the record —
-    only a record made with this very library build (lib_sha16), like pmc_summary."""
+    only a record made with this very library build (lib_sha16), like pmc_summary.  a3_order "exact": the
+    same tail with A3 in the reference's exact-instant order (KB_VARIANT_EXACT_LRU)."""
     best = None
     sha = lib_sha16()
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*converge*.json"))):
@@ -117,7 +118,8 @@ def committed_tail(cfg_key: str, mode: str):
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if d.get("workload", "").startswith(cfg_key) and d.get("failed_mode") == mode and d.get("lib_sha16") == sha:
+        if (d.get("workload", "").startswith(cfg_key) and d.get("failed_mode") == mode and d.get("lib_sha16") == sha
+                and d.get("a3_order", "window") == a3_order):
             best = {k: d[k] for k in ("converged_round", "tail_rounds_to_converge", "tail_rounds_run", "cap_rounds",
                                       "stopped_by") if k in d}
             best["source"] = os.path.relpath(p, ROOT)
@@ -416,7 +418,8 @@ def main() -> int:
                 "value": alive2 / dt2, "ms_per_step": dt2 / a.steps * 1e3,
                 "round_model_frac": round(rb2 / (dt2 / a.steps) / 1e9 / HBM_PEAK_GBS, 4),
                 "agree_frac_at_fault_end": round(s21["agree"] / max(s21["alive"], 1), 4),
-                "workload_full_tail": committed_tail(f"configs[2]: {a.nodes} peers", "socket_faithful")}}
+                "workload_full_tail": committed_tail(f"configs[2]: {a.nodes} peers", "socket_faithful"),
+                "workload_full_tail_exact_lru": committed_tail(f"configs[2]: {a.nodes} peers", "socket_faithful", "exact")}}
     seeds = None
     if world == 1 and a.seeds:
         # seeds 2 and 3 of the same synthetic workload, same K and W, each its own mesh
