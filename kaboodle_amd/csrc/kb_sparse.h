@@ -45,12 +45,13 @@ constexpr uint32_t SP_ACC = 1024;                 // per-workgroup accumulation 
 
 struct SpDev {
   uint32_t C, ECAP, nb;                           // ids, entries per row, |base|
+  uint32_t ESTR;                                  // row stride: ECAP rounded up to 4 (16-byte aligned rows)
   uint32_t k0, k1, loss_thr, churn_thr;
   int32_t fault_end;
   uint32_t failed_mode, pgroups;
   int32_t pstart, pend;
   uint32_t uniform, L, capk, capj;
-  uint32_t* ent;                                  // [C][ECAP] sorted packed entries
+  uint32_t* ent;                                  // [C][ESTR] sorted packed entries
   uint32_t* ne;                                   // [C] entries in use
   uint8_t* based;                                 // [C] members = base Δ x (1) or x (0)
   uint32_t* n; uint32_t* fp; uint8_t* dirty; int32_t* last_bcast; uint32_t* a3cur;
@@ -78,7 +79,34 @@ __device__ inline bool sp_part(const SpDev& d, int32_t r, uint32_t a, uint32_t b
   return ((uint64_t)a * d.pgroups / d.C) != ((uint64_t)b * d.pgroups / d.C);
 }
 __device__ inline bool sp_bbit(const SpDev& d, uint32_t j) { return (d.bbits[j >> 5] >> (j & 31)) & 1u; }
-__device__ inline uint32_t* sp_row(const SpDev& d, uint32_t i) { return d.ent + (size_t)i * d.ECAP; }
+__device__ inline uint32_t* sp_row(const SpDev& d, uint32_t i) { return d.ent + (size_t)i * d.ESTR; }
+// a row's entries e[k..n) move up one place and v lands at e[k] (insertion; n < ESTR), in 16-byte steps from the
+// top of the row's aligned groups down (a thread per row: a quarter of the memory instructions of a word loop)
+__device__ inline void sp_ins_at(uint32_t* e, uint32_t k, uint32_t n, uint32_t v) {
+  uint4* e4 = reinterpret_cast<uint4*>(e);
+  const uint32_t gk = k >> 2, kk = k & 3u;
+  uint32_t g = n >> 2;
+  uint4 cur = e4[g];
+  for (; g > gk; --g) {
+    const uint4 lo = e4[g - 1];
+    e4[g] = make_uint4(lo.w, cur.x, cur.y, cur.z);
+    cur = lo;
+  }
+  e4[gk] = make_uint4(kk == 0 ? v : cur.x, kk < 1 ? cur.x : (kk == 1 ? v : cur.y),
+                      kk < 2 ? cur.y : (kk == 2 ? v : cur.z), kk < 3 ? cur.z : (kk == 3 ? v : cur.w));
+}
+// e[k] leaves: e[k+1..n) move down one place (removal), the same 16-byte steps upward
+__device__ inline void sp_del_at(uint32_t* e, uint32_t k, uint32_t n) {
+  uint4* e4 = reinterpret_cast<uint4*>(e);
+  const uint32_t gk = k >> 2, gl = (n - 1) >> 2, kk = k & 3u;
+  uint4 cur = e4[gk];
+  for (uint32_t g = gk; g <= gl; ++g) {
+    const uint4 nx = g < gl ? e4[g + 1] : make_uint4(0, 0, 0, 0);
+    const uint32_t lo = g == gk ? kk : 0u;                   // words below k keep their place
+    e4[g] = make_uint4(lo > 0 ? cur.x : cur.y, lo > 1 ? cur.y : cur.z, lo > 2 ? cur.z : cur.w, nx.x);
+    cur = nx;
+  }
+}
 __device__ inline uint32_t sp_word(const U4& w, uint32_t k) { return k == 0 ? w.x : k == 1 ? w.y : k == 2 ? w.z : w.w; }
 // first entry index whose id is >= j (entries are id << 9 | low bits, so e < j << 9 iff its id < j)
 __device__ inline uint32_t sp_lb(const uint32_t* e, uint32_t n, uint32_t j) {
@@ -137,14 +165,13 @@ __device__ inline void sp_put(const SpDev& d, uint32_t i, uint32_t j, uint8_t b,
   uint32_t* e = sp_row(d, i);
   const uint32_t n = d.ne[i];
   if (!xf && !eb) {
-    if (l.has) { for (uint32_t q = l.k; q + 1 < n; ++q) e[q] = e[q + 1]; d.ne[i] = n - 1; }
+    if (l.has) { sp_del_at(e, l.k, n); d.ne[i] = n - 1; }
     return;
   }
   const uint32_t v = (j << 9) | (xf ? SP_XF : 0u) | eb;
   if (l.has) { e[l.k] = v; return; }
   if (n >= d.ECAP) { sp_err(d, DERR_SPARSE); return; }
-  for (uint32_t q = n; q > l.k; --q) e[q] = e[q - 1];
-  e[l.k] = v;
+  sp_ins_at(e, l.k, n, v);
   d.ne[i] = n + 1;
 }
 

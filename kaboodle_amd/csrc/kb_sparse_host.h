@@ -195,6 +195,7 @@ static int sp_create(const kb_config* cfg, SpSim** out) {
   SpDev& d = S->d;
   d.C = C;
   d.ECAP = cfg->sparse_row_cap ? std::min<uint32_t>(cfg->sparse_row_cap, C) : std::min<uint32_t>(C, 4096u);
+  d.ESTR = (d.ECAP + 3u) & ~3u;
   d.nb = cfg->init_mode == KB_INIT_CONVERGED ? cfg->initial_nodes : 0u;
   d.k0 = (uint32_t)cfg->seed; d.k1 = (uint32_t)(cfg->seed >> 32);
   d.loss_thr = cfg->loss_threshold; d.churn_thr = cfg->churn_threshold; d.fault_end = cfg->fault_end_round;
@@ -209,7 +210,7 @@ static int sp_create(const kb_config* cfg, SpSim** out) {
   for (uint32_t j = 0; j < C; ++j) default_identity(j, Lid, &S->h_ident[(size_t)j * MAXID]);
   hipError_t e = hipSuccess;
 #define SA(ptr, n) if (e == hipSuccess) e = sp_alloc(S, &(ptr), (n))
-  SA(d.ent, (size_t)C * d.ECAP); SA(d.ne, C); SA(d.based, C); SA(d.n, C); SA(d.fp, C); SA(d.dirty, C);
+  SA(d.ent, (size_t)C * d.ESTR); SA(d.ne, C); SA(d.based, C); SA(d.n, C); SA(d.fp, C); SA(d.dirty, C);
   SA(d.last_bcast, C); SA(d.a3cur, C); SA(d.susp, (size_t)C * SLOTS); SA(d.cur, (size_t)C * CSLOTS);
   SA(d.paq, (size_t)C * PAQ); SA(d.paq_n, C); SA(d.alive, C); SA(d.start_round, C); SA(d.idset, C); SA(d.ext, C);
   SA(d.cseg, C); SA(d.segmul, C); SA(d.seglen, C); SA(d.bbits, C / 32 + 1); SA(d.bcnt, (size_t)C + 1);
@@ -515,7 +516,7 @@ static int sp_entries(SpSim* S, uint32_t node, std::vector<uint32_t>& e, uint8_t
   HIPCHK(hipMemcpy(&n, S->d.ne + node, 4, hipMemcpyDeviceToHost));
   HIPCHK(hipMemcpy(based, S->d.based + node, 1, hipMemcpyDeviceToHost));
   e.resize(n);
-  if (n) HIPCHK(hipMemcpy(e.data(), S->d.ent + (size_t)node * S->d.ECAP, 4ull * n, hipMemcpyDeviceToHost));
+  if (n) HIPCHK(hipMemcpy(e.data(), S->d.ent + (size_t)node * S->d.ESTR, 4ull * n, hipMemcpyDeviceToHost));
   return KB_OK;
 }
 static int sp_read_row(SpSim* S, uint32_t node, std::vector<uint8_t>& rw) {   // canonical bytes (0 = not a member)
@@ -927,15 +928,15 @@ static int sp_footprint(SpSim* S, uint64_t* out, size_t cap) {
   out[0] = nb; out[1] = 0; out[2] = 0; out[3] = mx; out[4] = 4 * tot; out[5] = C;
   // exceptions / explicit stamps: counted over the entries of a bounded sample of rows would be approximate;
   // count them exactly on the host in chunks
-  const size_t chunk = std::max<size_t>(1, (size_t)(256u << 20) / (4ull * S->d.ECAP));
+  const size_t chunk = std::max<size_t>(1, (size_t)(256u << 20) / (4ull * S->d.ESTR));
   std::vector<uint32_t> buf;
   for (uint32_t i0 = 0; i0 < C; i0 += (uint32_t)chunk) {
     const uint32_t i1 = (uint32_t)std::min<size_t>(C, i0 + chunk);
-    buf.resize((size_t)(i1 - i0) * S->d.ECAP);
-    HIPCHK(hipMemcpy(buf.data(), S->d.ent + (size_t)i0 * S->d.ECAP, 4ull * buf.size(), hipMemcpyDeviceToHost));
+    buf.resize((size_t)(i1 - i0) * S->d.ESTR);
+    HIPCHK(hipMemcpy(buf.data(), S->d.ent + (size_t)i0 * S->d.ESTR, 4ull * buf.size(), hipMemcpyDeviceToHost));
     for (uint32_t i = i0; i < i1; ++i)
       for (uint32_t q = 0; q < ne[i]; ++q) {
-        const uint32_t x = buf[(size_t)(i - i0) * S->d.ECAP + q];
+        const uint32_t x = buf[(size_t)(i - i0) * S->d.ESTR + q];
         out[1] += (x & SP_XF) != 0; out[2] += (x & 255u) != 0;
       }
   }
