@@ -94,7 +94,8 @@ def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: in
         last = done or stopped_by == "budget" or r == rounds - 1
         if r % fp_every == fp_every - 1 or last:
             fp = g.sparse_footprint()
-            rec.update({"exceptions_per_row": round(fp["exceptions"] / n, 3), "stamps_per_row": round(fp["stamps"] / n, 2),
+            rec.update({"entries": fp["exceptions"] + fp["stamps"],
+                        "exceptions_per_row": round(fp["exceptions"] / n, 3), "stamps_per_row": round(fp["stamps"] / n, 2),
                         "max_row_entries": fp["max_row_entries"], "bytes_per_row": round(fp["bytes"] / n, 1)})
             for i in rng.choice(n, check_rows, replace=False):
                 got, want = fp_of_peers(g, lib, int(i))
@@ -110,12 +111,27 @@ def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: in
     rounds = r + 1
     st = g.stats()
     fails += check_invariants(st, n, rounds)
+    # a bench-style line for this layout: peer-rounds/s over the run, and the HBM roofline of the
+    # layout's own algorithmic bytes per round — every row's entry list read once (4 B per entry, the sampled
+    # footprints' mean), 32 B per message record, 4 B per KnownPeers payload id
+    wall = sum(t["ms"] for t in traj if "ms" in t and t["round"] >= 0) / 1e3
+    nrec = sum(t.get("sent", 0) for t in traj)
+    ents = [t["entries"] for t in traj if "entries" in t]
+    b_round = (4.0 * (sum(ents) / len(ents) if ents else 0.0) + 32.0 * nrec / max(len(traj), 1)
+               + 4.0 * st["sent_kp_ids"] / rounds)
+    ms_round = wall * 1e3 / max(len(traj), 1)
+    bench_line = {"metric": "simulated peer-rounds/sec", "value": n * len(traj) / wall if wall else None,
+                  "unit": "peer-rounds/s", "ms_per_round": round(ms_round, 3), "rounds_timed": len(traj),
+                  "roofline": {"bound": "hbm", "bytes_per_round": int(b_round),
+                               "achieved": round(b_round / (ms_round / 1e3) / 1e9, 1) if ms_round else None,
+                               "peak": 8000.0, "unit": "GB/s",
+                               "frac": round(b_round / (ms_round / 1e3) / 8e12, 4) if ms_round else None}}
     kb = g.kernel_breakdown()
     round_ms, nr = g.kernel_time(1)
     g.close()
     return {"nodes": n, "rounds": rounds, "row_cap": row_cap, "create_s": round(t_create, 1), "fault_end_round": fault_end,
             "stat_flags": stat_flags, "converged_round": converged_round, "stopped_by": stopped_by,
-            "wall_s": round(time.time() - t_start, 1), "trajectory": traj,
+            "wall_s": round(time.time() - t_start, 1), "bench_line": bench_line, "trajectory": traj,
             "kernels_ms_per_round": {k: round(v["ms"] / rounds, 3) for k, v in sorted(kb.items(), key=lambda x: -x[1]["ms"])},
             "gpu_round_ms_mean": round(round_ms / max(nr, 1), 2), "final_stats": st, "failures": fails}
 
