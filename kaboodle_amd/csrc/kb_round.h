@@ -237,17 +237,29 @@ __global__ void k_churn_leave(Dev d, int32_t r) {
 // churn joins take fresh ids in order: an id some instance bound (started through the API, a restart's new
 // address) or given an identity is skipped.  The round's few dozen joins run in one thread.
 __global__ void k_churn_join(Dev d, int32_t r) {
-  if (threadIdx.x || blockIdx.x) return;
-  const uint32_t leaves = d.ctr[C_LEAVES];
+  // one wave: the fresh ids (never bound, no identity set: the oracle's serial walk) are found 64 at a time by
+  // a ballot and started in parallel, in id order, as many as peers left
+  if (blockIdx.x || threadIdx.x >= 64) return;
+  const uint32_t l = threadIdx.x, leaves = d.ctr[C_LEAVES];
   uint32_t nf = d.ctr[C_NEXTFREE], joins = 0;
-  for (uint32_t k = 0; k < leaves; ++k) {
-    while (nf < d.C && (d.start_round[nf] != NONE_ROUND || d.idset[nf])) nf++;
-    if (nf >= d.C) break;
-    node_start(d, nf++, r);
-    joins++;
+  while (joins < leaves && nf < d.C) {
+    const uint32_t j = nf + l, need = leaves - joins;
+    const bool fresh = j < d.C && d.start_round[j] == NONE_ROUND && !d.idset[j];
+    const unsigned long long fm = __ballot(fresh);
+    const uint32_t rank = __popcll(fm & ((1ull << l) - 1ull)), nfresh = __popcll(fm);
+    if (fresh && rank < need) node_start(d, j, r);
+    if (nfresh >= need) {                                   // the need-th fresh id was the last one started
+      nf += (uint32_t)__ffsll((long long)__ballot(fresh && rank == need - 1));   // one past it
+      joins = leaves;
+    } else {
+      nf += 64;
+      joins += nfresh;
+    }
   }
-  d.ctr[C_NEXTFREE] = nf; d.ctr[C_LEAVES] = 0;
-  if (d.lo == 0) { d.stats[S_CLEAVE] += leaves; d.stats[S_CJOIN] += joins; }   // replicated: counted once
+  if (l == 0) {
+    d.ctr[C_NEXTFREE] = nf < d.C ? nf : d.C; d.ctr[C_LEAVES] = 0;
+    if (d.lo == 0) { d.stats[S_CLEAVE] += leaves; d.stats[S_CJOIN] += joins; }   // replicated: counted once
+  }
 }
 
 // ---- running set bitset + count, and its fingerprint (what a converged node reports) -----------
