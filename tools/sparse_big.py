@@ -62,9 +62,10 @@ def check_invariants(st: dict, n: int, rounds: int) -> list[str]:
 def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: int = 9, verbose: bool = True,
         fault_end: int = -1, stat_flags: int = 0, until_converged: bool = False, budget_s: float = 0.0,
         print_every: int = 1, fp_every: int = 4) -> dict:
+    import kaboodle_amd
     import parity
     from kaboodle_amd._ffi import Sim
-    lib = parity.gpu_lib()
+    lib = kaboodle_amd.lib()                                  # honours KB_LIB_PATH (A/B builds)
     case = scenario(n, every, seed, row_cap, fault_end=fault_end, stat_flags=stat_flags)
     t0 = time.time()
     g = Sim(lib, case["cfg"])
