@@ -113,6 +113,26 @@ class Mesh {
   };
   Peer peer(uint32_t id) const { return Peer(h_, id); }
 
+  // real instances in the mesh: an external peer's records out, its datagrams in
+  struct Record { kb_unicast rec; std::vector<uint32_t> ids; };
+  void set_external(uint32_t id) { check(kb_sim_set_external(h_, id), "kb_sim_set_external"); }
+  void inject(const kb_unicast& rec, const std::vector<uint32_t>& ids = {}) {
+    kb_unicast m = rec;
+    m.pay_len = (uint32_t)ids.size();
+    check(kb_sim_inject(h_, &m, ids.empty() ? nullptr : ids.data()), "kb_sim_inject");
+  }
+  std::vector<Record> exported() {                    // drains: (round, wave, sender, seq) order
+    size_t n = 0, ni = 0;
+    check(kb_sim_exported(h_, nullptr, 0, &n, nullptr, 0, &ni), "kb_sim_exported");
+    std::vector<kb_unicast> v(n);
+    std::vector<uint32_t> ids(ni);
+    check(kb_sim_exported(h_, v.data(), v.size(), &n, ids.data(), ids.size(), &ni), "kb_sim_exported");
+    std::vector<Record> out;
+    for (size_t k = 0; k < n; ++k)
+      out.push_back({v[k], std::vector<uint32_t>(ids.begin() + v[k].pay_off, ids.begin() + v[k].pay_off + v[k].pay_len)});
+    return out;
+  }
+
  private:
   kb_sim* h_ = nullptr;
 };

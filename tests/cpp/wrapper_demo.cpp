@@ -26,6 +26,19 @@ int main(int argc, char** argv) {
     printf("events 0: disc %zu dep %zu changed %d fp %08x\n", ev.discovered.size(), ev.departed.size(),
            (int)ev.fingerprint_changed, ev.fingerprint);
     for (uint32_t i = 0; i < 4; ++i) printf("peer %u fp %08x n %zu\n", i, m.peer(i).fingerprint(), m.peer(i).peers().size());
+    // an external peer (a real instance behind a bridge): its Ping in, the Ack out
+    kb_config c2 = kb::Mesh::defaults();
+    c2.capacity = 8; c2.initial_nodes = 4; c2.init_mode = KB_INIT_CONVERGED;
+    kb::Mesh x(c2);
+    x.set_external(6);
+    x.step(1);
+    kb_unicast ping{};
+    ping.sender = 6; ping.dest = 1; ping.kind = KB_WIRE_PING;
+    x.inject(ping);
+    x.step(1);
+    size_t acks = 0;
+    for (const auto& r : x.exported()) acks += r.rec.dest == 6 && r.rec.sender == 1 && r.rec.kind == KB_WIRE_ACK;
+    printf("external acks %zu\n", acks);
     printf("mesh ok\n");
   } catch (const kb::Error& e) {
     printf("error %d %s\n", e.code, e.what());

@@ -42,3 +42,4 @@ def test_wrapper_on_gpu(tmp_path):
     out = subprocess.run([build(tmp_path), "--gpu"], capture_output=True, text=True, check=True).stdout
     assert out.count("fp 981285c8") == 5 and "mesh ok" in out
     assert "events 0: disc 4 dep 0 changed 1 fp 981285c8" in out
+    assert "external acks 1" in out                # kb_sim_set_external / kb_sim_inject / kb_sim_exported
