@@ -99,34 +99,34 @@ __host__ __device__ inline uint8_t enc(int32_t t, int32_t r) {
 
 // ---- wave helpers (wave64) ---------------------------------------------------------------------
 __device__ inline uint32_t lane() { return __lane_id(); }
-__device__ inline uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Cross-lane scans and reductions by DPP (VALU data movement inside and across the four 16-lane rows): no
+// LDS instruction and no LDS round trip per step, which the ds_bpermute forms (__shfl_*) cost — each of their
+// six steps waited on the LDS pipe.  Lanes that are inactive contribute the operation's identity; the
+// reductions return the value of the last active lane's inclusive scan, broadcast (wave-uniform).
+template <uint32_t ID, typename Op>
+__device__ __attribute__((always_inline)) inline uint32_t wave_iscan(uint32_t x, Op op) {
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)x, 0x111, 0xF, 0xF, false));   // row_shr:1
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)x, 0x112, 0xF, 0xF, false));   // row_shr:2
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)x, 0x114, 0xF, 0xF, false));   // row_shr:4
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)x, 0x118, 0xF, 0xF, false));   // row_shr:8
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)x, 0x142, 0xA, 0xF, false));   // row_bcast:15
+  x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)x, 0x143, 0xC, 0xF, false));   // row_bcast:31
+  return x;
 }
-__device__ inline uint32_t wave_min(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { uint32_t t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
-  return v;
+__device__ __attribute__((always_inline)) inline uint32_t wave_last(uint32_t x) {
+  const unsigned long long ex = __builtin_amdgcn_read_exec();
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63 - __builtin_clzll(ex));
 }
-__device__ inline uint32_t wave_max(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { uint32_t t = __shfl_xor(v, o, 64); v = t > v ? t : v; }
-  return v;
-}
-__device__ inline uint32_t wave_or(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
-  return v;
-}
+struct OpAdd { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; } };
+struct OpMin { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a < b ? a : b; } };
+struct OpMax { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; } };
+struct OpOr { __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return a | b; } };
+__device__ inline uint32_t wave_sum(uint32_t v) { return wave_last(wave_iscan<0u>(v, OpAdd{})); }
+__device__ inline uint32_t wave_min(uint32_t v) { return wave_last(wave_iscan<0xFFFFFFFFu>(v, OpMin{})); }
+__device__ inline uint32_t wave_max(uint32_t v) { return wave_last(wave_iscan<0u>(v, OpMax{})); }
+__device__ inline uint32_t wave_or(uint32_t v) { return wave_last(wave_iscan<0u>(v, OpOr{})); }
 // exclusive prefix sum across the 64 lanes
-__device__ inline uint32_t wave_excl(uint32_t v) {
-  const uint32_t l = lane();
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) { uint32_t t = __shfl_up(x, o, 64); if (l >= (uint32_t)o) x += t; }
-  return x - v;
-}
+__device__ inline uint32_t wave_excl(uint32_t v) { return wave_iscan<0u>(v, OpAdd{}) - v; }
 // s_waitcnt lgkmcnt(0) only (gfx9 encoding: vmcnt 63, expcnt 7): LDS/SMEM done, memory ops may fly
 __device__ inline void wait_lds() { __builtin_amdgcn_s_waitcnt(0xC07F); }
 __device__ inline uint32_t bcast(uint32_t v, int src) { return __shfl(v, src, 64); }
