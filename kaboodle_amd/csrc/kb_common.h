@@ -290,28 +290,30 @@ __device__ inline void l1_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "
 // fingerprint of row i by one wave: refold the stale checkpoints (lane k <-> segment k), then an
 // ordered tree combine of the 64 checkpoints.  `extra` = segments changed by the caller and not yet
 // recorded in sdirty.  Returns the same value in every lane.
-// Wave-wide combine of per-lane (raw, cnt) pieces in lane order; lane 0 ends with the total.  The
-// subtree counts of all six levels are formed first so the six Z^cnt loads are in flight together.
+// Wave-wide combine of per-lane (raw, cnt) pieces in lane order; every lane ends with the total.  The tree's
+// four levels inside each 16-lane row move data by DPP (no LDS round trip), their counts first so the four
+// Z^cnt loads are in flight together; the four row totals are then combined from scalar registers.
 __device__ inline void wave_combine(const Dev& d, uint32_t& raw, uint32_t& cnt) {
   const uint32_t l = lane();
-  uint32_t oc[6], zp[6];
+  uint32_t oc[4], zp[4];
   uint32_t c = cnt;
+  oc[0] = dpp_shl<1>(c); if ((l & 1) == 0) c += oc[0];
+  oc[1] = dpp_shl<2>(c); if ((l & 3) == 0) c += oc[1];
+  oc[2] = dpp_shl<4>(c); if ((l & 7) == 0) c += oc[2];
+  oc[3] = dpp_shl<8>(c); if ((l & 15) == 0) c += oc[3];
+  const uint32_t c0 = rdl(c, 0), c1 = rdl(c, 16), c2 = rdl(c, 32), c3 = rdl(c, 48);
+  auto zpw = [&](uint32_t k) __attribute__((always_inline)) { return d.uniform ? d.zpow[k <= d.C ? k : 0] : xpow8_dev(k); };
 #pragma unroll
-  for (int t = 0; t < 6; ++t) {
-    const uint32_t st = 1u << t;
-    oc[t] = __shfl_down(c, st, 64);
-    if ((l & (2 * st - 1)) == 0 && l + st < 64) c += oc[t];
-  }
-#pragma unroll
-  for (int t = 0; t < 6; ++t) zp[t] = d.uniform ? d.zpow[oc[t] <= d.C ? oc[t] : 0] : 0u;
-#pragma unroll
-  for (int t = 0; t < 6; ++t) {
-    const uint32_t st = 1u << t;
-    const uint32_t oraw = __shfl_down(raw, st, 64);
-    if ((l & (2 * st - 1)) == 0 && l + st < 64)
-      raw = multmodp(d.uniform ? zp[t] : xpow8_dev(oc[t]), raw) ^ oraw;
-  }
-  cnt = c;
+  for (int t = 0; t < 4; ++t) zp[t] = zpw(oc[t]);
+  const uint32_t z1 = zpw(c1), z3 = zpw(c3), z23 = zpw(c2 + c3);
+  uint32_t o;
+  o = dpp_shl<1>(raw); if ((l & 1) == 0) raw = multmodp(zp[0], raw) ^ o;
+  o = dpp_shl<2>(raw); if ((l & 3) == 0) raw = multmodp(zp[1], raw) ^ o;
+  o = dpp_shl<4>(raw); if ((l & 7) == 0) raw = multmodp(zp[2], raw) ^ o;
+  o = dpp_shl<8>(raw); if ((l & 15) == 0) raw = multmodp(zp[3], raw) ^ o;
+  const uint32_t r0 = rdl(raw, 0), r1 = rdl(raw, 16), r2 = rdl(raw, 32), r3 = rdl(raw, 48);
+  raw = multmodp(z23, multmodp(z1, r0) ^ r1) ^ (multmodp(z3, r2) ^ r3);
+  cnt = c0 + c1 + c2 + c3;
 }
 
 // Checkpoint of segment `lane` of row i with the stale ones (sd) refolded and stored: one per lane when
@@ -331,7 +333,7 @@ __device__ __attribute__((always_inline)) inline uint2 refold_stale(const Dev& d
       const uint32_t h0 = k * nh + (l * nh) / 64, h1 = k * nh + ((l + 1) * nh) / 64;
       for (uint32_t h = h0; h < h1; ++h) fold_half(d, ztab, h, hb[h], raw, cnt);
       wave_combine(d, raw, cnt);
-      raw = bcast(raw, 0); cnt = bcast(cnt, 0);
+      raw = rdl(raw, 0); cnt = rdl(cnt, 0);
       if (l == k) { sp = make_uint2(raw, cnt); d.segp[(size_t)i * NSEG + k] = sp; }
     }
   } else if ((sd >> l) & 1ull) {
@@ -350,7 +352,7 @@ __device__ __attribute__((always_inline)) inline uint32_t wave_fp(const Dev& d, 
   const uint2 sp = refold_stale(d, ztab, i, sd);
   uint32_t raw = sp.x, cnt = sp.y;
   wave_combine(d, raw, cnt);
-  raw = bcast(raw, 0); cnt = bcast(cnt, 0);
+  raw = rdl(raw, 0); cnt = rdl(cnt, 0);
   if (l == 0 && sd) atomicAnd(&d.sdirty[i], ~sd);
   return finish_fp(d, raw, cnt);
 }

@@ -125,11 +125,18 @@ __device__ inline uint32_t wave_sum(uint32_t v) { return wave_last(wave_iscan<0u
 __device__ inline uint32_t wave_min(uint32_t v) { return wave_last(wave_iscan<0xFFFFFFFFu>(v, OpMin{})); }
 __device__ inline uint32_t wave_max(uint32_t v) { return wave_last(wave_iscan<0u>(v, OpMax{})); }
 __device__ inline uint32_t wave_or(uint32_t v) { return wave_last(wave_iscan<0u>(v, OpOr{})); }
+// lane l + ST's value inside l's 16-lane row, 0 past the row's end (DPP row_shl)
+template <uint32_t ST> __device__ __attribute__((always_inline)) inline uint32_t dpp_shl(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + ST, 0xF, 0xF, false);
+}
 // exclusive prefix sum across the 64 lanes
 __device__ inline uint32_t wave_excl(uint32_t v) { return wave_iscan<0u>(v, OpAdd{}) - v; }
 // s_waitcnt lgkmcnt(0) only (gfx9 encoding: vmcnt 63, expcnt 7): LDS/SMEM done, memory ops may fly
 __device__ inline void wait_lds() { __builtin_amdgcn_s_waitcnt(0xC07F); }
-__device__ inline uint32_t bcast(uint32_t v, int src) { return __shfl(v, src, 64); }
+__device__ inline uint32_t bcast(uint32_t v, int src) { return __shfl(v, src, 64); }   // src may differ per lane
+// lane src's value when src is the same in every lane (a loop index, a ballot's first bit): v_readlane into
+// a scalar register instead of an LDS permute round trip
+__device__ inline uint32_t rdl(uint32_t v, int src) { return (uint32_t)__builtin_amdgcn_readlane((int)v, src); }
 // Make this wave's earlier global stores visible to its own later loads (same CU; workgroup scope).
 __device__ inline void wave_mem_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");

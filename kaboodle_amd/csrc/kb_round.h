@@ -128,10 +128,9 @@ __global__ __launch_bounds__(256) void k_a3_exact(Dev d, uint32_t* part, int32_t
       }
       const unsigned long long m = wave_min_u64(lm);                // keys are distinct: rotated ids differ
       if (m == ~0ull || m >= wave_fifth(top)) break;
-      const uint32_t b = __shfl(bm, (int)__builtin_ctzll(__ballot(lm == m)), 64);
+      const uint32_t b = rdl(bm, (int)__builtin_ctzll(__ballot(lm == m)));
       int32_t smin = a3x_block<true, false>(d, i, b, cur, E, srow, brow, trow, top);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) { const int32_t t = __shfl_xor(smin, o, 64); smin = t < smin ? t : smin; }
+      smin = (int32_t)(wave_min((uint32_t)smin ^ 0x80000000u) ^ 0x80000000u);   // signed minimum
       if (l == 0) lbrow[b] = smin;                                   // exact now
       if (l == (b & 63)) {
 #pragma unroll
@@ -679,7 +678,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KB_RP_WPE, 
         while (depm) {
           const uint32_t q = (uint32_t)(__ffsll((long long)depm) - 1);
           depm &= depm - 1;
-          const uint32_t s_q = bcast(b.sender, q);
+          const uint32_t s_q = rdl(b.sender, q);
           const unsigned long long killers = __ballot(((actm >> l) & 1ull) && b.peer == s_q) & ((1ull << q) - 1ull);
           if (killers) actm &= ~(1ull << q);
         }
@@ -1135,8 +1134,8 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     if (l == 0) BP[NB] = nB;
     if (tdbg) { wait_lds(); tp1 = wall_clock64(); }
     if (small_lists) {                                      // new joiners in list order: entries l and l + 64
-      const unsigned long long w0 = ((unsigned long long)bcast((uint32_t)(nmv >> 32), 0) << 32) | bcast((uint32_t)nmv, 0);
-      const unsigned long long w1 = ((unsigned long long)bcast((uint32_t)(nmv >> 32), 1) << 32) | bcast((uint32_t)nmv, 1);
+      const unsigned long long w0 = ((unsigned long long)rdl((uint32_t)(nmv >> 32), 0) << 32) | rdl((uint32_t)nmv, 0);
+      const unsigned long long w1 = ((unsigned long long)rdl((uint32_t)(nmv >> 32), 1) << 32) | rdl((uint32_t)nmv, 1);
       if (l < pb.nj && ((w0 >> l) & 1ull)) J[__popcll(w0 & ((1ull << l) - 1ull))] = js0;
       if (l + 64 < pb.nj && ((w1 >> l) & 1ull)) J[__popcll(w0) + __popcll(w1 & ((1ull << l) - 1ull))] = js1;
     } else {
@@ -1156,7 +1155,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
         const uint32_t u0 = __shfl_down(v0, o, 64), u1 = __shfl_down(v1, o, 64);
         if (l + o < 64) { v0 = u0 < v0 ? u0 : v0; v1 = u1 < v1 ? u1 : v1; }
       }
-      const uint32_t m1 = bcast(v1, 0);
+      const uint32_t m1 = rdl(v1, 0);
       v0 = m1 < v0 ? m1 : v0;
       if (l < nnew) JM[l] = v0;
       if (l + 64 < nnew) JM[l + 64] = v1;
@@ -1169,8 +1168,8 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     for (uint32_t wj = 0; wj < pb.JW; ++wj) {
       unsigned long long rmw, nmw;
       if (small_lists) {
-        rmw = ((unsigned long long)bcast((uint32_t)(rmv >> 32), (int)wj) << 32) | bcast((uint32_t)rmv, (int)wj);
-        nmw = ((unsigned long long)bcast((uint32_t)(nmv >> 32), (int)wj) << 32) | bcast((uint32_t)nmv, (int)wj);
+        rmw = ((unsigned long long)rdl((uint32_t)(rmv >> 32), (int)wj) << 32) | rdl((uint32_t)rmv, (int)wj);
+        nmw = ((unsigned long long)rdl((uint32_t)(nmv >> 32), (int)wj) << 32) | rdl((uint32_t)nmv, (int)wj);
       } else {
         rmw = rm[wj]; nmw = nm[wj];
       }
@@ -1180,7 +1179,7 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
         rmw &= rmw - 1;
         const uint32_t upto = ins_before + __popcll(nmw & ((2ull << bit) - 1ull));   // new joiners <= K
         const uint32_t expect = nbase_i + upto;
-        const uint32_t a = small_lists ? (K < 64 ? bcast(js0, (int)K) : bcast(js1, (int)(K - 64))) : pb.bjoin[K].sender;
+        const uint32_t a = small_lists ? (K < 64 ? rdl(js0, (int)K) : rdl(js1, (int)(K - 64))) : pb.bjoin[K].sender;
         const uint32_t nk = nB - (nnew - upto), cap = d.capj;
         uint32_t* pay = ob.pay + poff;
         const Prp P = prp_make(nk, philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1));

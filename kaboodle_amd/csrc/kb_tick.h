@@ -21,14 +21,14 @@ __device__ __attribute__((always_inline)) inline void tick_a2(const Dev& d, cons
   const uint32_t nsusp = __popcll(occm);
   const uint32_t m = n - 1 - nsusp;                       // Known && != self (:571-577)
   uint32_t myrank = 0;                                    // ascending-peer order of occupied slots
-  for (int k = 0; k < SLOTS; ++k) if (((occm >> k) & 1ull) && bcast(me.peer, k) < me.peer) myrank++;
+  for (int k = 0; k < SLOTS; ++k) if (((occm >> k) & 1ull) && rdl(me.peer, k) < me.peer) myrank++;
   uint32_t npick = 0, nind = 0, nrem = 0;
   uint32_t indirect[SLOTS], removed[SLOTS];
   for (uint32_t t = 0; t < nsusp; ++t) {
     const unsigned long long who = __ballot(occ && myrank == t);
     const int k = __ffsll((long long)who) - 1;
-    const uint32_t peer = bcast(me.peer, k);
-    const int32_t kind = (int32_t)bcast((uint32_t)me.kind, k), since = (int32_t)bcast((uint32_t)me.since, k);
+    const uint32_t peer = rdl(me.peer, k);
+    const int32_t kind = (int32_t)rdl((uint32_t)me.kind, k), since = (int32_t)rdl((uint32_t)me.since, k);
     if (r - since < PING_TIMEOUT) continue;
     if (kind == SK_WFP) {
       const uint32_t kk = m < (uint32_t)NUM_INDIRECT ? m : (uint32_t)NUM_INDIRECT;
@@ -65,7 +65,7 @@ __device__ __attribute__((always_inline)) inline void tick_a2(const Dev& d, cons
     uint32_t ex[SLOTS + 1];                               // excluded members: self, the suspects
     ex[0] = i;
 #pragma unroll
-    for (int k = 0; k < SLOTS; ++k) ex[k + 1] = ((occm >> k) & 1ull) ? bcast(me.peer, k) : 0xFFFFFFFFu;
+    for (int k = 0; k < SLOTS; ++k) ex[k + 1] = ((occm >> k) & 1ull) ? rdl(me.peer, k) : 0xFFFFFFFFu;
     uint32_t maxrank = 0;
     for (uint32_t q = 0; q < npick; ++q) maxrank = pr[q] > maxrank ? pr[q] : maxrank;
     const uint32_t n4 = d.NWR / 4;
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void k_tick_scan(Dev d, BcastSlots bs, int32_t
   const int first = __ffsll((long long)m) - 1;
   uint32_t base = 0;
   if (lane() == (uint32_t)first) base = atomicAdd(&d.ctr[C_TICK], (uint32_t)__popcll(m));
-  list[bcast(base, first) + __popcll(m & ((1ull << lane()) - 1ull))] = i;
+  list[rdl(base, first) + __popcll(m & ((1ull << lane()) - 1ull))] = i;
 }
 
 // ---- A2 handle_suspected_peers (:558-653) for the nodes k_tick_scan listed, one wave per node
@@ -252,11 +252,13 @@ __global__ __launch_bounds__(256) void k_fp_rows(Dev d) {
       if (c) { raw = multmodp(z[k], raw) ^ x; cnt += c; }
     }
   }
-#pragma unroll
-  for (uint32_t st = 1; st < FP_LANES; st <<= 1) {    // combine (part, part + st) for part % 2st == 0
-    const uint32_t r2 = __shfl_down(raw, st, 64), c2 = __shfl_down(cnt, st, 64);
+  static_assert(FP_LANES == 8, "the combine below is three DPP levels inside a 16-lane row");
+  auto level = [&](uint32_t r2, uint32_t c2, uint32_t st) __attribute__((always_inline)) {   // (part, part + st), part % 2st == 0
     if (on && (part & (2 * st - 1)) == 0) { raw = multmodp(d.zpow[c2], raw) ^ r2; cnt += c2; }
-  }
+  };
+  { const uint32_t r2 = dpp_shl<1>(raw), c2 = dpp_shl<1>(cnt); level(r2, c2, 1); }
+  { const uint32_t r2 = dpp_shl<2>(raw), c2 = dpp_shl<2>(cnt); level(r2, c2, 2); }
+  { const uint32_t r2 = dpp_shl<4>(raw), c2 = dpp_shl<4>(cnt); level(r2, c2, 4); }
   if (on && part == 0) { d.fp[i] = finish_fp(d, raw, cnt); d.dirty[i] = 0; }
 }
 

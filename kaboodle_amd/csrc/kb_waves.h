@@ -330,7 +330,7 @@ __global__ __launch_bounds__(256) void k_pack(Dev d, OutBuf ob, XState x) {
     while (kpm) {                                    // payload ids: the whole wave on each list
       const int src = __ffsll((long long)kpm) - 1;
       kpm &= kpm - 1;
-      const uint32_t from = bcast(m.off, src), to = bcast(ppos, src), len = bcast(pl, src);
+      const uint32_t from = rdl(m.off, src), to = rdl(ppos, src), len = rdl(pl, src);
       for (uint32_t e = l; e < len; e += 64) x.spay[to + e] = ob.pay[from + e];
     }
   }
@@ -460,7 +460,7 @@ __device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d
         // software pipeline over the batch's (message, 640-id chunk) items: the ids of the next item are
         // loaded while the current item's arms run, so a message costs its arms, not arms + a load trip
         auto load = [&](uint32_t j, uint32_t e0, uint32_t (&pv)[KP_UNROLL]) __attribute__((always_inline)) {
-          const uint32_t off = bcast(moff, (int)j), len = bcast(mlen, (int)j);
+          const uint32_t off = rdl(moff, (int)j), len = rdl(mlen, (int)j);
 #pragma unroll
           for (int u = 0; u < KP_UNROLL; ++u) {
             const uint32_t e = e0 + 64u * u + l;
@@ -469,16 +469,16 @@ __device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d
         };
         auto next = [&](uint32_t& j, uint32_t& e0) __attribute__((always_inline)) {
           e0 += 64 * KP_UNROLL;
-          if (e0 >= bcast(mlen, (int)j)) { e0 = 0; ++j; }
+          if (e0 >= rdl(mlen, (int)j)) { e0 = 0; ++j; }
         };
         uint32_t j = 0, e0 = 0;
-        while (j < cnt && bcast(mlen, (int)j) == 0) ++j;
+        while (j < cnt && rdl(mlen, (int)j) == 0) ++j;
         uint32_t pv[KP_UNROLL];
         if (j < cnt) load(j, e0, pv);
         while (j < cnt) {
           uint32_t jn = j, en = e0;
           next(jn, en);
-          while (jn < cnt && bcast(mlen, (int)jn) == 0) ++jn;
+          while (jn < cnt && rdl(mlen, (int)jn) == 0) ++jn;
           uint32_t pn[KP_UNROLL];
           if (jn < cnt) load(jn, en, pn);
           // the item's arms in three batched phases (all membership reads, then all atomics, then the
@@ -634,7 +634,7 @@ __device__ __attribute__((always_inline)) inline void kp_small_body(const Dev& d
         if (q0 + l < nk) { const Msg m = ib.msgs[wc.kin[k0 + q0 + l]]; moff = m.off; mlen = m.a; }
         const uint32_t qn = nk - q0 < 64 ? nk - q0 : 64u;
         for (uint32_t j = 0; j < qn; ++j) {
-          const uint32_t off = bcast(moff, (int)j), len = bcast(mlen, (int)j);
+          const uint32_t off = rdl(moff, (int)j), len = rdl(mlen, (int)j);
           for (uint32_t e0 = 0; e0 < len; e0 += 64 * KPS_UNROLL) {
             uint32_t pv[KPS_UNROLL], wv_[KPS_UNROLL], ob_[KPS_UNROLL];
 #pragma unroll
@@ -1021,29 +1021,35 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
       w_bytes += 8 * NSEG + 4 * 64 + (uint64_t)__popcll(sd) * (5 * (d.SEGW / 8) + 8);   // checkpoints, Z^n row, refolds
       const uint2 sp = refold_stale(d, ztab, i, sd);
       uint32_t raw = sp.x, cnt = sp.y, c = sp.y;
-      uint32_t oc[6], zp[6];
+      // inclusive suffix scan, lane k -> segments k..63: inside each 16-lane row by DPP, then each row's
+      // lanes combined with the total of the rows after it (formed from the row totals in scalar registers)
+      uint32_t oc[4], zp[4];
+      oc[0] = dpp_shl<1>(c); c += oc[0];
+      oc[1] = dpp_shl<2>(c); c += oc[1];
+      oc[2] = dpp_shl<4>(c); c += oc[2];
+      oc[3] = dpp_shl<8>(c); c += oc[3];
+      const uint32_t c1 = rdl(c, 16), c2 = rdl(c, 32), c3 = rdl(c, 48);
+      const uint32_t row = l >> 4;
+      const uint32_t sc = row == 0 ? c1 + c2 + c3 : (row == 1 ? c2 + c3 : (row == 2 ? c3 : 0u));
 #pragma unroll
-      for (int t = 0; t < 6; ++t) {               // inclusive suffix scan: lane k -> segments k..63
-        const uint32_t st = 1u << t;
-        oc[t] = __shfl_down(c, st, 64);
-        if (l + st >= 64) oc[t] = 0;
-        c += oc[t];
-      }
-#pragma unroll
-      for (int t = 0; t < 6; ++t) zp[t] = d.zpow[oc[t]];
-#pragma unroll
-      for (int t = 0; t < 6; ++t) {
-        const uint32_t st = 1u << t;
-        const uint32_t oraw = __shfl_down(raw, st, 64);
-        if (l + st < 64) raw = multmodp(zp[t], raw) ^ oraw;
-      }
+      for (int t = 0; t < 4; ++t) zp[t] = d.zpow[oc[t]];
+      const uint32_t zs = d.zpow[sc], z3 = d.zpow[c3], z23 = d.zpow[c2 + c3];
+      uint32_t o;
+      o = dpp_shl<1>(raw); raw = multmodp(zp[0], raw) ^ o;
+      o = dpp_shl<2>(raw); raw = multmodp(zp[1], raw) ^ o;
+      o = dpp_shl<4>(raw); raw = multmodp(zp[2], raw) ^ o;
+      o = dpp_shl<8>(raw); raw = multmodp(zp[3], raw) ^ o;
+      const uint32_t r1 = rdl(raw, 16), r2 = rdl(raw, 32), r3 = rdl(raw, 48);
+      const uint32_t s1 = multmodp(z3, r2) ^ r3, s0 = multmodp(z23, r1) ^ s1;
+      raw = multmodp(zs, raw) ^ (row == 0 ? s0 : (row == 1 ? s1 : (row == 2 ? r3 : 0u)));
+      c += sc;
       cnt = c;
       s_suf[wv][l] = make_uint2(raw, cnt);
       if (l == 0) s_suf[wv][NSEG] = make_uint2(0, 0);
       wait_lds();
       __builtin_amdgcn_wave_barrier();
-      R = bcast(raw, 0);
-      if (bcast(cnt, 0) != n) set_err(d, DERR_FP);
+      R = rdl(raw, 0);
+      if (rdl(cnt, 0) != n) set_err(d, DERR_FP);
       if (l == 0 && sd) atomicAnd(&d.sdirty[i], ~sd);
       segs = 0;
       inc = true; dirty = false; fpstale = true;
@@ -1131,7 +1137,7 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
             } else {                                  // few: the whole wave on each insertion
               for (unsigned long long mm = insm; mm; mm &= mm - 1) {
                 const int q = __ffsll((long long)mm) - 1;
-                const uint32_t x = bcast(lm.sender, q), k = seg_of(d, x);
+                const uint32_t x = rdl(lm.sender, q), k = seg_of(d, x);
                 const uint32_t hs = x >> 3, nh = (k + 1) * (d.SEGW / 8) - hs;
                 w_bytes += 5ull * nh + 12;
                 uint32_t praw = 0, pcnt = 0;
@@ -1141,7 +1147,7 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
                   fold_half(d, ztab, h, m8, praw, pcnt);
                 }
                 wave_combine(d, praw, pcnt);
-                praw = bcast(praw, 0); pcnt = bcast(pcnt, 0);
+                praw = rdl(praw, 0); pcnt = rdl(pcnt, 0);
                 const uint2 su = s_suf[wv][k + 1];
                 const uint32_t Bx = multmodp(d.zpow[su.y], praw) ^ su.x;
                 const uint32_t K = mulzc(ztab, Bx, 1) ^ Bx ^ multmodp(d.zpow[pcnt + su.y], d.cseg[x]);
@@ -1151,7 +1157,7 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
             if (tdbg) t_ins += wall_clock64() - tb;
           }
         }
-        g = bcast(mine, (int)(t & 63));
+        g = rdl(mine, (int)(t & 63));
       } else {      // beyond SORT_MAX: next smallest index above the previous one
         if (t == 0 && l == 0) path_hit(d, PATH_PROC_UNSORTED);
         uint32_t best = 0xFFFFFFFFu;
@@ -1165,9 +1171,9 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
       Msg m;
       if (sorted) {
         const int src = (int)(t & 63);
-        m.dest = bcast(lm.dest, src); m.sender = bcast(lm.sender, src); m.seq = bcast(lm.seq, src);
-        m.kind = bcast(lm.kind, src); m.a = bcast(lm.a, src); m.fp = bcast(lm.fp, src); m.n = bcast(lm.n, src);
-        m.off = bcast(lm.off, src);
+        m.dest = rdl(lm.dest, src); m.sender = rdl(lm.sender, src); m.seq = rdl(lm.seq, src);
+        m.kind = rdl(lm.kind, src); m.a = rdl(lm.a, src); m.fp = rdl(lm.fp, src); m.n = rdl(lm.n, src);
+        m.off = rdl(lm.off, src);
       } else {
         m = ib.msgs[g];
       }
@@ -1175,7 +1181,7 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
       if (s != last_sender) {                         // prologue: insert(sender, Known(now)) (:406-415)
         bool was;
         uint8_t b;
-        if (sorted) { was = bcast(pre_was, (int)(t & 63)) != 0; b = (uint8_t)bcast(pre_b, (int)(t & 63)); }
+        if (sorted) { was = rdl(pre_was, (int)(t & 63)) != 0; b = (uint8_t)rdl(pre_b, (int)(t & 63)); }
         else { was = (bw[s >> 5] >> (s & 31)) & 1u; b = was ? rw[s] : ST_UNKNOWN; }
         if (b == ST_SUSPECT && l < SLOTS && s_susp[wv][l].kind && s_susp[wv][l].peer == s) {
           lat_sample(d, i, s, s_susp[wv][l].since, r);
@@ -1185,7 +1191,7 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
         if (!was) {
           dbg_ins++;
           n++; segs |= seg_bit(d, s);
-          if (inc) { R = mulzc(ztab, R, 1) ^ bcast(Kx, (int)(t & 63)); fpstale = true; }
+          if (inc) { R = mulzc(ztab, R, 1) ^ rdl(Kx, (int)(t & 63)); fpstale = true; }
           else dirty = true;
           if (l == 0) const_cast<uint32_t*>(bw)[s >> 5] |= 1u << (s & 31);   // single writer of this row
         }
