@@ -129,6 +129,16 @@ __device__ inline uint32_t wave_or(uint32_t v) { return wave_last(wave_iscan<0u>
 template <uint32_t ST> __device__ __attribute__((always_inline)) inline uint32_t dpp_shl(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + ST, 0xF, 0xF, false);
 }
+// lane (l ^ J)'s value: DPP for partners inside a 16-lane row (J <= 8), an LDS permute across rows
+template <uint32_t J> __device__ __attribute__((always_inline)) inline uint32_t shfl_xor_c(uint32_t x) {
+  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
+  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
+  else if constexpr (J == 4 || J == 8) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + J, 0xF, 0xF, false);   // row_shl:J
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 + J, 0xF, 0xF, false);   // row_shr:J
+    return (lane() & J) ? dn : up;
+  } else return __shfl_xor(x, (int)J, 64);
+}
 // exclusive prefix sum across the 64 lanes
 __device__ inline uint32_t wave_excl(uint32_t v) { return wave_iscan<0u>(v, OpAdd{}) - v; }
 // s_waitcnt lgkmcnt(0) only (gfx9 encoding: vmcnt 63, expcnt 7): LDS/SMEM done, memory ops may fly

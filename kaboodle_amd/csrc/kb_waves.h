@@ -994,15 +994,22 @@ void k_proc(Dev d, OutBuf ib, OutBuf ob, WaveCtl wc, int32_t r_arg, const uint32
     uint32_t mine = l < icnt ? wc.inbox[ibase + l] : 0xFFFFFFFFu;
     const bool small = icnt <= 64, sorted = icnt <= sort_max(d);
     if (small) {
+      // bitonic stages up to the inbox's power of two: after stage k the lanes [0, k) are ascending, and every
+      // lane at or past icnt holds the maximum, so stage K >= icnt leaves the inbox sorted in lanes [0, icnt)
+      auto step = [&](uint32_t o, uint32_t k, uint32_t j) __attribute__((always_inline)) {
+        const bool up = (l & k) == 0, lower = (l & j) == 0;
+        const uint32_t mn = o < mine ? o : mine, mx = o < mine ? mine : o;
+        mine = (lower == up) ? mn : mx;
+      };
 #pragma unroll
-      for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          const uint32_t o = __shfl_xor(mine, j, 64);
-          const bool up = (l & k) == 0, lower = (l & j) == 0;
-          const uint32_t mn = o < mine ? o : mine, mx = o < mine ? mine : o;
-          mine = (lower == up) ? mn : mx;
-        }
+      for (uint32_t k = 2; k <= 64; k <<= 1) {
+        if (icnt <= k / 2) break;                      // wave-uniform
+        if (k >= 64) step(shfl_xor_c<32>(mine), k, 32);
+        if (k >= 32) step(shfl_xor_c<16>(mine), k, 16);
+        if (k >= 16) step(shfl_xor_c<8>(mine), k, 8);
+        if (k >= 8) step(shfl_xor_c<4>(mine), k, 4);
+        if (k >= 4) step(shfl_xor_c<2>(mine), k, 2);
+        step(shfl_xor_c<1>(mine), k, 1);
       }
     }
     uint32_t dbg_fp = 0, dbg_ins = 0, dbg_kpr = 0, dbg_log = 0, dbg_base = 0;
