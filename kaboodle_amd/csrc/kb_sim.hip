@@ -341,6 +341,10 @@ struct kb_sim {
   Dev d;
   int device;
   hipStream_t st;
+  // side stream: kernels off the round's critical path (the running set's fingerprint, the latency sweep)
+  // run beside it, forked from and joined back into st by events
+  hipStream_t st2 = nullptr;
+  hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
   uint32_t C, W, S;                    // capacity, row stride, row-sweep column splits
   // row shard: this handle holds rows [lo, hi) of the mesh, R = hi - lo
   uint32_t lo, hi, R;
@@ -465,11 +469,19 @@ static void prof_events(kb_sim* s, int kid, hipEvent_t* a, hipEvent_t* b) {
 }
 // every kernel of the round is launched through here: the dispatch packet itself records the events
 template <typename F, typename... Args>
-static void klaunch(kb_sim* s, int kid, F kern, dim3 grid, dim3 block, uint32_t lds, Args... args) {
+static void klaunch_on(kb_sim* s, hipStream_t stream, int kid, F kern, dim3 grid, dim3 block, uint32_t lds, Args... args) {
   hipEvent_t a, b;
   prof_events(s, kid, &a, &b);
-  hipExtLaunchKernelGGL(kern, grid, block, lds, s->st, a, b, 0, args...);
+  hipExtLaunchKernelGGL(kern, grid, block, lds, stream, a, b, 0, args...);
 }
+template <typename F, typename... Args>
+static void klaunch(kb_sim* s, int kid, F kern, dim3 grid, dim3 block, uint32_t lds, Args... args) {
+  klaunch_on(s, s->st, kid, kern, grid, block, lds, args...);
+}
+// fork side work k onto st2 after everything st has queued so far / join it back into st
+static void side_fork(kb_sim* s, int k) { (void)hipEventRecord(s->ev_fork[k], s->st); (void)hipStreamWaitEvent(s->st2, s->ev_fork[k], 0); }
+static void side_done(kb_sim* s, int k) { (void)hipEventRecord(s->ev_join[k], s->st2); }
+static void side_join(kb_sim* s, int k) { (void)hipStreamWaitEvent(s->st, s->ev_join[k], 0); }
 // fold the first n records (complete: their round has ended) into the per-kernel sums
 static void prof_resolve(kb_sim* s, size_t n) {
   n = std::min(n, s->krec.size());
@@ -585,6 +597,11 @@ static void destroy_shard(kb_sim* s) {
   if (s->wave_exec) (void)hipGraphExecDestroy(s->wave_exec);
   if (s->wave_graph) (void)hipGraphDestroy(s->wave_graph);
   if (s->st) (void)hipStreamDestroy(s->st);
+  if (s->st2) (void)hipStreamDestroy(s->st2);
+  for (int k = 0; k < 2; ++k) {
+    if (s->ev_fork[k]) (void)hipEventDestroy(s->ev_fork[k]);
+    if (s->ev_join[k]) (void)hipEventDestroy(s->ev_join[k]);
+  }
   delete s->xf;
   delete s;
 }
@@ -704,6 +721,10 @@ constexpr uint32_t KB_FOLD_WAVES = 16384;                            // fold wav
   }
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
+  if (hipStreamCreateWithFlags(&s->st2, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
+  for (int k = 0; k < 2; ++k)
+    if (hipEventCreateWithFlags(&s->ev_fork[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&s->ev_join[k], hipEventDisableTiming) != hipSuccess) { destroy_shard(s); seterr("events"); return KB_IO_ERROR; }
   if (hipHostMalloc((void**)&s->h_pin, 4 * PIN_WORDS, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
     s->h_pin = nullptr; destroy_shard(s); seterr("pinned buffer"); return KB_IO_ERROR;
   }
@@ -1205,9 +1226,6 @@ static int step_round(kb_sim* s) {
     klaunch(s, KI_CHURN_LEAVE, k_churn_leave, dim3(gall), dim3(tb), 0, d, r);
     klaunch(s, KI_CHURN_JOIN, k_churn_join, dim3(1), dim3(64), 0, d, r);
   }
-  klaunch(s, KI_ALIVE_BITS, k_alive_bits, dim3((d.NWR + tb - 1) / tb), dim3(tb), 0, d);
-  klaunch(s, KI_TRUEFP_PART, k_truefp_part, dim3(TRUEFP_G), dim3(256), 0, d, d.tfpart);
-  klaunch(s, KI_TRUEFP_FIN, k_truefp_fin, dim3(1), dim3(64), 0, d, d.tfpart);
   klaunch(s, KI_LOG_MARK, k_log_mark, dim3(gnode), dim3(tb), 0, d, r);
   // 2. broadcasts of round r-1 (with the external peers' Joins)
   if (!s->inj_join.empty()) { const int rc = merge_ext_joins(st, s->bjoin, &s->nj, s->inj_join, 0, C); if (rc) return rc; }
@@ -1295,9 +1313,19 @@ static int step_round(kb_sim* s) {
               blocks * wpb);
     }
   }
-  if (lat_fail)
-    klaunch(s, KI_LAT_SWEEP, k_lat_sweep, dim3((lat_stride(R) / 8 + 255) / 256, std::min<uint32_t>(s->nf, 16384)), dim3(256), 0, d,
+  // beside the Join responses: the running set and its fingerprint (read by the tick's agreement count; the
+  // set changed last with the churn), and the latency sweep (writes latency entries only; the tick's A2 and
+  // the waves write them next)
+  side_fork(s, 0);
+  klaunch_on(s, s->st2, KI_ALIVE_BITS, k_alive_bits, dim3((d.NWR + tb - 1) / tb), dim3(tb), 0, d);
+  klaunch_on(s, s->st2, KI_TRUEFP_PART, k_truefp_part, dim3(TRUEFP_G), dim3(256), 0, d, d.tfpart);
+  klaunch_on(s, s->st2, KI_TRUEFP_FIN, k_truefp_fin, dim3(1), dim3(64), 0, d, d.tfpart);
+  side_done(s, 0);
+  if (lat_fail) {
+    klaunch_on(s, s->st2, KI_LAT_SWEEP, k_lat_sweep, dim3((lat_stride(R) / 8 + 255) / 256, std::min<uint32_t>(s->nf, 16384)), dim3(256), 0, d,
             (const BCast*)s->bfail, (const uint32_t*)s->bf_gid, s->nf, s->fnamed);
+    side_done(s, 1);
+  }
   // the Probes queued since the last round travel with this round's broadcasts (after Failed and Join)
   s->probes.swap(s->probe_q);
   s->probe_q.clear();
@@ -1403,12 +1431,14 @@ static int step_round(kb_sim* s) {
     }
   }
   // 3. tick
+  if (lat_fail) side_join(s, 1);
   klaunch(s, KI_TICK_SCAN, k_tick_scan, dim3(gnode), dim3(tb), 0, d, s->bs, r, s->slow);                       // A1; list the A2 nodes
   klaunch(s, KI_TICK_PRE, k_tick_pre, dim3(std::min<uint32_t>(gwave, 1024)), dim3(256), 0, d, o0, s->bs, r, s->slow);   // A2 per listed node
   // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded
   if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
   if (d.uniform) klaunch(s, KI_FP_ROWS, k_fp_rows, dim3((FP_LANES * R + tb - 1) / tb), dim3(tb), 0, d);
   if (d.tst) klaunch(s, KI_A3_EXACT, k_a3_exact, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);   // exact A3 order
+  side_join(s, 0);
   klaunch(s, KI_TICK_POST, k_tick_post, dim3(gnode), dim3(tb), 0, d, s->ro, o0, r);
   if (ninj) {                                          // the external peers' wave-0 emissions, after the tick's
     klaunch(s, KI_EVENTS, k_inject, dim3(1), dim3(64), 0, d, o0, (const XRec*)s->d_inj, ninj, (const uint32_t*)s->d_inj_ids);
