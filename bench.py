@@ -24,8 +24,10 @@ Also reported, on the same JSON line:
                 event pair costs ≈5 us of dispatch overhead; k_proc's eight launches a round would add
                 ≈0.05 ms); the other kernels' times, k_proc's included, come from an untimed replay of
                 the same rounds (same seed: the simulation is deterministic, bit for bit) with events on
-                every launch.  `gaps` = round_gpu_ms minus the kernels (launch gaps, host hand-offs), so the
-                rows sum to round_gpu_ms;
+                every launch.  The kernels the simulator runs on its side stream, beside the Join responses
+                (SIDE_KERNELS, marked "stream": "side"), overlap the round's other kernels and are left out of
+                the sum; `gaps` = round_gpu_ms minus the other kernels (launch gaps, host hand-offs, and what
+                the overlap costs them), so those rows sum to round_gpu_ms;
   roofline      the kernel with the most time per round: algorithmic bytes per launch (counted in-kernel)
                 / its mean HIP-event launch duration, against 8 TB/s; `traffic` = measured HBM bytes per
                 launch from the rocprofv3 PMC summary committed under profiles/ for this exact command
@@ -52,6 +54,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM [CDNA4]")
 LAT_TABLE_MAX = 64 << 30        # bytes of latency table per GPU beyond which --latency is dropped
 KT_ROUND = 1                    # kb_sim_kernel_time kind of the whole round
+# kernels on the simulator's side stream (kb_sim.hip step_round: side_fork / side_join), overlapping the round's
+SIDE_KERNELS = ("k_alive_bits", "k_truefp_part", "k_truefp_fin", "k_lat_sweep")
 CHURN_RESERVE = 8192            # fresh ids kept for churn joins: capacity does not depend on --steps
 
 
@@ -361,7 +365,10 @@ def main() -> int:
             if pmc and name in pmc:
                 e["traffic_per_launch"] = pmc[name].get("hbm_bytes_per_launch")
             table[name] = e
-        kern_sum = sum(v["ms_per_round"] for v in table.values())
+        for name in SIDE_KERNELS:
+            if name in table:
+                table[name]["stream"] = "side"
+        kern_sum = sum(v["ms_per_round"] for n, v in table.items() if n not in SIDE_KERNELS)
         gaps = round(round_ms / nr - kern_sum, 4)
         counted = [n for n, v in table.items() if "achieved_GBs" in v]
         top = max(table, key=lambda n: table[n]["ms_per_round"])
