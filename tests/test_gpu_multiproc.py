@@ -4,7 +4,7 @@ rendezvous) with the same collective discipline as RCCL: every rank makes the sa
 and reads the counters together; row inspection is answered by the rank holding the row.  The unique id is made
 on rank 0 and reaches the other rank over torch.distributed (gloo), as bench.py shares the RCCL id.
 
-Two processes, each holding half the rows, must reproduce the oracle every round: counters, every fingerprint
+Two (or four) processes, each holding its share of the rows, must reproduce the oracle every round: counters, every fingerprint
 and per-node scalar, whole rows, suspect and curious tables, and the broadcast lists — the reference's UDP
 transport between instances (src/kaboodle.rs:188-226) carried between processes."""
 import os
@@ -62,8 +62,9 @@ def _rank_main(rank, world, port, name, q):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("name", ["churn_loss_512", "stop_start", "partition_heal", "fresh_ids", "identity_change"])
-def test_two_processes_equal_oracle(name):
+@pytest.mark.parametrize("name,world", [("churn_loss_512", 2), ("stop_start", 2), ("partition_heal", 2), ("fresh_ids", 2),
+                                        ("identity_change", 2), ("churn_loss_512", 4), ("partition_heal", 4)])
+def test_processes_equal_oracle(name, world):
     import multiprocessing as mp
     import kaboodle_amd
     kaboodle_amd.require_gpu()
@@ -72,7 +73,7 @@ def test_two_processes_equal_oracle(name):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(k, 2, port, name, q)) for k in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(k, world, port, name, q)) for k in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -85,7 +86,8 @@ def test_two_processes_equal_oracle(name):
         assert p.exitcode == 0
     o = Sim(parity.oracle_lib(), case["cfg"])
     parity.setup(o, case)
-    assert res[0][0] == 0 and res[0][1] == res[1][0] and res[1][1] == case["cfg"].capacity   # the rows, split in two
+    assert res[0][0] == 0 and res[world - 1][1] == case["cfg"].capacity                    # the rows, split in `world`
+    assert all(res[k][1] == res[k + 1][0] for k in range(world - 1))
     for r in range(rounds):
         parity.apply_events((o,), case, r)
         o.step(1)
