@@ -1076,7 +1076,7 @@ static int launch_waves(kb_sim* s, int32_t rk) {
        // then the small ones (a wave per destination), which also set up nb.cap / nb.cnt
       const uint32_t ks = (d.NWR <= KP_LDS_WORDS && !(d.dbg & KB_DBG_KP_HBM)) ? KP_COLS : 1u;
       const uint32_t groups = std::max<uint32_t>(1u, std::min<uint32_t>((R + 1023) / 1024 * (ks > 1 ? 2u : 1u), 512u / ks));
-constexpr uint32_t KB_KPS_PER_CU = 1;
+      constexpr uint32_t KB_KPS_PER_CU = 1;        // small-group workgroups per CU (2: no faster, profiles/r04u2_ab_unrolls.txt)
       const uint32_t small = std::max<uint32_t>((R + 1023) / 1024, KB_KPS_PER_CU * s->ncu);
       klaunch(s, KI_KP, k_kp, dim3(ks * groups + small), dim3(1024), (uint32_t)kp_lds_bytes(d.NWR), d, ib, s->wc, r,
               nb, ks * groups);
