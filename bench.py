@@ -83,6 +83,9 @@ def parse(argv=None):
     ap.add_argument("--no-modes", action="store_true", help="skip the socket_faithful line (N = 1)")
     ap.add_argument("--failed-mode", choices=("sim_sender", "socket_faithful"), default="sim_sender",
                     help="Q1: Failed(p) honoured (sim_sender, the headline) or never (socket_faithful)")
+    ap.add_argument("--a3-order", choices=("window", "exact"), default="window",
+                    help="A3's five oldest: the 1-byte stamp window with a sweep front (window) or the reference's "
+                         "exact instants (exact: KB_VARIANT_EXACT_LRU, DESIGN.md §2.11)")
     return ap.parse_args(argv)
 
 
@@ -215,11 +218,13 @@ def rank_config(a, rank: int, world: int, local: int):
     shard = sharded(a, world)
     peers = a.nodes * world if (shard and getattr(a, "weak", False)) else a.nodes
     reserve = max(CHURN_RESERVE, int(peers * a.churn * (total + 8) * 1.5))   # 8192 up to ~80 churn rounds at 64K
+    from kaboodle_amd._ffi import KB_VARIANT_EXACT_LRU
     mode = KB_FAILED_SOCKET_FAITHFUL if getattr(a, "failed_mode", "sim_sender") == "socket_faithful" else KB_FAILED_SIM_SENDER
     return SimConfig(capacity=peers + reserve, initial_nodes=peers, init_mode=KB_INIT_CONVERGED, loss=a.loss,
                      churn=a.churn, fault_end_round=total, seed=a.seed + (0 if shard else 1000 * rank),
                      device=local if world > 1 else -1, failed_mode=mode,
-                     track_latency=int(latency_on(a, peers + reserve, world if shard else 1)))
+                     track_latency=int(latency_on(a, peers + reserve, world if shard else 1)),
+                     variant=KB_VARIANT_EXACT_LRU if getattr(a, "a3_order", "window") == "exact" else 0)
 
 
 def latency_on(a, capacity: int, shards: int) -> bool:
@@ -326,7 +331,7 @@ def main() -> int:
                 "workload_tail_rounds_run": extra,
                 "workload_agree_frac_at_fault_end": round(st["agree"] / max(st["alive"], 1), 4),
                 "workload_agree_frac_final": round(s3["agree"] / max(s3["alive"], 1), 4),
-                "workload_full_tail": committed_tail(f"configs[2]: {a.nodes} peers", a.failed_mode)}
+                "workload_full_tail": committed_tail(f"configs[2]: {a.nodes} peers", a.failed_mode, a.a3_order)}
         if not shard:
             # how far the views are from agreement: |known_i| against the running count (0 = right size)
             import numpy as np
@@ -387,7 +392,7 @@ def main() -> int:
             "scaling": "weak" if (getattr(a, "weak", False) or (world > 1 and not shard)) else "strong",
             "vs_baseline": None, "dtype": "u8",
             "data": "synthetic (Philox-keyed loss/churn/targets, seed-determined)",
-            "config": {"workload": workload, "failed_mode": a.failed_mode, "peers": peers, "peers_per_gpu": (peers + world - 1) // world if shard else peers,
+            "config": {"workload": workload, "failed_mode": a.failed_mode, "a3_order": a.a3_order, "peers": peers, "peers_per_gpu": (peers + world - 1) // world if shard else peers,
                        "capacity": capacity,
                        "loss": a.loss, "churn": a.churn,
                        "parallelism": (f"rowshard{world}" if shard else f"replicas{world}") if world > 1 else "single",
@@ -427,6 +432,33 @@ def main() -> int:
                 "agree_frac_at_fault_end": round(s21["agree"] / max(s21["alive"], 1), 4),
                 "workload_full_tail": committed_tail(f"configs[2]: {a.nodes} peers", "socket_faithful"),
                 "workload_full_tail_exact_lru": committed_tail(f"configs[2]: {a.nodes} peers", "socket_faithful", "exact")}}
+        # the other A3 order on the same workload, seeds, K and W: the reference's exact instants
+        # (src/kaboodle.rs:662-675) against the 1-byte window, each kernel of its round from a profiled replay
+        other = "window" if a.a3_order == "exact" else "exact"
+        c = copy.copy(a)
+        c.a3_order = other
+        ccfg4 = rank_config(c, rank, world, local)
+        with kaboodle_amd.Mesh(ccfg4) as m4:
+            m4.step(a.warmup)
+            torch.cuda.synchronize()
+            dt4, alive4, s40, s41 = timed_rounds(m4, a.steps, world)
+        ms_head = dt / a.steps * 1e3
+        ent = {"value": alive4 / dt4, "ms_per_step": dt4 / a.steps * 1e3,
+               "cost_vs_headline": round(dt4 / a.steps * 1e3 / ms_head, 3),
+               "agree_frac_at_fault_end": round(s41["agree"] / max(s41["alive"], 1), 4),
+               "workload_full_tail_socket_faithful": committed_tail(f"configs[2]: {a.nodes} peers", "socket_faithful", other)}
+        if not a.no_replay:
+            with kaboodle_amd.Mesh(ccfg4) as rp4:
+                rp4.set_profiling(2)
+                rp4.step(a.warmup)
+                rp4.reset_kernel_time()
+                rp4.step(a.steps)
+                kb4 = rp4.kernel_breakdown()
+                rms4, rn4 = rp4.kernel_time(KT_ROUND)
+            ent["round_gpu_ms"] = round(rms4 / max(rn4, 1), 4)
+            ent["kernels_ms_per_round"] = {n: round(k["ms"] / max(rn4, 1), 4)
+                                           for n, k in sorted(kb4.items(), key=lambda kv: -kv[1]["ms"])[:12]}
+        modes["exact_lru" if other == "exact" else "window"] = ent
     seeds = None
     if world == 1 and a.seeds:
         # seeds 2 and 3 of the same synthetic workload, same K and W, each its own mesh

@@ -18,7 +18,7 @@ KB_DBG_PHASEB_HBM, KB_DBG_RESP_HBM, KB_DBG_KP_HBM, KB_DBG_KP_BIG_SMALL, KB_DBG_P
 KB_DBG_ALL = 31                  # every wide-row variant
 KB_DBG_WAVE_GRAPH = 32           # the receive window as a replayed HIP graph
 KB_DBG_RESP_WAVE_HBM = 64        # Join responses by wave, rows read in place (rows > 110K ids)
-KB_VARIANT_SAME_WINDOW_BCAST, KB_VARIANT_EXACT_LRU = 1, 2   # oracle-only
+KB_VARIANT_SAME_WINDOW_BCAST, KB_VARIANT_EXACT_LRU = 1, 2   # the first oracle-only, the second on the GPU too
 KB_STAT_NO_SF_FAILED_DROPS = 1
 KB_VARIANT_SPARSE_ROWS = 4       # the configs[4] layout: oracle and the HIP library (unsharded)
 KB_LATENCY_NONE = 0xFFFFFFFF
@@ -122,8 +122,9 @@ class SimConfig:
     device: int = -1
     debug_flags: int = 0         # KB_DBG_*: force the wide-row kernel variants (test surface)
     track_latency: int = 0       # 1: keep the ping-latency EWMA reported by peer_states
-    variant: int = 0             # KB_VARIANT_*: oracle-only alternative semantics (deviation measurements), or
-                                 # KB_VARIANT_SPARSE_ROWS (the configs[4] layout, also on the GPU)
+    variant: int = 0             # KB_VARIANT_*: SAME_WINDOW_BCAST (oracle-only deviation measurement), EXACT_LRU
+                                 # (the reference's exact A3 order, oracle and GPU), SPARSE_ROWS (the configs[4]
+                                 # layout, oracle and GPU, unsharded or as row shards)
     sparse_row_cap: int = 0      # KB_VARIANT_SPARSE_ROWS on the GPU: entries per row (0: min(capacity, 4096))
     stat_flags: int = 0          # KB_STAT_*: KB_STAT_NO_SF_FAILED_DROPS skips socket_faithful Failed drop counts
 

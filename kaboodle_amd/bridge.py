@@ -65,13 +65,16 @@ MAX_RECORDS_PER_ROUND = 33             # kb_sim_inject: unicast records per exte
 
 class Bridge:
     def __init__(self, mesh, broadcast_port: int | None = None, interface: Interface | None = None,
-                 sockets=None, forward_broadcasts: bool = False, auto_attach=()):
+                 sockets=None, forward_broadcasts: bool = False, auto_attach=(), max_peer_sockets: int = 16384):
         """sockets = (broadcast_in, broadcast_out, broadcast_addr, unicast) overrides the network setup
         (tests use loopback sockets; peer sockets then bind on the unicast socket's IP); otherwise the
         reference's sockets are created on `interface` (default: best_available_interface(), as Kaboodle::new
         does, src/lib.rs:98).  forward_broadcasts: also send the mesh's Join / Failed broadcasts.
-        auto_attach: ids (never bound by a simulated instance) handed to real instances as they show up."""
+        auto_attach: ids (never bound by a simulated instance) handed to real instances as they show up.
+        max_peer_sockets: at most this many simulated peers get a socket (an address on the wire); beyond it, or
+        when the OS refuses a socket, what needed one is dropped and counted instead of raising mid-round."""
         self.mesh = mesh
+        self.max_peer_sockets = max_peer_sockets
         self.forward_broadcasts = forward_broadcasts
         if sockets is not None:
             self.bin, self.bout, self.baddr, self.usock = sockets
@@ -98,7 +101,7 @@ class Bridge:
         self.stats = {"probes_in": 0, "external_join": 0, "external_failed": 0, "undecodable": 0,
                       "probe_responses_out": 0, "broadcasts_out": 0, "joins_in": 0, "unicast_in": 0,
                       "unicast_out": 0, "unknown_sender": 0, "unmapped_addr": 0, "inject_refused": 0,
-                      "send_failed": 0, "delayed": 0}
+                      "send_failed": 0, "delayed": 0, "no_socket": 0}
 
     # ---- addresses ----
     def attach(self, addr, node: int, identity: bytes | None = None) -> int:
@@ -127,23 +130,39 @@ class Bridge:
             self._set_identity(x, identity)
         return x
 
-    def peer_socket(self, node: int) -> socket.socket:
-        """The real socket of simulated peer `node` (bound on first use)."""
+    def peer_socket(self, node: int) -> socket.socket | None:
+        """The real socket of simulated peer `node` (bound on first use; it is that peer's address for good, so
+        sockets are never recycled).  None when no socket can be had: max_peer_sockets reached, or the OS refused
+        one (EMFILE, ...) — the caller drops what needed it and counts it (stats["no_socket"])."""
         s = self.psock.get(node)
         if s is None:
-            s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
-            s.bind((self.ip, 0))
-            s.setblocking(False)
+            if len(self.psock) >= self.max_peer_sockets:
+                self.stats["no_socket"] += 1
+                return None
+            try:
+                s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+            except OSError:
+                self.stats["no_socket"] += 1
+                return None
+            try:
+                s.bind((self.ip, 0))
+                s.setblocking(False)
+            except OSError:
+                s.close()
+                self.stats["no_socket"] += 1
+                return None
             self.psock[node] = s
             self.sim_of[s.getsockname()] = node
             self.sel.register(s, selectors.EVENT_READ, node)
         return s
 
     def addr_for(self, node: int):
-        """The wire address of id `node`: an external peer's real address, a simulated peer's socket."""
+        """The wire address of id `node`: an external peer's real address, a simulated peer's socket (None: no
+        socket could be bound for it)."""
         if node in self.ext_addr:
             return self.ext_addr[node]
-        return self.peer_socket(node).getsockname()
+        s = self.peer_socket(node)
+        return s.getsockname() if s is not None else None
 
     def node_for(self, addr) -> int | None:
         """The id behind a wire address (None: an address the mesh has no id for)."""
@@ -251,26 +270,43 @@ class Bridge:
         "broadcast")]."""
         out = []
         for rnd, responder, probe, prober, ident in self.mesh.probe_responses():
-            out.append((prober, wire.encode("ProbeResponse", identity=ident), self.peer_socket(responder),
-                        "probe_response"))
+            sock = self.peer_socket(responder)
+            if sock is None:
+                self.stats["send_failed"] += 1
+                continue
+            out.append((prober, wire.encode("ProbeResponse", identity=ident), sock, "probe_response"))
         if self.ext_addr:
             for (_r, _w, sender, dest, _seq, kind, a, fp, n, ids) in self.mesh.exported():
                 name = UNICAST_KINDS[kind]
+                sock = self.peer_socket(sender)
                 kw = {}
                 if name in ("PingRequest", "Ack"):
                     kw["peer"] = self.addr_for(a)
                 if name in ("Ack", "KnownPeersRequest"):
                     kw["fingerprint"], kw["num_peers"] = fp, n
                 if name == "KnownPeers":
-                    kw["peers"] = [(self.addr_for(j), self.mesh.identity(j)) for j in ids]
-                out.append((self.ext_addr[dest], wire.encode(name, identity=self.mesh.identity(sender), **kw),
-                            self.peer_socket(sender), "unicast"))
+                    peers = [(self.addr_for(j), j) for j in ids]
+                    self.stats["unmapped_addr"] += sum(1 for ad, _ in peers if ad is None)
+                    kw["peers"] = [(ad, self.mesh.identity(j)) for ad, j in peers if ad is not None]
+                if sock is None or kw.get("peer", ()) is None:   # no socket to send from, or none for the named peer
+                    self.stats["send_failed"] += 1
+                    continue
+                out.append((self.ext_addr[dest], wire.encode(name, identity=self.mesh.identity(sender), **kw), sock,
+                            "unicast"))
         for kind, sender, peer in (self.mesh.broadcasts() if self.forward_broadcasts else ()):
             if kind == "Join":
-                out.append((self.baddr, wire.encode("Join", identity=self.mesh.identity(sender),
-                                                    peer=self.addr_for(sender)), self.bout, "broadcast"))
+                ad = self.addr_for(sender)
+                if ad is None:
+                    self.stats["send_failed"] += 1
+                    continue
+                out.append((self.baddr, wire.encode("Join", identity=self.mesh.identity(sender), peer=ad), self.bout,
+                            "broadcast"))
             else:
-                out.append((self.baddr, wire.encode("Failed", peer=self.addr_for(peer)), self.bout, "broadcast"))
+                ad = self.addr_for(peer)
+                if ad is None:
+                    self.stats["send_failed"] += 1
+                    continue
+                out.append((self.baddr, wire.encode("Failed", peer=ad), self.bout, "broadcast"))
         return out
 
     def run_round(self) -> dict:

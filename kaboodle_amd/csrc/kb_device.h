@@ -101,8 +101,11 @@ __host__ __device__ inline uint8_t enc(int32_t t, int32_t r) {
 __device__ inline uint32_t lane() { return __lane_id(); }
 // Cross-lane scans and reductions by DPP (VALU data movement inside and across the four 16-lane rows): no
 // LDS instruction and no LDS round trip per step, which the ds_bpermute forms (__shfl_*) cost — each of their
-// six steps waited on the LDS pipe.  Lanes that are inactive contribute the operation's identity; the
-// reductions return the value of the last active lane's inclusive scan, broadcast (wave-uniform).
+// six steps waited on the LDS pipe.  Precondition: EXEC is the full wave or a prefix of it (lanes 0..k-1) —
+// every call site is wave-convergent.  Inactive lanes then sit after every active one and contribute the
+// operation's identity; a gap in EXEC would NOT: DPP treats a disabled source lane as invalid, so a shift that
+// reads across the gap drops the partial sums below it.  The reductions return the value of the last active
+// lane's inclusive scan, broadcast (wave-uniform).
 template <uint32_t ID, typename Op>
 __device__ __attribute__((always_inline)) inline uint32_t wave_iscan(uint32_t x, Op op) {
   x = op(x, (uint32_t)__builtin_amdgcn_update_dpp((int)ID, (int)x, 0x111, 0xF, 0xF, false));   // row_shr:1

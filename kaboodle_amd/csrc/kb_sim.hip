@@ -580,6 +580,20 @@ static int upload_segments(kb_sim* s) {
 
 #include "kb_sparse_host.h"
 
+// a handle answered by the sparse-row engine: the whole mesh (xf null) or one row shard of it (owns xf)
+static int sp_wrap(const kb_config* cfg, int rank, int world, Xfer* xf, kb_sim** out) {
+  if (cfg->capacity == 0 || cfg->capacity > 7800000u || cfg->initial_nodes > cfg->capacity || cfg->id_len > MAXID ||
+      cfg->max_waves == 0 || cfg->max_waves > 64) { seterr("config out of range"); delete xf; return KB_INVALID_ARGUMENT; }
+  SpSim* sp = nullptr;
+  const int rc = sp_create(cfg, rank, world, xf, &sp);
+  if (rc) return rc;
+  kb_sim* s = new kb_sim();
+  s->cfg = *cfg; s->C = cfg->capacity; s->sp = sp; s->device = sp->device; s->rank = rank; s->world = world;
+  s->lo = sp->lo; s->hi = sp->hi; s->R = sp->R;
+  *out = s;
+  return KB_OK;
+}
+
 static void free_all(kb_sim* s) {
   for (void* p : s->allocs) (void)hipFree(p);
   s->allocs.clear();
@@ -748,17 +762,16 @@ constexpr uint32_t KB_FOLD_WAVES = 16384;                            // fold wav
   return KB_OK;
 }
 
+static void destroy_one(kb_sim* s) {                 // a dense shard, or a sparse handle (its engine owns the exchange)
+  if (s->sp) { sp_destroy(s->sp); delete s; return; }
+  destroy_shard(s);
+}
+
 extern "C" int kb_sim_create(const kb_config* cfg, kb_sim** out) {
   if (cfg && out && cfg->abi_version == KB_ABI_VERSION && (cfg->variant & KB_VARIANT_SPARSE_ROWS)) {
     if (cfg->capacity == 0 || cfg->capacity > 7800000u || cfg->initial_nodes > cfg->capacity || cfg->id_len > MAXID ||
         cfg->max_waves == 0 || cfg->max_waves > 64) { seterr("config out of range"); return KB_INVALID_ARGUMENT; }
-    SpSim* sp = nullptr;
-    const int rc = sp_create(cfg, &sp);
-    if (rc) return rc;
-    kb_sim* s = new kb_sim();
-    s->cfg = *cfg; s->C = cfg->capacity; s->sp = sp; s->device = sp->device; s->world = 1; s->R = s->C; s->hi = s->C;
-    *out = s;
-    return KB_OK;
+    return sp_wrap(cfg, 0, 1, nullptr, out);
   }
   return create_shard(cfg, 0, 1, nullptr, out);
 }
@@ -796,11 +809,11 @@ extern "C" int kb_sim_create_rank(const kb_config* cfg, int32_t rank, int32_t wo
     const size_t mb = wm ? (size_t)atoll(wm) : 256;
     IpcXfer* x = new IpcXfer();
     if (!x->init(rank, world, unique_id, mb << 20)) { seterr(x->error()); delete x; return KB_IO_ERROR; }
-    return create_shard(cfg, rank, world, x, out);
+    return (cfg->variant & KB_VARIANT_SPARSE_ROWS) ? sp_wrap(cfg, rank, world, x, out) : create_shard(cfg, rank, world, x, out);
   }
   RcclXfer* x = new RcclXfer();
   if (!x->init(rank, world, unique_id)) { seterr(x->error()); delete x; return KB_IO_ERROR; }
-  return create_shard(cfg, rank, world, x, out);
+  return (cfg->variant & KB_VARIANT_SPARSE_ROWS) ? sp_wrap(cfg, rank, world, x, out) : create_shard(cfg, rank, world, x, out);
 }
 
 extern "C" int kb_sim_create_local(const kb_config* cfg, int32_t shards, kb_sim** out) {
@@ -808,13 +821,15 @@ extern "C" int kb_sim_create_local(const kb_config* cfg, int32_t shards, kb_sim*
   kb_sim* g = new kb_sim();
   g->cfg = *cfg; g->C = cfg->capacity; g->world = shards; g->R = 0;
   g->hub = new LocalHub(shards);
+  const bool sparse = cfg->abi_version == KB_ABI_VERSION && (cfg->variant & KB_VARIANT_SPARSE_ROWS);
   for (int k = 0; k < shards; ++k) {
     LocalXfer* x = new LocalXfer();
     x->rank = k; x->world = shards; x->hub = g->hub;
     kb_sim* s = nullptr;
-    const int rc = create_shard(cfg, k, shards, x, &s);
-    if (rc) { for (kb_sim* t : g->shards) destroy_shard(t); delete g->hub; delete g; return rc; }
+    const int rc = sparse ? sp_wrap(cfg, k, shards, x, &s) : create_shard(cfg, k, shards, x, &s);
+    if (rc) { for (kb_sim* t : g->shards) destroy_one(t); delete g->hub; delete g; return rc; }
     s->in_group = true;
+    if (s->sp) s->sp->in_group = true;
     g->shards.push_back(s);
   }
   g->device = g->shards[0]->device;
@@ -824,9 +839,9 @@ extern "C" int kb_sim_create_local(const kb_config* cfg, int32_t shards, kb_sim*
 
 extern "C" int kb_sim_destroy(kb_sim* s) {
   if (!s) return KB_INVALID_ARGUMENT;
-  if (s->sp) { sp_destroy(s->sp); delete s; return KB_OK; }
+  if (s->sp) { destroy_one(s); return KB_OK; }
   if (!s->shards.empty()) {
-    for (kb_sim* t : s->shards) destroy_shard(t);
+    for (kb_sim* t : s->shards) destroy_one(t);
     delete s->hub;
     delete s;
     return KB_OK;
@@ -836,7 +851,7 @@ extern "C" int kb_sim_destroy(kb_sim* s) {
 }
 
 extern "C" int kb_sim_shard_info(kb_sim* s, int32_t* rank, int32_t* world, uint32_t* lo, uint32_t* hi) {
-  if (s && s->sp && rank && world && lo && hi) { *rank = 0; *world = 1; *lo = 0; *hi = s->C; return KB_OK; }
+  if (s && s->sp && rank && world && lo && hi) { *rank = s->sp->rank; *world = s->sp->world; *lo = s->sp->lo; *hi = s->sp->hi; return KB_OK; }
   if (!s || !rank || !world || !lo || !hi) return KB_INVALID_ARGUMENT;
   if (!s->shards.empty()) { *rank = 0; *world = s->world; *lo = 0; *hi = s->C; return KB_OK; }
   *rank = s->rank; *world = s->world; *lo = s->lo; *hi = s->hi;
@@ -908,6 +923,20 @@ static int grow_wave0(kb_sim* s, size_t need_msg, size_t need_pay) {
       s->msg_cap = (uint32_t)cap;
     }
   }
+  return KB_OK;
+}
+
+// External peers' export buffers hold every record a round routes to them.  A real instance's Join
+// (kb_sim_inject KB_WIRE_JOIN) draws KnownPeers responses from ~1 % of the running peers, capj ids each
+// (src/kaboodle.rs:284-304, :356-392): so before the window the buffers grow to the wave-0 totals (all Join
+// responses and injected payloads, an upper bound of what wave 0 can export) plus a fixed allowance for the
+// later waves' replies.  They are empty at a round's start (drained after every round), so nothing is copied.
+constexpr uint32_t XREC_MIN = 1u << 16, XIDS_MIN = 1u << 22;
+static int size_exports(kb_sim* s, uint64_t recs, uint64_t ids) {
+  const uint64_t nr = recs + XREC_MIN, ni = ids + XIDS_MIN;
+  if (nr > 0xFFFFFFFFull || ni > 0xFFFFFFFFull) { seterr("export buffer beyond 2^32 entries"); return KB_CAPACITY; }
+  if (nr > s->d.xrec_cap) { HIPCHK(regrow(s, &s->d.xrec, nr + nr / 4)); s->d.xrec_cap = (uint32_t)std::min<uint64_t>(nr + nr / 4, 0xFFFFFFFFull); s->buf_gen++; }
+  if (ni > s->d.xids_cap) { HIPCHK(regrow(s, &s->d.xids, ni + ni / 4)); s->d.xids_cap = (uint32_t)std::min<uint64_t>(ni + ni / 4, 0xFFFFFFFFull); s->buf_gen++; }
   return KB_OK;
 }
 
@@ -1382,6 +1411,7 @@ static int step_round(kb_sim* s) {
       const int rc = grow_wave0(s, msg_tot, pay_tot);
       if (rc) return rc;
     }
+    if (s->n_ext) { const int rc = size_exports(s, msg_tot, pay_tot); if (rc) return rc; }
     if (resp_nodes) {
       const uint32_t grid = std::min<uint32_t>(resp_nodes, 4096);   // (the workgroup path: 2 per CU when it serves only
                                                                    // the few responders the wave path lists)
@@ -1543,6 +1573,20 @@ static kb_sim* owner(kb_sim* g, uint32_t node) {                 // the shard ho
   for (kb_sim* t : g->shards) if (node >= t->lo && node < t->hi) return t;
   return nullptr;
 }
+// a kb_sim_create_local group of sparse-row shards: mesh-changing calls go to every shard, row inspection to the
+// shard holding the row, replicated facts to the first shard
+static bool sp_grp(const kb_sim* s) { return s && !s->shards.empty() && s->shards[0]->sp; }
+#define SPG_ALL(call)                                                     \
+  if (sp_grp(s)) {                                                        \
+    for (kb_sim* t_ : s->shards) { const int rc_ = call(t_); if (rc_) return rc_; } \
+    return KB_OK;                                                         \
+  }
+#define SPG_OWNER(node, call)                                             \
+  if (sp_grp(s)) {                                                        \
+    if (node >= s->C) return KB_INVALID_ARGUMENT;                         \
+    return call(owner(s, node));                                          \
+  }
+#define SPG_FIRST(call) if (sp_grp(s)) return call(s->shards[0]);
 
 // every shard of a group steps in its own thread; a failing shard aborts the others' rendezvous
 static int group_step(kb_sim* g, uint32_t rounds) {
@@ -1555,8 +1599,8 @@ static int group_step(kb_sim* g, uint32_t rounds) {
     th.emplace_back([&, k] {
       kb_sim* s = g->shards[k];
       (void)hipSetDevice(s->device);
-      for (uint32_t q = 0; q < rounds && rc[k] == KB_OK; ++q) rc[k] = step_round(s);
-      if (rc[k] == KB_OK && sync_st(s) != hipSuccess) { rc[k] = KB_IO_ERROR; g_err = "stream"; }
+      for (uint32_t q = 0; q < rounds && rc[k] == KB_OK; ++q) rc[k] = s->sp ? sp_step(s->sp, 1) : step_round(s);
+      if (rc[k] == KB_OK && !s->sp && sync_st(s) != hipSuccess) { rc[k] = KB_IO_ERROR; g_err = "stream"; }
       if (rc[k] != KB_OK) { err[k] = g_err; g->hub->abort(); }
     });
   for (auto& t : th) t.join();
@@ -1635,6 +1679,7 @@ static int ever_bound(kb_sim* s, uint32_t node, int* ever) {
 }
 extern "C" int kb_sim_start_node(kb_sim* s, uint32_t node) {
   if (s && s->sp) return chk(s, node) ? KB_INVALID_ARGUMENT : sp_start_node(s->sp, node);
+  SPG_ALL([&](kb_sim* t) { return kb_sim_start_node(t, node); });
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
   kb_sim* h = is_group(s) ? s->shards[0] : s;        // lifecycle facts are replicated on every shard
   int run = 0, ever = 0;
@@ -1646,6 +1691,7 @@ extern "C" int kb_sim_start_node(kb_sim* s, uint32_t node) {
 }
 extern "C" int kb_sim_stop_node(kb_sim* s, uint32_t node) {
   if (s && s->sp) return chk(s, node) ? KB_INVALID_ARGUMENT : sp_stop_node(s->sp, node);
+  SPG_ALL([&](kb_sim* t) { return kb_sim_stop_node(t, node); });
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_stop_node(t, node); });
   s->events.push_back(Event{node, EV_STOP, node, 0});
@@ -1671,6 +1717,17 @@ static int restart_apply(kb_sim* s, uint32_t node, uint32_t to) {
 }
 extern "C" int kb_sim_restart_node(kb_sim* s, uint32_t node, uint32_t* new_node) {
   if (s && s->sp) return (chk(s, node) || !new_node) ? KB_INVALID_ARGUMENT : sp_restart_node(s->sp, node, new_node);
+  if (sp_grp(s)) {                                   // every shard allocates the same fresh id (replicated counter)
+    if (chk(s, node) || !new_node) return KB_INVALID_ARGUMENT;
+    for (size_t k = 0; k < s->shards.size(); ++k) {
+      uint32_t to = 0;
+      const int rc = kb_sim_restart_node(s->shards[k], node, &to);
+      if (rc) return rc;
+      if (k && to != *new_node) { seterr("shards allocated different fresh ids"); return KB_IO_ERROR; }
+      *new_node = to;
+    }
+    return KB_OK;
+  }
   if (chk(s, node) || !new_node) return KB_INVALID_ARGUMENT;
   kb_sim* h = is_group(s) ? s->shards[0] : s;
   if (h->h_moved[node]) { seterr("the instance bound here restarted at a fresh address"); return KB_INVALID_OPERATION; }
@@ -1698,6 +1755,7 @@ extern "C" int kb_sim_restart_node(kb_sim* s, uint32_t node, uint32_t* new_node)
 }
 extern "C" int kb_sim_is_running(kb_sim* s, uint32_t node, int* running) {
   if (s && s->sp) return (chk(s, node) || !running) ? KB_INVALID_ARGUMENT : sp_is_running(s->sp, node, running);
+  SPG_FIRST([&](kb_sim* t) { return kb_sim_is_running(t, node, running); });
   if (chk(s, node) || !running) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_is_running(s->shards[0], node, running);
   uint8_t a = 0;
@@ -1707,6 +1765,7 @@ extern "C" int kb_sim_is_running(kb_sim* s, uint32_t node, int* running) {
 }
 extern "C" int kb_sim_ping_addrs(kb_sim* s, uint32_t node, const uint32_t* peers, size_t n) {
   if (s && s->sp) return (chk(s, node) || (n && !peers)) ? KB_INVALID_ARGUMENT : sp_ping_addrs(s->sp, node, peers, n);
+  SPG_ALL([&](kb_sim* t) { return kb_sim_ping_addrs(t, node, peers, n); });
   if (chk(s, node) || (n && !peers)) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_ping_addrs(t, node, peers, n); });
   for (size_t k = 0; k < n; ++k) if (peers[k] >= s->C) return KB_INVALID_ARGUMENT;
@@ -1730,6 +1789,7 @@ extern "C" int kb_sim_ping_addrs(kb_sim* s, uint32_t node, const uint32_t* peers
 }
 extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* identity, size_t len) {
   if (s && s->sp) return (chk(s, node) || len > MAXID || (len && !identity)) ? KB_INVALID_ARGUMENT : sp_set_identity(s->sp, node, identity, len);
+  SPG_ALL([&](kb_sim* t) { return kb_sim_set_identity(t, node, identity, len); });
   if (chk(s, node) || len > MAXID || (len && !identity)) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_set_identity(t, node, identity, len); });
   if (s->h_moved[node]) { seterr("the instance bound here restarted at a fresh address"); return KB_INVALID_OPERATION; }
@@ -1755,6 +1815,7 @@ extern "C" int kb_sim_set_identity(kb_sim* s, uint32_t node, const uint8_t* iden
 }
 extern "C" int kb_sim_identity(kb_sim* s, uint32_t node, uint8_t* buf, size_t cap, size_t* len) {
   if (s && s->sp) return (chk(s, node) || !len) ? KB_INVALID_ARGUMENT : sp_identity(s->sp, node, buf, cap, len);
+  SPG_FIRST([&](kb_sim* t) { return kb_sim_identity(t, node, buf, cap, len); });
   if (chk(s, node) || !len) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_identity(s->shards[0], node, buf, cap, len);   // replicated per id
   *len = s->h_idlen[node];
@@ -1766,6 +1827,7 @@ extern "C" int kb_sim_identity(kb_sim* s, uint32_t node, uint8_t* buf, size_t ca
 // ---- discovery (src/discovery.rs:30-89, src/kaboodle.rs:305-331) ----------------------------------
 extern "C" int kb_sim_probe(kb_sim* s, const kb_wire_addr* prober) {
   if (s && s->sp) { if (!prober) return KB_INVALID_ARGUMENT; s->sp->probe_q.push_back(*prober); return KB_OK; }
+  SPG_ALL([&](kb_sim* t) { return kb_sim_probe(t, prober); });
   if (!s || !prober) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_probe(t, prober); });
   s->probe_q.push_back(*prober);
@@ -1776,7 +1838,10 @@ extern "C" int kb_sim_probe_responses(kb_sim* s, kb_probe_response* out, size_t 
   if (!s || !n) return KB_INVALID_ARGUMENT;
   if (is_group(s)) {                                 // every shard's responders, merged in canonical order
     std::vector<kb_probe_response> all;
-    for (kb_sim* t : s->shards) all.insert(all.end(), t->presp.begin(), t->presp.end());
+    for (kb_sim* t : s->shards) {
+      const std::vector<kb_probe_response>& v = t->sp ? t->sp->presp : t->presp;
+      all.insert(all.end(), v.begin(), v.end());
+    }
     std::stable_sort(all.begin(), all.end(), [](const kb_probe_response& a, const kb_probe_response& b) {
       return a.round != b.round ? a.round < b.round : a.responder != b.responder ? a.responder < b.responder : a.probe < b.probe;
     });
@@ -1784,7 +1849,7 @@ extern "C" int kb_sim_probe_responses(kb_sim* s, kb_probe_response* out, size_t 
     if (!out) return KB_OK;
     if (cap < all.size()) return KB_CAPACITY;
     if (!all.empty()) memcpy(out, all.data(), all.size() * sizeof(kb_probe_response));
-    for (kb_sim* t : s->shards) t->presp.clear();
+    for (kb_sim* t : s->shards) { t->presp.clear(); if (t->sp) t->sp->presp.clear(); }
     return KB_OK;
   }
   *n = s->presp.size();
@@ -1798,6 +1863,7 @@ extern "C" int kb_sim_probe_responses(kb_sim* s, kb_probe_response* out, size_t 
 static_assert(sizeof(XRec) == sizeof(kb_unicast), "XRec mirrors kb_unicast");
 extern "C" int kb_sim_set_external(kb_sim* s, uint32_t node) {
   if (s && s->sp) return chk(s, node) ? KB_INVALID_ARGUMENT : sp_set_external(s->sp, node);
+  SPG_ALL([&](kb_sim* t) { return kb_sim_set_external(t, node); });
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
   kb_sim* h = is_group(s) ? s->shards[0] : s;
   if (h->h_ext.empty()) h->h_ext.assign(s->C, 0);
@@ -1814,7 +1880,7 @@ extern "C" int kb_sim_set_external(kb_sim* s, uint32_t node) {
     HIPCHK(hipMemcpy(t->d.ext + node, &o, 1, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(t->d.idset + node, &o, 1, hipMemcpyHostToDevice));
     if (!t->d.xrec) {
-      t->d.xrec_cap = 1u << 16; t->d.xids_cap = 1u << 22;
+      t->d.xrec_cap = XREC_MIN; t->d.xids_cap = XIDS_MIN;   // grown per round (size_exports)
       HIPCHK(talloc(t, &t->d.xrec, t->d.xrec_cap)); HIPCHK(talloc(t, &t->d.xids, t->d.xids_cap));
       t->buf_gen++;                                  // a captured receive window holds the old Dev
     }
@@ -1825,6 +1891,7 @@ extern "C" int kb_sim_set_external(kb_sim* s, uint32_t node) {
 }
 extern "C" int kb_sim_inject(kb_sim* s, const kb_unicast* m, const uint32_t* ids) {
   if (s && s->sp) return sp_inject(s->sp, m, ids);
+  SPG_ALL([&](kb_sim* t) { return kb_sim_inject(t, m, ids); });
   if (!s || !m || m->sender >= s->C || m->dest >= s->C || (m->kind > K_KPR && m->kind != KB_WIRE_JOIN) || (m->pay_len && !ids))
     return KB_INVALID_ARGUMENT;
   kb_sim* h = is_group(s) ? s->shards[0] : s;
@@ -1859,10 +1926,11 @@ extern "C" int kb_sim_exported(kb_sim* s, kb_unicast* out, size_t cap, size_t* n
   std::vector<uint32_t> all_ids;
   const std::vector<kb_sim*> hs = is_group(s) ? s->shards : std::vector<kb_sim*>{s};
   for (kb_sim* t : hs)
-    for (const kb_unicast& u : t->xq) {
+    for (const kb_unicast& u : (t->sp ? t->sp->xq : t->xq)) {
+      const std::vector<uint32_t>& xi = t->sp ? t->sp->xq_ids : t->xq_ids;
       kb_unicast v = u;
       v.pay_off = (uint32_t)all_ids.size();
-      all_ids.insert(all_ids.end(), t->xq_ids.begin() + u.pay_off, t->xq_ids.begin() + u.pay_off + u.pay_len);
+      all_ids.insert(all_ids.end(), xi.begin() + u.pay_off, xi.begin() + u.pay_off + u.pay_len);
       std::sort(all_ids.begin() + v.pay_off, all_ids.end());   // a KnownPeers map has no order: ascending ids
       all.push_back(v);
     }
@@ -1874,13 +1942,14 @@ extern "C" int kb_sim_exported(kb_sim* s, kb_unicast* out, size_t cap, size_t* n
   if (cap < all.size() || (!all_ids.empty() && (!ids || cap_ids < all_ids.size()))) { seterr("export buffer too small"); return KB_CAPACITY; }
   if (!all.empty()) memcpy(out, all.data(), all.size() * sizeof(kb_unicast));
   if (!all_ids.empty()) memcpy(ids, all_ids.data(), 4 * all_ids.size());
-  for (kb_sim* t : hs) { t->xq.clear(); t->xq_ids.clear(); }
+  for (kb_sim* t : hs) { t->xq.clear(); t->xq_ids.clear(); if (t->sp) { t->sp->xq.clear(); t->sp->xq_ids.clear(); } }
   return KB_OK;
 }
 
 // the last round's Join / Failed broadcasts (whole mesh; sender order, a node's Join before its Failed)
 extern "C" int kb_sim_broadcasts(kb_sim* s, kb_broadcast* out, size_t cap, size_t* n) {
   if (s && s->sp) return n ? sp_broadcasts(s->sp, out, cap, n) : KB_INVALID_ARGUMENT;
+  SPG_FIRST([&](kb_sim* t) { return kb_sim_broadcasts(t, out, cap, n); });
   if (!s || !n) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_broadcasts(s->shards[0], out, cap, n);   // every shard holds the lists
   std::vector<BCast> j(s->nj), f(s->nf);
@@ -1903,6 +1972,7 @@ extern "C" int kb_sim_broadcasts(kb_sim* s, kb_broadcast* out, size_t cap, size_
 }
 extern "C" int kb_sim_fingerprint(kb_sim* s, uint32_t node, uint32_t* fp) {
   if (s && s->sp) return (chk(s, node) || !fp) ? KB_INVALID_ARGUMENT : sp_fingerprint(s->sp, node, fp);
+  SPG_OWNER(node, [&](kb_sim* t) { return kb_sim_fingerprint(t, node, fp); });
   if (chk(s, node) || !fp) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_fingerprint(t, node, fp); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -1936,6 +2006,7 @@ extern "C" int kb_sim_fingerprints(kb_sim* s, uint32_t* fps, size_t cap) {
 }
 extern "C" int kb_sim_true_fingerprint(kb_sim* s, uint32_t* fp) {
   if (s && s->sp) return fp ? sp_true_fingerprint(s->sp, fp) : KB_INVALID_ARGUMENT;
+  SPG_FIRST([&](kb_sim* t) { return kb_sim_true_fingerprint(t, fp); });
   if (!s || !fp) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_true_fingerprint(s->shards[0], fp);
   k_alive_bits<<<(s->d.NWR + 255) / 256, 256, 0, s->st>>>(s->d);
@@ -1947,6 +2018,7 @@ extern "C" int kb_sim_true_fingerprint(kb_sim* s, uint32_t* fp) {
   return KB_OK;
 }
 extern "C" int kb_sim_dump_row(kb_sim* s, uint32_t node, uint8_t* rw, size_t cap) {
+  SPG_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_row(t, node, rw, cap); });
   if (s && s->sp) {
     if (chk(s, node) || !rw || cap < s->C) return KB_INVALID_ARGUMENT;
     std::vector<uint8_t> v;
@@ -1964,6 +2036,7 @@ extern "C" int kb_sim_dump_row(kb_sim* s, uint32_t node, uint8_t* rw, size_t cap
   return KB_OK;
 }
 extern "C" int kb_sim_peers(kb_sim* s, uint32_t node, uint32_t* peers, size_t cap, size_t* n) {
+  SPG_OWNER(node, [&](kb_sim* t) { return kb_sim_peers(t, node, peers, cap, n); });
   if (s && s->sp) {
     if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
     std::vector<uint8_t> rw;
@@ -1987,6 +2060,7 @@ extern "C" int kb_sim_peers(kb_sim* s, uint32_t node, uint32_t* peers, size_t ca
 }
 extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, size_t cap, size_t* n) {
   if (s && s->sp) return (chk(s, node) || !n) ? KB_INVALID_ARGUMENT : sp_peer_states(s->sp, node, out, cap, n);
+  SPG_OWNER(node, [&](kb_sim* t) { return kb_sim_peer_states(t, node, out, cap, n); });
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_peer_states(t, node, out, cap, n); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -2030,6 +2104,7 @@ extern "C" int kb_sim_peer_states(kb_sim* s, uint32_t node, kb_peer_state* out, 
 }
 extern "C" int kb_sim_watch(kb_sim* s, uint32_t node) {
   if (s && s->sp) return chk(s, node) ? KB_INVALID_ARGUMENT : sp_watch(s->sp, node);
+  SPG_OWNER(node, [&](kb_sim* t) { return kb_sim_watch(t, node); });
   if (chk(s, node)) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_watch(t, node); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -2044,6 +2119,8 @@ extern "C" int kb_sim_watch(kb_sim* s, uint32_t node) {
 }
 extern "C" int kb_sim_events(kb_sim* s, uint32_t node, uint32_t* discovered, size_t cap_d, size_t* n_d,
                              uint32_t* departed, size_t cap_p, size_t* n_p, uint32_t* fp, int* fp_changed) {
+  SPG_OWNER(node, [&](kb_sim* t) {
+    return kb_sim_events(t, node, discovered, cap_d, n_d, departed, cap_p, n_p, fp, fp_changed); });
   if (s && s->sp) {
     if (chk(s, node) || !n_d || !n_p || !fp || !fp_changed) return KB_INVALID_ARGUMENT;
     return sp_events(s->sp, node, discovered, cap_d, n_d, departed, cap_p, n_p, fp, fp_changed);
@@ -2097,6 +2174,17 @@ static int fold_stats(kb_sim* s) {
 }
 extern "C" int kb_sim_stats(kb_sim* s, kb_stats* out) {
   if (s && s->sp) return out ? sp_stats_out(s->sp, out) : KB_INVALID_ARGUMENT;
+  if (sp_grp(s)) {                                   // the counters summed over the shards, replicated facts from one
+    if (!out) return KB_INVALID_ARGUMENT;
+    unsigned long long st[NSTAT] = {0};
+    for (kb_sim* t : s->shards) {
+      unsigned long long v[NSTAT];
+      const int rc = sp_read_stats(t->sp, v);
+      if (rc) return rc;
+      for (int k = 0; k < NSTAT; ++k) st[k] += v[k];
+    }
+    return sp_stats_fill(s->shards[0]->sp, st, out);
+  }
   if (!s || !out) return KB_INVALID_ARGUMENT;
   { const int rc = fold_stats(s); if (rc) return rc; }
   unsigned long long st[NSTAT];
@@ -2172,6 +2260,7 @@ extern "C" int kb_sim_dump_scalars(kb_sim* s, int32_t* out, size_t cap) {
 }
 extern "C" int kb_sim_dump_suspects(kb_sim* s, uint32_t node, int32_t* out, size_t cap, size_t* n) {
   if (s && s->sp) return (chk(s, node) || !n) ? KB_INVALID_ARGUMENT : sp_dump_suspects(s->sp, node, out, cap, n);
+  SPG_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_suspects(t, node, out, cap, n); });
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_suspects(t, node, out, cap, n); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -2186,6 +2275,7 @@ extern "C" int kb_sim_dump_suspects(kb_sim* s, uint32_t node, int32_t* out, size
 }
 extern "C" int kb_sim_dump_curious(kb_sim* s, uint32_t node, int32_t* out, size_t cap, size_t* n) {
   if (s && s->sp) return (chk(s, node) || !n) ? KB_INVALID_ARGUMENT : sp_dump_curious(s->sp, node, out, cap, n);
+  SPG_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_curious(t, node, out, cap, n); });
   if (chk(s, node) || !n) return KB_INVALID_ARGUMENT;
   GROUP_OWNER(node, [&](kb_sim* t) { return kb_sim_dump_curious(t, node, out, cap, n); });
   if (chk_row(s, node)) return KB_INVALID_ARGUMENT;
@@ -2260,6 +2350,7 @@ extern "C" int kb_sim_reset_kernel_time(kb_sim* s) {
 // rows: shard 0's for a group, like kb_sim_kernel_time
 extern "C" int kb_sim_kernel_bytes(kb_sim* s, int kind, uint64_t* bytes) {
   if (s && s->sp) { if (!bytes) return KB_INVALID_ARGUMENT; *bytes = 0; return KB_INVALID_ARGUMENT; }
+  SPG_FIRST([&](kb_sim* t) { return kb_sim_kernel_bytes(t, kind, bytes); });
   if (!s || !bytes) return KB_INVALID_ARGUMENT;
   if (is_group(s)) return kb_sim_kernel_bytes(s->shards[0], kind, bytes);
   const int k = kt_kid(kind), b = k < 0 ? -1 : kbytes_stat(k);
@@ -2269,6 +2360,7 @@ extern "C" int kb_sim_kernel_bytes(kb_sim* s, int kind, uint64_t* bytes) {
 }
 extern "C" int kb_sim_set_profiling(kb_sim* s, int level) {
   if (s && s->sp) { if (level < 0 || level > 2) return KB_INVALID_ARGUMENT; s->sp->prof_level = level; return KB_OK; }
+  SPG_ALL([&](kb_sim* t) { return kb_sim_set_profiling(t, level); });
   if (!s || level < 0 || level > 2) return KB_INVALID_ARGUMENT;
   GROUP_ALL([&](kb_sim* t) { return kb_sim_set_profiling(t, level); });
   s->prof_level = level;
@@ -2303,6 +2395,7 @@ extern "C" int kb_sim_kernel_breakdown(kb_sim* s, kb_kernel_time* out, size_t ca
 // group, the largest over its shards
 extern "C" int kb_sim_host_syncs(kb_sim* s, uint64_t* n) {
   if (s && s->sp) { if (!n) return KB_INVALID_ARGUMENT; *n = s->sp->host_syncs; return KB_OK; }
+  SPG_FIRST([&](kb_sim* t) { return kb_sim_host_syncs(t, n); });
   if (!s || !n) return KB_INVALID_ARGUMENT;
   if (is_group(s)) {
     uint64_t m = 0;
@@ -2316,6 +2409,7 @@ extern "C" int kb_sim_host_syncs(kb_sim* s, uint64_t* n) {
 // OR of the PATH_* bits (kb_common.h) of the kernel variants that did work since creation
 extern "C" int kb_sim_debug_paths(kb_sim* s, uint32_t* mask) {
   if (s && s->sp) { if (!mask) return KB_INVALID_ARGUMENT; *mask = 0; return KB_OK; }
+  SPG_FIRST([&](kb_sim* t) { return kb_sim_debug_paths(t, mask); });
   if (!s || !mask) return KB_INVALID_ARGUMENT;
   if (is_group(s)) {
     uint32_t m = 0;
@@ -2329,6 +2423,7 @@ extern "C" int kb_sim_debug_paths(kb_sim* s, uint32_t* mask) {
 // development counters (test surface): [A3 rows scanned, rows scanned past their first chunk, chunks read]
 extern "C" int kb_sim_debug_counters(kb_sim* s, uint64_t* out, size_t cap) {
   if (s && s->sp) { if (!out || cap < 3) return KB_INVALID_ARGUMENT; out[0] = out[1] = out[2] = 0; return KB_OK; }
+  SPG_FIRST([&](kb_sim* t) { return kb_sim_debug_counters(t, out, cap); });
   if (!s || !out || cap < 3) return KB_INVALID_ARGUMENT;
   kb_sim* h = is_group(s) ? s->shards[0] : s;
   { const int rc = fold_stats(h); if (rc) return rc; }
@@ -2339,6 +2434,17 @@ extern "C" int kb_sim_debug_counters(kb_sim* s, uint64_t* out, size_t cap) {
 }
 extern "C" int kb_sim_sparse_footprint(kb_sim* s, uint64_t* out, size_t cap) {
   if (!s || !out) return KB_INVALID_ARGUMENT;
+  if (sp_grp(s)) {                                   // summed over the shards' rows (the largest row: the max)
+    if (cap < 6) return KB_INVALID_ARGUMENT;
+    uint64_t t[6];
+    memset(out, 0, 6 * sizeof(uint64_t));
+    for (kb_sim* sh : s->shards) {
+      const int rc = sp_footprint(sh->sp, t, 6);
+      if (rc) return rc;
+      for (int k = 0; k < 6; ++k) out[k] = k == 3 ? std::max(out[k], t[k]) : out[k] + t[k];
+    }
+    return KB_OK;
+  }
   if (!s->sp) { seterr("not a KB_VARIANT_SPARSE_ROWS handle"); return KB_INVALID_OPERATION; }
   return sp_footprint(s->sp, out, cap);
 }

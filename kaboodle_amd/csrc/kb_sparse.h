@@ -43,8 +43,14 @@ constexpr uint32_t SP_NONE = 0xFFFFFFFFu;
 constexpr uint32_t DERR_SPARSE = 10;              // a row's entry list outgrew kb_config.sparse_row_cap
 constexpr uint32_t SP_ACC = 1024;                 // per-workgroup accumulation slots of the counters
 
+// Row shards: a handle holds the rows of ids [lo, hi).  Row tables (ent .. paq_n below, and the
+// host's per-node scratch arrays) have hi - lo rows and are biased by -lo rows, so kernels index them with global
+// ids; per-id tables (alive, start_round, idset, ext, the base and identity tables) cover all C ids on every shard
+// and are kept identical by replaying the same lifecycle on each.
 struct SpDev {
   uint32_t C, ECAP, nb;                           // ids, entries per row, |base|
+  uint32_t lo, hi;                                // this shard's rows (0, C unsharded)
+  uint32_t rank0;                                 // this shard adds the replicated counters (churn) to the stats
   uint32_t ESTR;                                  // row stride: ECAP rounded up to 4 (16-byte aligned rows)
   uint32_t k0, k1, loss_thr, churn_thr;
   int32_t fault_end;
@@ -79,6 +85,8 @@ __device__ inline bool sp_part(const SpDev& d, int32_t r, uint32_t a, uint32_t b
   return ((uint64_t)a * d.pgroups / d.C) != ((uint64_t)b * d.pgroups / d.C);
 }
 __device__ inline bool sp_bbit(const SpDev& d, uint32_t j) { return (d.bbits[j >> 5] >> (j & 31)) & 1u; }
+__device__ inline bool sp_local(const SpDev& d, uint32_t i) { return i >= d.lo && i < d.hi; }
+__device__ inline uint32_t sp_gid(const SpDev& d) { return d.lo + blockIdx.x * blockDim.x + threadIdx.x; }   // row kernels
 __device__ inline uint32_t* sp_row(const SpDev& d, uint32_t i) { return d.ent + (size_t)i * d.ESTR; }
 // a row's entries e[k..n) move up one place and v lands at e[k] (insertion; n < ESTR), in 16-byte steps from the
 // top of the row's aligned groups down (a thread per row: a quarter of the memory instructions of a word loop)
@@ -389,21 +397,23 @@ __device__ inline uint32_t sp_reply_bound(uint32_t k) {
 }
 
 // ---- round kernels ------------------------------------------------------------------------------------
-__global__ void k_sp_init(SpDev d, uint32_t n0, uint32_t converged) {
+__global__ void k_sp_init(SpDev d, uint32_t n0, uint32_t converged) {   // over all ids: per-id facts, then the local rows
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= d.C) return;
-  d.last_bcast[i] = NONE_ROUND; d.start_round[i] = NONE_ROUND; d.a3cur[i] = i;
+  d.start_round[i] = i < n0 ? 0 : NONE_ROUND;
+  if (i < n0) d.alive[i] = 1;
+  if (!sp_local(d, i)) return;
+  d.last_bcast[i] = NONE_ROUND; d.a3cur[i] = i;
   d.based[i] = (i < d.nb || d.nb == 0) ? 1 : 0;
   if (i >= n0) return;
-  d.alive[i] = 1; d.start_round[i] = 0;
   sp_insert_known(d, i, i, 0, 0);                 // known_peers.insert(self, Known(now)) src/kaboodle.rs:145-152
   d.dirty[i] = 1;
   if (converged) { d.n[i] = n0; d.last_bcast[i] = -1000; }   // running for a while: no Join at round 0
 }
 // stamp window: explicit Known stamps shift down by 64; the ones that saturate become implicit
 __global__ void k_sp_rebase(SpDev d) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.C) return;
+  const uint32_t i = sp_gid(d);
+  if (i >= d.hi) return;
   uint32_t* e = sp_row(d, i);
   const uint32_t n = d.ne[i];
   uint32_t o = 0;
@@ -421,6 +431,7 @@ __global__ void k_sp_rebase(SpDev d) {
 // lifecycle (src/lib.rs:136-183, src/kaboodle.rs:114-185)
 __device__ inline void sp_node_start(const SpDev& d, uint32_t i, int32_t r) {
   d.alive[i] = 1; d.start_round[i] = r;
+  if (!sp_local(d, i)) return;                    // the row's part: on the shard holding it
   sp_insert_known(d, i, i, r, r);
   d.dirty[i] = 1;
   d.last_bcast[i] = NONE_ROUND;
@@ -428,10 +439,14 @@ __device__ inline void sp_node_start(const SpDev& d, uint32_t i, int32_t r) {
   d.paq_n[i] = 0; d.a3cur[i] = i;
 }
 __device__ inline void sp_node_stop(const SpDev& d, uint32_t i) {
+  d.alive[i] = 0;
+  if (!sp_local(d, i)) return;
   sp_remove(d, i, i);
-  d.alive[i] = 0; d.paq_n[i] = 0;
+  d.paq_n[i] = 0;
 }
-// Kaboodle::start on a stopped instance: a fresh address that inherits the map
+// a restart whose row a sharded mesh moved between shards first (sp_move_row): the start of the fresh address
+constexpr uint32_t EV_START_MOVED = 3;
+// Kaboodle::start on a stopped instance: a fresh address that inherits the map; unsharded
 __device__ inline void sp_node_restart(const SpDev& d, uint32_t from, uint32_t to, int32_t r) {
   const uint32_t n = d.ne[from];
   const uint32_t* a = sp_row(d, from);
@@ -448,10 +463,34 @@ __global__ void k_sp_events(SpDev d, const Event* ev, uint32_t nev, int32_t r) {
     const uint32_t i = ev[k].node;
     if (ev[k].kind == EV_STOP) { if (d.alive[i]) sp_node_stop(d, i); }
     else if (ev[k].kind == EV_RESTART) sp_node_restart(d, ev[k].src, i, r);
+    else if (ev[k].kind == EV_START_MOVED) sp_node_start(d, i, r);
     else if (!d.alive[i]) sp_node_start(d, i, r);
   }
 }
-__global__ void k_sp_churn_leave(SpDev d, int32_t r) {
+// a restart's map across shards (sharded meshes): the old address's row packed on the shard holding it, unpacked
+// into the fresh address's row on the shard holding that (the rest of the restart is EV_START_MOVED)
+constexpr uint32_t SP_PACK_HDR = 4 + 4 * SLOTS;   // ne, based, n, pad, the suspect slots; then ESTR entries
+__global__ void k_sp_row_pack(SpDev d, uint32_t from, uint32_t* buf) {
+  const uint32_t n = d.ne[from];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    buf[0] = n; buf[1] = d.based[from]; buf[2] = d.n[from]; buf[3] = 0;
+    const Susp* s = d.susp + (size_t)from * SLOTS;
+    for (int k = 0; k < SLOTS; ++k) { buf[4 + 4 * k] = s[k].peer; buf[5 + 4 * k] = (uint32_t)s[k].since; buf[6 + 4 * k] = (uint32_t)s[k].kind; buf[7 + 4 * k] = 0; }
+  }
+  const uint32_t* e = sp_row(d, from);
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) buf[SP_PACK_HDR + q] = e[q];
+}
+__global__ void k_sp_row_unpack(SpDev d, uint32_t to, const uint32_t* buf) {
+  const uint32_t n = buf[0];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    d.ne[to] = n; d.based[to] = (uint8_t)buf[1]; d.n[to] = buf[2]; d.dirty[to] = 1;
+    Susp* s = d.susp + (size_t)to * SLOTS;
+    for (int k = 0; k < SLOTS; ++k) { s[k].peer = buf[4 + 4 * k]; s[k].since = (int32_t)buf[5 + 4 * k]; s[k].kind = (int32_t)buf[6 + 4 * k]; s[k].pad = 0; }
+  }
+  uint32_t* e = sp_row(d, to);
+  for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) e[q] = buf[SP_PACK_HDR + q];
+}
+__global__ void k_sp_churn_leave(SpDev d, int32_t r) {   // over all ids: every shard replays the lifecycle
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   unsigned long long left = 0;
   if (i < d.C && d.alive[i] && d.start_round[i] != r &&
@@ -470,7 +509,7 @@ __global__ void k_sp_churn_join(SpDev d, int32_t r) {
     joins++;
   }
   d.ctr[C_NEXTFREE] = nf; d.ctr[C_LEAVES] = 0;
-  d.stats[S_CLEAVE] += leaves; d.stats[S_CJOIN] += joins;
+  if (d.rank0) { d.stats[S_CLEAVE] += leaves; d.stats[S_CJOIN] += joins; }   // replicated: counted once
 }
 
 // the running set's fingerprint: SP_TFP contiguous id ranges folded by a thread each, then combined in order
@@ -510,7 +549,7 @@ struct SpBc {
   const BCast* bfail; uint32_t nf;
   uint32_t fcounted;                             // the Failed group was counted by k_sp_bfail_sf (socket_faithful)
   const BCast* bjoin; uint32_t nj; uint32_t JW;
-  uint32_t* jnew; uint32_t* jresp;               // [C][JW] bits: the entry inserted its joiner / got a response
+  uint32_t* jnew; uint32_t* jresp;               // [local rows][JW] bits: the entry inserted its joiner / got a response
   uint32_t* jr_n; uint32_t* jr_pay;              // per node: responses, their payload ids
   uint32_t np; uint2* presp; uint32_t* presp_n; uint32_t presp_cap;
 };
@@ -524,10 +563,10 @@ __device__ inline bool sp_should_respond(const SpDev& d, uint32_t i, uint32_t c2
   return (int64_t)mulhi(u, 100) < pct;
 }
 __global__ __launch_bounds__(256) void k_sp_bcast(SpDev d, SpBc bc, int32_t r) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = sp_gid(d);
   unsigned long long lost = 0, removed = 0, presp = 0, plost = 0, jresp = 0;
   uint32_t nresp = 0, pay = 0;
-  if (i < d.C && d.alive[i] && d.start_round[i] < r) {
+  if (i < d.hi && d.alive[i] && d.start_round[i] < r) {
     const bool fl = sp_faults(d, r) && d.loss_thr;
     // partition groups: the receiver's once, each entry's precomputed by k_sp_bcast_write (BCast.pad)
     const bool pact = d.pgroups > 1 && r >= d.pstart && r < d.pend;
@@ -557,9 +596,9 @@ __global__ __launch_bounds__(256) void k_sp_bcast(SpDev d, SpBc bc, int32_t r) {
       }
       if (ls) { lost++; continue; }
       if (!sp_insert_known(d, i, b.sender, r, r)) continue;
-      bc.jnew[(size_t)i * bc.JW + (k >> 5)] |= 1u << (k & 31);
+      bc.jnew[(size_t)(i - d.lo) * bc.JW + (k >> 5)] |= 1u << (k & 31);
       if (!sp_should_respond(d, i, (uint32_t)P_RESPOND << 24, b.sender, r)) continue;
-      bc.jresp[(size_t)i * bc.JW + (k >> 5)] |= 1u << (k & 31);
+      bc.jresp[(size_t)(i - d.lo) * bc.JW + (k >> 5)] |= 1u << (k & 31);
       const uint32_t m = d.n[i];
       nresp++; pay += (d.uniform && m > d.capj) ? d.capj : m;
     }
@@ -575,7 +614,7 @@ __global__ __launch_bounds__(256) void k_sp_bcast(SpDev d, SpBc bc, int32_t r) {
     }
     jresp = nresp;
   }
-  if (i < d.C) { bc.jr_n[i] = nresp; bc.jr_pay[i] = pay; }
+  if (i < d.hi) { bc.jr_n[i] = nresp; bc.jr_pay[i] = pay; }
   const int idx[5] = {S_BDROP, S_RMFAILED, S_PROBERESP, S_LOSS, S_JRESP};
   const unsigned long long v[5] = {lost, removed, presp, plost, jresp};
   sp_stats(d, idx, v);
@@ -592,8 +631,8 @@ __global__ __launch_bounds__(256) void k_sp_bcast(SpDev d, SpBc bc, int32_t r) {
 constexpr uint32_t SP_FK_LDS = 1024;              // 16-byte groups (4096 entries) staged per pass
 __global__ __launch_bounds__(256) void k_sp_bfail_sf(SpDev d, const uint4* __restrict__ fkey, uint32_t nf, int32_t r) {
   __shared__ uint4 sk[SP_FK_LDS];
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool act = i < d.C && d.alive[i] && d.start_round[i] < r;
+  const uint32_t i = sp_gid(d);
+  const bool act = i < d.hi && d.alive[i] && d.start_round[i] < r;
   const bool fl = sp_faults(d, r) && d.loss_thr;
   const bool pact = d.pgroups > 1 && r >= d.pstart && r < d.pend;
   const uint32_t rg = pact ? (uint32_t)((uint64_t)i * d.pgroups / d.C) : 0u;
@@ -667,10 +706,10 @@ __device__ inline void sp_heapsort(uint32_t* a, uint32_t n) {
 // region after nothing (they come first).  The map a response lists is the map as it stood when that
 // entry was handled: the final row minus the joiners later entries inserted (Join entries only insert).
 __global__ __launch_bounds__(256) void k_sp_jresp(SpDev d, SpBc bc, SpOut o0, int32_t r) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.C || !bc.jr_n[i]) return;
-  const uint32_t* jn = bc.jnew + (size_t)i * bc.JW;
-  const uint32_t* jr = bc.jresp + (size_t)i * bc.JW;
+  const uint32_t i = sp_gid(d);
+  if (i >= d.hi || !bc.jr_n[i]) return;
+  const uint32_t* jn = bc.jnew + (size_t)(i - d.lo) * bc.JW;
+  const uint32_t* jr = bc.jresp + (size_t)(i - d.lo) * bc.JW;
   uint32_t later = 0;                                        // new joiners of entries after the current one
   for (uint32_t w = 0; w < bc.JW; ++w) later += __popc(jn[w]);
   uint32_t seq = 0, pc = 0;
@@ -726,8 +765,8 @@ __global__ __launch_bounds__(256) void k_sp_jresp(SpDev d, SpBc bc, SpOut o0, in
 
 // wave-0 region bounds: the node's Join responses + its tick's emissions (A2 PingRequests, A3, A4)
 __global__ void k_sp_bound0(SpDev d, const uint32_t* jr_n, uint32_t* ecap) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.C) return;
+  const uint32_t i = sp_gid(d);
+  if (i >= d.hi) return;
   uint32_t b = 0;
   if (d.alive[i]) {
     uint32_t sc = 0;
@@ -738,13 +777,13 @@ __global__ void k_sp_bound0(SpDev d, const uint32_t* jr_n, uint32_t* ecap) {
 }
 
 // ---- tick (src/kaboodle.rs:746-779) ---------------------------------------------------------------
-struct SpTickOut { uint32_t* bj; uint32_t* bnf; uint32_t* bfp; };   // Join flag, Failed count, Failed peers [C][8]
+struct SpTickOut { uint32_t* bj; uint32_t* bnf; uint32_t* bfp; };   // per row: Join flag, Failed count, Failed peers [8]
 __global__ __launch_bounds__(256) void k_sp_tick(SpDev d, SpOut o0, const uint32_t* jr_n, SpTickOut bo, const uint32_t* tfp,
                                                  int32_t r) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = sp_gid(d);
   unsigned long long rmt = 0, agree = 0, run = 0;
-  if (i < d.C) { bo.bj[i] = 0; bo.bnf[i] = 0; o0.en[i] = jr_n[i]; }
-  if (i < d.C && d.alive[i]) {
+  if (i < d.hi) { bo.bj[i] = 0; bo.bnf[i] = 0; o0.en[i] = jr_n[i]; }
+  if (i < d.hi && d.alive[i]) {
     uint32_t seq = jr_n[i];
     // A1 maybe_broadcast_join (:228-251)
     if (d.last_bcast[i] == NONE_ROUND || (r - d.last_bcast[i] >= REBROADCAST && d.n[i] <= 1)) { bo.bj[i] = 1; d.last_bcast[i] = r; }
@@ -840,18 +879,21 @@ __global__ __launch_bounds__(256) void k_sp_tick(SpDev d, SpOut o0, const uint32
     if (tr) atomicAdd(&s[1], tr);
   }
 }
-__global__ void k_sp_bcast_write(SpDev d, SpTickOut bo, const uint32_t* joff, const uint32_t* foff, BCast* bjoin, BCast* bfail,
-                                 uint32_t* fkey) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.C) return;
+// the shard's broadcast lists (sender order); sharded meshes all-gather them into the round's lists afterwards
+__global__ void k_sp_bcast_write(SpDev d, SpTickOut bo, const uint32_t* joff, const uint32_t* foff, BCast* bjoin, BCast* bfail) {
+  const uint32_t i = sp_gid(d);
+  if (i >= d.hi) return;
   uint32_t bseq = 0;
   const uint32_t g = d.pgroups > 1 ? (uint32_t)((uint64_t)i * d.pgroups / d.C) : 0u;   // the sender's partition group
   if (bo.bj[i]) bjoin[joff[i]] = BCast{i, i, bseq++, g};
   const uint32_t nf = bo.bnf[i];
-  for (uint32_t q = 0; q < nf; ++q) {
-    bfail[foff[i] + q] = BCast{i, bo.bfp[(size_t)i * SLOTS + q], bseq++, g};
-    fkey[foff[i] + q] = (i << 8) | (g & 255u);     // k_sp_bfail_sf's packed entry (partition groups <= 255)
-  }
+  for (uint32_t q = 0; q < nf; ++q) bfail[foff[i] + q] = BCast{i, bo.bfp[(size_t)i * SLOTS + q], bseq++, g};
+}
+// k_sp_bfail_sf's packed Failed list: sender << 8 | partition group (groups <= 255), four entries per 16 bytes
+__global__ void k_sp_fkey(const BCast* bfail, uint32_t nf, uint32_t* fkey) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nf) fkey[k] = (bfail[k].sender << 8) | (bfail[k].pad & 255u);
+  else if (k < ((nf + 3) & ~3u)) fkey[k] = 0xFFFFFFFFu;      // the last group's padding
 }
 
 // ---- receive window (src/kaboodle.rs:394-548) -----------------------------------------------------
@@ -873,7 +915,10 @@ __global__ __launch_bounds__(256) void k_sp_route(SpDev d, SpRoute rt, int32_t r
     sp_count_sent(m, s);
     uint8_t st = 0;
     if (!d.alive[m.dest]) {
-      if (d.ext[m.dest]) { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, rt.pay, r, w); xp++; }
+      if (d.ext[m.dest]) {                                             // a partition cuts it off too
+        if (sp_part(d, r, m.sender, m.dest)) part++;
+        else { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, rt.pay, r, w); xp++; }
+      }
       else dead++;
     }
     else if (sp_part(d, r, m.sender, m.dest)) part++;
@@ -920,8 +965,8 @@ __global__ __launch_bounds__(256) void k_sp_window(SpDev d, const Msg* msgs, uin
 // payload bound of the node's KnownPeersRequest replies: each <= capk ids (larger ones are dropped) and <= its
 // fresh stamps, which are explicit entries now or prologue insertions of this wave
 __global__ void k_sp_paybound(SpDev d, const uint32_t* kprc, const uint32_t* icnt, uint32_t* pb) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.C) return;
+  const uint32_t i = sp_gid(d);
+  if (i >= d.hi) return;
   const uint32_t k = kprc[i];
   pb[i] = k ? k * min(d.capk, d.ne[i] + icnt[i]) : 0u;
 }
@@ -946,10 +991,10 @@ __device__ inline void sp_maybe_sync(const SpDev& d, const SpOut& o, uint32_t i,
 // (compiled for 8 waves per SIMD: a thread per row waits on dependent loads, so occupancy is its throughput;
 // 130 -> 64 VGPRs measured 13.5 -> 12.0 ms a round at 1M peers)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_sp_handle(SpDev d, SpWave v, SpOut o, int32_t r) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t i = sp_gid(d);
   unsigned long long oversize = 0, curovf = 0;
-  if (i < d.C) o.en[i] = 0;
-  if (i < d.C && v.icnt[i]) {
+  if (i < d.hi) o.en[i] = 0;
+  if (i < d.hi && v.icnt[i]) {
     uint32_t* ib = v.inbox + v.ioff[i];
     const uint32_t cnt = v.icnt[i];
     for (uint32_t q = 0; q < cnt; ++q) ib[q] |= (v.in[ib[q]].kind != K_KP) ? 0x80000000u : 0u;
@@ -960,8 +1005,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
       ib[b] = x;
     }
     uint32_t seq = 0, pc = 0;
-    const uint32_t* idl = nullptr;
-    (void)idl;
     for (uint32_t q = 0; q < cnt; ++q) {
       const Msg m = v.in[ib[q] & 0x7FFFFFFFu];
       const uint32_t from = m.sender;
@@ -1027,14 +1070,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
 }
 // the emitted records, node by node (sender order, seq order inside), become the next wave's records
 __global__ void k_sp_compact(SpDev d, SpOut o, const uint32_t* ooff, Msg* next) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= d.C) return;
+  const uint32_t i = sp_gid(d);
+  if (i >= d.hi) return;
   const uint32_t n = o.en[i];
   const Msg* src = o.stage + o.eoff[i];
   Msg* dst = next + ooff[i];
   for (uint32_t q = 0; q < n; ++q) dst[q] = src[q];
 }
-// round results: agreement, convergence, running peers summed over rounds
+// round results: agreement and running peers of this shard's rows (sharded meshes then sum them over the ranks),
+// running peers summed over rounds; then convergence from the mesh's totals (k_sp_round_conv)
 __global__ __launch_bounds__(1024) void k_sp_round_end(SpDev d, int32_t r) {
   unsigned long long a = 0, al = 0;
   for (uint32_t k = threadIdx.x; k < SP_ACC; k += blockDim.x) {
@@ -1047,11 +1091,107 @@ __global__ __launch_bounds__(1024) void k_sp_round_end(SpDev d, int32_t r) {
   if (threadIdx.x == 0) {
     d.ctr[C_LASTAGREE] = (uint32_t)a; d.ctr[C_LASTALIVE] = (uint32_t)al;
     d.stats[S_ALIVER] += al;
-    if (al && a == al) {
-      if ((int32_t)d.ctr[C_FIRSTCONV] < 0) d.ctr[C_FIRSTCONV] = (uint32_t)r;
-      d.ctr[C_LASTCONV] = (uint32_t)r;
-    }
   }
+}
+__global__ void k_sp_round_conv(SpDev d, int32_t r) {
+  if (threadIdx.x || blockIdx.x) return;
+  const uint32_t a = d.ctr[C_LASTAGREE], al = d.ctr[C_LASTALIVE];
+  if (al && a == al) {
+    if ((int32_t)d.ctr[C_FIRSTCONV] < 0) d.ctr[C_FIRSTCONV] = (uint32_t)r;
+    d.ctr[C_LASTCONV] = (uint32_t)r;
+  }
+}
+
+// ---- row shards: the delivery waves' exchange ----------------------------------------------
+// The records of a wave are routed on the shard of their sender (dead receiver, partition and the Philox loss
+// are keyed on the message, so the shard cannot change them), bucketed by the rank holding the destination's row
+// in (sender, seq) order, all-to-all-v'd with their KnownPeers ids, and counted per destination on arrival.  The
+// received blocks come in rank order = sender order, so a record's index keeps the (sender, seq) order the
+// handler sorts by, exactly as in the unsharded wave.
+struct SpX {
+  uint32_t world, R, S;                               // ranks, local rows, rows per rank (rank of id j = j / S)
+  uint32_t* xcnt; uint32_t* xpay;                     // [world][R] delivered records / KnownPeers ids per (rank, sender)
+  uint32_t* xoff; uint32_t* xpoff;                    // their exclusive scans (rank-major: each rank's block contiguous)
+  uint32_t* xb;                                       // [2 * world] records, then ids, to each rank
+  Msg* smsg; uint32_t* spay;                          // send buffers
+};
+__global__ __launch_bounds__(256) void k_sp_route_x(SpDev d, SpRoute rt, SpX x, int32_t r, uint32_t w) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long s[6] = {0, 0, 0, 0, 0, 0}, dead = 0, part = 0, loss = 0, xp = 0;
+  if (k < rt.M) {
+    const Msg m = rt.msgs[k];
+    sp_count_sent(m, s);
+    uint8_t st = 0;
+    if (!d.alive[m.dest]) {
+      if (d.ext[m.dest]) {                                             // a partition cuts it off too
+        if (sp_part(d, r, m.sender, m.dest)) part++;
+        else { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, rt.pay, r, w); xp++; }
+      }
+      else dead++;
+    }
+    else if (sp_part(d, r, m.sender, m.dest)) part++;
+    else if (sp_faults(d, r) && d.loss_thr &&
+             philox(m.sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m.seq, d.k0, d.k1).x < d.loss_thr) loss++;
+    else {
+      st = 1;
+      const size_t c = (size_t)(m.dest / x.S) * x.R + (m.sender - d.lo);
+      atomicAdd(&x.xcnt[c], 1u);
+      if (m.kind == K_KP && m.a) atomicAdd(&x.xpay[c], m.a);
+    }
+    rt.status[k] = st;
+  }
+  const int idx[10] = {S_PING, S_PINGREQ, S_ACK, S_KP, S_KPR, S_KPIDS, S_DEAD, S_PART, S_LOSS, S_EXPORT};
+  const unsigned long long v[10] = {s[0], s[1], s[2], s[3], s[4], s[5], dead, part, loss, xp};
+  sp_stats(d, idx, v);
+}
+// per rank: records and ids it receives from this shard (the blocks of the rank-major scans)
+__global__ void k_sp_xbound(SpX x, const uint32_t* tot) {
+  const uint32_t k = threadIdx.x;
+  if (k >= x.world) return;
+  const size_t a = (size_t)k * x.R, b = (size_t)(k + 1) * x.R;
+  x.xb[k] = (k + 1 < x.world ? x.xoff[b] : tot[0]) - x.xoff[a];
+  x.xb[x.world + k] = (k + 1 < x.world ? x.xpoff[b] : tot[1]) - x.xpoff[a];
+}
+// a thread per sender: its delivered records, in seq order, into each destination rank's block; a KnownPeers
+// record's ids follow it, its offset made relative to the block (the receiver adds where the block lands)
+__global__ __launch_bounds__(256) void k_sp_pack(SpDev d, SpX x, const Msg* msgs, const uint8_t* status, const uint32_t* pay,
+                                                 const uint32_t* ooff, const uint32_t* en) {
+  const uint32_t i = sp_gid(d);
+  if (i >= d.hi) return;
+  const uint32_t n = en[i], li = i - d.lo;
+  if (!n) return;
+  uint32_t c[XMAX], pc[XMAX];
+  for (uint32_t q = 0; q < x.world; ++q) { c[q] = 0; pc[q] = 0; }
+  for (uint32_t q = 0; q < n; ++q) {
+    const uint32_t k = ooff[i] + q;
+    if (!status[k]) continue;
+    Msg m = msgs[k];
+    const uint32_t dr = m.dest / x.S;
+    const size_t cell = (size_t)dr * x.R + li;
+    if (m.kind == K_KP) {
+      const uint32_t po = x.xpoff[cell] + pc[dr];
+      for (uint32_t t = 0; t < m.a; ++t) x.spay[po + t] = pay[m.off + t];
+      m.off = po - x.xpoff[(size_t)dr * x.R];
+      pc[dr] += m.a;
+    }
+    x.smsg[x.xoff[cell] + c[dr]] = m;
+    c[dr]++;
+  }
+}
+// the received records: KnownPeers offsets into the received id blocks, then per destination the delivered
+// count, the reply bound and the KnownPeersRequests (k_sp_route's delivered branch)
+struct SpRecvBlocks { uint32_t p0[XMAX]; };
+__global__ __launch_bounds__(256) void k_sp_recv(SpRoute rt, SpX x, SpRecvBlocks rb) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= rt.M) return;
+  Msg* mp = const_cast<Msg*>(rt.msgs) + k;
+  const Msg m = *mp;
+  if (m.kind == K_KP) mp->off = m.off + rb.p0[m.sender / x.S];
+  rt.status[k] = 1;
+  atomicAdd(&rt.icnt[m.dest], 1u);
+  const uint32_t b = sp_reply_bound(m.kind);
+  if (b) atomicAdd(&rt.ebound[m.dest], b);
+  if (m.kind == K_KPR) atomicAdd(&rt.kprc[m.dest], 1u);
 }
 __global__ __launch_bounds__(256) void k_sp_stats_fold(SpDev d) {
   const uint32_t k = blockIdx.x;
@@ -1064,13 +1204,13 @@ __global__ __launch_bounds__(256) void k_sp_stats_fold(SpDev d) {
   if (threadIdx.x == 0 && t) d.stats[k] += t;
 }
 __global__ void k_sp_fp_all(SpDev d) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < d.C) (void)sp_fp(d, i);
+  const uint32_t i = sp_gid(d);
+  if (i < d.hi) (void)sp_fp(d, i);
 }
 __global__ void k_sp_fp_one(SpDev d, uint32_t i) { if (!threadIdx.x && !blockIdx.x) (void)sp_fp(d, i); }
 __global__ void k_sp_mark_dirty(SpDev d) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < d.C) d.dirty[i] = 1;
+  const uint32_t i = sp_gid(d);
+  if (i < d.hi) d.dirty[i] = 1;
 }
 
 }  // namespace kb

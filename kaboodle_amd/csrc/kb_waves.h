@@ -85,7 +85,10 @@ __global__ __launch_bounds__(256) void k_route(Dev d, OutBuf ob, WaveCtl wc, int
     uint8_t st = 0;
     if (last) win++;
     else if (!d.alive[m.dest]) {
-      if (d.ext[m.dest]) { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, ob.pay, r, w); xp++; }
+      if (d.ext[m.dest]) {                                             // a partition cuts it off too
+        if (part_blocks(d, r, m.sender, m.dest)) part++;
+        else { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, ob.pay, r, w); xp++; }
+      }
       else dead++;
     }
     else if (part_blocks(d, r, m.sender, m.dest)) part++;
@@ -257,7 +260,10 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
     uint8_t st = 0;
     if (last) win++;
     else if (!d.alive[m.dest]) {
-      if (d.ext[m.dest]) { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, ob.pay, r, w); xp++; }   // the sender's shard exports
+      if (d.ext[m.dest]) {                                             // the sender's shard exports (partition: dropped)
+        if (part_blocks(d, r, m.sender, m.dest)) part++;
+        else { export_rec(d.ctr, d.xrec, d.xrec_cap, d.xids, d.xids_cap, m, ob.pay, r, w); xp++; }
+      }
       else dead++;
     }
     else if (part_blocks(d, r, m.sender, m.dest)) part++;

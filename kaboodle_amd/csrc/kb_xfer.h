@@ -212,7 +212,10 @@ struct IpcXfer : Xfer {
   size_t wbytes = 0;
   std::vector<char*> peer;                               // the other ranks' windows, mapped here
   std::string err, name;
-  bool fail(const std::string& what) { err = what; if (sh) sh->aborted.store(1); return false; }
+  bool unlinked = false;
+  // rank 0 created the segment's name: every failure path removes it (no /dev/shm leftovers from failed runs)
+  void unlink_name() { if (rank == 0 && !name.empty() && !unlinked) { shm_unlink(name.c_str()); unlinked = true; } }
+  bool fail(const std::string& what) { err = what; if (sh) sh->aborted.store(1); unlink_name(); return false; }
   bool barrier() {
     const uint64_t g = sh->gen.load(std::memory_order_acquire);
     if (sh->arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)world) {
@@ -235,12 +238,12 @@ struct IpcXfer : Xfer {
     int fd2 = fd;
     for (int t = 0; fd2 < 0 && r != 0 && t < 20000; ++t) { usleep(1000); fd2 = shm_open(name.c_str(), O_RDWR, 0600); }
     if (fd2 < 0) { err = "shm_open " + name; return false; }
-    if (r == 0 && ftruncate(fd2, (off_t)shsz) != 0) { close(fd2); err = "ftruncate"; return false; }
+    if (r == 0 && ftruncate(fd2, (off_t)shsz) != 0) { close(fd2); return fail("ftruncate"); }
     struct stat stt;
     for (int t = 0; t < 20000; ++t) { if (fstat(fd2, &stt) == 0 && (size_t)stt.st_size >= shsz) break; usleep(1000); }
     void* p = mmap(nullptr, shsz, PROT_READ | PROT_WRITE, MAP_SHARED, fd2, 0);
     close(fd2);
-    if (p == MAP_FAILED) { err = "mmap"; return false; }
+    if (p == MAP_FAILED) return fail("mmap");
     sh = static_cast<IpcShared*>(p);                      // zero-filled by ftruncate: counters start at 0
     if (hipMalloc((void**)&win, wbytes) != hipSuccess) return fail("window allocation");
     if (hipIpcGetMemHandle(&sh->handle[r], win) != hipSuccess) return fail("hipIpcGetMemHandle");
@@ -258,7 +261,7 @@ struct IpcXfer : Xfer {
       peer[k] = static_cast<char*>(q);
     }
     if (!barrier()) return fail("IPC attach barrier");
-    if (r == 0) shm_unlink(name.c_str());                 // every rank has it mapped: no name left behind
+    unlink_name();                                        // every rank has it mapped: no name left behind
     return true;
   }
   ~IpcXfer() override {

@@ -1118,6 +1118,7 @@ static int run_waves(kbo_sim* s, int32_t r) {
     for (size_t k = 0; k < M; ++k) {
       omsg* m = &all[k];
       if (!s->alive[m->dest] && s->ext[m->dest]) {      /* to an external peer: leaves the simulated transport */
+        if (partition_blocks(s, r, m->sender, m->dest)) { s->st.drop_partition++; continue; }   /* unless cut off */
         if (s->nxp == s->capxp) { s->capxp = s->capxp ? 2 * s->capxp : 64; s->xp = (kb_unicast*)realloc(s->xp, s->capxp * sizeof(kb_unicast)); }
         kb_unicast* x = &s->xp[s->nxp++];
         memset(x, 0, sizeof *x);

@@ -174,3 +174,22 @@ def test_networking_plumbing():
     if ifs:
         best = networking.best_available_interface()
         assert best in ifs and (best.is_ipv6 or not any(i.is_ipv6 for i in ifs))
+
+
+def test_bridge_survives_socket_exhaustion():
+    """a simulated peer that cannot get a socket (max_peer_sockets, or EMFILE from the OS) costs the
+    datagrams that needed it (counted), never an exception after the round's exports were drained."""
+    from kaboodle_amd.bridge import Bridge
+    with Sim(parity.oracle_lib(), SimConfig(capacity=8, initial_nodes=0, id_len=5, seed=3)) as mesh:
+        bin_ = _udp()
+        bin_.setblocking(False)
+        uni = _udp()
+        for i in range(2):
+            mesh.start_node(i)
+        br = Bridge(mesh, sockets=(bin_, bin_, bin_.getsockname(), uni), max_peer_sockets=0)
+        assert br.peer_socket(3) is None and br.addr_for(3) is None and br.stats["no_socket"] == 2
+        br.run_round()
+        mesh.probe(("127.0.0.1", 9))
+        br.run_round()                     # both peers answer the Probe: no socket to answer from
+        assert br.stats["send_failed"] == 2 and br.stats["probe_responses_out"] == 0
+        br.close()

@@ -26,7 +26,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, name, q):
+def _case(name, sparse):
+    case, rounds = CASES[name]
+    if sparse:
+        from kaboodle_amd._ffi import KB_VARIANT_SPARSE_ROWS
+        case = parity.with_cfg(case, variant=KB_VARIANT_SPARSE_ROWS, track_latency=0)
+    return case, rounds
+
+
+def _rank_main(rank, world, port, name, q, sparse=False):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -39,7 +47,7 @@ def _rank_main(rank, world, port, name, q):
         from kaboodle_amd._ffi import Sim, ipc_unique_id
         lib = par.gpu_lib()
         uid = bench.share_uid(rank, lambda: ipc_unique_id(lib))
-        case, rounds = CASES[name]
+        case, rounds = _case(name, sparse)
         g = Sim(lib, case["cfg"], rank=rank, world=world, uid=uid)
         _, _, lo, hi = g.shard_info()
         par.setup(g, case)
@@ -62,18 +70,22 @@ def _rank_main(rank, world, port, name, q):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("name,world", [("churn_loss_512", 2), ("stop_start", 2), ("partition_heal", 2), ("fresh_ids", 2),
-                                        ("identity_change", 2), ("churn_loss_512", 4), ("partition_heal", 4)])
-def test_processes_equal_oracle(name, world):
+@pytest.mark.parametrize("name,world,sparse", [("churn_loss_512", 2, False), ("stop_start", 2, False),
+                                               ("partition_heal", 2, False), ("fresh_ids", 2, False),
+                                               ("identity_change", 2, False), ("churn_loss_512", 4, False),
+                                               ("partition_heal", 4, False),
+                                               # configs[4]'s sparse rows as rank processes
+                                               ("churn_loss_512", 2, True), ("stop_start", 2, True)])
+def test_processes_equal_oracle(name, world, sparse):
     import multiprocessing as mp
     import kaboodle_amd
     kaboodle_amd.require_gpu()
     from kaboodle_amd._ffi import Sim
-    case, rounds = CASES[name]
+    case, rounds = _case(name, sparse)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(k, world, port, name, q)) for k in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(k, world, port, name, q, sparse)) for k in range(world)]
     for p in procs:
         p.start()
     res = {}

@@ -95,3 +95,16 @@ def test_sparse_partition_heal(gpu, n, rounds, every, flags):
     assert (fo["rows_based"], fo["exceptions"], fo["stamps"]) == (fg["rows_based"], fg["exceptions"], fg["stamps"]), (fo, fg)
     o.close()
     g.close()
+
+
+SHARD_CASES = [c for c in CASES if c[1]["cfg"].capacity > 4]   # config1_2x2's 4 ids cannot make 3 shards
+
+
+@pytest.mark.parametrize("name,case,rounds", SHARD_CASES, ids=[c[0] for c in SHARD_CASES])
+def test_sparse_sharded_parity_every_round(gpu, name, case, rounds):
+    """The standard matrix on sparse rows split into 3 row shards inside one process (kb_sim_create_local): every
+    wave's records routed on the sender's shard and all-to-all-v'd to the receiver's, the broadcast lists
+    all-gathered, restarts moving the row (and its observer) between shards (src/kaboodle.rs:188-226, :394-548) —
+    the complete state equals the oracle's every round."""
+    ok, msg, _ = parity.run_case(sparse(case), rounds, shards=3)
+    assert ok, f"{name} (sparse rows, 3 shards): {msg}"

@@ -137,6 +137,85 @@ def run(n: int, rounds: int, every: int, row_cap: int, check_rows: int, seed: in
             "gpu_round_ms_mean": round(round_ms / max(nr, 1), 2), "final_stats": st, "failures": fails}
 
 
+def digest_diff(a, b, rng, nrows: int) -> list[str]:
+    """Two GPU handles of one mesh (e.g. unsharded and as row shards): counters, every fingerprint and per-node
+    scalar, and for sampled nodes the whole row, suspect/curious tables and peer_states."""
+    out = []
+    sa, sb = a.stats(), b.stats()
+    out += [f"stats.{k}: {v} != {sb[k]}" for k, v in sa.items() if sb[k] != v]
+    fa, fb = a.fingerprints(), b.fingerprints()
+    if not np.array_equal(fa, fb):
+        out.append(f"fingerprints: {int((fa != fb).sum())} differ, first {np.argwhere(fa != fb)[:3].ravel().tolist()}")
+    if not np.array_equal(a.scalars(), b.scalars()):
+        out.append("scalars differ")
+    for i in rng.choice(a.capacity, nrows, replace=False):
+        i = int(i)
+        if not np.array_equal(a.row(i), b.row(i)):
+            out.append(f"row {i} differs")
+        if a.suspects(i) != b.suspects(i) or a.curious(i) != b.curious(i):
+            out.append(f"suspect/curious table {i} differs")
+        if a.peer_states(i) != b.peer_states(i):
+            out.append(f"peer_states {i} differ")
+        if out:
+            break
+    return out
+
+
+def run_twin(case: dict, rounds: int, shards: int, nrows: int = 4, check_rows: int = 2, seed: int = 3,
+             verbose: bool = False, externals=(), join_rounds=()) -> dict:
+    """The mesh unsharded and as `shards` in-process row shards (kb_sim_create_local: every wave's records
+    all-to-all-v'd between the shards, the broadcast lists all-gathered), stepped in lock step: digest_diff every
+    round, and generate_fingerprint(peers()) on sampled rows of the sharded mesh.  The two handles are resident
+    together (the sparse layout: a few GB per mesh at 1M-4M peers)."""
+    import kaboodle_amd
+    import parity
+    from kaboodle_amd._ffi import Sim
+    lib = kaboodle_amd.lib()
+    cfg = case["cfg"]
+    a, b = Sim(lib, cfg), Sim(lib, cfg, shards=shards)
+    for x in externals:                        # real instances outside the mesh (kb_sim_set_external, DESIGN.md §9)
+        a.set_external(x)
+        b.set_external(x)
+    rng = np.random.default_rng(seed)
+    fails, traj = [], []
+    exported = {"records": 0, "ids": 0, "kp_to_ext": 0}
+    for r in range(rounds):
+        parity.apply_events((a, b), case, r)
+        if r in join_rounds:                   # each external instance broadcasts Join (src/kaboodle.rs:228-251)
+            for x in externals:
+                a.inject(x, 0, parity.K_JOIN, 0, 0, 0)
+                b.inject(x, 0, parity.K_JOIN, 0, 0, 0)
+        ta = time.time(); a.step(1); ta = time.time() - ta
+        tb = time.time(); b.step(1); tb = time.time() - tb
+        d = digest_diff(a, b, rng, nrows)
+        if externals:
+            ea, eb = a.exported(), b.exported()
+            if ea != eb:
+                d.append(f"exports differ: {len(ea)} vs {len(eb)} records")
+            exported["records"] += len(ea)
+            exported["ids"] += sum(len(e[9]) for e in ea)
+            exported["kp_to_ext"] += sum(1 for e in ea if e[5] == parity.K_KP)
+        if d:
+            fails.append(f"round {r}: " + "; ".join(d[:4]))
+            break
+        for i in rng.choice(cfg.capacity, check_rows, replace=False):
+            got, want = fp_of_peers(b, lib, int(i))
+            if got != want:
+                fails.append(f"round {r} row {i}: fingerprint {got:#x} != generate_fingerprint(peers()) {want:#x}")
+        st = b.stats()
+        rec = {"round": r, "ms_unsharded": round(ta * 1e3, 1), "ms_sharded": round(tb * 1e3, 1), "agree": st["agree"],
+               "drop_partition": st["drop_partition"], "bcast_failed": st["bcast_failed"]}
+        traj.append(rec)
+        if verbose:
+            print(json.dumps(rec), flush=True)
+    st = b.stats()
+    fp = b.sparse_footprint()
+    a.close()
+    b.close()
+    return {"nodes": cfg.capacity, "shards": shards, "rounds": len(traj), "trajectory": traj, "final_stats": st,
+            "footprint": fp, "exported": exported, "failures": fails}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--nodes", type=int, default=4 * 1024 * 1024)
