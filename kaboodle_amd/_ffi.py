@@ -44,6 +44,10 @@ class KbPeerState(C.Structure):
                 ("identity_len", C.c_uint32), ("identity", C.c_uint8 * 32)]
 
 
+PEER_STATE_DTYPE = [("peer", "<u4"), ("state", "<u4"), ("since", "<i4"), ("latency_ms", "<u4"), ("identity_len", "<u4"),
+                    ("identity", "u1", (32,))]    # KbPeerState's layout (52 B, no padding)
+
+
 class KbStats(C.Structure):
     _fields_ = [
         ("round", C.c_int32), ("alive", C.c_uint32), ("agree", C.c_uint32),
@@ -377,6 +381,18 @@ class Sim:
         arr = (KbPeerState * max(n.value, 1))()
         self.lib.call("sim_peer_states", self.h, node, arr, n.value, C.byref(n))
         return [(a.peer, a.state, a.since, a.latency_ms, bytes(a.identity[: a.identity_len])) for a in arr[: n.value]]
+
+    def peer_states_array(self, node: int):
+        """peer_states as one numpy record array (the fields of kb_peer_state): peer_states() without a Python
+        tuple per entry (64K-entry rows).  Identity bytes past identity_len are whatever the library wrote there
+        (zero-filled buffer), so equal arrays mean equal peer_states(), not the converse."""
+        import numpy as np
+        n = C.c_size_t()
+        self.lib.call("sim_peer_states", self.h, node, None, 0, C.byref(n))
+        a = np.zeros(max(n.value, 1), dtype=PEER_STATE_DTYPE)
+        self.lib.call("sim_peer_states", self.h, node, C.cast(a.ctypes.data, C.POINTER(KbPeerState)), n.value,
+                      C.byref(n))
+        return a[: n.value]
 
     # -- discovery (src/discovery.rs:30-89, src/kaboodle.rs:305-331) --
     def probe(self, prober) -> None:

@@ -48,10 +48,18 @@ __global__ void k_rebase(Dev d, int32_t r) {
 // lower bound, tlb (instant) with the block's smallest rotated id: a block is scanned only while its bound is below
 // the fifth key found so far, and the scan makes its tlb exact.  k_rebase lowers tlb for every entry it saturates;
 // a refresh leaves it low (still a bound).  Only a row with fewer than five saturated candidates reads its live bytes.
+// 64-bit keys: the DPP scan of kb_device.h on both halves (identity ~0), the minimum read from the last lane
+template <int CTRL, int RM>
+__device__ __attribute__((always_inline)) inline unsigned long long min64_dpp(unsigned long long x) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)x, CTRL, RM, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)(uint32_t)(x >> 32), CTRL, RM, 0xF, false);
+  const unsigned long long y = ((unsigned long long)hi << 32) | lo;
+  return y < x ? y : x;
+}
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) { const unsigned long long t = __shfl_xor(v, o, 64); v = t < v ? t : v; }
-  return v;
+  v = min64_dpp<0x111, 0xF>(v); v = min64_dpp<0x112, 0xF>(v); v = min64_dpp<0x114, 0xF>(v);
+  v = min64_dpp<0x118, 0xF>(v); v = min64_dpp<0x142, 0xA>(v); v = min64_dpp<0x143, 0xC>(v);
+  return ((unsigned long long)wave_last((uint32_t)(v >> 32)) << 32) | wave_last((uint32_t)v);
 }
 __device__ inline unsigned long long wave_fifth(const unsigned long long top[5]) {   // the wave's 5th smallest key
   unsigned long long t0 = top[0], t1 = top[1], t2 = top[2], t3 = top[3], t4 = top[4], m = ~0ull;
@@ -71,6 +79,18 @@ __device__ inline int32_t a3x_block(const Dev& d, uint32_t i, uint32_t b, uint32
   if (!bw) return smin;
   const uint4 sv = *reinterpret_cast<const uint4*>(srow + j0);
   const uint32_t s4[4] = {sv.x, sv.y, sv.z, sv.w};
+  int32_t t16[16];                                                   // the lane's 16 instants: four 16-byte loads
+  if (SAT) {
+    uint32_t anc = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 16; ++t) anc |= (((s4[t >> 2] >> (8 * (t & 3))) & 0xFFu) == ST_ANCIENT) ? (1u << t) : 0u;
+    if (anc & bw) {
+      const int4* tp = reinterpret_cast<const int4*>(trow + j0);
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) { const int4 v = tp[q]; t16[4 * q] = v.x; t16[4 * q + 1] = v.y; t16[4 * q + 2] = v.z; t16[4 * q + 3] = v.w; }
+    }
+  }
+#pragma unroll
   for (uint32_t t = 0; t < 16; ++t) {
     if (!((bw >> t) & 1u)) continue;
     const uint32_t j = j0 + t;
@@ -80,7 +100,7 @@ __device__ inline int32_t a3x_block(const Dev& d, uint32_t i, uint32_t b, uint32
     int32_t inst;
     if (sb == ST_ANCIENT) {
       if (!SAT) continue;
-      inst = trow[j];
+      inst = t16[t];
       smin = inst < smin ? inst : smin;
     } else {
       if (!LIVE) continue;
@@ -772,9 +792,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KB_RP_WPE, 
     __builtin_amdgcn_wave_barrier();
     tick(2);
     // ---- (2) A3 candidates ----
-    uint32_t top[5];
-    w_bytes += a3_scan<LDSB>(d, i, cur, rw, B, top, a3c);
-    if (l < 10) ro.part[(size_t)i * 10 + l] = l < 5 ? (l == 0 ? top[0] : l == 1 ? top[1] : l == 2 ? top[2] : l == 3 ? top[3] : top[4]) : 0xFFFFFFFFu;
+    if (!d.tst) {                                     // KB_VARIANT_EXACT_LRU: k_a3_exact writes the keys
+      uint32_t top[5];
+      w_bytes += a3_scan<LDSB>(d, i, cur, rw, B, top, a3c);
+      if (l < 10) ro.part[(size_t)i * 10 + l] = l < 5 ? (l == 0 ? top[0] : l == 1 ? top[1] : l == 2 ? top[2] : l == 3 ? top[3] : top[4]) : 0xFFFFFFFFu;
+    }
     tick(3);
     // ---- (3) write back the changed segments of the bitset ----
     if (LDSB && segs) {

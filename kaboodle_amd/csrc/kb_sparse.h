@@ -256,17 +256,23 @@ __device__ inline uint32_t sp_fold(const SpDev& d, uint32_t i) {
   }
   const uint32_t Z = d.zpow[1];
   uint32_t raw = 0, pos = 0, cnt = 0;
-  for (uint32_t q = 0; q < n; ++q) {
-    const uint32_t x = e[q];
-    if (!(x & SP_XF)) continue;
-    const uint32_t j = x >> 9;
-    if (based) {                                  // the base's members in [pos, j), one multiply
-      const uint32_t c = d.bcnt[j] - d.bcnt[pos];
-      raw = multmodp(d.zpow[c], raw ^ d.bpre[pos]) ^ d.bpre[j];
-      cnt += c;
+  const uint4* e4 = reinterpret_cast<const uint4*>(e);
+  for (uint32_t g = 0; g < (n + 3u) >> 2; ++g) {  // 16-byte loads (rows are 16-byte aligned)
+    const uint4 q4 = e4[g];
+    const uint32_t w4[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) {
+      const uint32_t x = w4[t];
+      if (4u * g + t >= n || !(x & SP_XF)) continue;
+      const uint32_t j = x >> 9;
+      if (based) {                                // the base's members in [pos, j), one multiply
+        const uint32_t c = d.bcnt[j] - d.bcnt[pos];
+        raw = multmodp(d.zpow[c], raw ^ d.bpre[pos]) ^ d.bpre[j];
+        cnt += c;
+      }
+      if (!based || !sp_bbit(d, j)) { raw = multmodp(Z, raw) ^ d.cseg[j]; cnt++; }   // a member outside the base
+      pos = j + 1;
     }
-    if (!based || !sp_bbit(d, j)) { raw = multmodp(Z, raw) ^ d.cseg[j]; cnt++; }   // a member outside the base
-    pos = j + 1;
   }
   if (based) {
     const uint32_t c = d.bcnt[d.C] - d.bcnt[pos];
@@ -1024,29 +1030,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
         }
         case K_KP: {                                         // :448-472
           const uint32_t* p = v.pay_in + m.off;
-          for (uint32_t k = 0; k < m.a; ++k)
-            if (sp_get(d, i, p[k]) == ST_UNKNOWN) sp_insert_known(d, i, p[k], r - SHARE_AGE, r);
+          for (uint32_t k = 0; k < m.a; ++k) {               // one lookup per id: insert_known of an unknown id
+            const uint32_t j = p[k];
+            const SpLook l = sp_look(d, i, j);
+            if (sp_byte(d, i, j, l) != ST_UNKNOWN) continue;
+            sp_put(d, i, j, enc(r - SHARE_AGE, r), l);
+            d.n[i] += 1; d.dirty[i] = 1;
+          }
           break;
         }
         case K_KPR: {                                        // :473-512
+          // one pass over the row in 16-byte loads: the fresh ids are written into the payload region as they are
+          // counted (within its room), and kept only if the reply is deliverable
           const uint32_t fresh = enc(r - (SHARE_AGE - 1), r);
-          const uint32_t* e = sp_row(d, i);
+          const uint4* e4 = reinterpret_cast<const uint4*>(sp_row(d, i));
           const uint32_t n = d.ne[i];
+          const uint32_t room = o.pcap[i] > pc ? o.pcap[i] - pc : 0u;
+          uint32_t* pay = o.pay + o.poff[i] + pc;
           uint32_t c = 0;
           uint64_t sz = 8u + d.seglen[i] - ADDR_LEN + 4u + 8u;  // envelope: identity, tag, map length
-          for (uint32_t k = 0; k < n; ++k) {
-            const uint32_t j = e[k] >> 9;
-            if ((e[k] & 255u) >= fresh && j != i && j != from) { c++; sz += 10u + 8u + d.seglen[j] - ADDR_LEN; }
+          for (uint32_t g = 0; g < (n + 3u) >> 2; ++g) {
+            const uint4 q4 = e4[g];
+            const uint32_t w4[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t) {
+              const uint32_t x = w4[t], j = x >> 9;
+              if (4u * g + t < n && (x & 255u) >= fresh && j != i && j != from) {
+                if (c < room) pay[c] = j;
+                c++;
+                sz += 10u + 8u + (d.uniform ? d.L : d.seglen[j]) - ADDR_LEN;
+              }
+            }
           }
           if (sz > (uint64_t)BUFSZ) oversize++;              // truncated at the receiver: undeliverable (Q3)
-          else if (pc + c > o.pcap[i]) sp_err(d, DERR_PAYLOAD);
+          else if (c > room) sp_err(d, DERR_PAYLOAD);
           else {
-            uint32_t* pay = o.pay + o.poff[i] + pc;
-            uint32_t t = 0;
-            for (uint32_t k = 0; k < n; ++k) {
-              const uint32_t j = e[k] >> 9;
-              if ((e[k] & 255u) >= fresh && j != i && j != from) pay[t++] = j;
-            }
             sp_emit(d, o, i, seq, from, K_KP, c, 0, 0, o.poff[i] + pc);
             pc += c;
           }

@@ -85,12 +85,15 @@ def diff_peer_states(o: Sim, g: Sim, nodes) -> list[str]:
     since round, latency) for every entry; it must also list exactly the ids peers() reports."""
     out = []
     for i in nodes:
-        a, b = o.peer_states(int(i)), g.peer_states(int(i))
-        if a != b:
-            bad = [(x, y) for x, y in zip(a, b) if x != y][:2]
-            out.append(f"peer_states[{i}]: {len(a)} vs {len(b)} entries, first differing {bad}")
-            break
-        if [p for p, *_ in b] != g.peers(int(i)):
+        a, b = o.peer_states_array(int(i)), g.peer_states_array(int(i))
+        if a.tobytes() != b.tobytes():              # the arrays carry the bytes past identity_len too: decide on tuples
+            a, b = o.peer_states(int(i)), g.peer_states(int(i))
+            if a != b:
+                bad = [(x, y) for x, y in zip(a, b) if x != y][:2]
+                out.append(f"peer_states[{i}]: {len(a)} vs {len(b)} entries, first differing {bad}")
+                break
+            b = g.peer_states_array(int(i))
+        if not np.array_equal(b["peer"], np.asarray(g.peers(int(i)), dtype=np.uint32)):
             out.append(f"peer_states[{i}] ids != peers()")
             break
     return out

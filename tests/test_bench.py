@@ -17,7 +17,7 @@ def test_driver_config_is_the_parity_config():
     from test_gpu_fullsize import BENCH_CFG
     cfg = _cfg(["--gpus", "1", "--steps", "20", "--warmup", "5"])
     for f in ("capacity", "initial_nodes", "init_mode", "loss", "churn", "fault_end_round", "seed", "failed_mode",
-              "track_latency", "max_waves", "id_len"):
+              "track_latency", "max_waves", "id_len", "variant"):
         assert getattr(cfg, f) == getattr(BENCH_CFG, f), f
 
 

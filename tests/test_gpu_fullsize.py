@@ -17,12 +17,13 @@ import numpy as np
 import pytest
 
 import parity
-from kaboodle_amd._ffi import KB_INIT_CONVERGED, Sim, SimConfig
+from kaboodle_amd._ffi import KB_INIT_CONVERGED, KB_VARIANT_EXACT_LRU, Sim, SimConfig
 
 pytestmark = pytest.mark.gpu
 
 BENCH_CFG = SimConfig(capacity=65536 + 8192, initial_nodes=65536, init_mode=KB_INIT_CONVERGED, loss=0.01,
-                      churn=0.001, fault_end_round=25, seed=1, track_latency=1)   # bench.rank_config, --steps 20 --warmup 5
+                      churn=0.001, fault_end_round=25, seed=1, track_latency=1,
+                      variant=KB_VARIANT_EXACT_LRU)   # bench.rank_config, --steps 20 --warmup 5 (A3 in exact-instant order)
 
 
 class Pair:

@@ -25,6 +25,7 @@ if [ "$PMC" = pmc ]; then
   done
   CAP=$(python3 -c "import json;print(json.load(open('$OUT/bench.json'))['config']['capacity'])")
   WL=$(python3 -c "import json;print(json.load(open('$OUT/bench.json'))['config']['workload'])")
-  python3 tools/prof_summary.py pmc $OUT "{\"workload\": \"$WL\", \"capacity\": $CAP, \"steps\": $STEPS, \"warmup\": $WARM, \"failed_mode\": \"sim_sender\", \"command\": \"python3 $CMD\"}" > $OUT/pmc.json || exit 1
+  A3=$(python3 -c "import json;print(json.load(open('$OUT/bench.json'))['config']['a3_order'])")
+  python3 tools/prof_summary.py pmc $OUT "{\"workload\": \"$WL\", \"capacity\": $CAP, \"steps\": $STEPS, \"warmup\": $WARM, \"failed_mode\": \"sim_sender\", \"a3_order\": \"$A3\", \"command\": \"python3 $CMD\"}" > $OUT/pmc.json || exit 1
   head -30 $OUT/pmc.json
 fi
