@@ -612,11 +612,17 @@ int kbo_sim_create(const kb_config* cfg, kbo_sim** out) {
   }
   if (cfg->variant & KB_VARIANT_EXACT_LRU) {
     s->tst = (int32_t*)malloc(C * C * sizeof(int32_t));
-    if (s->tst) for (size_t k = 0; k < C * C; ++k) s->tst[k] = INT32_MIN / 2;   /* converged start: ancient, ties */
+    if (s->tst) {                           /* converged start: ancient, ties (first touch spread over threads) */
+#pragma omp parallel for schedule(static)
+      for (size_t i = 0; i < C; ++i) for (size_t k = 0; k < C; ++k) s->tst[i * C + k] = INT32_MIN / 2;
+    }
   }
   if (cfg->track_latency) {
     s->lat = (uint16_t*)malloc(C * C * sizeof(uint16_t));
-    if (s->lat) memset(s->lat, 0xFF, C * C * sizeof(uint16_t));
+    if (s->lat) {
+#pragma omp parallel for schedule(static)
+      for (size_t i = 0; i < C; ++i) memset(s->lat + i * C, 0xFF, C * sizeof(uint16_t));
+    }
   }
   if ((!s->stamp && !s->sr) || !s->susp || !s->cur || (cfg->track_latency && !s->lat)) {
     seterr("out of host memory"); kbo_sim_destroy(s); return KB_CAPACITY;

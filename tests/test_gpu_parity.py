@@ -112,7 +112,7 @@ def test_parity_resp_wave_rows_in_place(gpu, name):
         g.close()
 
 
-@pytest.mark.parametrize("name", ["churn_loss_512", "partition_heal", "identity_change", "hot_inbox"])
+@pytest.mark.parametrize("name", ["partition_heal", "identity_change", "hot_inbox"])
 def test_parity_wave_graph(gpu, name):
     """The receive window captured once as a HIP graph and replayed every round (KB_DBG_WAVE_GRAPH, the
     env KB_WAVE_GRAPH=1 path): same results, including across set_identity (which must drop the graph)."""
@@ -201,7 +201,7 @@ def test_wide_row_paths_are_hit(gpu):
         assert g.debug_paths() & (128 | 64) and not g.debug_paths() & (1 | 8)
 
 
-@pytest.mark.parametrize("name", ["churn_loss_512", "config2_join_1k", "partition_heal"])
+@pytest.mark.parametrize("name", ["config2_join_1k", "partition_heal"])
 def test_parity_wide_row_paths_sharded(gpu, name):
     case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}[name]
     ok, msg, _ = parity.run_case(parity.with_cfg(case, debug_flags=KB_DBG_ALL, track_latency=1), rounds, shards=3,

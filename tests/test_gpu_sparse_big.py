@@ -70,7 +70,7 @@ def test_sparse_1m_sharded(gpu):
     fingerprint and scalar, sampled rows, suspect/curious tables, peer_states), with the 4M test's size-independent
     checks: generate_fingerprint(peers()) on sampled rows and the counters' invariants."""
     from kaboodle_amd._ffi import KB_FAILED_SOCKET_FAITHFUL, KB_INIT_CONVERGED, KB_VARIANT_SPARSE_ROWS, SimConfig
-    n, rounds, ext = 1 << 20, 10, (1 << 20) + 1
+    n, rounds, ext = 1 << 20, 7, (1 << 20) + 1
     cfg = SimConfig(capacity=n + 64, initial_nodes=n, init_mode=KB_INIT_CONVERGED, loss=0.01, seed=21,
                     failed_mode=KB_FAILED_SOCKET_FAITHFUL, variant=KB_VARIANT_SPARSE_ROWS, sparse_row_cap=2048)
     # an external instance (a real Kaboodle behind the bridge, DESIGN.md §9) broadcasts Join at round 3: ~1 % of the
