@@ -995,14 +995,26 @@ __device__ inline void sp_maybe_sync(const SpDev& d, const SpOut& o, uint32_t i,
 }
 // handle_incoming_messages (:394-548) for one node: its inbox in (KnownPeers first, then sender, seq) order
 // (compiled for 8 waves per SIMD: a thread per row waits on dependent loads, so occupancy is its throughput;
-// 130 -> 64 VGPRs measured 13.5 -> 12.0 ms a round at 1M peers)
+// 130 -> 64 VGPRs measured 13.5 -> 12.0 ms a round at 1M peers).
+//   A KnownPeers list longer than SP_KP_WAVE ids is applied by the whole wave first: the lanes look its ids up in
+// parallel (a binary search each) and lane 0 inserts the few unknown ones, re-checking each (a list may repeat an
+// id).  One thread looking up a 567-id list alone was the wave's tail (≈ 5,000 dependent loads).  The arms of the
+// inbox's KnownPeers group insert only unknown ids and its prologues set their senders Known(now), so inside the
+// group they commute; the group comes first in the inbox, so applying its long arms before every prologue leaves
+// the same row (src/kaboodle.rs:448-472).
+constexpr uint32_t SP_KP_WAVE = 4;
+constexpr uint32_t SP_KPR_ILP = 4;               // KnownPeersRequest reply scan: 16-byte row loads in flight per step
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_sp_handle(SpDev d, SpWave v, SpOut o, int32_t r) {
   const uint32_t i = sp_gid(d);
   unsigned long long oversize = 0, curovf = 0;
   if (i < d.hi) o.en[i] = 0;
-  if (i < d.hi && v.icnt[i]) {
-    uint32_t* ib = v.inbox + v.ioff[i];
-    const uint32_t cnt = v.icnt[i];
+  const bool act = i < d.hi && v.icnt[i];
+  uint32_t* ib = nullptr;
+  uint32_t cnt = 0;
+  bool big = false;
+  if (act) {
+    ib = v.inbox + v.ioff[i];
+    cnt = v.icnt[i];
     for (uint32_t q = 0; q < cnt; ++q) ib[q] |= (v.in[ib[q]].kind != K_KP) ? 0x80000000u : 0u;
     for (uint32_t a = 1; a < cnt; ++a) {                     // insertion sort (inboxes are short)
       const uint32_t x = ib[a];
@@ -1010,6 +1022,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
       while (b > 0 && ib[b - 1] > x) { ib[b] = ib[b - 1]; --b; }
       ib[b] = x;
     }
+    for (uint32_t q = 0; q < cnt && !(ib[q] & 0x80000000u); ++q) big |= v.in[ib[q]].a > SP_KP_WAVE;
+  }
+  unsigned long long pend = __ballot(big);
+  if (pend) wave_mem_sync();                                 // the sorted inboxes, read by every lane below
+  for (; pend; pend &= pend - 1) {
+    const uint32_t ri = rdl(i, __ffsll((long long)pend) - 1);
+    const uint32_t* rib = v.inbox + v.ioff[ri];
+    const uint32_t rcnt = v.icnt[ri];
+    uint32_t added = 0;
+    for (uint32_t q = 0; q < rcnt; ++q) {
+      const uint32_t x = rib[q];
+      if (x & 0x80000000u) break;                            // past the KnownPeers group
+      const Msg m = v.in[x];
+      if (m.a <= SP_KP_WAVE) continue;
+      const uint32_t* p = v.pay_in + m.off;
+      for (uint32_t k0 = 0; k0 < m.a; k0 += 64) {
+        const bool in = k0 + lane() < m.a;
+        const uint32_t j = in ? p[k0 + lane()] : 0u;
+        const unsigned long long um = __ballot(in && sp_get(d, ri, j) == ST_UNKNOWN);
+        for (unsigned long long u = um; u; u &= u - 1) {
+          const uint32_t jj = rdl(j, __ffsll((long long)u) - 1);
+          if (lane() == 0) {
+            const SpLook l = sp_look(d, ri, jj);
+            if (sp_byte(d, ri, jj, l) == ST_UNKNOWN) { sp_put(d, ri, jj, enc(r - SHARE_AGE, r), l); added++; }
+          }
+        }
+        if (um) wave_mem_sync();                             // lane 0's row writes before the next lookups
+      }
+    }
+    if (lane() == 0 && added) { d.n[ri] += added; d.dirty[ri] = 1; }
+    wave_mem_sync();
+  }
+  if (act) {
     uint32_t seq = 0, pc = 0;
     for (uint32_t q = 0; q < cnt; ++q) {
       const Msg m = v.in[ib[q] & 0x7FFFFFFFu];
@@ -1029,6 +1074,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
           break;
         }
         case K_KP: {                                         // :448-472
+          if (m.a > SP_KP_WAVE) break;                       // applied by the wave above
           const uint32_t* p = v.pay_in + m.off;
           for (uint32_t k = 0; k < m.a; ++k) {               // one lookup per id: insert_known of an unknown id
             const uint32_t j = p[k];
@@ -1049,16 +1095,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
           uint32_t* pay = o.pay + o.poff[i] + pc;
           uint32_t c = 0;
           uint64_t sz = 8u + d.seglen[i] - ADDR_LEN + 4u + 8u;  // envelope: identity, tag, map length
-          for (uint32_t g = 0; g < (n + 3u) >> 2; ++g) {
-            const uint4 q4 = e4[g];
-            const uint32_t w4[4] = {q4.x, q4.y, q4.z, q4.w};
+          const uint32_t ng = (n + 3u) >> 2;
+          for (uint32_t g0 = 0; g0 < ng; g0 += SP_KPR_ILP) {
+            uint4 q4[SP_KPR_ILP];                            // the step's loads issued before any is used
 #pragma unroll
-            for (uint32_t t = 0; t < 4; ++t) {
-              const uint32_t x = w4[t], j = x >> 9;
-              if (4u * g + t < n && (x & 255u) >= fresh && j != i && j != from) {
-                if (c < room) pay[c] = j;
-                c++;
-                sz += 10u + 8u + (d.uniform ? d.L : d.seglen[j]) - ADDR_LEN;
+            for (uint32_t u = 0; u < SP_KPR_ILP; ++u) q4[u] = g0 + u < ng ? e4[g0 + u] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (uint32_t u = 0; u < SP_KPR_ILP; ++u) {
+              const uint32_t g = g0 + u, w4[4] = {q4[u].x, q4[u].y, q4[u].z, q4[u].w};
+#pragma unroll
+              for (uint32_t t = 0; t < 4; ++t) {
+                const uint32_t x = w4[t], j = x >> 9;
+                if (4u * g + t < n && (x & 255u) >= fresh && j != i && j != from) {
+                  if (c < room) pay[c] = j;
+                  c++;
+                  sz += 10u + 8u + (d.uniform ? d.L : d.seglen[j]) - ADDR_LEN;
+                }
               }
             }
           }

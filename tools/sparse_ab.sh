@@ -7,7 +7,7 @@ mkdir -p $OUT
 for rep in 1 2; do
   for v in "$@"; do
     KB_LIB_PATH=kaboodle_amd/variants/$v.so timeout -k 10 200 python3 tools/sparse_big.py --nodes 1048576 --rounds 120 \
-      --fault-end 40 --no-sf-failed-drops --print-every 40 --fp-every 1000 --check-rows 0 --out $OUT/$v.$rep.json > $OUT/$v.$rep.log 2>&1 || { tail -5 $OUT/$v.$rep.log; exit 1; }
+      --fault-end 40 --print-every 40 --fp-every 1000 --check-rows 0 --out $OUT/$v.$rep.json > $OUT/$v.$rep.log 2>&1 || { tail -5 $OUT/$v.$rep.log; exit 1; }
     python3 -c "import json; d=json.load(open('$OUT/$v.$rep.json')); print('$v.$rep', d['gpu_round_ms_mean'], d['kernels_ms_per_round']['k_sp_handle'])"
   done
 done
