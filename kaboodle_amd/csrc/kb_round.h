@@ -61,14 +61,15 @@ __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
   v = min64_dpp<0x118, 0xF>(v); v = min64_dpp<0x142, 0xA>(v); v = min64_dpp<0x143, 0xC>(v);
   return ((unsigned long long)wave_last((uint32_t)(v >> 32)) << 32) | wave_last((uint32_t)v);
 }
-__device__ inline unsigned long long wave_fifth(const unsigned long long top[5]) {   // the wave's 5th smallest key
-  unsigned long long t0 = top[0], t1 = top[1], t2 = top[2], t3 = top[3], t4 = top[4], m = ~0ull;
+// the wave's five smallest keys, ascending (~0: fewer); keys are distinct (rotated ids), so one lane pops each
+__device__ inline void wave_top5(const unsigned long long top[5], unsigned long long m5[5]) {
+  unsigned long long t0 = top[0], t1 = top[1], t2 = top[2], t3 = top[3], t4 = top[4];
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    m = wave_min_u64(t0);
+    const unsigned long long m = wave_min_u64(t0);
+    m5[k] = m;
     if (m != ~0ull && t0 == m) { t0 = t1; t1 = t2; t2 = t3; t3 = t4; t4 = ~0ull; }
   }
-  return m;
 }
 template <bool SAT, bool LIVE>
 __device__ inline int32_t a3x_block(const Dev& d, uint32_t i, uint32_t b, uint32_t cur, int32_t E, const uint8_t* srow,
@@ -115,59 +116,128 @@ __device__ inline int32_t a3x_block(const Dev& d, uint32_t i, uint32_t b, uint32
   return smin;
 }
 constexpr uint32_t A3X_KPL = 8;                                     // bounds per lane: rows up to 512K ids
+// one saturated-block scan's operands, loaded before any is used: member bits, stamp bytes and the 16 instants of
+// the lane's 16 ids (every scanned block holds a saturated entry by its bound, so its instants are read anyway)
+struct A3Blk { uint32_t bw; uint4 sv; int4 t[4]; };
+__device__ __attribute__((always_inline)) inline void a3x_load(const uint8_t* srow, const uint32_t* brow, const int32_t* trow,
+                                                               uint32_t b, A3Blk& x) {
+  const uint32_t j0 = (b << 10) + 16 * lane();
+  x.bw = (brow[j0 >> 5] >> (j0 & 31)) & 0xFFFFu;
+  x.sv = *reinterpret_cast<const uint4*>(srow + j0);
+  const int4* tp = reinterpret_cast<const int4*>(trow + j0);
+#pragma unroll
+  for (uint32_t q = 0; q < 4; ++q) x.t[q] = tp[q];
+}
+// the saturated entries of a loaded block into the lane's five smallest keys; returns the lane's saturated minimum
+__device__ __attribute__((always_inline)) inline int32_t a3x_sat(uint32_t i, uint32_t C, uint32_t b, uint32_t cur,
+                                                                 const A3Blk& x, unsigned long long top[5]) {
+  const uint32_t j0 = (b << 10) + 16 * lane();
+  const uint32_t s4[4] = {x.sv.x, x.sv.y, x.sv.z, x.sv.w};
+  const int32_t t16[16] = {x.t[0].x, x.t[0].y, x.t[0].z, x.t[0].w, x.t[1].x, x.t[1].y, x.t[1].z, x.t[1].w,
+                           x.t[2].x, x.t[2].y, x.t[2].z, x.t[2].w, x.t[3].x, x.t[3].y, x.t[3].z, x.t[3].w};
+  int32_t smin = INT32_MAX;
+#pragma unroll
+  for (uint32_t t = 0; t < 16; ++t) {
+    const uint32_t j = j0 + t;
+    if (!((x.bw >> t) & 1u) || j >= C || j == i || ((s4[t >> 2] >> (8 * (t & 3))) & 0xFFu) != ST_ANCIENT) continue;
+    const int32_t inst = t16[t];
+    smin = inst < smin ? inst : smin;
+    const uint32_t rot = j > cur ? j - cur - 1 : j + C - cur - 1;
+    unsigned long long key = ((unsigned long long)((uint32_t)inst ^ 0x80000000u) << 32) | rot;
+    if (key >= top[4]) continue;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) { if (key < top[q]) { const unsigned long long y = top[q]; top[q] = key; key = y; } }
+  }
+  return smin;
+}
+// the lane's smallest (bound, rotated start) block key and its block
+__device__ __attribute__((always_inline)) inline unsigned long long a3x_lane_min(const int32_t lbk[A3X_KPL],
+                                                                                 const uint32_t rkey[A3X_KPL], uint32_t& bm) {
+  unsigned long long lm = ~0ull;
+#pragma unroll
+  for (uint32_t k = 0; k < A3X_KPL; ++k) {
+    if (lbk[k] == INT32_MAX) continue;
+    const unsigned long long key = ((unsigned long long)((uint32_t)lbk[k] ^ 0x80000000u) << 32) | rkey[k];
+    if (key < lm) { lm = key; bm = lane() + 64 * k; }
+  }
+  return lm;
+}
+__device__ __attribute__((always_inline)) inline void a3x_drop(int32_t lbk[A3X_KPL], uint32_t b) {   // b's owner lane
+  const bool own = lane() == (b & 63);
+#pragma unroll
+  for (uint32_t k = 0; k < A3X_KPL; ++k) lbk[k] = (own && k == (b >> 6)) ? INT32_MAX : lbk[k];   // a select per k: no
+}                                                                    // indexed (scratch) store
+// the row pass's keys (rank << 24 | rotated id; 0xFFFFFFFF: none) of the five found, for k_tick_post
+__device__ __attribute__((always_inline)) inline void write_a3_keys(uint32_t* part, uint32_t i, uint32_t l,
+                                                                    const unsigned long long m5[5]) {
+  uint32_t o = 0xFFFFFFFFu;
+#pragma unroll
+  for (uint32_t k = 0; k < 5; ++k)
+    if (l == k && m5[k] != ~0ull) o = (k << 24) | (uint32_t)(m5[k] & 0xFFFFFFu);
+  if (l < 10) part[(size_t)i * 10 + l] = o;
+}
+// A wave per row.  The row's first step issues every load it needs at once (alive, the sweep front, the block
+// bounds); each later step takes the block of smallest bound key and loads its bits, stamps and instants together
+// (one memory round trip per block instead of three).  The wave's five smallest keys are formed once per step after a
+// scan (none before the first) and serve the exit test and the answer: five 64-bit DPP minima, the kernel's largest VALU
+// item (a converged start's five ancient candidates sit in the sweep front's block: one scan and one top-five per row,
+// whose minima are also the answer).
 __global__ __launch_bounds__(256) void k_a3_exact(Dev d, uint32_t* part, int32_t r) {
   const uint32_t i = d.lo + blockIdx.x * 4 + (threadIdx.x >> 6), l = lane();
-  if (i >= d.hi || !d.alive[i]) return;
-  const uint32_t C = d.C, cur = d.a3cur[i], NB = d.W >> 10;
+  if (i >= d.hi) return;
+  const uint32_t C = d.C, NB = d.W >> 10;
+  const bool narrow = NB <= 64 * A3X_KPL;
+  int32_t* lbrow = d.tlb + (size_t)i * NB;
+  int32_t lbk[A3X_KPL];
+  if (narrow) {
+#pragma unroll
+    for (uint32_t k = 0; k < A3X_KPL; ++k) {
+      const uint32_t b = l + 64 * k;
+      lbk[k] = (b < NB && (b << 10) < C) ? lbrow[b] : INT32_MAX;      // INT32_MAX: nothing saturated (or no ids)
+    }
+  }
+  const uint32_t cur = d.a3cur[i];
+  if (!d.alive[i]) return;
   const int32_t E = epoch_base(r);
   unsigned long long top[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
   const uint8_t* srow = row_of(d, i);
   const uint32_t* brow = bits_of(d, i);
   const int32_t* trow = d.tst + (size_t)i * d.W;
-  if (NB > 64 * A3X_KPL) {                                           // wider rows: one pass over everything
+  if (!narrow) {                                                     // wider rows: one pass over everything
     for (uint32_t b = 0; b < NB; ++b) a3x_block<true, true>(d, i, b, cur, E, srow, brow, trow, top);
   } else {
-    int32_t* lbrow = d.tlb + (size_t)i * NB;
     const uint32_t p = cur + 1 == C ? 0 : cur + 1;                   // the sweep front: rotated id 0
-    int32_t lbk[A3X_KPL];
-    unsigned long long rkey[A3X_KPL];                                // the block's smallest rotated id
+    uint32_t rkey[A3X_KPL];                                          // the block's smallest rotated id
 #pragma unroll
     for (uint32_t k = 0; k < A3X_KPL; ++k) {
-      const uint32_t b = l + 64 * k, lo = b << 10, hi = lo + 1023 < C - 1 ? lo + 1023 : C - 1;
-      lbk[k] = (b < NB && lo < C) ? lbrow[b] : INT32_MAX;            // INT32_MAX: nothing saturated (or no ids)
-      rkey[k] = (p >= lo && p <= hi) ? 0 : (lo > p ? lo - p : lo + C - p);
+      const uint32_t lo = (l + 64 * k) << 10, hi = lo + 1023 < C - 1 ? lo + 1023 : C - 1;
+      rkey[k] = (p >= lo && p <= hi) ? 0u : (lo > p ? lo - p : lo + C - p);
     }
+    unsigned long long m5[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};  // the wave's five smallest keys so far
     for (;;) {
-      unsigned long long lm = ~0ull;
+      const unsigned long long fifth = m5[4];
       uint32_t bm = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < A3X_KPL; ++k) {
-        if (lbk[k] == INT32_MAX) continue;
-        const unsigned long long key = ((unsigned long long)((uint32_t)lbk[k] ^ 0x80000000u) << 32) | rkey[k];
-        if (key < lm) { lm = key; bm = l + 64 * k; }
-      }
+      const unsigned long long lm = a3x_lane_min(lbk, rkey, bm);
       const unsigned long long m = wave_min_u64(lm);                // keys are distinct: rotated ids differ
-      if (m == ~0ull || m >= wave_fifth(top)) break;
+      if (m == ~0ull || m >= fifth) break;
       const uint32_t b = rdl(bm, (int)__builtin_ctzll(__ballot(lm == m)));
-      int32_t smin = a3x_block<true, false>(d, i, b, cur, E, srow, brow, trow, top);
+      a3x_drop(lbk, b);
+      A3Blk x;
+      a3x_load(srow, brow, trow, b, x);
+      int32_t smin = a3x_sat(i, C, b, cur, x, top);
       smin = (int32_t)(wave_min((uint32_t)smin ^ 0x80000000u) ^ 0x80000000u);   // signed minimum
       if (l == 0) lbrow[b] = smin;                                   // exact now
-      if (l == (b & 63)) {
-#pragma unroll
-        for (uint32_t k = 0; k < A3X_KPL; ++k) if (k == (b >> 6)) lbk[k] = INT32_MAX;   // scanned
-      }
+      wave_top5(top, m5);
     }
-    if (wave_fifth(top) == ~0ull)                                    // fewer than five saturated: the live bytes
-      for (uint32_t b = 0; b < NB; ++b) a3x_block<false, true>(d, i, b, cur, E, srow, brow, trow, top);
+    if (m5[4] != ~0ull) {                                            // five saturated: the last step's five are the
+      write_a3_keys(part, i, l, m5);                                 // answer (no scan after it)
+      return;
+    }
+    for (uint32_t b = 0; b < NB; ++b) a3x_block<false, true>(d, i, b, cur, E, srow, brow, trow, top);   // + live bytes
   }
-  uint32_t out[5];
-#pragma unroll
-  for (int k = 0; k < 5; ++k) {                        // keys are distinct (rotated ids): one lane pops each minimum
-    const unsigned long long m = wave_min_u64(top[0]);
-    out[k] = m == ~0ull ? 0xFFFFFFFFu : ((uint32_t)k << 24) | (uint32_t)(m & 0xFFFFFFu);
-    if (m != ~0ull && top[0] == m) { top[0] = top[1]; top[1] = top[2]; top[2] = top[3]; top[3] = top[4]; top[4] = ~0ull; }
-  }
-  if (l < 10) part[(size_t)i * 10 + l] = l < 5 ? (l == 0 ? out[0] : l == 1 ? out[1] : l == 2 ? out[2] : l == 3 ? out[3] : out[4]) : 0xFFFFFFFFu;
+  unsigned long long m5[5];
+  wave_top5(top, m5);
+  write_a3_keys(part, i, l, m5);
 }
 
 // ---- lifecycle: API start/stop in call order, then churn (src/lib.rs:136-183) ------------------

@@ -1,7 +1,7 @@
-"""Quick timing of the HIP simulator on a config (dev tool): quick_perf.py N ROUNDS [sim|sock] [lat]."""
+"""Quick timing of the HIP simulator on a config (dev tool): quick_perf.py N ROUNDS [sim|sock] [lat] [exact]."""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from kaboodle_amd._ffi import SimConfig, KB_INIT_CONVERGED, KB_FAILED_SOCKET_FAITHFUL, KB_FAILED_SIM_SENDER
+from kaboodle_amd._ffi import SimConfig, KB_INIT_CONVERGED, KB_FAILED_SOCKET_FAITHFUL, KB_FAILED_SIM_SENDER, KB_VARIANT_EXACT_LRU
 import kaboodle_amd
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 R = int(sys.argv[2]) if len(sys.argv) > 2 else 10
@@ -9,7 +9,8 @@ MODE = KB_FAILED_SOCKET_FAITHFUL if (len(sys.argv) > 3 and sys.argv[3] == "sock"
 # the bench's sizing (bench.rank_config): capacity = peers + churn reserve for the run
 cfg = SimConfig(capacity=N + max(4096, int(N * 0.001 * (R + 10) * 1.5)), initial_nodes=N, init_mode=KB_INIT_CONVERGED,
                 loss=0.01, churn=0.001, seed=1, failed_mode=MODE, track_latency=int("lat" in sys.argv[4:]),
-                debug_flags=int(os.environ.get("KB_QP_DBG", "0"), 0))   # KB_QP_DBG: force kernel variants (A/B)
+                debug_flags=int(os.environ.get("KB_QP_DBG", "0"), 0),   # KB_QP_DBG: force kernel variants (A/B)
+                variant=KB_VARIANT_EXACT_LRU if "exact" in sys.argv[4:] else 0)   # exact: bench.py's default A3 order
 t = time.time(); m = kaboodle_amd.Mesh(cfg); print("create", round(time.time() - t, 2), flush=True)
 m.step(2)
 m.reset_kernel_time()
