@@ -1,4 +1,4 @@
-"""Per-round wall time of the benched workload (dev tool, GPU): python tools/round_series.py [rounds]
+"""Per-round wall time of the benched workload (dev tool, GPU): python tools/round_series.py [rounds] [exact|window]
 
 bench.py's configs[2] mesh (same capacity, seed, faults), stepped one round at a time with a device sync
 after each, so the transient of the converged start (KnownPeersRequest replies under the size cap while
@@ -13,7 +13,8 @@ import bench  # noqa: E402
 import kaboodle_amd  # noqa: E402
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 40
-sys.argv = [sys.argv[0], "--steps", str(rounds - 5), "--warmup", "5"]
+order = sys.argv[2] if len(sys.argv) > 2 else "exact"          # A3 order (bench.py's --a3-order; default exact)
+sys.argv = [sys.argv[0], "--steps", str(rounds - 5), "--warmup", "5", "--a3-order", order]
 a = bench.parse()
 cfg = bench.rank_config(a, 0, 1, 0)
 out = []
