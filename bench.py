@@ -55,7 +55,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md "HBM [CD
 LAT_TABLE_MAX = 64 << 30        # bytes of latency table per GPU beyond which --latency is dropped
 KT_ROUND = 1                    # kb_sim_kernel_time kind of the whole round
 # kernels on the simulator's side stream (kb_sim.hip step_round: side_fork / side_join), overlapping the round's
-SIDE_KERNELS = ("k_alive_bits", "k_truefp_part", "k_truefp_fin", "k_lat_sweep")
+SIDE_KERNELS = ("k_alive_bits", "k_truefp_part", "k_truefp_fin", "k_lat_sweep", "k_a3_exact")
 CHURN_RESERVE = 8192            # fresh ids kept for churn joins: capacity does not depend on --steps
 
 

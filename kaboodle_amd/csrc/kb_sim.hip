@@ -344,7 +344,7 @@ struct kb_sim {
   // side stream: kernels off the round's critical path (the running set's fingerprint, the latency sweep)
   // run beside it, forked from and joined back into st by events
   hipStream_t st2 = nullptr;
-  hipEvent_t ev_fork[2] = {nullptr, nullptr}, ev_join[2] = {nullptr, nullptr};
+  hipEvent_t ev_fork[3] = {nullptr, nullptr, nullptr}, ev_join[3] = {nullptr, nullptr, nullptr};   // side work 0-2
   uint32_t C, W, S;                    // capacity, row stride, row-sweep column splits
   // row shard: this handle holds rows [lo, hi) of the mesh, R = hi - lo
   uint32_t lo, hi, R;
@@ -612,7 +612,7 @@ static void destroy_shard(kb_sim* s) {
   if (s->wave_graph) (void)hipGraphDestroy(s->wave_graph);
   if (s->st) (void)hipStreamDestroy(s->st);
   if (s->st2) (void)hipStreamDestroy(s->st2);
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < 3; ++k) {
     if (s->ev_fork[k]) (void)hipEventDestroy(s->ev_fork[k]);
     if (s->ev_join[k]) (void)hipEventDestroy(s->ev_join[k]);
   }
@@ -736,7 +736,7 @@ constexpr uint32_t KB_FOLD_WAVES = 16384;                            // fold wav
   s->wc.msg_cap = s->msg_cap; s->wc.pay_cap = s->pay_cap;
   if (hipStreamCreateWithFlags(&s->st, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
   if (hipStreamCreateWithFlags(&s->st2, hipStreamNonBlocking) != hipSuccess) { destroy_shard(s); seterr("stream"); return KB_IO_ERROR; }
-  for (int k = 0; k < 2; ++k)
+  for (int k = 0; k < 3; ++k)
     if (hipEventCreateWithFlags(&s->ev_fork[k], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&s->ev_join[k], hipEventDisableTiming) != hipSuccess) { destroy_shard(s); seterr("events"); return KB_IO_ERROR; }
   if (hipHostMalloc((void**)&s->h_pin, 4 * PIN_WORDS, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
@@ -1464,11 +1464,19 @@ static int step_round(kb_sim* s) {
   if (lat_fail) side_join(s, 1);
   klaunch(s, KI_TICK_SCAN, k_tick_scan, dim3(gnode), dim3(tb), 0, d, s->bs, r, s->slow);                       // A1; list the A2 nodes
   klaunch(s, KI_TICK_PRE, k_tick_pre, dim3(std::min<uint32_t>(gwave, 1024)), dim3(256), 0, d, o0, s->bs, r, s->slow);   // A2 per listed node
+  // exact A3 order beside the fold: it reads what A2 left (member bits, stamps, instants, bounds) and writes only
+  // the five keys and the bounds, which nothing else reads before k_tick_post; the fold and the row fingerprints
+  // write checkpoints and fingerprints only
+  if (d.tst) {
+    side_fork(s, 2);
+    klaunch_on(s, s->st2, KI_A3_EXACT, k_a3_exact, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);
+    side_done(s, 2);
+  }
   // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded
   if (d.uniform) klaunch(s, KI_FOLD, k_fold, dim3(((R + 63) / 64 + 3) / 4 * s->S), dim3(256), 0, d, FoldArgs{s->S});
   if (d.uniform) klaunch(s, KI_FP_ROWS, k_fp_rows, dim3((FP_LANES * R + tb - 1) / tb), dim3(tb), 0, d);
-  if (d.tst) klaunch(s, KI_A3_EXACT, k_a3_exact, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);   // exact A3 order
   side_join(s, 0);
+  if (d.tst) side_join(s, 2);
   klaunch(s, KI_TICK_POST, k_tick_post, dim3(gnode), dim3(tb), 0, d, s->ro, o0, r);
   if (ninj) {                                          // the external peers' wave-0 emissions, after the tick's
     klaunch(s, KI_EVENTS, k_inject, dim3(1), dim3(64), 0, d, o0, (const XRec*)s->d_inj, ninj, (const uint32_t*)s->d_inj_ids);
