@@ -151,21 +151,23 @@ __device__ __attribute__((always_inline)) inline int32_t a3x_sat(uint32_t i, uin
   return smin;
 }
 // the lane's smallest (bound, rotated start) block key and its block
-__device__ __attribute__((always_inline)) inline unsigned long long a3x_lane_min(const int32_t lbk[A3X_KPL],
-                                                                                 const uint32_t rkey[A3X_KPL], uint32_t& bm) {
+template <uint32_t KPL>
+__device__ __attribute__((always_inline)) inline unsigned long long a3x_lane_min(const int32_t lbk[KPL], const uint32_t rkey[KPL],
+                                                                                 uint32_t& bm) {
   unsigned long long lm = ~0ull;
 #pragma unroll
-  for (uint32_t k = 0; k < A3X_KPL; ++k) {
+  for (uint32_t k = 0; k < KPL; ++k) {
     if (lbk[k] == INT32_MAX) continue;
     const unsigned long long key = ((unsigned long long)((uint32_t)lbk[k] ^ 0x80000000u) << 32) | rkey[k];
     if (key < lm) { lm = key; bm = lane() + 64 * k; }
   }
   return lm;
 }
-__device__ __attribute__((always_inline)) inline void a3x_drop(int32_t lbk[A3X_KPL], uint32_t b) {   // b's owner lane
+template <uint32_t KPL>
+__device__ __attribute__((always_inline)) inline void a3x_drop(int32_t lbk[KPL], uint32_t b) {   // b's owner lane
   const bool own = lane() == (b & 63);
 #pragma unroll
-  for (uint32_t k = 0; k < A3X_KPL; ++k) lbk[k] = (own && k == (b >> 6)) ? INT32_MAX : lbk[k];   // a select per k: no
+  for (uint32_t k = 0; k < KPL; ++k) lbk[k] = (own && k == (b >> 6)) ? INT32_MAX : lbk[k];   // a select per k: no
 }                                                                    // indexed (scratch) store
 // the row pass's keys (rank << 24 | rotated id; 0xFFFFFFFF: none) of the five found, for k_tick_post
 __device__ __attribute__((always_inline)) inline void write_a3_keys(uint32_t* part, uint32_t i, uint32_t l,
@@ -181,63 +183,68 @@ __device__ __attribute__((always_inline)) inline void write_a3_keys(uint32_t* pa
 // (one memory round trip per block instead of three).  The wave's five smallest keys are formed once per step after a
 // scan (none before the first) and serve the exit test and the answer: five 64-bit DPP minima, the kernel's largest VALU
 // item (a converged start's five ancient candidates sit in the sweep front's block: one scan and one top-five per row,
-// whose minima are also the answer).
-__global__ __launch_bounds__(256) void k_a3_exact(Dev d, uint32_t* part, int32_t r) {
-  const uint32_t i = d.lo + blockIdx.x * 4 + (threadIdx.x >> 6), l = lane();
-  if (i >= d.hi) return;
-  const uint32_t C = d.C, NB = d.W >> 10;
-  const bool narrow = NB <= 64 * A3X_KPL;
+// whose minima are also the answer).  KPL: block bounds per lane, the row's 1024-id blocks over 64 lanes (2 up to
+// 128K ids, 8 up to 512K): the bound selection is a quarter of the instructions at 64K rows with KPL 2.
+template <uint32_t KPL>
+__device__ __attribute__((always_inline)) inline void a3x_narrow(const Dev& d, uint32_t* part, int32_t r, uint32_t i,
+                                                                 uint32_t cur, bool alive) {
+  const uint32_t l = lane(), C = d.C, NB = d.W >> 10;
   int32_t* lbrow = d.tlb + (size_t)i * NB;
-  int32_t lbk[A3X_KPL];
-  if (narrow) {
+  int32_t lbk[KPL];
 #pragma unroll
-    for (uint32_t k = 0; k < A3X_KPL; ++k) {
-      const uint32_t b = l + 64 * k;
-      lbk[k] = (b < NB && (b << 10) < C) ? lbrow[b] : INT32_MAX;      // INT32_MAX: nothing saturated (or no ids)
-    }
+  for (uint32_t k = 0; k < KPL; ++k) {
+    const uint32_t b = l + 64 * k;
+    lbk[k] = (b < NB && (b << 10) < C) ? lbrow[b] : INT32_MAX;        // INT32_MAX: nothing saturated (or no ids)
   }
-  const uint32_t cur = d.a3cur[i];
-  if (!d.alive[i]) return;
+  if (!alive) return;
   const int32_t E = epoch_base(r);
   unsigned long long top[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
   const uint8_t* srow = row_of(d, i);
   const uint32_t* brow = bits_of(d, i);
   const int32_t* trow = d.tst + (size_t)i * d.W;
-  if (!narrow) {                                                     // wider rows: one pass over everything
-    for (uint32_t b = 0; b < NB; ++b) a3x_block<true, true>(d, i, b, cur, E, srow, brow, trow, top);
-  } else {
-    const uint32_t p = cur + 1 == C ? 0 : cur + 1;                   // the sweep front: rotated id 0
-    uint32_t rkey[A3X_KPL];                                          // the block's smallest rotated id
+  const uint32_t p = cur + 1 == C ? 0 : cur + 1;                     // the sweep front: rotated id 0
+  uint32_t rkey[KPL];                                                // the block's smallest rotated id
 #pragma unroll
-    for (uint32_t k = 0; k < A3X_KPL; ++k) {
-      const uint32_t lo = (l + 64 * k) << 10, hi = lo + 1023 < C - 1 ? lo + 1023 : C - 1;
-      rkey[k] = (p >= lo && p <= hi) ? 0u : (lo > p ? lo - p : lo + C - p);
-    }
-    unsigned long long m5[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};  // the wave's five smallest keys so far
-    for (;;) {
-      const unsigned long long fifth = m5[4];
-      uint32_t bm = 0;
-      const unsigned long long lm = a3x_lane_min(lbk, rkey, bm);
-      const unsigned long long m = wave_min_u64(lm);                // keys are distinct: rotated ids differ
-      if (m == ~0ull || m >= fifth) break;
-      const uint32_t b = rdl(bm, (int)__builtin_ctzll(__ballot(lm == m)));
-      a3x_drop(lbk, b);
-      A3Blk x;
-      a3x_load(srow, brow, trow, b, x);
-      int32_t smin = a3x_sat(i, C, b, cur, x, top);
-      smin = (int32_t)(wave_min((uint32_t)smin ^ 0x80000000u) ^ 0x80000000u);   // signed minimum
-      if (l == 0) lbrow[b] = smin;                                   // exact now
-      wave_top5(top, m5);
-    }
-    if (m5[4] != ~0ull) {                                            // five saturated: the last step's five are the
-      write_a3_keys(part, i, l, m5);                                 // answer (no scan after it)
-      return;
-    }
-    for (uint32_t b = 0; b < NB; ++b) a3x_block<false, true>(d, i, b, cur, E, srow, brow, trow, top);   // + live bytes
+  for (uint32_t k = 0; k < KPL; ++k) {
+    const uint32_t lo = (l + 64 * k) << 10, hi = lo + 1023 < C - 1 ? lo + 1023 : C - 1;
+    rkey[k] = (p >= lo && p <= hi) ? 0u : (lo > p ? lo - p : lo + C - p);
   }
+  unsigned long long m5[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};    // the wave's five smallest keys so far
+  for (;;) {
+    const unsigned long long fifth = m5[4];
+    uint32_t bm = 0;
+    const unsigned long long lm = a3x_lane_min<KPL>(lbk, rkey, bm);
+    const unsigned long long m = wave_min_u64(lm);                  // keys are distinct: rotated ids differ
+    if (m == ~0ull || m >= fifth) break;
+    const uint32_t b = rdl(bm, (int)__builtin_ctzll(__ballot(lm == m)));
+    a3x_drop<KPL>(lbk, b);
+    A3Blk x;
+    a3x_load(srow, brow, trow, b, x);
+    int32_t smin = a3x_sat(i, C, b, cur, x, top);
+    smin = (int32_t)(wave_min((uint32_t)smin ^ 0x80000000u) ^ 0x80000000u);   // signed minimum
+    if (l == 0) lbrow[b] = smin;                                     // exact now
+    wave_top5(top, m5);
+  }
+  if (m5[4] == ~0ull) {                                              // fewer than five saturated: + the live bytes
+    for (uint32_t b = 0; b < NB; ++b) a3x_block<false, true>(d, i, b, cur, E, srow, brow, trow, top);
+    wave_top5(top, m5);
+  }
+  write_a3_keys(part, i, l, m5);                                     // the last step's five: no scan after it
+}
+__global__ __launch_bounds__(256) void k_a3_exact(Dev d, uint32_t* part, int32_t r) {
+  const uint32_t i = d.lo + blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= d.hi) return;
+  const uint32_t NB = d.W >> 10, cur = d.a3cur[i];
+  const bool alive = d.alive[i] != 0;
+  if (NB <= 64 * 2) { a3x_narrow<2>(d, part, r, i, cur, alive); return; }
+  if (NB <= 64 * A3X_KPL) { a3x_narrow<A3X_KPL>(d, part, r, i, cur, alive); return; }
+  if (!alive) return;                                                // wider rows: one pass over everything
+  unsigned long long top[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
+  const int32_t E = epoch_base(r);
+  for (uint32_t b = 0; b < NB; ++b) a3x_block<true, true>(d, i, b, cur, E, row_of(d, i), bits_of(d, i), d.tst + (size_t)i * d.W, top);
   unsigned long long m5[5];
   wave_top5(top, m5);
-  write_a3_keys(part, i, l, m5);
+  write_a3_keys(part, i, lane(), m5);
 }
 
 // ---- lifecycle: API start/stop in call order, then churn (src/lib.rs:136-183) ------------------
