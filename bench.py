@@ -378,7 +378,8 @@ def main() -> int:
         kern_sum = sum(v["ms_per_round"] for n, v in table.items() if n not in SIDE_KERNELS)
         gaps = round(round_ms / nr - kern_sum, 4)
         counted = [n for n, v in table.items() if "achieved_GBs" in v]
-        top = max(table, key=lambda n: table[n]["ms_per_round"])
+        # the critical-path kernel: side-stream kernels overlap others, and their event spans stretch with them
+        top = max((n for n in table if n not in SIDE_KERNELS), key=lambda n: table[n]["ms_per_round"])
         dominant = top if top in counted else max(counted, key=lambda n: table[n]["ms_per_round"])
         dk, db = table[dominant], bd[dominant]
         roof = {"bound": "hbm", "kernel": dominant, "achieved": dk["achieved_GBs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
