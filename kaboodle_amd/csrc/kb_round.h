@@ -150,6 +150,44 @@ __device__ __attribute__((always_inline)) inline int32_t a3x_sat(uint32_t i, uin
   }
   return smin;
 }
+// 32-bit keys for the common case: (min(instant − base, 255) << 24) | rotated id, base = the first scanned block's
+// bound, the smallest bound of the row (blocks are scanned in bound order), so no key's offset is negative.  The map
+// keeps the order of every key whose offset is below 255 and puts the rest above them all, so when the fifth
+// smallest 32-bit key has an offset below 255 the five are exactly the five smallest 64-bit keys; otherwise (or with
+// fewer than five saturated) the row is redone with 64-bit keys.  Rotated ids fit 24 bits: the narrow path holds
+// rows up to 512K ids.
+__device__ __attribute__((always_inline)) inline int32_t a3x_sat32(uint32_t i, uint32_t C, uint32_t b, uint32_t cur,
+                                                                   int32_t base, const A3Blk& x, uint32_t top[5]) {
+  const uint32_t j0 = (b << 10) + 16 * lane();
+  const uint32_t s4[4] = {x.sv.x, x.sv.y, x.sv.z, x.sv.w};
+  const int32_t t16[16] = {x.t[0].x, x.t[0].y, x.t[0].z, x.t[0].w, x.t[1].x, x.t[1].y, x.t[1].z, x.t[1].w,
+                           x.t[2].x, x.t[2].y, x.t[2].z, x.t[2].w, x.t[3].x, x.t[3].y, x.t[3].z, x.t[3].w};
+  int32_t smin = INT32_MAX;
+#pragma unroll
+  for (uint32_t t = 0; t < 16; ++t) {
+    const uint32_t j = j0 + t;
+    if (!((x.bw >> t) & 1u) || j >= C || j == i || ((s4[t >> 2] >> (8 * (t & 3))) & 0xFFu) != ST_ANCIENT) continue;
+    const int32_t inst = t16[t];
+    smin = inst < smin ? inst : smin;
+    const uint32_t off = (uint32_t)inst - (uint32_t)base;              // inst >= base: exact as unsigned
+    const uint32_t rot = j > cur ? j - cur - 1 : j + C - cur - 1;
+    uint32_t key = ((off < 255u ? off : 255u) << 24) | rot;
+    if (key >= top[4]) continue;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) { const uint32_t lo = key < top[q] ? key : top[q], hi = key < top[q] ? top[q] : key; top[q] = lo; key = hi; }
+  }
+  return smin;
+}
+// the wave's five smallest 32-bit keys, ascending (~0: fewer); keys are distinct (rotated ids)
+__device__ inline void wave_top5_32(const uint32_t top[5], uint32_t m5[5]) {
+  uint32_t t0 = top[0], t1 = top[1], t2 = top[2], t3 = top[3], t4 = top[4];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    const uint32_t m = wave_min(t0);
+    m5[k] = m;
+    if (m != ~0u && t0 == m) { t0 = t1; t1 = t2; t2 = t3; t3 = t4; t4 = ~0u; }
+  }
+}
 // the lane's smallest (bound, rotated start) block key and its block
 template <uint32_t KPL>
 __device__ __attribute__((always_inline)) inline unsigned long long a3x_lane_min(const int32_t lbk[KPL], const uint32_t rkey[KPL],
@@ -197,8 +235,6 @@ __device__ __attribute__((always_inline)) inline void a3x_narrow(const Dev& d, u
     lbk[k] = (b < NB && (b << 10) < C) ? lbrow[b] : INT32_MAX;        // INT32_MAX: nothing saturated (or no ids)
   }
   if (!alive) return;
-  const int32_t E = epoch_base(r);
-  unsigned long long top[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
   const uint8_t* srow = row_of(d, i);
   const uint32_t* brow = bits_of(d, i);
   const int32_t* trow = d.tst + (size_t)i * d.W;
@@ -209,27 +245,69 @@ __device__ __attribute__((always_inline)) inline void a3x_narrow(const Dev& d, u
     const uint32_t lo = (l + 64 * k) << 10, hi = lo + 1023 < C - 1 ? lo + 1023 : C - 1;
     rkey[k] = (p >= lo && p <= hi) ? 0u : (lo > p ? lo - p : lo + C - p);
   }
+  {                                                                  // 32-bit keys (above): the common case
+    uint32_t top[5] = {~0u, ~0u, ~0u, ~0u, ~0u}, m5[5] = {~0u, ~0u, ~0u, ~0u, ~0u};
+    int32_t base = 0;
+    bool redo = false;
+    for (;;) {
+      unsigned long long fifth = ~0ull;                              // the fifth key as a 64-bit key
+      if (m5[4] != ~0u) {
+        const uint32_t h = m5[4] >> 24;
+        if (h == 255u) { redo = true; break; }
+        fifth = ((unsigned long long)((uint32_t)(base + (int32_t)h) ^ 0x80000000u) << 32) | (m5[4] & 0xFFFFFFu);
+      }
+      uint32_t bm = 0;
+      const unsigned long long lm = a3x_lane_min<KPL>(lbk, rkey, bm);
+      const unsigned long long m = wave_min_u64(lm);                // keys are distinct: rotated ids differ
+      if (m == ~0ull || m >= fifth) break;
+      const uint32_t b = rdl(bm, (int)__builtin_ctzll(__ballot(lm == m)));
+      if (m5[0] == ~0u && top[0] == ~0u) base = (int32_t)((uint32_t)(m >> 32) ^ 0x80000000u);   // first scan: its bound
+      a3x_drop<KPL>(lbk, b);
+      A3Blk x;
+      a3x_load(srow, brow, trow, b, x);
+      int32_t smin = a3x_sat32(i, C, b, cur, base, x, top);
+      smin = (int32_t)(wave_min((uint32_t)smin ^ 0x80000000u) ^ 0x80000000u);   // signed minimum
+      if (l == 0) lbrow[b] = smin;                                   // exact now
+      wave_top5_32(top, m5);
+    }
+    if (!redo && m5[4] != ~0u) {                                     // the last step's five: no scan after it
+      uint32_t o = 0xFFFFFFFFu;
+#pragma unroll
+      for (uint32_t k = 0; k < 5; ++k) if (l == k) o = (k << 24) | (m5[k] & 0xFFFFFFu);
+      if (l < 10) part[(size_t)i * 10 + l] = o;
+      return;
+    }
+  }
+  // 64-bit keys: instants 255 or more above the first bound among the five, or fewer than five saturated (then the
+  // live bytes too).  The bounds the pass above made exact stay valid; every block is a candidate again.
+#pragma unroll
+  for (uint32_t k = 0; k < KPL; ++k) {
+    const uint32_t b = l + 64 * k;
+    lbk[k] = (b < NB && (b << 10) < C) ? lbrow[b] : INT32_MAX;
+  }
+  const int32_t E = epoch_base(r);
+  unsigned long long top[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
   unsigned long long m5[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};    // the wave's five smallest keys so far
   for (;;) {
     const unsigned long long fifth = m5[4];
     uint32_t bm = 0;
     const unsigned long long lm = a3x_lane_min<KPL>(lbk, rkey, bm);
-    const unsigned long long m = wave_min_u64(lm);                  // keys are distinct: rotated ids differ
+    const unsigned long long m = wave_min_u64(lm);
     if (m == ~0ull || m >= fifth) break;
     const uint32_t b = rdl(bm, (int)__builtin_ctzll(__ballot(lm == m)));
     a3x_drop<KPL>(lbk, b);
     A3Blk x;
     a3x_load(srow, brow, trow, b, x);
     int32_t smin = a3x_sat(i, C, b, cur, x, top);
-    smin = (int32_t)(wave_min((uint32_t)smin ^ 0x80000000u) ^ 0x80000000u);   // signed minimum
-    if (l == 0) lbrow[b] = smin;                                     // exact now
+    smin = (int32_t)(wave_min((uint32_t)smin ^ 0x80000000u) ^ 0x80000000u);
+    if (l == 0) lbrow[b] = smin;
     wave_top5(top, m5);
   }
   if (m5[4] == ~0ull) {                                              // fewer than five saturated: + the live bytes
     for (uint32_t b = 0; b < NB; ++b) a3x_block<false, true>(d, i, b, cur, E, srow, brow, trow, top);
     wave_top5(top, m5);
   }
-  write_a3_keys(part, i, l, m5);                                     // the last step's five: no scan after it
+  write_a3_keys(part, i, l, m5);
 }
 __global__ __launch_bounds__(256) void k_a3_exact(Dev d, uint32_t* part, int32_t r) {
   const uint32_t i = d.lo + blockIdx.x * 4 + (threadIdx.x >> 6);
