@@ -96,11 +96,22 @@ def lib_sha16() -> str:
     return hashlib.sha256(open(kaboodle_amd.LIB_PATH, "rb").read()).hexdigest()[:16]
 
 
+def same_build(d: dict) -> bool:
+    """A record made with this library: the same binary (lib_sha16), or the same sources and build command
+    (lib_src_sha16, kaboodle_amd/build.py: a rebuild of unchanged sources is not byte-identical).  An A/B build
+    loaded through KB_LIB_PATH matches by its binary only."""
+    import kaboodle_amd
+    from kaboodle_amd import build as kb_build
+    if d.get("lib_sha16") == lib_sha16():
+        return True
+    return (os.path.abspath(kaboodle_amd.LIB_PATH) == os.path.abspath(kb_build.OUT) and d.get("lib_src_sha16") is not None
+            and d.get("lib_src_sha16") == kb_build.src_sha16())
+
+
 def pmc_summary(cfg_key: str, capacity: int, steps: int, warmup: int, failed_mode: str, a3_order: str):
     """The latest committed PMC summary (tools/gpu_measure.sh -> profiles/*pmc*.json) taken on exactly this
     workload, capacity, step and warmup counts, with this very library build (lib_sha16): {kernel:
     {hbm_bytes_per_launch, hbm_bytes_per_round, ...}} over the timed rounds, and the summary's path."""
-    sha = lib_sha16()
     best, src = None, None
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
@@ -110,7 +121,7 @@ def pmc_summary(cfg_key: str, capacity: int, steps: int, warmup: int, failed_mod
         if (d.get("workload") == cfg_key and d.get("capacity") == capacity and d.get("steps") == steps and
                 d.get("warmup") == warmup and d.get("failed_mode", "sim_sender") == failed_mode and "kernels" in d
                 and d.get("a3_order", "window") == a3_order
-                and d.get("lib_sha16") == sha):
+                and same_build(d)):
             best, src = d["kernels"], os.path.relpath(p, ROOT)
     return best, src
 
@@ -121,13 +132,12 @@ def committed_tail(cfg_key: str, mode: str, a3_order: str = "window"):
     only a record made with this very library build (lib_sha16), like pmc_summary.  a3_order "exact": the
     same tail with A3 in the reference's exact-instant order (KB_VARIANT_EXACT_LRU)."""
     best = None
-    sha = lib_sha16()
     for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*converge*.json"))):
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
             continue
-        if (d.get("workload", "").startswith(cfg_key) and d.get("failed_mode") == mode and d.get("lib_sha16") == sha
+        if (d.get("workload", "").startswith(cfg_key) and d.get("failed_mode") == mode and same_build(d)
                 and d.get("a3_order", "window") == a3_order):
             best = {k: d[k] for k in ("converged_round", "tail_rounds_to_converge", "tail_rounds_run", "cap_rounds",
                                       "stopped_by") if k in d}

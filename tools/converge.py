@@ -21,6 +21,13 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def kb_src_sha16():
+    """the sources the in-tree library is built from (None for an A/B build loaded through KB_LIB_PATH)"""
+    import kaboodle_amd
+    from kaboodle_amd import build as kb_build
+    return kb_build.src_sha16() if os.path.abspath(kaboodle_amd.LIB_PATH) == os.path.abspath(kb_build.OUT) else None
+
+
 def lib_sha16() -> str:
     """the library build this record was made with (bench.py attaches a tail record only when it matches)"""
     import hashlib
@@ -105,7 +112,7 @@ def main() -> int:
            "converged_round": conv, "tail_rounds_to_converge": None if conv is None else conv - F + 1,
            "tail_rounds_run": traj[-1]["round"] - F + 1, "cap_rounds": cap,
            "stopped_by": "converged" if conv is not None else ("cap" if traj[-1]["round"] >= F + cap - 1 else "budget"),
-           "wall_s": round(time.time() - t0, 1), "lib_sha16": lib_sha16(), "trajectory": traj}
+           "wall_s": round(time.time() - t0, 1), "lib_sha16": lib_sha16(), "lib_src_sha16": kb_src_sha16(), "trajectory": traj}
     txt = json.dumps(out)
     print(json.dumps({k: v for k, v in out.items() if k != "trajectory"}), flush=True)
     if a.out:

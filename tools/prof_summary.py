@@ -118,6 +118,9 @@ def pmc(d, fields):
     lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "kaboodle_amd", "libkaboodle_sim.so")
     out["lib_sha16"] = (hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16]   # the build the counters measured
                         if os.path.exists(lib) else None)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from kaboodle_amd import build as kb_build                   # and its sources (bench.py matches either)
+    out["lib_src_sha16"] = kb_build.src_sha16()
     out["kernels"] = dict(sorted(kern.items(), key=lambda kv: -kv[1]["hbm_bytes_per_round"]))
     out["correction"] = ("FETCH_SIZE(KB)*1024, x2 only for " + ", ".join(sorted(STREAM16)) +
                          " (gfx950 half-count of 16 B/lane streaming reads; other kernels raw) + WRITE_SIZE(KB)*1024")
