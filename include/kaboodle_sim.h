@@ -118,8 +118,10 @@ enum {
   KB_DBG_PROC_UNSORTED = 16u,/* inboxes > 64 taken by k_proc's selection path (inboxes > SORT_MAX)       */
   KB_DBG_WAVE_GRAPH = 32u,   /* the unsharded receive window captured once as a HIP graph and replayed
                                 every round (also env KB_WAVE_GRAPH=1)                  */
-  KB_DBG_RESP_WAVE_HBM = 64u /* Join responses by wave with the rows read in place (the path of rows too
+  KB_DBG_RESP_WAVE_HBM = 64u,/* Join responses by wave with the rows read in place (the path of rows too
                                 wide for a wave's LDS copy, > 110K ids)                                */
+  KB_DBG_NO_UNION = 128u     /* row shards: Join responses travel as their id lists, not as one union per
+                                (source shard, joiner) (A/B and parity surface)          */
 };
 
 /* Per-peer state as reported by peer_states() (PeerState, src/structs.rs:27-41). */
@@ -310,7 +312,9 @@ int  kb_sim_dump_suspects(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, 
    from the rows in place).  Test surface.                                                          */
 int  kb_sim_debug_paths(kb_sim* sim, uint32_t* mask);
 /* Development counters since creation: [A3 rows scanned, rows scanned past their first 1024 ids,
-   1024-id stamp chunks read].  Test surface.                                                        */
+   1024-id stamp chunks read] and, with cap >= 5, the row-shard exchange's bytes [sent to other shards,
+   sent to every shard] (records and payload; summed over an in-process group's shards; 0 unsharded).
+   Test surface.                                                                                     */
 int  kb_sim_debug_counters(kb_sim* sim, uint64_t* out, size_t cap);
 /* Canonical curious table: for each entry sorted by peer: peer, nobs, obs[0..3] (6 x int32).       */
 int  kb_sim_dump_curious(kb_sim* sim, uint32_t node, int32_t* out, size_t cap, size_t* n);

@@ -18,6 +18,7 @@ KB_DBG_PHASEB_HBM, KB_DBG_RESP_HBM, KB_DBG_KP_HBM, KB_DBG_KP_BIG_SMALL, KB_DBG_P
 KB_DBG_ALL = 31                  # every wide-row variant
 KB_DBG_WAVE_GRAPH = 32           # the receive window as a replayed HIP graph
 KB_DBG_RESP_WAVE_HBM = 64        # Join responses by wave, rows read in place (rows > 110K ids)
+KB_DBG_NO_UNION = 128            # row shards: Join responses as id lists, not one union per (source shard, joiner)
 KB_VARIANT_SAME_WINDOW_BCAST, KB_VARIANT_EXACT_LRU = 1, 2   # the first oracle-only; the second on the GPU too (bench default)
 KB_STAT_NO_SF_FAILED_DROPS = 1
 KB_VARIANT_SPARSE_ROWS = 4       # the configs[4] layout: oracle and the HIP library (unsharded or row shards)

@@ -31,6 +31,9 @@ constexpr uint8_t ST_UNKNOWN = 0, ST_SUSPECT = 1, ST_ANCIENT = 2;
 constexpr int EPOCH = 64, EOFF = 192;
 // message kinds (SwimMessage, src/structs.rs:94-116)
 enum : uint32_t { K_PING = 0, K_PINGREQ = 1, K_ACK = 2, K_KP = 3, K_KPR = 4 };
+// sharded meshes only, never routed or handled as a message: one shard's union of the KnownPeers lists it delivers
+// to one of the round's joiners in wave 0, as a bitmap (kb_waves.h, k_union_pack)
+constexpr uint32_t K_KPU = 5;
 // Philox purposes
 enum : uint32_t { P_PING = 1, P_INDIRECT = 2, P_RESPOND = 3, P_TRUNC = 4, P_LOSS = 5, P_BLOSS = 6, P_CHURN = 7, P_PROBE = 8 };
 enum : int32_t { SK_WFP = 1, SK_WFIP = 2 };

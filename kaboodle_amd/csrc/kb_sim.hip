@@ -377,6 +377,8 @@ struct kb_sim {
   BCast* bfail; BCast* bjoin;          // the round's broadcast lists (whole mesh, sender order)
   BCast* bfail_loc; BCast* bjoin_loc;  // sharded: this shard's part, before the all-gather
   uint32_t nf, nj;
+  uint32_t ucap = 0;                   // Join-response union slots (sharded meshes, kb_waves.h UCAP)
+  uint64_t xbytes_cross = 0, xbytes_all = 0;   // bytes this shard's waves sent to other shards / to every shard
   BcastSlots bs;
   uint32_t* join_off; uint32_t* fail_off;
   uint32_t* scan_tot; uint32_t* scan_tiles;
@@ -715,10 +717,13 @@ constexpr uint32_t KB_FOLD_WAVES = 16384;                            // fold wav
   AR(s->ro.part, 10);
   if (xf) {
     XState& x = s->xs;
-    x.world = (uint32_t)world; x.R = R; x.S = rows_per;
-    A(x.ostatus, s->msg_cap); A(x.xcnt, (size_t)world * R); A(x.xpay, (size_t)world * R);
-    A(x.xoff, (size_t)world * R); A(x.xpoff, (size_t)world * R); A(x.xb, 2 * world);
-    A(x.smsg, s->msg_cap); A(x.spay, s->pay_cap);
+    x.world = (uint32_t)world; x.R = R; x.S = rows_per; x.RS = R + 1;
+    x.NWW = d.NWR; x.nju = 0; x.uon = 0;
+    s->ucap = std::min<uint32_t>(UCAP, C);             // Join-response unions (kb_waves.h): slots and their reserve
+    A(x.ostatus, s->msg_cap); A(x.xcnt, (size_t)world * x.RS); A(x.xpay, (size_t)world * x.RS);
+    A(x.xoff, (size_t)world * x.RS); A(x.xpoff, (size_t)world * x.RS); A(x.xb, 2 * world);
+    A(x.smsg, (size_t)s->msg_cap + s->ucap); A(x.spay, (size_t)s->pay_cap + (size_t)s->ucap * x.NWW);
+    A(x.jslot, C); A(x.ubits, (size_t)s->ucap * x.NWW); A(x.uany, s->ucap);
     A(s->xall, std::max(2 * world * world, 3 * world));   // wave counts (2W per rank), round results (3 per rank)
     A(s->xstats, NSTAT);
     A(s->bfail_loc, (size_t)R * SLOTS); A(s->bjoin_loc, R);
@@ -728,6 +733,7 @@ constexpr uint32_t KB_FOLD_WAVES = 16384;                            // fold wav
 #undef AR
   if (e != hipSuccess) { seterr(std::string("device allocation failed: ") + hipGetErrorString(e)); destroy_shard(s); return KB_CAPACITY; }
   (void)hipMemset(L(s, d.kpr_big), 0xFF, 4ull * R);          // no round yet
+  if (xf) { (void)hipMemset(s->xs.jslot, 0xFF, 4ull * C); (void)hipMemset(s->xs.ubits, 0, 4ull * s->ucap * s->xs.NWW); }
   if (d.lat) { (void)hipMemset(d.lat, 0xFF, 2ull * lat_stride(R) * W); (void)hipMemset(s->fnamed, 0, 4ull * d.NWR); }   // all None
   if (d.tst) {
     (void)hipMemsetD32(d.tst + (size_t)s->lo * W, INT32_MIN / 2, (size_t)R * W);   // a converged start: ancient, all tied
@@ -910,7 +916,7 @@ static int grow_wave0(kb_sim* s, size_t need_msg, size_t need_pay) {
     if (cap < need_pay) { seterr("Join-response payload beyond 2^32 ids"); return KB_CAPACITY; }
     HIPCHK(regrow(s, &o0.pay, cap));
     o0.pay_cap = (uint32_t)cap;
-    if (s->xf && cap > s->pay_cap) { HIPCHK(regrow(s, &s->xs.spay, cap)); s->pay_cap = (uint32_t)cap; }
+    if (s->xf && cap > s->pay_cap) { HIPCHK(regrow(s, &s->xs.spay, cap + (size_t)s->ucap * s->xs.NWW)); s->pay_cap = (uint32_t)cap; }
   }
   if (need_msg > o0.msg_cap) {
     const size_t cap = std::min(lim, need_msg + need_msg / 4);
@@ -919,7 +925,7 @@ static int grow_wave0(kb_sim* s, size_t need_msg, size_t need_pay) {
     o0.msg_cap = (uint32_t)cap;
     if (cap > s->msg_cap) {                  // slot-indexed buffers cover the larger outbox
       if (!s->xf) { HIPCHK(regrow(s, &s->wc.status, cap)); HIPCHK(regrow(s, &s->wc.inbox, cap)); HIPCHK(regrow(s, &s->wc.kin, cap)); }
-      else { HIPCHK(regrow(s, &s->xs.ostatus, cap)); HIPCHK(regrow(s, &s->xs.smsg, cap)); }
+      else { HIPCHK(regrow(s, &s->xs.ostatus, cap)); HIPCHK(regrow(s, &s->xs.smsg, cap + s->ucap)); }
       s->msg_cap = (uint32_t)cap;
     }
   }
@@ -969,8 +975,9 @@ static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb,
   const int W = s->world, me = s->rank;
   XState& x = s->xs;
   hipStream_t st = s->st;
+  if (x.uon) klaunch(s, KI_XBOUND, k_union_count, dim3(1), dim3(256), 0, x);   // the unions' records, counted
   {
-    ScanArgs a = scan_args(s, (uint32_t)W * s->R, s->scan_tot + 16);
+    ScanArgs a = scan_args(s, (uint32_t)W * x.RS, s->scan_tot + 16);
     a.narr = 2;
     a.in[0] = x.xcnt; a.out[0] = x.xoff;
     a.in[1] = x.xpay; a.out[1] = x.xpoff;
@@ -978,6 +985,7 @@ static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb,
   }
   klaunch(s, KI_XBOUND, k_xbound, dim3(1), dim3(64), 0, x, s->scan_tot + 16);
   klaunch(s, KI_PACK, k_pack, dim3((s->R + 3) / 4), dim3(256), 0, s->d, ob, x);
+  if (x.uon) klaunch(s, KI_PACK, k_union_pack, dim3(x.nju), dim3(256), 0, x);
   if (!s->xf->allgather_u32(x.xb, s->xall, 2 * W, st)) { seterr(s->xf->error()); return KB_IO_ERROR; }
   k_publish<<<1, 1, 0, st>>>(s->xall, 2 * W * W, s->d_pin, ++s->pin_seq);   // counts -> host, then the wait
   { const int rc = wait_pin(s, s->pin_seq); if (rc) return rc; }
@@ -993,6 +1001,9 @@ static int exchange_wave(kb_sim* s, OutBuf& ob, uint32_t& nrecv, RecvBlocks& rb,
     rc[k] = s->h_xall[(size_t)k * 2 * W + me]; prc[k] = s->h_xall[(size_t)k * 2 * W + W + me];
     sd[k] = so; so += sc[k]; psd[k] = pso; pso += psc[k];
     rd[k] = ro; ro += rc[k]; prd[k] = pro; pro += prc[k];
+    const uint64_t b = sizeof(Msg) * (uint64_t)sc[k] + 4ull * psc[k];
+    s->xbytes_all += b;
+    if (k != me) s->xbytes_cross += b;
   }
   int rcode = ensure_recv(s, ro, pro);
   if (rcode) return rcode;
@@ -1059,14 +1070,20 @@ static int launch_waves(kb_sim* s, int32_t rk) {
       klaunch(s, KI_ROUTE, k_route, dim3(gnode), dim3(tb), 0, d, ob, s->wc, r, w, last);
       if (last) break;
     } else {
-      HIPCHK(hipMemsetAsync(s->xs.xcnt, 0, 4ull * s->world * R, st));
-      HIPCHK(hipMemsetAsync(s->xs.xpay, 0, 4ull * s->world * R, st));
+      HIPCHK(hipMemsetAsync(s->xs.xcnt, 0, 4ull * s->world * s->xs.RS, st));
+      HIPCHK(hipMemsetAsync(s->xs.xpay, 0, 4ull * s->world * s->xs.RS, st));
+      // wave 0: the round's joiners' slots for the Join-response unions
+      s->xs.nju = w == 0 && !last ? std::min<uint32_t>(s->nj, s->ucap) : 0u;
+      s->xs.uon = s->xs.nju && !(d.dbg & KB_DBG_NO_UNION) ? 1u : 0u;
+      s->xs.bjoin = s->bjoin;
+      if (s->xs.uon) klaunch(s, KI_ROUTE_X, k_union_slots, dim3((s->xs.nju + 255) / 256), dim3(256), 0, s->xs);
       klaunch(s, KI_ROUTE_X, k_route_x, dim3(gnode), dim3(tb), 0, d, ob, s->xs, r, w, last);
       if (last) break;
       RecvBlocks rb;
       memset(&rb, 0, sizeof rb);
       bool any = true;
       int rc = exchange_wave(s, ob, nrecv, rb, any);
+      s->xs.uon = 0;
       if (rc) return rc;
       if (!any) break;                                 // no record anywhere: the rest of the round's waves are empty
       ib.msgs = s->rmsg; ib.pay = s->rpay;
@@ -2438,6 +2455,11 @@ extern "C" int kb_sim_debug_counters(kb_sim* s, uint64_t* out, size_t cap) {
   unsigned long long v[3];
   HIPCHK(hipMemcpy(v, h->d.stats + S_A3ROWS, sizeof v, hipMemcpyDeviceToHost));
   for (int k = 0; k < 3; ++k) out[k] = v[k];
+  if (cap >= 5) {                                    // the row-shard exchange's bytes (sharded meshes; 0 otherwise)
+    out[3] = out[4] = 0;
+    if (is_group(s)) for (kb_sim* t : s->shards) { out[3] += t->xbytes_cross; out[4] += t->xbytes_all; }
+    else { out[3] = s->xbytes_cross; out[4] = s->xbytes_all; }
+  }
   return KB_OK;
 }
 extern "C" int kb_sim_sparse_footprint(kb_sim* s, uint64_t* out, size_t cap) {

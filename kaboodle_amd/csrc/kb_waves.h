@@ -229,14 +229,24 @@ __global__ __launch_bounds__(256) void k_scatter(Dev d, OutBuf ob, WaveCtl wc, i
 // unchanged on it.
 // ================================================================================================
 constexpr uint32_t XMAX = 8;        // shards per mesh
+constexpr uint32_t UCAP = 1024;     // joiners of one round whose Join responses travel as a union (the rest as lists)
 struct XState {
   uint32_t world, R, S;             // shards, local rows, rows per shard
+  uint32_t RS;                      // R + 1: per destination shard the senders' slots, then the unions' slot
   uint8_t* ostatus;                 // per outbox slot: 1 = delivered
-  uint32_t* xcnt; uint32_t* xpay;   // [world][R] delivered records / payload ids per (dest shard, sender)
+  uint32_t* xcnt; uint32_t* xpay;   // [world][RS] delivered records / payload ids per (dest shard, sender | unions)
   uint32_t* xoff; uint32_t* xpoff;  // exclusive scans of xcnt / xpay (flattened) = send positions
   uint32_t* xb;                     // [2 * world] records, payload ids sent to each shard
   Msg* smsg; uint32_t* spay;        // send buffers
+  // the Join-response union (wave 0): joiner slot of every id (~0: none), one bitmap of NWW words per slot, and
+  // whether this shard delivered anything to the slot's joiner; bjoin = the round's Join list (slot = entry)
+  uint32_t* jslot; uint32_t* ubits; uint32_t* uany; const BCast* bjoin;
+  uint32_t nju, NWW, uon;           // slots in use, words per bitmap, unions on (wave 0 of a round with joiners)
 };
+// the union slot a delivered record's ids go to, or ~0 (they travel with the record)
+__device__ inline uint32_t x_union_slot(const XState& x, const Msg& m) {
+  return (x.uon && m.kind == K_KP && m.a) ? x.jslot[m.dest] : 0xFFFFFFFFu;
+}
 
 __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int32_t r, uint32_t w, int last) {
   __shared__ uint32_t s_ex[4][64], s_base[4][64];
@@ -271,9 +281,11 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
              philox(m.sender, (uint32_t)r, ((uint32_t)P_LOSS << 24) | w, m.seq, d.k0, d.k1).x < d.loss_thr) loss++;
     else {
       st = 1;
-      const uint32_t slot = (m.dest / x.S) * x.R + (m.sender - d.lo);
+      const uint32_t slot = (m.dest / x.S) * x.RS + (m.sender - d.lo);
       atomicAdd(&x.xcnt[slot], 1u);
-      if (m.kind == K_KP && m.a) atomicAdd(&x.xpay[slot], m.a);
+      const uint32_t e = x_union_slot(x, m);
+      if (e != 0xFFFFFFFFu) x.uany[e] = 1u;                           // its ids go to the joiner's union
+      else if (m.kind == K_KP && m.a) atomicAdd(&x.xpay[slot], m.a);
     }
     if (!last) x.ostatus[g] = st;
   }
@@ -289,10 +301,54 @@ __global__ __launch_bounds__(256) void k_route_x(Dev d, OutBuf ob, XState x, int
 __global__ void k_xbound(XState x, const uint32_t* tot) {
   const uint32_t k = threadIdx.x;
   if (k >= x.world) return;
-  const uint32_t a1 = k + 1 < x.world ? x.xoff[(k + 1) * x.R] : tot[0];
-  const uint32_t p1 = k + 1 < x.world ? x.xpoff[(k + 1) * x.R] : tot[1];
-  x.xb[k] = a1 - x.xoff[k * x.R];
-  x.xb[x.world + k] = p1 - x.xpoff[k * x.R];
+  const uint32_t a1 = k + 1 < x.world ? x.xoff[(k + 1) * x.RS] : tot[0];
+  const uint32_t p1 = k + 1 < x.world ? x.xpoff[(k + 1) * x.RS] : tot[1];
+  x.xb[k] = a1 - x.xoff[k * x.RS];
+  x.xb[x.world + k] = p1 - x.xpoff[k * x.RS];
+}
+
+// ---- The Join-response union.  In wave 0 of a sharded round every delivered KnownPeers record
+// whose destination is one of the round's joiners (a Join sender, slot e < UCAP) travels without its ids: they
+// are ORed into one bitmap per joiner, sent once per (source shard, joiner) as a K_KPU record in the unions' slot
+// of the joiner's shard.  The joiner's KnownPeers group inserts every listed id it does not know; those arms
+// commute with each other and with the group's prologues (src/kaboodle.rs:448-472), so one arm
+// over the union leaves the same row as the lists' arms, and every record keeps its prologue.  A joiner's ≈ 650
+// responses of 567 ids (≈ 1.5 MB) become at most one bitmap of W/8 bytes per source shard.
+__global__ void k_union_slots(XState x) {   // the round's slots: joiner -> slot, no union yet
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= x.nju) return;
+  x.uany[e] = 0u;
+  x.jslot[x.bjoin[e].sender] = e;
+}
+__global__ void k_union_count(XState x) {   // one record + one bitmap per union, in the unions' slot of its shard
+  for (uint32_t e = threadIdx.x; e < x.nju; e += blockDim.x) {
+    if (!x.uany[e]) continue;
+    const uint32_t k = x.bjoin[e].sender / x.S;
+    atomicAdd(&x.xcnt[k * x.RS + x.R], 1u);
+    atomicAdd(&x.xpay[k * x.RS + x.R], x.NWW);
+  }
+}
+// after k_pack: a workgroup per slot writes its union (position: the slots before it that go to the same shard)
+// and clears the bitmap and the joiner's slot for the next round
+__global__ __launch_bounds__(256) void k_union_pack(XState x) {
+  __shared__ uint32_t s_c[4];
+  const uint32_t e = blockIdx.x, t = threadIdx.x;
+  const uint32_t jid = x.bjoin[e].sender, k = jid / x.S;
+  const bool any = x.uany[e] != 0u;
+  uint32_t c = 0;
+  if (any)
+    for (uint32_t f = t; f < e; f += blockDim.x) c += (x.uany[f] && x.bjoin[f].sender / x.S == k) ? 1u : 0u;
+  c = wave_sum(c);
+  if (lane() == 0) s_c[t >> 6] = c;
+  __syncthreads();
+  if (any) {
+    const uint32_t idx = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+    const uint32_t mpos = x.xoff[k * x.RS + x.R] + idx, ppos = x.xpoff[k * x.RS + x.R] + idx * x.NWW;
+    uint32_t* U = x.ubits + (size_t)e * x.NWW;
+    for (uint32_t w = t; w < x.NWW; w += blockDim.x) { x.spay[ppos + w] = U[w]; U[w] = 0u; }
+    if (t == 0) x.smsg[mpos] = Msg{jid, jid, 0xFFFFFFFFu, K_KPU, x.NWW, 0u, 0u, ppos - x.xpoff[k * x.RS]};
+  }
+  if (t == 0) x.jslot[jid] = 0xFFFFFFFFu;
 }
 
 // one wave per sender: its delivered records in seq order, 64 at a time, to their shard blocks;
@@ -305,8 +361,8 @@ __global__ __launch_bounds__(256) void k_pack(Dev d, OutBuf ob, XState x) {
   uint32_t run[XMAX], prun[XMAX];
 #pragma unroll
   for (uint32_t k = 0; k < XMAX; ++k) {
-    run[k] = k < x.world ? x.xoff[k * x.R + il] : 0u;
-    prun[k] = k < x.world ? x.xpoff[k * x.R + il] : 0u;
+    run[k] = k < x.world ? x.xoff[k * x.RS + il] : 0u;
+    prun[k] = k < x.world ? x.xpoff[k * x.RS + il] : 0u;
   }
   for (uint32_t c = 0; c < cnt; c += 64) {
     const uint32_t q = c + l;
@@ -314,7 +370,8 @@ __global__ __launch_bounds__(256) void k_pack(Dev d, OutBuf ob, XState x) {
     bool del = false;
     if (q < cnt) { m = ob.msgs[base + q]; del = x.ostatus[base + q] == 1; }
     const uint32_t ds = del ? m.dest / x.S : XMAX;
-    const uint32_t pl = (del && m.kind == K_KP) ? m.a : 0u;
+    const uint32_t ue = del ? x_union_slot(x, m) : 0xFFFFFFFFu;     // ids to a union: the record travels without them
+    const uint32_t pl = (del && m.kind == K_KP && ue == 0xFFFFFFFFu) ? m.a : 0u;
     uint32_t pos = 0, ppos = 0;
 #pragma unroll
     for (uint32_t k = 0; k < XMAX; ++k) {
@@ -329,7 +386,8 @@ __global__ __launch_bounds__(256) void k_pack(Dev d, OutBuf ob, XState x) {
     }
     if (del) {
       Msg o = m;
-      if (m.kind == K_KP) o.off = ppos - x.xpoff[ds * x.R];
+      if (ue != 0xFFFFFFFFu) { o.a = 0; o.off = 0; }
+      else if (m.kind == K_KP) o.off = ppos - x.xpoff[ds * x.RS];
       x.smsg[pos] = o;
     }
     unsigned long long kpm = __ballot(pl != 0);
@@ -338,6 +396,14 @@ __global__ __launch_bounds__(256) void k_pack(Dev d, OutBuf ob, XState x) {
       kpm &= kpm - 1;
       const uint32_t from = rdl(m.off, src), to = rdl(ppos, src), len = rdl(pl, src);
       for (uint32_t e = l; e < len; e += 64) x.spay[to + e] = ob.pay[from + e];
+    }
+    unsigned long long um = __ballot(ue != 0xFFFFFFFFu);
+    while (um) {                                     // ids into their joiner's union: the whole wave on each list
+      const int src = __ffsll((long long)um) - 1;
+      um &= um - 1;
+      const uint32_t from = rdl(m.off, src), len = rdl(m.a, src);
+      uint32_t* U = x.ubits + (size_t)rdl(ue, src) * x.NWW;
+      for (uint32_t e = l; e < len; e += 64) { const uint32_t id = ob.pay[from + e]; atomicOr(&U[id >> 5], 1u << (id & 31)); }
     }
   }
 }
@@ -349,7 +415,7 @@ __global__ __launch_bounds__(256) void k_route_recv(Dev d, OutBuf ib, WaveCtl wc
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g < n) {
     const Msg m = ib.msgs[g];
-    if (m.kind == K_KP) {
+    if (m.kind == K_KP || m.kind == K_KPU) {           // (K_KPU: a shard's union of its Join responses to m.dest)
       uint32_t src = 0;
       while (src + 1 < rb.world && rb.m0[src + 1] <= g) ++src;
       ib.msgs[g].off = m.off + rb.p0[src];
@@ -461,7 +527,8 @@ __device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d
       for (uint32_t q0 = wv; q0 < nk; q0 += 64 * nwv) {
         const uint32_t qm = q0 + l * nwv;
         uint32_t moff = 0, mlen = 0;
-        if (qm < nk) { const Msg m = ib.msgs[wc.kin[k0 + qm]]; moff = m.off; mlen = m.a; }
+        bool uni = false;                               // a union (K_KPU): a bitmap, armed below
+        if (qm < nk) { const Msg m = ib.msgs[wc.kin[k0 + qm]]; moff = m.off; uni = m.kind == K_KPU; mlen = uni ? 0u : m.a; }
         const uint32_t cnt = q0 + 64 * nwv <= nk ? 64u : (nk - q0 + nwv - 1) / nwv;
         // software pipeline over the batch's (message, 640-id chunk) items: the ids of the next item are
         // loaded while the current item's arms run, so a message costs its arms, not arms + a load trip
@@ -511,6 +578,16 @@ __device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d
           for (int u = 0; u < KP_UNROLL; ++u) pv[u] = pn[u];
           j = jn; e0 = en;
         }
+        for (unsigned long long um = __ballot(uni); um; um &= um - 1) {   // unions: this part's words, 64 at a time
+          const uint32_t off = rdl(moff, __ffsll((long long)um) - 1);
+          for (uint32_t w = w0 + l; w < w1; w += 64) {
+            const uint32_t u = ib.pay[off + w];
+            const uint32_t cur = u ? (lds ? B[w - w0] : __hip_atomic_load(&B[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) : ~0u;
+            uint32_t nw = u & ~cur;
+            if (nw) nw &= ~atomicOr(&B[w - w0], nw);     // the bits this lane set first
+            for (; nw; nw &= nw - 1) { const uint32_t p = 32 * w + (uint32_t)__builtin_ctz(nw); rw[p] = old; segs |= seg_bit(d, p); added++; }
+          }
+        }
       }
       __syncthreads();
       if (tdbg) tp[1] = wall_clock64();
@@ -524,6 +601,7 @@ __device__ __attribute__((always_inline)) inline void kp_group_body(const Dev& d
     __syncthreads();
     for (uint32_t q = t; q < nk; q += T) {             // prologues
       const Msg m = ib.msgs[wc.kin[k0 + q]];
+      if (m.kind == K_KPU) continue;                   // a union is no envelope
       const uint32_t s = m.sender;
       if ((s >> 5) < w0 || (s >> 5) >= w1) continue;     // another workgroup's part
       // byte update by CAS on its word: exactly one envelope per (dest, sender) sees the transition to
@@ -636,11 +714,20 @@ __device__ __attribute__((always_inline)) inline void kp_small_body(const Dev& d
       // costs two HBM round trips, not two per 64 ids.  The records of up to 64 messages are fetched at
       // once (lane k holds message q0 + k).
       for (uint32_t q0 = 0; q0 < nk; q0 += 64) {
-        uint32_t moff = 0, mlen = 0;
-        if (q0 + l < nk) { const Msg m = ib.msgs[wc.kin[k0 + q0 + l]]; moff = m.off; mlen = m.a; }
+        uint32_t moff = 0, mlen = 0, mkind = 0;
+        if (q0 + l < nk) { const Msg m = ib.msgs[wc.kin[k0 + q0 + l]]; moff = m.off; mlen = m.a; mkind = m.kind; }
         const uint32_t qn = nk - q0 < 64 ? nk - q0 : 64u;
         for (uint32_t j = 0; j < qn; ++j) {
           const uint32_t off = rdl(moff, (int)j), len = rdl(mlen, (int)j);
+          if (rdl(mkind, (int)j) == K_KPU) {                // a union: the row's words, 64 at a time
+            for (uint32_t w = l; w < len; w += 64) {
+              const uint32_t u = ib.pay[off + w];
+              uint32_t nw = u ? u & ~__hip_atomic_load(&B[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+              if (nw) nw &= ~atomicOr(&B[w], nw);
+              for (; nw; nw &= nw - 1) { const uint32_t p = 32 * w + (uint32_t)__builtin_ctz(nw); rw[p] = old; segs |= seg_bit(d, p); added++; }
+            }
+            continue;
+          }
           for (uint32_t e0 = 0; e0 < len; e0 += 64 * KPS_UNROLL) {
             uint32_t pv[KPS_UNROLL], wv_[KPS_UNROLL], ob_[KPS_UNROLL];
 #pragma unroll
@@ -669,7 +756,9 @@ __device__ __attribute__((always_inline)) inline void kp_small_body(const Dev& d
       __builtin_amdgcn_s_waitcnt(0);
       __builtin_amdgcn_wave_barrier();
       for (uint32_t q = l; q < nk; q += 64) {             // prologues (as k_kp_group)
-        const uint32_t s = ib.msgs[wc.kin[k0 + q]].sender;
+        const Msg m = ib.msgs[wc.kin[k0 + q]];
+        if (m.kind == K_KPU) continue;                    // a union is no envelope
+        const uint32_t s = m.sender;
         uint32_t* wp = reinterpret_cast<uint32_t*>(rw + (s & ~3u));
         const uint32_t sh = 8 * (s & 3u);
         uint32_t ow = __hip_atomic_load(wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), prevb;

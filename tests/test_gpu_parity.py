@@ -250,6 +250,29 @@ def test_sharded_parity_every_round(gpu, name, case, rounds, shards):
     assert ok, f"{name}: {msg}"
 
 
+@pytest.mark.parametrize("name", ["churn_loss_512", "config2_join_1k", "partition_heal"])
+def test_join_response_unions(gpu, name):
+    """The Join-response union exchange: row shards whose wave-0 KnownPeers lists to the round's
+    joiners cross as one bitmap per (source shard, joiner) equal the oracle every round (the lists' arms commute,
+    src/kaboodle.rs:448-472), and so does the same mesh with the lists shipped whole (KB_DBG_NO_UNION); the unions
+    cross fewer bytes whenever Join responses cross shards."""
+    import ctypes as C
+    from kaboodle_amd._ffi import KB_DBG_NO_UNION
+    case, rounds = {n: (c, r) for n, c, r in parity.standard_cases()}[name]
+    xb = {}
+    for flags in (0, KB_DBG_NO_UNION):
+        g = Sim(gpu, parity.with_cfg(case, debug_flags=flags)["cfg"], shards=4)
+        ok, msg, st = parity.run_case(parity.with_cfg(case, debug_flags=flags), rounds, gpu=g)
+        assert ok, f"{name} (debug_flags={flags}): {msg}"
+        buf = (C.c_uint64 * 5)()
+        assert gpu.lib.kb_sim_debug_counters(g.h, buf, 5) == 0
+        xb[flags] = (buf[3], buf[4])
+        g.close()
+    assert xb[0][1] > 0 and xb[KB_DBG_NO_UNION][1] > 0, xb
+    if st["join_responses"]:
+        assert xb[0][0] < xb[KB_DBG_NO_UNION][0], xb
+
+
 def test_host_waits_per_round(gpu):
     """Host waits on the device per round (kb_sim_host_syncs): unsharded at most two pinned hand-offs (the
     wave-0 outbox size when Join responses exist, the round's results); a row-sharded round one hand-off
