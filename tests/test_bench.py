@@ -24,3 +24,25 @@ def test_driver_config_is_the_parity_config():
 def test_capacity_independent_of_steps():
     caps = {_cfg(["--steps", str(k), "--warmup", "5"]).capacity for k in (5, 20, 50)}
     assert caps == {65536 + bench.CHURN_RESERVE}
+
+
+def test_records_match_by_binary_or_sources(tmp_path, monkeypatch):
+    """bench.py attaches a PMC or convergence record made with this library: the same binary, or (hipcc's output
+    is not byte-reproducible) the same build inputs; a change to any input changes the source identity."""
+    import pytest
+    import kaboodle_amd
+    from kaboodle_amd import build as kb_build
+    if not os.path.exists(kaboodle_amd.LIB_PATH):
+        pytest.skip("library not built")
+    src = kb_build.src_sha16()
+    assert src == kb_build.src_sha16() and len(src) == 16
+    assert bench.same_build({"lib_sha16": bench.lib_sha16()})
+    assert bench.same_build({"lib_sha16": "0" * 16, "lib_src_sha16": src})
+    assert not bench.same_build({"lib_sha16": "0" * 16, "lib_src_sha16": "0" * 16})
+    assert not bench.same_build({"lib_sha16": "0" * 16})
+    dep = tmp_path / "kb_extra.h"
+    dep.write_text("// a build input\n")
+    monkeypatch.setattr(kb_build, "deps", lambda: [kb_build.SRC, str(dep)])
+    a = kb_build.src_sha16()
+    dep.write_text("// a build input, changed\n")
+    assert kb_build.src_sha16() != a

@@ -32,7 +32,14 @@ def _free_port():
 
 def _args(ns):
     return argparse.Namespace(nodes=ns.nodes, loss=0.01, churn=0.001, seed=ns.seed, warmup=ns.warmup, steps=ns.steps,
-                              replicas=False, weak=False, failed_mode="sim_sender")
+                              replicas=False, weak=False, failed_mode="sim_sender", a3_order=ns.a3_order)
+
+
+def _xbytes(lib, g):
+    """bytes this rank's waves sent to other ranks (kb_sim_debug_counters[3]; 0 on builds without the counter)"""
+    import ctypes as C
+    buf = (C.c_uint64 * 5)()
+    return int(buf[3]) if lib.lib.kb_sim_debug_counters(g.h, buf, 5) == 0 else 0
 
 
 def _rank(rank, world, port, ns, q):
@@ -50,17 +57,17 @@ def _rank(rank, world, port, ns, q):
         g = Sim(lib, cfg, rank=rank, world=world, uid=uid)
         g.step(a.warmup)
         g.stats()                                         # collective: drains the warmup
-        s0 = g.host_syncs()
+        s0, x0 = g.host_syncs(), _xbytes(lib, g)
         dist.barrier()
         t0 = time.perf_counter()
         g.step(a.steps)
         st = g.stats()                                    # collective; waits for the last round
         dt = time.perf_counter() - t0
         dist.barrier()
-        q.put((rank, dt, g.host_syncs() - s0, st, None))
+        q.put((rank, dt, g.host_syncs() - s0, st, None, _xbytes(lib, g) - x0))
         g.close()
     except Exception as e:  # noqa: BLE001 — reported to the parent
-        q.put((rank, 0.0, 0, None, repr(e)))
+        q.put((rank, 0.0, 0, None, repr(e), 0))
     finally:
         dist.destroy_process_group()
 
@@ -90,10 +97,12 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--a3-order", choices=("window", "exact"), default="exact")
     ap.add_argument("--out", default="")
     ns = ap.parse_args()
     import multiprocessing as mp
     res = {"workload": f"configs[2]: {ns.nodes} peers, converged start, 1% loss, 0.1%/round churn, latency on",
+           "a3_order": ns.a3_order,
            "steps": ns.steps, "warmup": ns.warmup, "device": "one MI355X shared by every rank", "runs": {}}
     base = None
     for w in ns.worlds:
@@ -111,16 +120,17 @@ def main() -> int:
                 p.start()
             out = {}
             for _ in procs:
-                rank, dt, syncs, st, err = q.get(timeout=600)
+                rank, dt, syncs, st, err, xb = q.get(timeout=600)
                 if err:
                     raise SystemExit(f"world {w} rank {rank}: {err}")
-                out[rank] = (dt, syncs, st)
+                out[rank] = (dt, syncs, st, xb)
             for p in procs:
                 p.join(timeout=60)
             dts = [out[k][0] for k in range(w)]
             same = base is None or all(out[k][2] == base for k in range(w))
             res["runs"][str(w)] = {"ms_per_round": round(1e3 * max(dts) / ns.steps, 3),
                                    "host_syncs_per_round": out[0][1] / ns.steps, "transport": "IPC (kb_ipc_unique_id)",
+                                   "bytes_to_other_ranks_per_round_per_rank": [round(out[k][3] / ns.steps) for k in range(w)],
                                    "counters_equal_unsharded": same}
             if not same:
                 raise SystemExit(f"world {w}: counters differ from the unsharded mesh")
