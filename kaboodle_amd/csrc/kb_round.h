@@ -1082,16 +1082,26 @@ __device__ inline uint32_t bm_rank(const uint32_t* S, const uint32_t* SP, uint32
 // The block (256 ids) holding member b: bracketed around the density guess b * ratio (ratio = nbu /
 // total, nbu = blocks up to the last non-empty one; rows are dense below it), falling back to the whole
 // range when the guess misses.  Any ratio gives the same answer.
+// The bracket's six prefix words are read at once and counted (no dependent search steps, so the
+// searches of a batch's keys overlap); *base = SP[block].  Only a missed guess searches.
 __device__ __attribute__((always_inline)) inline uint32_t bm_block(const uint32_t* SP, uint32_t nblk, float ratio,
-                                                                   uint32_t b) {
-  uint32_t lo = 0, hi = nblk;
-  {
-    uint32_t g = (uint32_t)((float)b * ratio);
-    g = g < nblk ? g : nblk - 1;
-    const uint32_t l2 = g >= 2 ? g - 2 : 0, h2 = g + 3 < nblk ? g + 3 : nblk;
-    if (SP[l2] <= b && b < SP[h2]) { lo = l2; hi = h2; }
+                                                                   uint32_t b, uint32_t* base) {
+  uint32_t g = (uint32_t)((float)b * ratio);
+  g = g < nblk ? g : nblk - 1;
+  const uint32_t l2 = g >= 2 ? g - 2 : 0, h2 = g + 3 < nblk ? g + 3 : nblk;   // h2 - l2 <= 5
+  uint32_t v[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) v[j] = SP[l2 + j < h2 ? l2 + j : h2];             // v[5] = SP[h2]
+  if (v[0] <= b && b < v[5]) {
+    uint32_t c = 0, bs = v[0];
+#pragma unroll
+    for (int j = 1; j < 5; ++j) { const bool le = v[j] <= b; c += le; bs = le ? v[j] : bs; }
+    *base = bs;
+    return l2 + c;
   }
+  uint32_t lo = 0, hi = nblk;
   while (hi - lo > 1) { const uint32_t mid = (lo + hi) >> 1; if (SP[mid] <= b) lo = mid; else hi = mid; }
+  *base = SP[lo];
   return lo;
 }
 // rem-th member of the 256-id block whose eight words are q0, q1
@@ -1117,24 +1127,37 @@ __device__ __attribute__((always_inline)) inline uint32_t block_pick(const uint4
 // b-th member (0-based) of bitset S with 256-id block prefix SP[0..nblk] (SP[nblk] = total > b); the
 // word and bit come from one 32-byte read of the block.
 __device__ inline uint32_t bm_select(const uint32_t* S, const uint32_t* SP, uint32_t nblk, float ratio, uint32_t b) {
-  const uint32_t lo = bm_block(SP, nblk, ratio, b);
+  uint32_t base;
+  const uint32_t lo = bm_block(SP, nblk, ratio, b, &base);
   const uint4 q0 = *reinterpret_cast<const uint4*>(S + lo * 8), q1 = *reinterpret_cast<const uint4*>(S + lo * 8 + 4);
-  return block_pick(q0, q1, lo, b - SP[lo]);
+  return block_pick(q0, q1, lo, b - base);
 }
 // The sampled Join response (src/kaboodle.rs:373-383 restated): pay[k] for k in
 // [k_first, cap) step `stride` = the select of rank prp(k) in the member set B minus the joiners
 // inserted after the response (J[upto..nnew), suffix minima JM), stepping over them (least fixed point
 // of e = #later joiners <= select(y + e)).  RESP_U keys per batch: their permutations, block searches and
 // 32-byte block reads are independent, so the loads of a batch are in flight together.
-constexpr uint32_t KB_RESP_U = 4;
+// The joiners are read through an accessor: J and its suffix minima JM in LDS (the workgroup path), or
+// held in a wave's registers (lane l: J[l], J[l + 64]; the wave path, whose LDS slice then holds no list).
+constexpr uint32_t KB_RESP_U = 2;   // 2 of 3 and 4 measured best with the wave path at 4 waves per SIMD
 constexpr int RESP_U = KB_RESP_U;
 constexpr int RESP_KMAX = 9;          // keys per lane at stride >= 64: cap <= 567 (src/kaboodle.rs:43, :373-383)
+struct JoinLds {
+  const uint32_t *J, *JM;
+  __device__ uint32_t min_from(uint32_t u) const { return JM[u]; }
+  __device__ uint32_t at(uint32_t f) const { return J[f]; }
+};
+struct JoinRegs {                     // f uniform over the active lanes (a loop over [upto, nnew))
+  uint32_t j0, j1, jmin;
+  __device__ uint32_t min_from(uint32_t) const { return jmin; }
+  __device__ uint32_t at(uint32_t f) const { return f < 64 ? rdl(j0, (int)f) : rdl(j1, (int)(f - 64)); }
+};
+template <class JA>
 __device__ __attribute__((always_inline)) inline void sampled_fill(uint32_t* pay, uint32_t k_first, uint32_t stride,
                                                                    uint32_t cap, const Prp& P, const uint32_t* B,
                                                                    const uint32_t* BP, uint32_t NB, float ratio,
-                                                                   const uint32_t* J, const uint32_t* JM, uint32_t upto,
-                                                                   uint32_t nnew) {
-  const uint32_t jmin = JM[upto];
+                                                                   const JA& J, uint32_t upto, uint32_t nnew) {
+  const uint32_t jmin = J.min_from(upto);
   // (1) the permutation images of this lane's keys, cycle-walked as one stream: each step is one
   // Feistel pass of the lane's current key, so the wave waits for the slowest lane's total passes,
   // not for the slowest lane of every key
@@ -1172,10 +1195,13 @@ __device__ __attribute__((always_inline)) inline void sampled_fill(uint32_t* pay
 #pragma unroll
   for (int q0 = 0; q0 < RESP_KMAX; q0 += RESP_U) {
     if ((uint32_t)q0 >= mcount) break;
-    uint32_t blk[RESP_U];
+    uint32_t blk[RESP_U], bb[RESP_U];
     uint4 b0[RESP_U], b1[RESP_U];
 #pragma unroll
-    for (int u = 0; u < RESP_U; ++u) blk[u] = q0 + u < RESP_KMAX ? bm_block(BP, NB, ratio, y[q0 + u < RESP_KMAX ? q0 + u : 0]) : 0u;
+    for (int u = 0; u < RESP_U; ++u) {
+      bb[u] = 0;
+      blk[u] = q0 + u < RESP_KMAX ? bm_block(BP, NB, ratio, y[q0 + u < RESP_KMAX ? q0 + u : 0], &bb[u]) : 0u;
+    }
 #pragma unroll
     for (int u = 0; u < RESP_U; ++u) {
       b0[u] = *reinterpret_cast<const uint4*>(B + blk[u] * 8);
@@ -1186,12 +1212,12 @@ __device__ __attribute__((always_inline)) inline void sampled_fill(uint32_t* pay
       const uint32_t q = q0 + u;
       if (q >= RESP_KMAX || q >= mcount) break;
       const uint32_t yq = y[q];
-      uint32_t xq = block_pick(b0[u], b1[u], blk[u], yq - BP[blk[u]]);
+      uint32_t xq = block_pick(b0[u], b1[u], blk[u], yq - bb[u]);
       if (xq >= jmin) {                               // rare: a later joiner may sit at or below xq
         uint32_t e = 0;
         while (true) {
           uint32_t c = 0;
-          for (uint32_t f = upto; f < nnew; ++f) c += J[f] <= xq;
+          for (uint32_t f = upto; f < nnew; ++f) c += J.at(f) <= xq;
           if (c == e) break;
           e = c;
           xq = bm_select(B, BP, NB, ratio, yq + e);
@@ -1237,8 +1263,10 @@ __device__ __attribute__((always_inline)) inline uint32_t block_prefix(const uin
 // only wave-level synchronisation.  Same arithmetic as k_resp_node's sampled path.
 constexpr uint32_t RW_JCAP = 128;
 // The slice also holds a copy of the row bitset, taken while the block prefix is counted (the same
-// loads): every sampled select then reads its 32-byte block from LDS instead of L2.
-__host__ __device__ inline uint32_t rwave_head(uint32_t NB) { return (NB + 1 + 2 * RW_JCAP + 1 + 3) & ~3u; }
+// loads): every sampled select then reads its 32-byte block from LDS instead of L2.  The joiner list
+// passes through the head before the prefix is counted there and then lives in registers, so a slice
+// is the prefix and the row: at the 64K bench's rows four workgroups fit a CU (4 waves per SIMD).
+__host__ __device__ inline uint32_t rwave_head(uint32_t NB) { return ((NB + 1 > RW_JCAP ? NB + 1 : RW_JCAP) + 3) & ~3u; }
 __host__ __device__ inline uint32_t rwave_words(uint32_t NW, uint32_t NB) { return rwave_head(NB) + NW; }
 __device__ inline bool resp_by_wave(const Dev& d, uint32_t i, uint32_t nnew, bool on) {
   return on && d.uniform && nnew <= RW_JCAP && d.n[i] - nnew > d.capj;
@@ -1248,14 +1276,13 @@ __device__ inline bool resp_by_wave(const Dev& d, uint32_t i, uint32_t nnew, boo
 // itself: nothing writes a row while the Join responses are built, and a responder's row stays in L2 across
 // its responses.  (The workgroup path instead copied each row to HBM scratch first.)
 template <bool SG>
-__global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint32_t* nodes, const uint32_t* nnodes_p,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_resp_wave(Dev d, PhaseB pb, const uint32_t* nodes, const uint32_t* nnodes_p,
                                                    OutBuf ob, int32_t r, uint32_t* rest) {
   extern __shared__ __attribute__((aligned(16))) uint32_t rw_lds[];
   const uint32_t NW = d.NWR, NB = d.W / 256;
   const uint32_t wv = threadIdx.x >> 6, l = lane(), nwv = blockDim.x >> 6;
   uint32_t* BP = rw_lds + (size_t)wv * (SG ? rwave_head(NB) : rwave_words(NW, NB));   // block prefix [NB + 1]
-  uint32_t* J = BP + NB + 1;                                    // this receiver's new joiners       [RW_JCAP]
-  uint32_t* JM = J + RW_JCAP;                                   // suffix minima of J                [RW_JCAP + 1]
+  uint32_t* Jt = BP;                                            // the new joiners, in passing      [RW_JCAP]
   uint32_t* S = BP + rwave_head(NB);                            // the row bitset (LDS copy)         [NW]
   const uint32_t nnodes = *nnodes_p;
   // A responder's HBM reads (its Join masks, header words, row bitset) are issued together, with the next
@@ -1280,6 +1307,8 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     const uint4* B4 = reinterpret_cast<const uint4*>(B);
     // the row into LDS, every load in flight, before the wave-path test: it fails for a few responders at
     // most (each then costs one wasted copy) and the copy's wait covers the loads above
+    const bool tdbg = (d.dev & 512) != 0;                   // phase timing (KB_DEV=512, KB_DEBUG_WAVES)
+    const uint64_t tps = tdbg ? wall_clock64() : 0;
     if (!SG) stage16(reinterpret_cast<uint4*>(S), B4, NW / 4, l, 64);
     uint32_t nnew = 0;
     if (small_lists) nnew = wave_sum((uint32_t)__popcll(nmv));
@@ -1291,8 +1320,36 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
       continue;
     }
     if (l == 0) path_hit(d, SG ? PATH_RESP_WAVE_HBM : PATH_RESP_WAVE);
-    const bool tdbg = (d.dev & 512) != 0;                   // phase timing (KB_DEV=512, KB_DEBUG_WAVES)
     uint64_t tp0 = tdbg ? wall_clock64() : 0, tp1 = 0, tp2 = 0;
+    if (small_lists) {                                      // new joiners in list order: entries l and l + 64
+      const unsigned long long w0 = ((unsigned long long)rdl((uint32_t)(nmv >> 32), 0) << 32) | rdl((uint32_t)nmv, 0);
+      const unsigned long long w1 = ((unsigned long long)rdl((uint32_t)(nmv >> 32), 1) << 32) | rdl((uint32_t)nmv, 1);
+      if (l < pb.nj && ((w0 >> l) & 1ull)) Jt[__popcll(w0 & ((1ull << l) - 1ull))] = js0;
+      if (l + 64 < pb.nj && ((w1 >> l) & 1ull)) Jt[__popcll(w0) + __popcll(w1 & ((1ull << l) - 1ull))] = js1;
+    } else {
+      for (uint32_t e = l; e < pb.nj; e += 64) {
+        if (!newbit(nm, e)) continue;
+        uint32_t pos = __popcll(nm[e >> 6] & ((1ull << (e & 63)) - 1ull));
+        for (uint32_t w2 = 0; w2 < (e >> 6); ++w2) pos += __popcll(nm[w2]);
+        Jt[pos] = pb.bjoin[e].sender;
+      }
+    }
+    wait_lds();
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t jr0 = l < nnew ? Jt[l] : 0xFFFFFFFFu, jr1 = l + 64 < nnew ? Jt[l + 64] : 0xFFFFFFFFu;
+    uint32_t sm0 = jr0, sm1 = jr1;                          // suffix minima of J[0..nnew), nnew <= 128
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u0 = __shfl_down(sm0, o, 64), u1 = __shfl_down(sm1, o, 64);
+      if (l + o < 64) { sm0 = u0 < sm0 ? u0 : sm0; sm1 = u1 < sm1 ? u1 : sm1; }
+    }
+    {
+      const uint32_t m1 = rdl(sm1, 0);
+      sm0 = m1 < sm0 ? m1 : sm0;
+    }
+    wait_lds();                                             // the list is out of the head before the prefix
+    __builtin_amdgcn_wave_barrier();
+    if (tdbg) tp1 = wall_clock64();
     const uint32_t per = (NB + 63) / 64;                    // block prefix, `per` blocks per lane
     uint32_t bc = 0, last = 0;
     const uint4* S4 = reinterpret_cast<const uint4*>(SG ? B : S);
@@ -1309,35 +1366,6 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     const float ratio = nB ? (float)nbu / (float)nB : 0.0f;
     for (uint32_t k = l * per; k < (l + 1) * per && k < NB; ++k) { const uint32_t c = BP[k]; BP[k] = ex; ex += c; }
     if (l == 0) BP[NB] = nB;
-    if (tdbg) { wait_lds(); tp1 = wall_clock64(); }
-    if (small_lists) {                                      // new joiners in list order: entries l and l + 64
-      const unsigned long long w0 = ((unsigned long long)rdl((uint32_t)(nmv >> 32), 0) << 32) | rdl((uint32_t)nmv, 0);
-      const unsigned long long w1 = ((unsigned long long)rdl((uint32_t)(nmv >> 32), 1) << 32) | rdl((uint32_t)nmv, 1);
-      if (l < pb.nj && ((w0 >> l) & 1ull)) J[__popcll(w0 & ((1ull << l) - 1ull))] = js0;
-      if (l + 64 < pb.nj && ((w1 >> l) & 1ull)) J[__popcll(w0) + __popcll(w1 & ((1ull << l) - 1ull))] = js1;
-    } else {
-      for (uint32_t e = l; e < pb.nj; e += 64) {
-        if (!newbit(nm, e)) continue;
-        uint32_t pos = __popcll(nm[e >> 6] & ((1ull << (e & 63)) - 1ull));
-        for (uint32_t w2 = 0; w2 < (e >> 6); ++w2) pos += __popcll(nm[w2]);
-        J[pos] = pb.bjoin[e].sender;
-      }
-    }
-    wait_lds();
-    __builtin_amdgcn_wave_barrier();
-    {                                                       // suffix minima of J[0..nnew), nnew <= 128
-      uint32_t v0 = l < nnew ? J[l] : 0xFFFFFFFFu, v1 = l + 64 < nnew ? J[l + 64] : 0xFFFFFFFFu;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t u0 = __shfl_down(v0, o, 64), u1 = __shfl_down(v1, o, 64);
-        if (l + o < 64) { v0 = u0 < v0 ? u0 : v0; v1 = u1 < v1 ? u1 : v1; }
-      }
-      const uint32_t m1 = rdl(v1, 0);
-      v0 = m1 < v0 ? m1 : v0;
-      if (l < nnew) JM[l] = v0;
-      if (l + 64 < nnew) JM[l + 64] = v1;
-      if (l == 0) JM[nnew] = 0xFFFFFFFFu;
-    }
     wait_lds();
     __builtin_amdgcn_wave_barrier();
     uint32_t poff = poff_i, q = 0, ins_before = 0;
@@ -1360,7 +1388,8 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
         const uint32_t nk = nB - (nnew - upto), cap = d.capj;
         uint32_t* pay = ob.pay + poff;
         const Prp P = prp_make(nk, philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1));
-        sampled_fill(pay, l, 64, cap, P, SG ? B : S, BP, NB, ratio, J, JM, upto, nnew);
+        const uint32_t jmin = upto < 64 ? rdl(sm0, (int)upto) : upto < 128 ? rdl(sm1, (int)(upto - 64)) : 0xFFFFFFFFu;
+        sampled_fill(pay, l, 64, cap, P, SG ? B : S, BP, NB, ratio, JoinRegs{jr0, jr1, jmin}, upto, nnew);
         if (l == 0) {
           Msg m; m.dest = a; m.sender = i; m.seq = q; m.kind = K_KP; m.a = cap; m.fp = 0; m.n = 0; m.off = poff;
           ob.msgs[ooff_i + q] = m;
@@ -1377,9 +1406,9 @@ __global__ __launch_bounds__(256) void k_resp_wave(Dev d, PhaseB pb, const uint3
     if (tdbg && l == 0) {
       __builtin_amdgcn_s_waitcnt(0);
       const uint64_t tp3 = wall_clock64();
-      atomicAdd(&d.ctr[C_DBG_TNODE], (uint32_t)(tp1 - tp0)); atomicAdd(&d.ctr[C_DBG_TBASE], (uint32_t)(tp2 - tp1));
+      atomicAdd(&d.ctr[C_DBG_TNODE], (uint32_t)(tp2 - tp1)); atomicAdd(&d.ctr[C_DBG_TBASE], (uint32_t)(tp1 - tp0));
       atomicAdd(&d.ctr[C_DBG_TINS], (uint32_t)(tp3 - tp2)); atomicAdd(&d.ctr[C_DBG_TSTART], 1u);
-      atomicAdd(&d.ctr[C_DBG_MSGS], q);
+      atomicAdd(&d.ctr[C_DBG_MSGS], q); atomicAdd(&d.ctr[C_DBG_TEND], (uint32_t)(tp0 - tps));
     }
     wait_lds();                                           // the LDS slice is reused by the next responder
     __builtin_amdgcn_wave_barrier();
@@ -1462,7 +1491,7 @@ __global__ __launch_bounds__(256) void k_resp_node(Dev d, PhaseB pb, const uint3
           const Prp P = prp_make(nk, philox(i, (uint32_t)r, (uint32_t)P_TRUNC << 24, a, d.k0, d.k1));
           const float ratio = nB ? (float)NB / (float)nB : 0.0f;
           if (jl) {                                      // later joiners = J[upto..nnew)
-            sampled_fill(pay, t, T, cap, P, B, BP, NB, ratio, J, JM, upto, nnew);
+            sampled_fill(pay, t, T, cap, P, B, BP, NB, ratio, JoinLds{J, JM}, upto, nnew);
           } else {
             for (uint32_t k = t; k < cap; k += T) {
               const uint32_t y = prp_eval(k, P);

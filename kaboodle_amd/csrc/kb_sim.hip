@@ -1472,8 +1472,8 @@ static int step_round(kb_sim* s) {
         uint32_t dbg[13];
         HIPCHK(hipMemcpyAsync(dbg, d.ctr + C_DBG_INS, 52, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        fprintf(stderr, "[kb] round %d k_resp_wave: responders %u, responses %u: staging+prefix %.1f us, joiners %.1f, "
-                "fills %.1f (sums over waves)\n", r, dbg[10], dbg[12], dbg[6] * 0.01, dbg[8] * 0.01, dbg[9] * 0.01);
+        fprintf(stderr, "[kb] round %d k_resp_wave: responders %u, responses %u: row staging %.1f us, joiners %.1f, prefix %.1f, "
+                "fills %.1f (sums over waves)\n", r, dbg[10], dbg[12], dbg[11] * 0.01, dbg[8] * 0.01, dbg[6] * 0.01, dbg[9] * 0.01);
       }
     }
   }

@@ -21,6 +21,8 @@ print(f"N={N} R={R} wall {dt/R*1e3:.2f} ms/round  rowpass {sw/n:.3f} ms ({m.kern
       f"fold {fo/max(nf,1):.3f} ms ({m.kernel_bytes(2)/max(fo*1e-3,1e-9)/1e9:.1f} GB/s)  round(ev) {rd/n:.3f} ms  "
       f"node-rounds/s {st['alive']*R/dt:.3e}", flush=True)
 print(st)
+kb = m.kernel_breakdown()                     # the byte-counted kernels' per-launch times (HIP events)
+print("kernels " + "  ".join(f"{k} {v['ms'] / max(v['launches'], 1):.4f}" for k, v in sorted(kb.items()) if v["launches"]), flush=True)
 import ctypes as C
 lib = kaboodle_amd.lib().lib
 buf = (C.c_uint64 * 3)()
