@@ -309,20 +309,31 @@ __device__ __attribute__((always_inline)) inline void a3x_narrow(const Dev& d, u
   }
   write_a3_keys(part, i, l, m5);
 }
+// One kernel per row width (the host picks by NB = W / 1024): each holds only its own path, so the 64K rows' KPL-2
+// kernel is not sized for the wider paths' registers (74 VGPRs, 6 waves per SIMD, instead of 105 and 4): beside the
+// fold it then takes more of each CU, and the round is 3 % shorter (`profiles/r06t_ab_a3_split.txt`).
+template <uint32_t KPL>
 __global__ __launch_bounds__(256) void k_a3_exact(Dev d, uint32_t* part, int32_t r) {
   const uint32_t i = d.lo + blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= d.hi) return;
-  const uint32_t NB = d.W >> 10, cur = d.a3cur[i];
+  const uint32_t cur = d.a3cur[i];
   const bool alive = d.alive[i] != 0;
-  if (NB <= 64 * 2) { a3x_narrow<2>(d, part, r, i, cur, alive); return; }
-  if (NB <= 64 * A3X_KPL) { a3x_narrow<A3X_KPL>(d, part, r, i, cur, alive); return; }
-  if (!alive) return;                                                // wider rows: one pass over everything
-  unsigned long long top[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
-  const int32_t E = epoch_base(r);
-  for (uint32_t b = 0; b < NB; ++b) a3x_block<true, true>(d, i, b, cur, E, row_of(d, i), bits_of(d, i), d.tst + (size_t)i * d.W, top);
-  unsigned long long m5[5];
-  wave_top5(top, m5);
-  write_a3_keys(part, i, lane(), m5);
+  if constexpr (KPL != 0) {
+    a3x_narrow<KPL>(d, part, r, i, cur, alive);
+  } else {
+    if (!alive) return;                                              // wider rows: one pass over everything
+    const uint32_t NB = d.W >> 10;
+    unsigned long long top[5] = {~0ull, ~0ull, ~0ull, ~0ull, ~0ull};
+    const int32_t E = epoch_base(r);
+    for (uint32_t b = 0; b < NB; ++b) a3x_block<true, true>(d, i, b, cur, E, row_of(d, i), bits_of(d, i), d.tst + (size_t)i * d.W, top);
+    unsigned long long m5[5];
+    wave_top5(top, m5);
+    write_a3_keys(part, i, lane(), m5);
+  }
+}
+__host__ __device__ inline uint32_t a3_kpl(uint32_t W) {               // 0: the wide path
+  const uint32_t NB = W >> 10;
+  return NB <= 64 * 2 ? 2u : NB <= 64 * A3X_KPL ? A3X_KPL : 0u;
 }
 
 // ---- lifecycle: API start/stop in call order, then churn (src/lib.rs:136-183) ------------------

@@ -1486,7 +1486,10 @@ static int step_round(kb_sim* s) {
   // write checkpoints and fingerprints only
   if (d.tst) {
     side_fork(s, 2);
-    klaunch_on(s, s->st2, KI_A3_EXACT, k_a3_exact, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);
+    const uint32_t kpl = a3_kpl(s->W);
+    if (kpl == 2) klaunch_on(s, s->st2, KI_A3_EXACT, k_a3_exact<2>, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);
+    else if (kpl) klaunch_on(s, s->st2, KI_A3_EXACT, k_a3_exact<A3X_KPL>, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);
+    else klaunch_on(s, s->st2, KI_A3_EXACT, k_a3_exact<0>, dim3((R + 3) / 4), dim3(256), 0, d, s->ro.part, r);
     side_done(s, 2);
   }
   // every checkpoint the round's membership changes (broadcasts, A2) made stale is refolded
