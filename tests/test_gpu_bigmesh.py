@@ -16,7 +16,8 @@ The runs cannot be resident together (≈ 160 GB each): each records its digests
 Oracle parity at scale: 131,072 peers (the dense CPU oracle needs 19 GB of host RAM and ≈ 10 s per round on
 the box's 16 cores there; the 372K oracle would need 145 GB and minutes per round), every fingerprint and
 sampled rows, 6 rounds: the first honoured Failed list (round 5) on rows wider than the LDS paths is checked
-against the oracle, not only GPU against GPU."""
+against the oracle, not only GPU against GPU; the same at 131,072 peers in the exact A3 order checks the
+exact kernel of 128K-512K-id rows (`k_a3_exact<8>`) against the oracle."""
 import ctypes as C
 import hashlib
 import json
@@ -112,6 +113,33 @@ def test_oracle_parity_131k():
     o = Sim(parity.oracle_lib(omp=True), cfg)
     g = Sim(parity.gpu_lib(), cfg)
     rng = np.random.default_rng(7)
+    try:
+        for r in range(6):
+            o.step(1)
+            g.step(1)
+            d = parity.compare_sampled(o, g, rng, nrows=6)
+            assert not d, f"round {r}: " + "; ".join(d[:4])
+        st = g.stats()
+        assert st["join_responses"] > 0 and st["removed_failed"] > 0
+    finally:
+        g.close()
+        o.close()
+
+
+def test_oracle_parity_131k_exact_order():
+    """The exact A3 order (KB_VARIANT_EXACT_LRU, the bench's default) on rows of 139,264 ids: 136 blocks of 1024
+    ids, so `k_a3_exact<8>` (the width between 128K and 512K ids) against the dense CPU oracle, which then holds
+    the C x C instants too (≈ 78 GB of host RAM beside the 19 GB of stamps).  Counters, every fingerprint and
+    per-node scalar, sampled rows, every round for 6 rounds."""
+    import kaboodle_amd
+    from kaboodle_amd._ffi import KB_VARIANT_EXACT_LRU
+    kaboodle_amd.require_gpu()
+    n = 131072
+    cfg = SimConfig(capacity=n + 8192, initial_nodes=n, init_mode=KB_INIT_CONVERGED, loss=0.01, churn=0.0001, seed=5,
+                    variant=KB_VARIANT_EXACT_LRU)
+    o = Sim(parity.oracle_lib(omp=True), cfg)
+    g = Sim(parity.gpu_lib(), cfg)
+    rng = np.random.default_rng(11)
     try:
         for r in range(6):
             o.step(1)
